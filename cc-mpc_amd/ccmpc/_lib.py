@@ -1,0 +1,102 @@
+"""ctypes binding of libccmpc.so (include/ccmpc.h).
+
+The library is built in-tree (``cc-mpc_amd/csrc/Makefile`` -> ``cc-mpc_amd/ccmpc/libccmpc.so``)
+so it travels with the repository snapshot.  There is no fallback: if the library is missing or
+its ABI does not match, every entry point raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.environ.get(
+    "CCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libccmpc.so"))
+ABI_VERSION = 1
+
+CCMPC_OK = 0
+CCMPC_F64 = 0
+CCMPC_F32 = 1
+
+STATUS = {
+    0: "ok", -1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
+    -4: "unsupported configuration", -10: "singular", -11: "no tangent", -12: "non-finite",
+    -13: "not PD", -14: "not PSD",
+}
+
+REC_SINGULAR, REC_NO_TANGENT, REC_NONFINITE, REC_NOT_PD, REC_NOT_PSD = -10, -11, -12, -13, -14
+
+# record layouts (ccmpc_halfspace / ccmpc_affine_rec, 128 bytes each)
+HALFSPACE_DTYPE = np.dtype([
+    ("n0", "<f8"), ("n1", "<f8"), ("d", "<f8"),
+    ("q00", "<f8"), ("q01", "<f8"), ("q11", "<f8"),
+    ("r00", "<f8"), ("r01", "<f8"), ("r11", "<f8"),
+    ("beta1", "<f8"), ("beta2", "<f8"), ("lower_bound", "<f8"),
+    ("mean0", "<f8"), ("mean1", "<f8"),
+    ("which", "<i4"), ("side", "<i4"), ("status", "<i4"), ("t_tau", "<i4"),
+])
+AFFINE_DTYPE = np.dtype([
+    ("n0", "<f8"), ("n1", "<f8"), ("d", "<f8"), ("margin", "<f8"), ("rhs", "<f8"),
+    ("mean0", "<f8"), ("mean1", "<f8"),
+    ("c00", "<f8"), ("c01", "<f8"), ("c11", "<f8"),
+    ("s00", "<f8"), ("s01", "<f8"), ("s11", "<f8"), ("m", "<f8"),
+    ("which", "<i4"), ("side", "<i4"), ("status", "<i4"), ("t", "<i4"),
+])
+assert HALFSPACE_DTYPE.itemsize == 128 and AFFINE_DTYPE.itemsize == 128
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_U64 = ctypes.c_uint64
+_D = ctypes.c_double
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); the exact export list of include/ccmpc.h
+SIGNATURES = {
+    "ccmpc_abi_version": (ctypes.c_int, []),
+    "ccmpc_last_error": (ctypes.c_char_p, []),
+    "ccmpc_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "ccmpc_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
+    "ccmpc_moments": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64, _I64, _P,
+                                     _SZ, _P, _P, _P]),
+    "ccmpc_minkowski": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _D, _D, _I32, _P, _P,
+                                       _P]),
+    "ccmpc_affine": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _D, _P, _P]),
+    "ccmpc_ideal_rollout": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _P, _U64,
+                                           _P, _P, _I64, _P, _P]),
+    "ccmpc_ideal_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
+    "ccmpc_ideal_moments": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _U64, _P,
+                                           _P, _SZ, _P, _P, _P, _P]),
+}
+
+
+class CcmpcError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libccmpc.so once; raise loudly if it is missing or has the wrong ABI."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CcmpcError(
+            f"libccmpc.so not found at {LIB_PATH}: build it with `make -C cc-mpc_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ccmpc_abi_version() != ABI_VERSION:
+        raise CcmpcError(f"libccmpc ABI {lib.ccmpc_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != CCMPC_OK:
+        msg = load().ccmpc_last_error().decode(errors="replace")
+        raise CcmpcError(f"{what} failed ({STATUS.get(rc, rc)}): {msg}")

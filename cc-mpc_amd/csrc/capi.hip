@@ -1,0 +1,29 @@
+// Error plumbing and version entry points of the C ABI (include/ccmpc.h).
+#include <string>
+
+#include "ccmpc_common.hpp"
+
+namespace ccmpc {
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+}  // namespace ccmpc
+
+extern "C" int ccmpc_abi_version(void) { return CCMPC_ABI_VERSION; }
+
+extern "C" const char *ccmpc_last_error(void) { return ccmpc::g_last_error.c_str(); }
+
+extern "C" const char *ccmpc_status_string(int status) {
+  switch (status) {
+    case CCMPC_OK: return "ok";
+    case CCMPC_ERR_ARG: return "invalid argument";
+    case CCMPC_ERR_LAUNCH: return "kernel launch failed";
+    case CCMPC_ERR_WORKSPACE: return "workspace too small";
+    case CCMPC_ERR_UNSUPPORTED: return "unsupported configuration";
+    case CCMPC_REC_SINGULAR: return "singular matrix (LinAlgError in the reference)";
+    case CCMPC_REC_NO_TANGENT: return "no real tangent (n^T Sigma n <= 0)";
+    case CCMPC_REC_NONFINITE: return "non-finite slope or moment";
+    case CCMPC_REC_NOT_PD: return "conditional covariance not positive definite";
+    case CCMPC_REC_NOT_PSD: return "covariance not positive semi-definite (complex sqrtm)";
+    default: return "unknown status";
+  }
+}

@@ -1,0 +1,91 @@
+// Shared device helpers for libccmpc (gfx950 / CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "ccmpc.h"
+
+namespace ccmpc {
+
+// ---- host-side error plumbing --------------------------------------------------------------
+void set_error(const std::string &msg);
+
+#define CCMPC_REQUIRE(cond, msg)                                                              \
+  do {                                                                                         \
+    if (!(cond)) {                                                                             \
+      ::ccmpc::set_error(std::string(__func__) + ": " + (msg));                                \
+      return CCMPC_ERR_ARG;                                                                    \
+    }                                                                                          \
+  } while (0)
+
+#define CCMPC_LAUNCH_CHECK()                                                                   \
+  do {                                                                                         \
+    hipError_t e_ = hipGetLastError();                                                         \
+    if (e_ != hipSuccess) {                                                                    \
+      ::ccmpc::set_error(std::string(__func__) + ": launch failed: " + hipGetErrorString(e_)); \
+      return CCMPC_ERR_LAUNCH;                                                                 \
+    }                                                                                          \
+  } while (0)
+
+inline hipStream_t as_stream(ccmpc_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+// ---- Philox4x32-10 (mirrors oracle/philox.py) ----------------------------------------------
+constexpr uint32_t STREAM_IDEAL_Z = 0x1DEA0001u;
+constexpr uint32_t STREAM_IDEAL_X0 = 0x1DEA0002u;
+constexpr uint32_t STREAM_SAMPLER_EPS = 0x5A4D0001u;
+constexpr uint32_t STREAM_SAMPLER_Z = 0x5A4D0002u;
+
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint64_t seed) {
+  uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return {c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ double uniform53(uint32_t a, uint32_t b) {
+  return (static_cast<double>(a >> 5) * 67108864.0 + static_cast<double>(b >> 6)) *
+         (1.0 / 9007199254740992.0);
+}
+
+// Box-Muller pair, float64 (oracle/philox.py normal_pair)
+__device__ __forceinline__ void normal_pair(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint64_t seed, double &z0, double &z1) {
+  const u32x4 w = philox4x32(c0, c1, c2, c3, seed);
+  const double u1 = 1.0 - uniform53(w.x, w.y);
+  const double u2 = uniform53(w.z, w.w);
+  const double r = sqrt(-2.0 * log(u1));
+  double s, c;
+  sincos(2.0 * M_PI * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// ---- 2x2 symmetric helpers -----------------------------------------------------------------
+struct Sym2 {
+  double a, b, c;  // [[a, b], [b, c]]
+};
+
+}  // namespace ccmpc

@@ -1,0 +1,177 @@
+/*
+ * ccmpc.h -- C ABI of libccmpc.so, the MI355X (gfx950) implementation of CC-MPC's
+ * Monte-Carlo prediction + MVOE chance-constraint path (planner v8ideal).
+ *
+ * The reference is pure Python (HyeontaeSung/CC-MPC, snapshot 2025-10-31).  Each entry point
+ * below replaces one stage of its hot path; the reference function it replaces is cited as
+ * file:line, relative to /root/reference/collect/in_simulation/midlevel/ unless stated.
+ * The host-side mirror of the reference interface (cc-mpc_amd/ccmpc) binds these with ctypes;
+ * INTEGRATION.md shows the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer unless its comment says "host".
+ *  - All buffers are caller-allocated; no entry point allocates, frees or synchronises, so every
+ *    call can be captured into a hipGraph.  Work is enqueued on `stream` (a hipStream_t; NULL =
+ *    the null stream).  Calls are reentrant per stream.
+ *  - Return value: CCMPC_OK (0) or a negative CCMPC_ERR_* code for bad arguments / launch
+ *    failures (ccmpc_last_error() gives the message, per host thread).  Numerical failures of a
+ *    single record (singular covariance, no real tangent, ...) do not fail the call; they are
+ *    reported in that record's `status` field with a CCMPC_REC_* code, mirroring where the
+ *    reference raises.
+ *
+ * Particle store ("plane-major SoA")
+ *  - positions[(2*t + c) * ld + i], c = 0 for x, 1 for y: plane 2t+c holds coordinate c at step
+ *    t of every particle.  Consecutive particles are consecutive in memory, so one wavefront
+ *    reads 64 particles of one plane as a single coalesced burst.
+ *  - A *cell* is one (obstacle vehicle, latent mode) pair; it owns particles
+ *    [cell_off[c], cell_off[c] + cell_cnt[c]) in every plane.  cell_off must be a multiple of 4
+ *    and ld a multiple of 4 (16-byte aligned 4-particle vectors).
+ *  - dtype CCMPC_F64: world-frame float64 (what predict_ideal writes, v8ideal/__init__.py:2667).
+ *    dtype CCMPC_F32: float32 relative to a per-cell origin (what Trajectron++ writes before
+ *    `+ minpos`, v8ideal/__init__.py:486); every reduction promotes to float64 first.
+ */
+#ifndef CCMPC_H
+#define CCMPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *ccmpc_stream_t; /* hipStream_t */
+
+#define CCMPC_ABI_VERSION 1
+
+/* call status */
+#define CCMPC_OK 0
+#define CCMPC_ERR_ARG -1
+#define CCMPC_ERR_LAUNCH -2
+#define CCMPC_ERR_WORKSPACE -3
+#define CCMPC_ERR_UNSUPPORTED -4
+
+/* per-record status (0 = ok) */
+#define CCMPC_REC_SINGULAR -10   /* inv(cov_tau) or solve(Sigma1, Sigma2) singular (LinAlgError) */
+#define CCMPC_REC_NO_TANGENT -11 /* n^T Sigma n <= 0: choose_closest_tangent returns None tuple */
+#define CCMPC_REC_NONFINITE -12  /* slope m or a moment is inf/nan (ref_y == mean_y, N_k < 2) */
+#define CCMPC_REC_NOT_PD -13     /* conditional covariance not PD (np.linalg.cholesky raises) */
+#define CCMPC_REC_NOT_PSD -14    /* sqrtm of an indefinite covariance would be complex */
+
+/* particle dtypes */
+#define CCMPC_F64 0
+#define CCMPC_F32 1
+
+/* One Minkowski/MVOE half-space (one (cell, t, tau) pair), 128 bytes.
+ * Constraint on the ego position x_t:  side=+1:  n . x_t >= d ;  side=-1:  n . x_t <= d
+ * (v8ideal/__init__.py:926-939).  The reference's (A, b) = (-n, -d) or (n, d). */
+typedef struct ccmpc_halfspace {
+  double n0, n1;          /* normal [-m, 1]                                            */
+  double d;               /* offset of the chosen slope-m tangent                      */
+  double q00, q01, q11;   /* Q  = MVOE(cov_infer*chi_r, cov_mu*chi_p)   (:915)           */
+  double r00, r01, r11;   /* QR = MVOE(Q, R^2 I)                        (:917-918)       */
+  double beta1, beta2;    /* fixed-point solutions of the two MVOE calls               */
+  double lower_bound;     /* compute_lower_bound(cov_infer, cov_mu, cov_t, eps) (:942)   */
+  double mean0, mean1;    /* ellipsoid centre = particle mean at step t (:896)         */
+  int32_t which;          /* 0: the "+" tangent, 1: the "-" tangent                    */
+  int32_t side;           /* +1 (>=) or -1 (<=)                                        */
+  int32_t status;         /* CCMPC_REC_* or 0                                          */
+  int32_t t_tau;          /* (t << 16) | tau                                           */
+} ccmpc_halfspace;
+
+/* One GMM-affine half-space (one (cell, t)), 128 bytes (v8ideal/__init__.py:1476-1515).
+ * side=+1:  n . x_t >= rhs = d + margin ;  side=-1:  n . x_t <= rhs = d - margin
+ * (plus the caller's S_big_repeated[0, t] term, which is a QP variable, not data). */
+typedef struct ccmpc_affine_rec {
+  double n0, n1, d;
+  double margin;          /* Gamma * || sqrtm(cov) [m, -1]^T ||_2                       */
+  double rhs;
+  double mean0, mean1;
+  double c00, c01, c11;   /* particle covariance at step t (ddof = 1)                  */
+  double s00, s01, s11;   /* sqrtm(cov)                                                */
+  double m;               /* slope -(ref_x - mean_x) / (ref_y - mean_y)                 */
+  int32_t which, side, status, t;
+} ccmpc_affine_rec;
+
+int ccmpc_abi_version(void);
+const char *ccmpc_last_error(void);
+const char *ccmpc_status_string(int status);
+
+/* ---------------------------------------------------------------------------------------
+ * Moment (Gram) reduction.  Replaces every np.mean / np.cov over particle clouds on the path:
+ *   v8ideal/__init__.py:864-875 (t=0 stats), :896 + makeconstraint.py:41-70 predict_moments
+ *   (each (t,tau) np.cov is a 4x4 block of out_cov), :1485-1493 (affine), :2584-2606
+ *   save_moments (mean_p0p1[t] = out_mean[t], cov_p0p1[t] = diagonal 2x2 block,
+ *   cross_cov[t][tau] = block (t, tau)).
+ * out_mean[c][t][2] (origin added back for F32), out_cov[c][2T][2T] (ddof = 1, symmetric).
+ * n_particles_bound >= sum(cell_cnt) sizes the grid, so counts may be produced on the device.
+ * T <= 40.  Deterministic: partial sums are combined in a fixed order.
+ * ------------------------------------------------------------------------------------- */
+size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_particles_bound);
+int ccmpc_moments(const void *positions, int dtype, int64_t ld, int64_t T,
+                  const double *origin /* [n_cells][2] for F32, NULL for F64 */,
+                  const int64_t *cell_off, const int64_t *cell_cnt, int64_t n_cells,
+                  int64_t n_particles_bound, void *workspace, size_t workspace_bytes,
+                  double *out_mean, double *out_cov, ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Minkowski / MVOE half-space assembly for every (cell, t, tau < t), from ccmpc_moments output.
+ * Replaces v8ideal/__init__.py:893-947 with makeconstraint.py predict_moments (:41-70),
+ * compute_mvoe (:7-38, called twice), choose_closest_tangent (:176-207) and
+ * compute_lower_bound (:282-303).
+ *  ref_traj[r][t][2]   reference trajectory r (host load_refT, :2768-2787), cell c uses
+ *                      r = cell_ref[c] (NULL -> 0)
+ *  cell_risk[c][3]     {chi_r = chi2.ppf(1-eps_ijt, 2), chi_p = chi2.ppf(0.9999, 2),
+ *                       gamma = norm.ppf(1-eps_ijt)}, eps_ijt = eps_ura[ov,k]/ph (:910-913)
+ *  R                   3.4 (:795); tol 1e-8, maxiter 1000 (makeconstraint.py:7)
+ *  out_rec[c][T(T-1)/2] in the reference's append order: pair p = t(t-1)/2 + tau
+ *  out_prob_lower[c][T] min over tau of the lower bound, 1.0 at t = 0 (:898, :943)
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_minkowski(const double *mean, const double *cov, int64_t T, int64_t n_cells,
+                    const double *ref_traj, const int32_t *cell_ref, const double *cell_risk,
+                    double R, double tol, int32_t maxiter, ccmpc_halfspace *out_rec,
+                    double *out_prob_lower, ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GMM-affine half-spaces for every (cell, t).  Replaces v8ideal/__init__.py:1470-1515.
+ *  cell_gamma[c] = norm.ppf(1 - eps_ura[ov,k]/ph) (:1481-1482); out_rec[c][T].
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_affine(const double *mean, const double *cov, int64_t T, int64_t n_cells,
+                 const double *ref_traj, const int32_t *cell_ref, const double *cell_gamma,
+                 double R, ccmpc_affine_rec *out_rec, ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * predict_ideal: affine conditional-Gaussian forward rollout (v8ideal/__init__.py:2620-2711)
+ * from the PREVIOUS planning step's moments, which stay device-resident (no pickle round trip).
+ *  prev_mean[s][T_src][2], prev_cov[s][2T_src][2T_src]  -- ccmpc_moments output of that step
+ *  src_cell[c]         the reference's data_idx fallback, resolved by the host (:2650-2656)
+ *  x0[c][2]            the shared initial draw (:2662-2665); NULL -> x0 = mean_0 + chol(cov_0) z,
+ *                      z = Philox pair (0, 0, rng_cell[c], STREAM_IDEAL_X0)
+ *  Z[c][t][2][n]       step noise (:2699-2700); NULL -> Philox pair (i, t, rng_cell[c], STREAM_IDEAL_Z)
+ *  rng_cell[c]         RNG stream id per cell (NULL -> c), so results are identical however the
+ *                      cells are sharded over GPUs
+ *  out positions: cell c occupies [c*S, c*S + n_samples) of every plane, S = n_samples rounded
+ *  up to a multiple of 4 (so the output is a valid ccmpc_moments store), dtype F64, slot t holds
+ *  x_{t+1} (the reference's slot quirk).  T <= T_src - 1, ld >= n_cells * S.
+ *  out_status[c]: 0 or CCMPC_REC_SINGULAR / CCMPC_REC_NOT_PD.
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_ideal_rollout(const double *prev_mean, const double *prev_cov, int64_t T_src,
+                        const int32_t *src_cell, int64_t n_cells, int64_t T, int64_t n_samples,
+                        const double *x0, const double *Z, uint64_t seed,
+                        const int32_t *rng_cell, double *out_positions, int64_t ld,
+                        int32_t *out_status, ccmpc_stream_t stream);
+
+/* Same rollout fused with the moment reduction: particles are generated in registers and
+ * reduced without ever being written to HBM (the reference's only consumer of the 1e6-row
+ * ideal trajectories is np.cov, :886-907 and :2586-2606).  Z must be NULL (Philox). */
+size_t ccmpc_ideal_moments_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_samples);
+int ccmpc_ideal_moments(const double *prev_mean, const double *prev_cov, int64_t T_src,
+                        const int32_t *src_cell, int64_t n_cells, int64_t T, int64_t n_samples,
+                        const double *x0, uint64_t seed, const int32_t *rng_cell,
+                        void *workspace, size_t workspace_bytes, double *out_mean,
+                        double *out_cov, int32_t *out_status, ccmpc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCMPC_H */

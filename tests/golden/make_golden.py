@@ -1,0 +1,213 @@
+"""Generate the golden fixtures that pin the oracle to the reference.
+
+Runs ONLY in the build container, where /root/reference exists.  It loads the reference's
+own math module by file path
+
+    /root/reference/collect/in_simulation/midlevel/v8ideal/makeconstraint.py
+
+(numpy + scipy only; the planner package around it needs carla/cvxpy/Trajectron++ and is not
+importable) and records inputs + outputs of its functions as .npz data.  The whole-cycle
+fixtures drive the reference's makeconstraint functions through the restated planner glue
+(oracle.ccmpc_oracle.minkowski_generator / affine_generator with mc=<reference module>), so the
+arithmetic inside every (t, tau) pair is the reference's.
+
+The reference RNG is unseeded (v8ideal/__init__.py:2664, :2699), so every random input is drawn
+here from a fixed numpy seed and stored in the fixture.
+
+Usage:  python tests/golden/make_golden.py      (rewrites tests/golden/*.npz)
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import ccmpc_oracle as orc  # noqa: E402
+
+REF_MC = "/root/reference/collect/in_simulation/midlevel/v8ideal/makeconstraint.py"
+
+
+def load_reference():
+    spec = importlib.util.spec_from_file_location("ref_makeconstraint", REF_MC)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def rand_spd(rng, scale=1.0, cond=10.0):
+    th = rng.uniform(0, np.pi)
+    R = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+    l1 = scale * rng.uniform(0.5, 2.0)
+    l2 = l1 / rng.uniform(1.0, cond)
+    return R @ np.diag([l1, l2]) @ R.T
+
+
+def random_walk_cell(rng, n, T, origin=(190.0, -80.0)):
+    """Trajectory cloud (n, T, 2): shared heading/speed mode + per-particle noise that
+    accumulates over t, so (t, tau) blocks are strongly correlated like real rollouts."""
+    heading = rng.uniform(-np.pi, np.pi)
+    speed = rng.uniform(3.0, 10.0)
+    p0 = np.array(origin) + rng.uniform(-10, 10, size=2)
+    dv = rng.normal(0, 0.8, size=(n, 1))
+    dh = rng.normal(0, 0.12, size=(n, 1))
+    steps = np.arange(1, T + 1)[None, :] * 0.5
+    h = heading + dh * steps
+    v = speed + dv
+    x = p0[0] + np.cumsum(v * np.cos(h) * 0.5, axis=1) + rng.normal(0, 0.05, size=(n, T))
+    y = p0[1] + np.cumsum(v * np.sin(h) * 0.5, axis=1) + rng.normal(0, 0.05, size=(n, T))
+    return np.stack((x, y), axis=-1)
+
+
+def pack_cells(cells):
+    counts = np.array([c.shape[0] for c in cells], dtype=np.int64)
+    flat = np.concatenate([c.reshape(-1, c.shape[1], 2) for c in cells], axis=0)
+    return counts, flat
+
+
+def make_ovs(cells_per_ov, T):
+    ovs = []
+    for cells in cells_per_ov:
+        K = len(cells)
+        pmf = np.array([c.shape[0] for c in cells], dtype=float)
+        pmf /= pmf.sum()
+        past = np.array([[cells[0][0, 0, 0] - 4.0, cells[0][0, 0, 1] - 1.0]])
+        yaws = [orc._step_yaws(c, past[-1], T) for c in cells]
+        centres = np.array([c[:, T - 1].mean(0) for c in cells])
+        ovs.append(orc.OVehicle(T, past, pmf, list(cells), yaws, centres, np.array([4.5, 2.5])))
+        assert ovs[-1].n_states == K
+    return ovs
+
+
+def main():
+    ref = load_reference()
+    rng = np.random.default_rng(20251015)
+    out = {}
+
+    # --- compute_mvoe (makeconstraint.py:7-38) ---------------------------------------
+    n = 160
+    S1 = np.zeros((n, 2, 2)); S2 = np.zeros((n, 2, 2))
+    for i in range(n):
+        S1[i] = rand_spd(rng, scale=10 ** rng.uniform(-3, 1), cond=10 ** rng.uniform(0, 3))
+        S2[i] = rand_spd(rng, scale=10 ** rng.uniform(-3, 1), cond=10 ** rng.uniform(0, 3))
+    S2[0] = np.diag([1e-12, 1e-12]) + S2[0] * 1e-9        # near-degenerate second ellipsoid
+    S2[1] = 3.4 ** 2 * np.eye(2)                          # the (Q, R^2 I) call shape
+    beta = np.zeros(n); Q = np.zeros((n, 2, 2))
+    for i in range(n):
+        beta[i], Q[i] = ref.compute_mvoe(S1[i], S2[i])
+    np.savez(os.path.join(HERE, "mvoe.npz"), S1=S1, S2=S2, beta=beta, Q=Q)
+
+    # --- predict_moments (makeconstraint.py:41-70) ------------------------------------
+    sizes = [5, 17, 64, 250, 1000, 2048]
+    pts, offs = [], [0]
+    ci, cm, ct = [], [], []
+    for s in sizes * 3:
+        cell = random_walk_cell(rng, s, 8)
+        t, tau = sorted(rng.choice(8, size=2, replace=False))[::-1]
+        p = np.stack((cell[:, t, 0], cell[:, t, 1], cell[:, tau, 0], cell[:, tau, 1]))
+        a, b, c = ref.predict_moments([p[0], p[1], p[2], p[3]])
+        pts.append(p); offs.append(offs[-1] + s)
+        ci.append(a); cm.append(b); ct.append(c)
+    np.savez(os.path.join(HERE, "predict_moments.npz"), points=np.concatenate(pts, axis=1),
+             offsets=np.array(offs), cov_infer=np.array(ci), cov_mu=np.array(cm),
+             cov_t=np.array(ct))
+
+    # --- choose_closest_tangent (makeconstraint.py:134-207) ---------------------------
+    n = 200
+    mu = rng.uniform(-100, 200, size=(n, 2))
+    Sig = np.array([rand_spd(rng, scale=rng.uniform(0.1, 20)) for _ in range(n)])
+    m = rng.normal(0, 3, size=n)
+    a = mu + rng.normal(0, 15, size=(n, 2))
+    a[:20] = mu[:20]                                     # equidistant -> strict '<' tie, idx 0
+    c = np.where(rng.uniform(size=n) < 0.5, 1.0, 3.4)
+    nn = np.zeros((n, 2)); dd = np.zeros(n); ww = np.zeros(n, dtype=np.int64)
+    for i in range(n):
+        nn[i], dd[i], ww[i] = ref.choose_closest_tangent(mu[i], Sig[i], c[i], m[i], a[i])
+    np.savez(os.path.join(HERE, "tangent.npz"), mu=mu, Sigma=Sig, m=m, a=a, c=c,
+             n=nn, d=dd, which=ww)
+
+    # --- compute_lower_bound / compute_scale (makeconstraint.py:259-303) ---------------
+    n = 120
+    CI = np.array([rand_spd(rng, scale=rng.uniform(0.01, 1)) for _ in range(n)])
+    CM = np.array([rand_spd(rng, scale=rng.uniform(0.01, 1)) for _ in range(n)])
+    CT = CI + CM
+    eps = 0.05 / rng.integers(1, 9, size=n) / rng.choice([6, 8, 12, 40], size=n)
+    gam = np.array([orc.scipy.stats.norm.ppf(1 - e) for e in eps])
+    lb = np.array([ref.compute_lower_bound(CI[i], CM[i], CT[i], eps[i]) for i in range(n)])
+    sc = np.array([ref.compute_scale(CI[i], CM[i], CT[i], gam[i]) for i in range(n)])
+    np.savez(os.path.join(HERE, "lower_bound.npz"), cov_infer=CI, cov_mu=CM, cov_t=CT,
+             eps=eps, gamma=gam, lower_bound=lb, scale=sc)
+
+    # --- whole Minkowski / affine cycles (v8ideal/__init__.py:781-964, :1378-1539) -----
+    for name, O, Ks, Ns, T in (("cycle_o2_t8", 2, (2, 1), (300, 180, 420), 8),
+                               ("cycle_o1_t12", 1, (2,), (256, 97), 12)):
+        cells_per_ov, flat_cells = [], []
+        it = iter(Ns)
+        for o in range(O):
+            cells = [random_walk_cell(rng, next(it), T) for _ in range(Ks[o])]
+            cells_per_ov.append(cells)
+            flat_cells.extend(cells)
+        ovs = make_ovs(cells_per_ov, T)
+        ego = np.array(cells_per_ov[0][0][:, 0].mean(0)) + np.array([-12.0, 3.0])
+        ref_traj = np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
+        mk = orc.minkowski_generator(ovs, T, T, ref_traj, mc=ref, with_l4=True)
+        af = orc.affine_generator(ovs, T, T, ref_traj, mc=ref, with_l4=False)
+        counts, flat = pack_cells(flat_cells)
+        recs = mk["records"]
+        A_union = np.array([[mk["A_union"][t][k][o] for t in range(T)]
+                            for o in range(O) for k in range(Ks[o])])
+        b_union = np.array([[mk["b_union"][t][k][o] for t in range(T)]
+                            for o in range(O) for k in range(Ks[o])])
+        mom = mk["moments"]
+        np.savez(
+            os.path.join(HERE, f"{name}.npz"),
+            T=T, K=np.array(Ks), counts=counts, positions=flat, ref_traj=ref_traj,
+            past=np.array([ov.past[-1] for ov in ovs]),
+            rec_cell=np.array([[r["ov"], r["k"], r["t"], r["tau"]] for r in recs]),
+            rec_n=np.array([r["n"] for r in recs]), rec_d=np.array([r["d"] for r in recs]),
+            rec_which=np.array([r["which"] for r in recs]),
+            rec_side=np.array([r["side"] for r in recs]),
+            rec_Q=np.array([r["Q"] for r in recs]), rec_QR=np.array([r["QR"] for r in recs]),
+            rec_beta=np.array([[r["beta1"], r["beta2"]] for r in recs]),
+            rec_lb=np.array([r["lb"] for r in recs]),
+            rec_mean=np.array([r["mean"] for r in recs]),
+            prob_lower_save=np.array(mk["prob_lower_save"], dtype=float),
+            aff_n=np.array([r["n"] for r in af["records"]]),
+            aff_d=np.array([r["d"] for r in af["records"]]),
+            aff_which=np.array([r["which"] for r in af["records"]]),
+            aff_side=np.array([r["side"] for r in af["records"]]),
+            aff_margin=np.array([r["margin"] for r in af["records"]]),
+            aff_rhs=np.array([r["rhs"] for r in af["records"]]),
+            A_union=A_union, b_union=b_union,
+            mom_mean=np.array([[mom["mean_p0p1"][o][k][t] for t in range(T)]
+                               for o in range(O) for k in range(Ks[o])]),
+            mom_cov=np.array([[mom["cov_p0p1"][o][k][t] for t in range(T)]
+                              for o in range(O) for k in range(Ks[o])]),
+            state_mean=np.array([[mk["ov_state_mean"][j][o][k] for j in range(3)]
+                                 for o in range(O) for k in range(Ks[o])], dtype=float),
+            state_cov=np.array([[mk["ov_state_cov"][j][o][k] for j in range(3)]
+                                for o in range(O) for k in range(Ks[o])], dtype=float),
+        )
+
+    # --- predict_ideal (v8ideal/__init__.py:2620-2711), injected x0 and Z --------------
+    T = 8
+    cells = [[random_walk_cell(rng, 400, T), random_walk_cell(rng, 250, T)]]
+    mom = orc.save_moments(cells, T)
+    Tn, ns = T - 1, 48
+    x0s = [[mom["mean_p0p1"][0][k][0] + rng.normal(0, 0.3, 2) for k in range(2)]]
+    Zs = [[[rng.normal(size=(ns, 2)) for _ in range(Tn)] for _ in range(2)]]
+    traj = orc.predict_ideal(mom, [2], Tn, ns, x0s=x0s, Zs=Zs)
+    np.savez(os.path.join(HERE, "ideal_rollout.npz"),
+             mean=np.array([[mom["mean_p0p1"][0][k][t] for t in range(T)] for k in range(2)]),
+             cov=np.array([[mom["cov_p0p1"][0][k][t] for t in range(T)] for k in range(2)]),
+             xcov=np.array([[[mom["cross_cov"][0][k][t][tau] if tau < t else np.zeros((2, 2))
+                              for tau in range(T)] for t in range(T)] for k in range(2)]),
+             x0=np.array(x0s[0]), Z=np.array(Zs[0]), traj=np.array([traj[0][k] for k in range(2)]))
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+"""Pin the CPU oracle to the reference: every golden vector in tests/golden was produced by the
+reference's own makeconstraint.py (see tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+from oracle import ccmpc_oracle as orc
+
+from _cycle_inputs import ovehicles_from_fixture
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+
+
+def test_mvoe_matches_reference(golden):
+    g = golden("mvoe")
+    for i in range(len(g["beta"])):
+        beta, Q, _ = orc.compute_mvoe(g["S1"][i], g["S2"][i])
+        assert beta == pytest.approx(g["beta"][i], rel=1e-12)
+        assert rel(Q, g["Q"][i]) < 1e-12
+
+
+def test_predict_moments_matches_reference(golden):
+    g = golden("predict_moments")
+    offs = g["offsets"]
+    for i in range(len(offs) - 1):
+        p = g["points"][:, offs[i]:offs[i + 1]]
+        ci, cm, ct = orc.predict_moments([p[0], p[1], p[2], p[3]])
+        assert rel(ci, g["cov_infer"][i]) < 1e-9   # Schur complement: cancellation-limited
+        assert rel(cm, g["cov_mu"][i]) < 1e-12
+        assert rel(ct, g["cov_t"][i]) < 1e-14
+
+
+def test_tangent_matches_reference_including_ties(golden):
+    g = golden("tangent")
+    for i in range(len(g["m"])):
+        n, d, which = orc.choose_closest_tangent(g["mu"][i], g["Sigma"][i], g["c"][i], g["m"][i],
+                                                 g["a"][i])
+        assert which == g["which"][i]
+        np.testing.assert_array_equal(n, g["n"][i])
+        assert d == pytest.approx(g["d"][i], rel=1e-15, abs=1e-12)
+    # a == mu (the first 20 cases): the two distances differ only by the rounding of
+    # proj +/- delta, and the reference's strict '<' resolves them both ways -- the oracle
+    # reproduces every one of those knife-edge picks bit-for-bit above.
+    assert 0 < np.sum(g["which"][:20]) < 20
+
+
+def test_lower_bound_and_scale_match_reference(golden):
+    g = golden("lower_bound")
+    for i in range(len(g["eps"])):
+        lb = orc.compute_lower_bound(g["cov_infer"][i], g["cov_mu"][i], g["cov_t"][i], g["eps"][i])
+        sc = orc.compute_scale(g["cov_infer"][i], g["cov_mu"][i], g["cov_t"][i], g["gamma"][i])
+        assert lb == pytest.approx(g["lower_bound"][i], rel=1e-12, abs=1e-15)
+        assert sc == pytest.approx(g["scale"][i], rel=1e-12)
+
+
+@pytest.mark.parametrize("name", ["cycle_o2_t8", "cycle_o1_t12"])
+def test_minkowski_cycle_matches_reference(golden, name):
+    g = golden(name)
+    T = int(g["T"])
+    ovs = ovehicles_from_fixture(g)
+    out = orc.minkowski_generator(ovs, T, T, g["ref_traj"])
+    recs = out["records"]
+    assert len(recs) == len(g["rec_d"])
+    cells = np.array([[r["ov"], r["k"], r["t"], r["tau"]] for r in recs])
+    np.testing.assert_array_equal(cells, g["rec_cell"])           # record order
+    np.testing.assert_array_equal([r["which"] for r in recs], g["rec_which"])
+    np.testing.assert_array_equal([r["side"] for r in recs], g["rec_side"])
+    for i, r in enumerate(recs):
+        assert rel(r["Q"], g["rec_Q"][i]) < 1e-10
+        assert rel(r["QR"], g["rec_QR"][i]) < 1e-10
+        assert r["d"] == pytest.approx(g["rec_d"][i], rel=1e-12)
+        assert r["lb"] == pytest.approx(g["rec_lb"][i], rel=1e-9, abs=1e-12)
+    np.testing.assert_allclose(np.array(out["prob_lower_save"], float), g["prob_lower_save"],
+                               rtol=1e-9)
+    K = g["K"]
+    A = np.array([[out["A_union"][t][k][o] for t in range(T)]
+                  for o in range(len(K)) for k in range(K[o])])
+    b = np.array([[out["b_union"][t][k][o] for t in range(T)]
+                  for o in range(len(K)) for k in range(K[o])])
+    np.testing.assert_allclose(A, g["A_union"], rtol=1e-14, atol=1e-15)
+    np.testing.assert_allclose(b, g["b_union"], rtol=1e-13)
+
+
+@pytest.mark.parametrize("name", ["cycle_o2_t8", "cycle_o1_t12"])
+def test_affine_cycle_matches_reference(golden, name):
+    g = golden(name)
+    T = int(g["T"])
+    out = orc.affine_generator(ovehicles_from_fixture(g), T, T, g["ref_traj"], with_l4=False)
+    recs = out["records"]
+    np.testing.assert_array_equal([r["which"] for r in recs], g["aff_which"])
+    np.testing.assert_array_equal([r["side"] for r in recs], g["aff_side"])
+    np.testing.assert_allclose([r["margin"] for r in recs], g["aff_margin"], rtol=1e-12)
+    np.testing.assert_allclose([r["rhs"] for r in recs], g["aff_rhs"], rtol=1e-13)
+
+
+def test_predict_ideal_with_injected_draws(golden):
+    g = golden("ideal_rollout")
+    mom = dict(mean_p0p1=[list(g["mean"])], cov_p0p1=[list(g["cov"])],
+               cross_cov=[[[list(g["xcov"][k][t]) for t in range(g["xcov"].shape[1])]
+                           for k in range(2)]])
+    ns, Tn = g["traj"].shape[1], g["traj"].shape[2]
+    traj = orc.predict_ideal(mom, [2], Tn, ns, x0s=[list(g["x0"])],
+                             Zs=[[list(g["Z"][k]) for k in range(2)]])
+    for k in range(2):
+        np.testing.assert_allclose(traj[0][k], g["traj"][k], rtol=1e-13)
+
+
+def test_ideal_data_idx_fallback():
+    """K grew since the moments were saved: extra modes reuse the last saved mode
+    (v8ideal/__init__.py:2650-2656)."""
+    rng = np.random.default_rng(0)
+    T = 5
+    cells = [[rng.normal(size=(200, T, 2)).cumsum(1)]]
+    mom = orc.save_moments(cells, T)
+    traj = orc.predict_ideal(mom, [3], T - 1, 16, seed=7)
+    assert set(traj[0].keys()) == {0, 1, 2}
+    # same source moments, different RNG cells -> same distribution, different draws
+    assert not np.allclose(traj[0][1], traj[0][2])
+
+
+def test_philox_known_answer():
+    """Philox4x32-10 known-answer vector (Salmon et al., Random123 kat_vectors: counter 0,
+    key 0)."""
+    from oracle import philox
+    w = philox.philox4x32(0, 0, 0, 0, 0)
+    assert [int(x) for x in w] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    w = philox.philox4x32(0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff,
+                          0xffffffffffffffff)
+    assert [int(x) for x in w] == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
