@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: MPC constraint-generation cycles/s (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): one scene, 4 obstacle vehicles, np = 5000 particles
+per OV, ph = 8, v8ideal's Minkowski/MVOE constraint-generation cycle
+(v8ideal/__init__.py:881-947 + the save_moments statistics): particle clouds already resident
+in HBM -> per-cell moments -> every (cell, t, tau) MVOE half-space record.  One "step" = one
+cycle, replayed as one hipGraph.  Synthetic seeded particle clouds (no Trajectron++ weights or
+CARLA exist here).
+
+Multi-GPU (torchrun, one process per GPU): every rank plans its own independent scene
+(weak scaling, no data-path collective); value = cycles completed by all ranks / max-over-ranks
+wall time.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "cc-mpc_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "MPC constraint-gen cycles/sec @20Hz (np=5000, ph=8); ellipsoid ΔF-norm vs ref"
+HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--O", type=int, default=4)
+    ap.add_argument("--N", type=int, default=5000)
+    ap.add_argument("--T", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-cycles", type=int, default=40)
+    return ap.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def time_kernel_live(fn, dev, reps=200):
+    """Average duration of one launch of `fn` on the current stream, HIP events bracketing
+    `reps` back-to-back launches (graph-free, so launches queue ahead of the GPU)."""
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize(dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e-3 / reps
+
+
+def cpu_baseline(ovs, ref, T, cycles):
+    """The oracle's loop-faithful restatement of v8ideal/__init__.py:881-947 on this host,
+    BLAS at 1 thread and at all threads; the faster is reported."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import ccmpc_oracle as orc
+    import scipy.stats
+    chi_p = scipy.stats.chi2.ppf(orc.TARGET_P, df=2)
+    O = len(ovs)
+
+    def one_cycle():
+        for o, cells in enumerate(ovs):
+            for k, traj in enumerate(cells):
+                eps = (orc.EPS_TOTAL / O) / T
+                chi_r = scipy.stats.chi2.ppf(1 - eps, df=2)
+                orc.minkowski_cell(np.vstack(traj), T, T, ref, eps, chi_r, chi_p)
+
+    best = None
+    ncpu = os.cpu_count() or 1
+    for threads in (1, ncpu):
+        with threadpool_limits(limits=threads):
+            for _ in range(2):
+                one_cycle()
+            ts = []
+            for _ in range(cycles):
+                t0 = time.perf_counter()
+                one_cycle()
+                ts.append(time.perf_counter() - t0)
+        med = statistics.median(ts)
+        if best is None or med < best[0]:
+            best = (med, threads, sum(ts))
+    return best
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist(args)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from ccmpc import cycle, engine, synthetic
+
+    # every rank plans its own scene: seed keyed by the global scene index
+    ovs, ref, _ = synthetic.scene(args.seed + rank, O=args.O, N=args.N, T=args.T)
+    K = [len(o) for o in ovs]
+    store = engine.ParticleStore.from_cells([c for o in ovs for c in o], device=dev)
+    cyc = cycle.MinkowskiCycle(store, K, ref).capture()
+
+    for _ in range(args.warmup):
+        cyc.replay()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cyc.replay()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+
+    h = cyc.records().reshape(-1)
+    assert np.all(h["status"] == 0), "non-ok constraint records"
+
+    # dominant kernel: the moment (Gram) reduction; algorithmic bytes = every particle
+    # coordinate read once (2T float64 per particle)
+    n_part = int(sum(store.counts))
+    alg_bytes = n_part * 2 * args.T * 8
+    t_mom = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev)
+    t_cycle_dev = time_kernel_live(cyc.run, dev)
+
+    value = world * args.steps / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "cycles/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded particle clouds; no Trajectron++ weights / CARLA offline)",
+        "config": {
+            "workload": "C2: 1 scene x 4 OVs, np=5000/OV, ph=8, Minkowski/MVOE "
+                        "constraint-gen cycle (moments + all (cell,t,tau) half-spaces), "
+                        "hipGraph replay, particles resident in HBM",
+            "scenes_per_gpu": 1, "O": args.O, "N_per_ov": args.N, "T": args.T, "K": K,
+            "cells": store.n_cells, "halfspaces_per_cycle": cyc.n_constraints,
+        },
+        "constraints_per_s": round(value * cyc.n_constraints, 1),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "ccmpc_moments (gram_partial_kernel + gram_finalize_kernel)",
+            "achieved": round(alg_bytes / t_mom / 1e9, 2),
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": round(alg_bytes / t_mom / HBM_PEAK, 5),
+            "traffic": None,
+            "alg_bytes_per_launch": alg_bytes,
+            "avg_launch_us": round(t_mom * 1e6, 3),
+            "eager_cycle_us": round(t_cycle_dev * 1e6, 3),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        med, threads, total = cpu_baseline(ovs, ref, args.T, args.cpu_cycles)
+        out["cpu_baseline"] = {
+            "value": round(1.0 / med, 3), "unit": "cycles/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_cycles} full C2 cycles (same scene), median; "
+                      f"{total:.1f} s of CPU work; oracle restatement of "
+                      "v8ideal/__init__.py:881-947 (numpy/scipy)",
+        }
+        out["speedup_vs_cpu"] = round(value / (1.0 / med), 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+"""Device-resident constraint-generation cycles with preallocated buffers.
+
+A cycle is what one planning step of v8ideal spends on chance constraints:
+
+  MinkowskiCycle  particles -> moments -> (cell, t, tau) MVOE half-spaces
+                  (compute_obstacle_constraints_GMM_Minkowski_idealprediction,
+                   v8ideal/__init__.py:881-947, plus the save_moments statistics :2575-2606
+                   which are the same moments)
+  AffineCycle     particles -> moments -> (cell, t) GMM-affine half-spaces (:1470-1515)
+
+Every buffer is allocated up front and every call enqueues on the current stream, so
+``capture()`` records the whole cycle into one hipGraph (torch.cuda.CUDAGraph) and ``replay()``
+costs one graph launch.
+"""
+import numpy as np
+import torch
+
+from . import engine, risk
+
+
+class MinkowskiCycle:
+    def __init__(self, store, K, ref_traj, ph=None, R=risk.R_COLLISION, tol=1e-8, maxiter=1000):
+        self.store = store
+        self.device = store.device
+        self.T = store.T
+        self.K = [int(k) for k in K]
+        assert sum(self.K) == store.n_cells
+        ph = self.T if ph is None else ph
+        C, T = store.n_cells, self.T
+        self.ref = torch.as_tensor(np.asarray(ref_traj, np.float64).reshape(-1, T, 2),
+                                   device=self.device)
+        self.risk = torch.as_tensor(risk.cell_risk(risk.eps_ura(self.K), self.K, ph),
+                                    device=self.device)
+        self.R, self.tol, self.maxiter = R, tol, maxiter
+        self.mean = torch.empty((C, T, 2), dtype=torch.float64, device=self.device)
+        self.cov = torch.empty((C, 2 * T, 2 * T), dtype=torch.float64, device=self.device)
+        P = max(T * (T - 1) // 2, 1)
+        self.rec = torch.empty((C, P, 128), dtype=torch.uint8, device=self.device)
+        self.prob_lower = torch.empty((C, T), dtype=torch.float64, device=self.device)
+        self.ws = engine.Workspace(self.device)
+        self.ws.get(engine._lib.load().ccmpc_moments_workspace_bytes(T, C, store.n_bound))
+        self.graph = None
+
+    def run(self):
+        engine.moments(self.store, self.mean, self.cov, self.ws)
+        engine.minkowski(self.mean, self.cov, self.ref, self.risk, R=self.R, tol=self.tol,
+                         maxiter=self.maxiter, out_rec=self.rec, out_prob_lower=self.prob_lower)
+
+    def capture(self, warmup=2):
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.run()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.run()
+        return self
+
+    def replay(self):
+        if self.graph is None:
+            self.run()
+        else:
+            self.graph.replay()
+
+    @property
+    def n_constraints(self):
+        return self.store.n_cells * (self.T * (self.T - 1) // 2)
+
+    def records(self):
+        return engine.halfspaces(self.rec)
+
+
+class AffineCycle:
+    def __init__(self, store, K, ref_traj, ph=None, R=risk.R_COLLISION):
+        self.store = store
+        self.device = store.device
+        self.T = store.T
+        self.K = [int(k) for k in K]
+        ph = self.T if ph is None else ph
+        C, T = store.n_cells, self.T
+        self.ref = torch.as_tensor(np.asarray(ref_traj, np.float64).reshape(-1, T, 2),
+                                   device=self.device)
+        self.gamma = torch.as_tensor(risk.cell_gamma(risk.eps_ura(self.K), self.K, ph),
+                                     device=self.device)
+        self.R = R
+        self.mean = torch.empty((C, T, 2), dtype=torch.float64, device=self.device)
+        self.cov = torch.empty((C, 2 * T, 2 * T), dtype=torch.float64, device=self.device)
+        self.rec = torch.empty((C, T, 128), dtype=torch.uint8, device=self.device)
+        self.ws = engine.Workspace(self.device)
+        self.ws.get(engine._lib.load().ccmpc_moments_workspace_bytes(T, C, store.n_bound))
+
+    def run(self):
+        engine.moments(self.store, self.mean, self.cov, self.ws)
+        engine.affine(self.mean, self.cov, self.ref, self.gamma, R=self.R, out_rec=self.rec)
+
+    def records(self):
+        return engine.affine_records(self.rec)

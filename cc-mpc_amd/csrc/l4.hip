@@ -1,0 +1,170 @@
+// Per-particle headings, bounding-box vertices and the L4 outer approximation.
+//
+// Replaces, for every (cell, t):
+//   yaws           ovehicle.py:72-76  atan2 of the step delta, step 0 measured from past[-1]
+//   vertices       v8ideal/__init__.py:627-640 (utility.npu.vertices_of_bboxes, restated from
+//                  midlevel/util.py:104-124): 4 corners of a lon x lat box at each particle
+//   A_union/b_union v8ideal/__init__.py:694-736 -> midlevel/util.py:171-200: A = [I; -I] R(theta)
+//                  with theta the mean heading, b = max over particles and corners of A v
+//   t=0 yaw stats  v8ideal/__init__.py:872, :875 (mean and ddof=1 variance of yaw at t=0)
+//
+// One workgroup per (cell, t): pass 1 sums the headings (block reduction in a fixed order, so
+// the mean is bitwise reproducible), pass 2 re-reads the two steps and takes the max of the four
+// projections.  Max is order-independent, so b is exact whatever the reduction order.
+#include "ccmpc_common.hpp"
+
+namespace ccmpc {
+
+template <typename P>
+__device__ __forceinline__ double world(const P *pos, int64_t ld, int row, int64_t i, double o) {
+  return static_cast<double>(pos[static_cast<int64_t>(row) * ld + i]) + o;
+}
+
+template <typename P>
+__device__ __forceinline__ double heading(const P *pos, int64_t ld, int t, int64_t i, double o0,
+                                          double o1, double px, double py) {
+  const double x = world(pos, ld, 2 * t, i, o0), y = world(pos, ld, 2 * t + 1, i, o1);
+  double xp, yp;
+  if (t == 0) {
+    xp = px;
+    yp = py;
+  } else {
+    xp = world(pos, ld, 2 * t - 2, i, o0);
+    yp = world(pos, ld, 2 * t - 1, i, o1);
+  }
+  return atan2(y - yp, x - xp);
+}
+
+__device__ __forceinline__ double block_sum(double v, double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  const int nw = blockDim.x >> 6;
+  for (int k = 0; k < nw; ++k) s += red[k];
+  __syncthreads();
+  return s;
+}
+
+__device__ __forceinline__ double block_max(double v, double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = -INFINITY;
+  const int nw = blockDim.x >> 6;
+  for (int k = 0; k < nw; ++k) s = fmax(s, red[k]);
+  __syncthreads();
+  return s;
+}
+
+template <typename P>
+__global__ __launch_bounds__(256) void l4_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
+    const double *__restrict__ past_last, const double *__restrict__ bbox,
+    double *__restrict__ out_A, double *__restrict__ out_b, double *__restrict__ out_yaw_mean,
+    double *__restrict__ out_yaw0_var, double *__restrict__ out_yaw,
+    double *__restrict__ out_vertices) {
+  __shared__ double red[16];
+  const int cell = blockIdx.x / T, t = blockIdx.x % T;
+  const int64_t off = cell_off[cell], n = cell_cnt[cell];
+  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
+  const double px = past_last[2 * cell], py = past_last[2 * cell + 1];
+  const double lon = bbox[2 * cell], lat = bbox[2 * cell + 1];
+  const P *base = pos + off;
+
+  // pass 1: headings, mean (and the t = 0 variance, shifted by the first particle's heading)
+  double s = 0.0, s1 = 0.0, s2 = 0.0;
+  const double shift = (t == 0 && n > 0) ? heading(base, ld, 0, 0, o0, o1, px, py) : 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const double y = heading(base, ld, t, i, o0, o1, px, py);
+    s += y;
+    if (t == 0) {
+      const double d = y - shift;
+      s1 += d;
+      s2 += d * d;
+    }
+    if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + off + i] = y;
+  }
+  const double nn = static_cast<double>(n);
+  const double theta = block_sum(s, red) / nn;
+  if (t == 0) {
+    const double a = block_sum(s1, red), b2 = block_sum(s2, red);
+    if (threadIdx.x == 0) out_yaw0_var[cell] = (b2 - a * a / nn) / (nn - 1.0);
+  }
+
+  // pass 2: corners and the four support values of A = [I; -I] R(theta)
+  const double ct = cos(theta), st = sin(theta);
+  const double A[4][2] = {{ct, st}, {-st, ct}, {-ct, -st}, {st, -ct}};
+  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const double yaw = heading(base, ld, t, i, o0, o1, px, py);
+    const double x = world(base, ld, 2 * t, i, o0), y = world(base, ld, 2 * t + 1, i, o1);
+    double S, C;
+    sincos(yaw, &S, &C);
+    // rows of Rot per corner (midlevel/util.py:109-118), disp = 0.5 * Rot @ [lon, lat]
+    const double dx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
+                          0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
+    const double dy[4] = {0.5 * (S * lon - C * lat), 0.5 * (S * lon + C * lat),
+                          0.5 * (-S * lon + C * lat), 0.5 * (-S * lon - C * lat)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double vx = x + dx[c], vy = y + dy[c];
+      if (out_vertices) {
+        double *vp = out_vertices + (static_cast<int64_t>(t) * 8 + 2 * c) * ld + off + i;
+        vp[0] = vx;
+        vp[ld] = vy;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx[r] = fmax(mx[r], A[r][0] * vx + A[r][1] * vy);
+    }
+  }
+  double bm[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bm[r] = block_max(mx[r], red);
+  if (threadIdx.x == 0) {
+    const int64_t ct_idx = static_cast<int64_t>(cell) * T + t;
+    for (int r = 0; r < 4; ++r) {
+      out_A[ct_idx * 8 + 2 * r] = A[r][0];
+      out_A[ct_idx * 8 + 2 * r + 1] = A[r][1];
+      out_b[ct_idx * 4 + r] = bm[r];
+    }
+    out_yaw_mean[ct_idx] = theta;
+  }
+}
+
+}  // namespace ccmpc
+
+using namespace ccmpc;
+
+extern "C" int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T,
+                        const double *origin, const int64_t *cell_off, const int64_t *cell_cnt,
+                        int64_t n_cells, const double *past_last, const double *bbox,
+                        double *out_A, double *out_b, double *out_yaw_mean,
+                        double *out_yaw0_var, double *out_yaw, double *out_vertices,
+                        ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
+  CCMPC_REQUIRE(n_cells >= 0 && n_cells * T < (int64_t(1) << 31), "bad n_cells");
+  if (n_cells == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(positions && cell_off && cell_cnt && past_last && bbox && out_A && out_b &&
+                    out_yaw_mean && out_yaw0_var,
+                "null pointer");
+  CCMPC_REQUIRE(dtype == CCMPC_F64 || dtype == CCMPC_F32, "bad dtype");
+  const dim3 grid(static_cast<unsigned>(n_cells * T));
+  if (dtype == CCMPC_F64)
+    hipLaunchKernelGGL((l4_kernel<double>), grid, dim3(256), 0, as_stream(stream),
+                       static_cast<const double *>(positions), ld, static_cast<int>(T), origin,
+                       cell_off, cell_cnt, past_last, bbox, out_A, out_b, out_yaw_mean,
+                       out_yaw0_var, out_yaw, out_vertices);
+  else
+    hipLaunchKernelGGL((l4_kernel<float>), grid, dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(positions), ld, static_cast<int>(T), origin,
+                       cell_off, cell_cnt, past_last, bbox, out_A, out_b, out_yaw_mean,
+                       out_yaw0_var, out_yaw, out_vertices);
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}

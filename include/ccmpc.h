@@ -171,6 +171,23 @@ int ccmpc_ideal_moments(const double *prev_mean, const double *prev_cov, int64_t
                         void *workspace, size_t workspace_bytes, double *out_mean,
                         double *out_cov, int32_t *out_status, ccmpc_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Headings, bounding-box vertices and L4 outer approximation for every (cell, t).
+ * Replaces ovehicle.py:72-76 (yaws = atan2 of step deltas, step 0 from past[-1]),
+ * v8ideal/__init__.py:627-640 (vertices_of_bboxes, restated from midlevel/util.py:104-124),
+ * :694-736 -> midlevel/util.py:171-200 (A = [I; -I] R(mean yaw), b = max_{particles, corners} A v)
+ * and the t = 0 yaw statistics of :872, :875.
+ *  past_last[c][2]   world-frame past[-1] of the cell's OV;  bbox[c][2] = {lon, lat}
+ *  out_A[c][T][4][2], out_b[c][T][4], out_yaw_mean[c][T], out_yaw0_var[c] (ddof = 1)
+ *  out_yaw (nullable)       pred_yaws in store layout [T][ld]
+ *  out_vertices (nullable)  corners in store layout [T][8][ld], plane 8t + 2 corner + xy
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T, const double *origin,
+             const int64_t *cell_off, const int64_t *cell_cnt, int64_t n_cells,
+             const double *past_last, const double *bbox, double *out_A, double *out_b,
+             double *out_yaw_mean, double *out_yaw0_var, double *out_yaw, double *out_vertices,
+             ccmpc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
