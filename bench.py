@@ -71,19 +71,30 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def time_kernel_live(fn, dev, reps=200):
-    """Average duration of one launch of `fn` on the current stream, HIP events bracketing
-    `reps` back-to-back launches (graph-free, so launches queue ahead of the GPU)."""
-    for _ in range(10):
-        fn()
+def time_kernel_live(fn, dev, per_graph=50, replays=20):
+    """Average device time of one launch of `fn`: `per_graph` launches captured back to back
+    into one hipGraph, replayed `replays` times between two HIP events on the capturing
+    stream (no host launch overhead in the interval; each launch still pays its kernel
+    boundary, which rocprof's per-kernel duration does not include)."""
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            fn()
+    g.replay()
     torch.cuda.synchronize(dev)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) * 1e-3 / reps
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(replays):
+        g.replay()
+    ev1.record()
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) * 1e-3 / (per_graph * replays)
 
 
 def cpu_baseline(ovs, ref, T, cycles):
@@ -149,12 +160,13 @@ def main():
     h = cyc.records().reshape(-1)
     assert np.all(h["status"] == 0), "non-ok constraint records"
 
-    # dominant kernel: the moment (Gram) reduction; algorithmic bytes = every particle
-    # coordinate read once (2T float64 per particle)
+    # dominant (and only) kernel of the cycle: moments_kernel<double,1,true> = the Gram
+    # reduction with the fused half-space tail; algorithmic bytes = every particle coordinate
+    # read once (2T float64 per particle) -- SURVEY.md 8d's 16 N T read term
     n_part = int(sum(store.counts))
     alg_bytes = n_part * 2 * args.T * 8
+    t_kernel = time_kernel_live(cyc.run, dev)
     t_mom = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev)
-    t_cycle_dev = time_kernel_live(cyc.run, dev)
 
     value = world * args.steps / elapsed
     out = {
@@ -180,15 +192,16 @@ def main():
         "constraints_per_s": round(value * cyc.n_constraints, 1),
         "roofline": {
             "bound": "hbm",
-            "kernel": "ccmpc_moments (gram_partial_kernel + gram_finalize_kernel)",
-            "achieved": round(alg_bytes / t_mom / 1e9, 2),
+            "kernel": "moments_kernel<double,1,true> (ccmpc_minkowski_cycle: MFMA Gram + "
+                      "last-arriver combine + MVOE half-spaces, one launch)",
+            "achieved": round(alg_bytes / t_kernel / 1e9, 2),
             "peak": HBM_PEAK / 1e9,
             "unit": "GB/s",
-            "frac": round(alg_bytes / t_mom / HBM_PEAK, 5),
+            "frac": round(alg_bytes / t_kernel / HBM_PEAK, 5),
             "traffic": None,
             "alg_bytes_per_launch": alg_bytes,
-            "avg_launch_us": round(t_mom * 1e6, 3),
-            "eager_cycle_us": round(t_cycle_dev * 1e6, 3),
+            "avg_launch_us": round(t_kernel * 1e6, 3),
+            "moments_only_avg_launch_us": round(t_mom * 1e6, 3),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:

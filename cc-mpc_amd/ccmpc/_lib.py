@@ -61,6 +61,14 @@ SIGNATURES = {
     "ccmpc_minkowski": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _D, _D, _I32, _P, _P,
                                        _P]),
     "ccmpc_affine": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _D, _P, _P]),
+    "ccmpc_minkowski_cycle": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64,
+                                             _I64, _P, _SZ, _P, _P, _P, _D, _D, _I32, _P, _P,
+                                             _P, _P, _P]),
+    "ccmpc_ideal_minkowski_cycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _U64,
+                                                   _P, _P, _SZ, _P, _P, _P, _D, _D, _I32, _P,
+                                                   _P, _P, _P, _P, _P]),
+    "ccmpc_sample_unicycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _D, _U64, _P,
+                                             _P, _I64, _P]),
     "ccmpc_ideal_rollout": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _P, _U64,
                                            _P, _P, _I64, _P, _P]),
     "ccmpc_ideal_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),

@@ -42,6 +42,14 @@ class MinkowskiCycle:
         self.graph = None
 
     def run(self):
+        """One launch: moments + every (cell, t, tau) half-space (ccmpc_minkowski_cycle)."""
+        engine.minkowski_cycle(self.store, self.ref, self.risk, R=self.R, tol=self.tol,
+                               maxiter=self.maxiter, workspace=self.ws, out_mean=self.mean,
+                               out_cov=self.cov, out_rec=self.rec,
+                               out_prob_lower=self.prob_lower)
+
+    def run_unfused(self):
+        """Same cycle as two C-ABI calls (ccmpc_moments, ccmpc_minkowski)."""
         engine.moments(self.store, self.mean, self.cov, self.ws)
         engine.minkowski(self.mean, self.cov, self.ref, self.risk, R=self.R, tol=self.tol,
                          maxiter=self.maxiter, out_rec=self.rec, out_prob_lower=self.prob_lower)

@@ -104,16 +104,20 @@ class ParticleStore:
 
 
 class Workspace:
-    """Grow-only device scratch buffer (pre-size it before graph capture)."""
+    """Grow-only device scratch buffer (pre-size it before graph capture).
+
+    Allocated zero-filled: its head holds the per-cell arrival counters of the one-launch
+    reductions, which must start at zero and which every call leaves at zero (ccmpc.h).
+    One Workspace per stream."""
 
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
-        self.buf = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.buf = torch.zeros(0, dtype=torch.uint8, device=self.device)
 
     def get(self, nbytes):
         nbytes = max(int(nbytes), 16)
         if self.buf.numel() < nbytes:
-            self.buf = torch.empty(nbytes + 4096, dtype=torch.uint8, device=self.device)
+            self.buf = torch.zeros(nbytes + 4096, dtype=torch.uint8, device=self.device)
         return self.buf
 
 
@@ -149,6 +153,101 @@ def minkowski(mean, cov, ref_traj, cell_risk, cell_ref=None, R=3.4, tol=1e-8, ma
                                    _p(out_rec), _p(out_prob_lower), _stream()),
                "ccmpc_minkowski")
     return out_rec, out_prob_lower
+
+
+def minkowski_cycle(store, ref_traj, cell_risk, cell_ref=None, R=3.4, tol=1e-8, maxiter=1000,
+                    workspace=None, out_mean=None, out_cov=None, out_rec=None,
+                    out_prob_lower=None):
+    """moments + Minkowski half-spaces in ONE launch (ccmpc_minkowski_cycle)."""
+    lib = _lib.load()
+    C, T = store.n_cells, store.T
+    dev = store.device
+    P = max(T * (T - 1) // 2, 1)
+    out_mean = out_mean if out_mean is not None else torch.empty((C, T, 2), dtype=torch.float64,
+                                                                 device=dev)
+    out_cov = out_cov if out_cov is not None else torch.empty((C, 2 * T, 2 * T),
+                                                              dtype=torch.float64, device=dev)
+    out_rec = out_rec if out_rec is not None else torch.empty((C, P, 128), dtype=torch.uint8,
+                                                              device=dev)
+    out_prob_lower = (out_prob_lower if out_prob_lower is not None
+                      else torch.empty((C, T), dtype=torch.float64, device=dev))
+    need = lib.ccmpc_moments_workspace_bytes(T, C, store.n_bound)
+    ws = (workspace or Workspace(dev)).get(need)
+    _lib.check(lib.ccmpc_minkowski_cycle(
+        _p(store.pos), store.ccmpc_dtype, store.ld, T, _p(store.origin), _p(store.cell_off),
+        _p(store.cell_cnt), C, store.n_bound, _p(ws), ws.numel(), _p(ref_traj), _p(cell_ref),
+        _p(cell_risk), float(R), float(tol), int(maxiter), _p(out_mean), _p(out_cov),
+        _p(out_rec), _p(out_prob_lower), _stream()), "ccmpc_minkowski_cycle")
+    return out_mean, out_cov, out_rec, out_prob_lower
+
+
+def ideal_minkowski_cycle(prev_mean, prev_cov, src_cell, T, n_samples, ref_traj, cell_risk,
+                          x0=None, seed=0, rng_cell=None, cell_ref=None, R=3.4, tol=1e-8,
+                          maxiter=1000, workspace=None):
+    """Shrinking-horizon step in one launch: predict_ideal -> moments -> half-spaces."""
+    lib = _lib.load()
+    C = src_cell.shape[0]
+    T_src = prev_mean.shape[1]
+    dev = prev_mean.device
+    P = max(T * (T - 1) // 2, 1)
+    out_mean = torch.empty((C, T, 2), dtype=torch.float64, device=dev)
+    out_cov = torch.empty((C, 2 * T, 2 * T), dtype=torch.float64, device=dev)
+    status = torch.empty(C, dtype=torch.int32, device=dev)
+    rec = torch.empty((C, P, 128), dtype=torch.uint8, device=dev)
+    pl = torch.empty((C, T), dtype=torch.float64, device=dev)
+    need = lib.ccmpc_ideal_moments_workspace_bytes(T, C, n_samples)
+    ws = (workspace or Workspace(dev)).get(need)
+    _lib.check(lib.ccmpc_ideal_minkowski_cycle(
+        _p(prev_mean), _p(prev_cov), T_src, _p(src_cell), C, T, n_samples, _p(x0),
+        int(seed) & (2**64 - 1), _p(rng_cell), _p(ws), ws.numel(), _p(ref_traj), _p(cell_ref),
+        _p(cell_risk), float(R), float(tol), int(maxiter), _p(out_mean), _p(out_cov), _p(status),
+        _p(rec), _p(pl), _stream()), "ccmpc_ideal_minkowski_cycle")
+    return out_mean, out_cov, status, rec, pl
+
+
+def l4(store, past_last, bbox, with_yaw=False, with_vertices=False):
+    """Headings, L4 outer approximation and t=0 yaw stats per (cell, t) (ccmpc_l4).
+    Returns dict(A [C,T,4,2], b [C,T,4], yaw_mean [C,T], yaw0_var [C], yaw?, vertices?)."""
+    lib = _lib.load()
+    C, T, dev = store.n_cells, store.T, store.device
+    out = dict(A=torch.empty((C, T, 4, 2), dtype=torch.float64, device=dev),
+               b=torch.empty((C, T, 4), dtype=torch.float64, device=dev),
+               yaw_mean=torch.empty((C, T), dtype=torch.float64, device=dev),
+               yaw0_var=torch.empty((C,), dtype=torch.float64, device=dev))
+    out["yaw"] = (torch.empty((T, store.ld), dtype=torch.float64, device=dev) if with_yaw
+                  else None)
+    out["vertices"] = (torch.empty((T * 8, store.ld), dtype=torch.float64, device=dev)
+                       if with_vertices else None)
+    past_last = torch.as_tensor(np.asarray(past_last, np.float64).reshape(C, 2), device=dev)
+    bbox = torch.as_tensor(np.asarray(bbox, np.float64).reshape(C, 2), device=dev)
+    _lib.check(lib.ccmpc_l4(_p(store.pos), store.ccmpc_dtype, store.ld, T, _p(store.origin),
+                            _p(store.cell_off), _p(store.cell_cnt), C, _p(past_last), _p(bbox),
+                            _p(out["A"]), _p(out["b"]), _p(out["yaw_mean"]), _p(out["yaw0_var"]),
+                            _p(out["yaw"]), _p(out["vertices"]), _stream()), "ccmpc_l4")
+    return out
+
+
+def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="cuda"):
+    """GMM-latent particle sampler.  init_state (O,4), latent_pmf (O,L), gmm (O,L,T,5).
+    Returns (z [O,N] int32, F32 ParticleStore in sample order: one cell per OV)."""
+    lib = _lib.load()
+    dev = require_device(device)
+    init_state = np.asarray(init_state, np.float64).reshape(-1, 4)
+    O = init_state.shape[0]
+    pmf = np.asarray(latent_pmf, np.float64).reshape(O, -1)
+    L = pmf.shape[1]
+    cdf = np.cumsum(pmf, axis=1)
+    gmm = np.ascontiguousarray(np.asarray(gmm, np.float32).reshape(O, L, T, 5))
+    store = ParticleStore(T, [N] * O, dtype=torch.float32, device=dev, origin=np.zeros((O, 2)))
+    z = torch.empty((O, N), dtype=torch.int32, device=dev)
+    t_init = torch.as_tensor(init_state, device=dev)
+    t_cdf = torch.as_tensor(cdf, device=dev)
+    t_gmm = torch.as_tensor(gmm, device=dev)
+    _lib.check(lib.ccmpc_sample_unicycle(_p(t_init), _p(t_cdf), L, _p(t_gmm), O, N, T, float(dt),
+                                         int(seed) & (2**64 - 1), _p(z), _p(store.pos), store.ld,
+                                         _stream()), "ccmpc_sample_unicycle")
+    store._keepalive = (t_init, t_cdf, t_gmm)
+    return z, store
 
 
 def affine(mean, cov, ref_traj, cell_gamma, cell_ref=None, R=3.4, out_rec=None):

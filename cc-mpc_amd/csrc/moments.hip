@@ -1,4 +1,5 @@
-// Segmented moment (Gram) reduction of particle clouds -- the dominant kernel of the path.
+// Segmented moment (Gram) reduction of particle clouds -- the dominant kernel of the path --
+// optionally fused with the Minkowski/MVOE half-space assembly of each finished cell.
 //
 // Replaces every np.mean / np.cov the reference runs over particle clouds
 // (v8ideal/__init__.py:864-875, :896, :907 -> makeconstraint.py:41-70, :1485-1493,
@@ -6,7 +7,7 @@
 // every one of those 4x4 matrices is a block of ONE 2T x 2T covariance per cell, so the
 // particle cloud is read exactly once.
 //
-// Design (gfx950):
+// Design (gfx950), ONE launch per call:
 //  * Work item = (cell, chunk of `chunk` particles), one wavefront per workgroup.
 //  * The Gram matrix G = X X^T of the shifted data X[r][p] = pos[r][p] - pos[r][first]
 //    (r = 2t + xy) runs on the f64 matrix core: v_mfma_f64_16x16x4_f64 takes A[i][k] from lane
@@ -19,23 +20,30 @@
 //    group k -- summation order is irrelevant for a Gram sum.
 //  * Shift by the cell's first particle (shifted one-pass formula): positions sit around
 //    x ~ 200 m with sub-metre spread, and the un-shifted one-pass form loses every digit.
-//  * Partial slabs per item are summed in a fixed order by the finalize kernel (bitwise
-//    reproducible; no float atomics).
+//  * Each item publishes its partial slab write-through and takes a per-cell ticket; the last
+//    arriver combines the cell (gram.hpp) and, in the cycle variant, immediately builds the
+//    cell's T(T-1)/2 half-spaces -- no kernel boundary between moments and constraints.
+#include "constraints.hpp"
 #include "gram.hpp"
 
 namespace ccmpc {
 
-template <typename P, int RB>
-__global__ __launch_bounds__(64) void gram_partial_kernel(
-    const P *__restrict__ pos, int64_t ld, int T, const int64_t *__restrict__ cell_off,
-    const int64_t *__restrict__ cell_cnt, int n_cells, int64_t chunk,
-    double *__restrict__ partial) {
+template <typename P, int RB, bool MINK>
+__global__ __launch_bounds__(64) void moments_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
+    int64_t chunk, double *__restrict__ partial, int32_t *__restrict__ counters,
+    double *__restrict__ out_mean, double *__restrict__ out_cov, MinkParams mp) {
   constexpr int NT = n_tiles(RB);
   constexpr int NACC = (NT == 1) ? 2 : 1;  // two chains hide MFMA latency when there is one tile
+  constexpr int D = 16 * RB;
+  __shared__ double shift_lds[D];
+  __shared__ double S_lds[D];
+  __shared__ double lb_s[MINK ? 40 * 39 / 2 : 1];
   int cell;
-  int64_t cidx;
+  int64_t cidx, first;
   const int64_t item = blockIdx.x;
-  if (!locate_item(item, cell_cnt, n_cells, chunk, cell, cidx)) return;
+  if (!locate_item(item, cell_cnt, n_cells, chunk, cell, cidx, first)) return;
 
   const int lane = threadIdx.x;
   const int r = lane & 15;
@@ -54,7 +62,7 @@ __global__ __launch_bounds__(64) void gram_partial_kernel(
     const int R = 16 * b + r;
     live[b] = R < rows;
     rowp[b] = pos + static_cast<int64_t>(live[b] ? R : 0) * ld + off;
-    sh[b] = live[b] ? static_cast<double>(rowp[b][0]) : 0.0;
+    sh[b] = (live[b] && cnt > 0) ? static_cast<double>(rowp[b][0]) : 0.0;
   }
 
   d4 acc[NACC][NT];
@@ -97,47 +105,79 @@ __global__ __launch_bounds__(64) void gram_partial_kernel(
     for (int b = 0; b < RB; ++b) s1[b] += (v[b][0] + v[b][1]) + (v[b][2] + v[b][3]);
   }
 
-  double *slab = partial + item * slab_doubles(RB);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    d4 s = acc[0][t];
-    if (NACC == 2) s += acc[NACC - 1][t];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) slab[t * 256 + k * 64 + lane] = s[k];
-  }
+  constexpr int E = slab_doubles(RB);
+  publish_slab<RB, NACC>(partial + item * E, acc, s1);
+  const int64_t nit = items_of(cnt, chunk);
+  if (!arrive_last(counters + cell, nit)) return;
+
+  // ---- last arriver of this cell: combine, then (cycle variant) the half-spaces ----------
 #pragma unroll
   for (int b = 0; b < RB; ++b) {
-    double x = s1[b];
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
-    if (lane < 16) slab[NT * 256 + b * 16 + lane] = x;
+    if (g == 0) shift_lds[16 * b + r] = sh[b];
   }
+  __syncthreads();
+  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
+  double *mean = out_mean + static_cast<int64_t>(cell) * rows;
+  double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
+  reduce_cell<RB>(partial + first * E, nit, cnt, T, shift_lds, S_lds, o0, o1, mean, cov);
+  if (MINK) minkowski_cell(cov, mean, T, cell, mp, lb_s, lane, 64);
 }
 
-template <typename P, int RB>
-static void launch_moments(const P *pos, int64_t ld, int T, const double *origin,
-                           const int64_t *off, const int64_t *cnt, int n_cells, int64_t chunk,
-                           int64_t items, double *partial, double *mean, double *cov,
-                           hipStream_t s) {
-  hipLaunchKernelGGL((gram_partial_kernel<P, RB>), dim3(static_cast<unsigned>(items)), dim3(64),
-                     0, s, pos, ld, T, off, cnt, n_cells, chunk, partial);
-  hipLaunchKernelGGL((gram_finalize_kernel<P, RB>), dim3(n_cells), dim3(256), 0, s, pos, ld, T,
-                     static_cast<const double *>(nullptr), origin, off, cnt, int64_t(0), chunk,
-                     partial, mean, cov);
+template <typename P, int RB, bool MINK>
+static void launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
+                   const int64_t *cnt, int n_cells, int64_t chunk, int64_t items, double *partial,
+                   int32_t *counters, double *mean, double *cov, const MinkParams &mp,
+                   hipStream_t s) {
+  hipLaunchKernelGGL((moments_kernel<P, RB, MINK>), dim3(static_cast<unsigned>(items)), dim3(64),
+                     0, s, pos, ld, T, origin, off, cnt, n_cells, chunk, partial, counters, mean,
+                     cov, mp);
 }
 
-template <typename P>
-static int dispatch_moments(const P *pos, int64_t ld, int T, const double *origin,
-                            const int64_t *off, const int64_t *cnt, int n_cells, int64_t chunk,
-                            int64_t items, double *partial, double *mean, double *cov,
-                            hipStream_t s) {
+template <typename P, bool MINK>
+static int dispatch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
+                    const int64_t *cnt, int n_cells, int64_t chunk, int64_t items,
+                    double *partial, int32_t *counters, double *mean, double *cov,
+                    const MinkParams &mp, hipStream_t s) {
   switch (row_blocks(T)) {
-    case 1: launch_moments<P, 1>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, mean, cov, s); break;
-    case 2: launch_moments<P, 2>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, mean, cov, s); break;
-    case 3: launch_moments<P, 3>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, mean, cov, s); break;
-    case 4: launch_moments<P, 4>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, mean, cov, s); break;
-    case 5: launch_moments<P, 5>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, mean, cov, s); break;
+    case 1: launch<P, 1, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
+    case 2: launch<P, 2, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
+    case 3: launch<P, 3, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
+    case 4: launch<P, 4, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
+    case 5: launch<P, 5, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
     default: return CCMPC_ERR_UNSUPPORTED;
+  }
+  return CCMPC_OK;
+}
+
+template <bool MINK>
+static int run(const void *positions, int dtype, int64_t ld, int64_t T, const double *origin,
+               const int64_t *cell_off, const int64_t *cell_cnt, int64_t n_cells,
+               int64_t n_bound, void *workspace, double *out_mean, double *out_cov,
+               const MinkParams &mp, ccmpc_stream_t stream, const char *who) {
+  const int64_t chunk = pick_chunk(n_bound);
+  const int64_t items = max_items(n_cells, n_bound, chunk);
+  int32_t *counters = static_cast<int32_t *>(workspace);
+  double *partial = reinterpret_cast<double *>(static_cast<char *>(workspace) +
+                                               counter_bytes(n_cells));
+  hipStream_t s = as_stream(stream);
+  const int Ti = static_cast<int>(T), nc = static_cast<int>(n_cells);
+  int rc;
+  if (dtype == CCMPC_F64)
+    rc = dispatch<double, MINK>(static_cast<const double *>(positions), ld, Ti, origin, cell_off,
+                                cell_cnt, nc, chunk, items, partial, counters, out_mean, out_cov,
+                                mp, s);
+  else
+    rc = dispatch<float, MINK>(static_cast<const float *>(positions), ld, Ti, origin, cell_off,
+                               cell_cnt, nc, chunk, items, partial, counters, out_mean, out_cov,
+                               mp, s);
+  if (rc != CCMPC_OK) {
+    set_error(std::string(who) + ": unsupported T");
+    return rc;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(who) + ": launch failed: " + hipGetErrorString(e));
+    return CCMPC_ERR_LAUNCH;
   }
   return CCMPC_OK;
 }
@@ -149,44 +189,52 @@ using namespace ccmpc;
 extern "C" size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells,
                                                 int64_t n_particles_bound) {
   if (T < 1 || T > kMaxT || n_cells < 0 || n_particles_bound < 0) return 0;
-  const int64_t chunk = pick_chunk(T, n_particles_bound);
+  const int64_t chunk = pick_chunk(n_particles_bound);
   const int64_t items = max_items(n_cells, n_particles_bound, chunk);
-  return static_cast<size_t>(items) * slab_doubles(row_blocks(T)) * sizeof(double);
+  return counter_bytes(n_cells) +
+         static_cast<size_t>(items) * slab_doubles(row_blocks(T)) * sizeof(double);
 }
+
+#define CHECK_STORE_ARGS()                                                                     \
+  CCMPC_REQUIRE(T >= 1 && T <= kMaxT, "T must be in [1, 40]");                                 \
+  CCMPC_REQUIRE(n_cells >= 0 && n_cells < (1 << 30), "bad n_cells");                           \
+  if (n_cells == 0) return CCMPC_OK;                                                           \
+  CCMPC_REQUIRE(positions && cell_off && cell_cnt && out_mean && out_cov, "null pointer");     \
+  CCMPC_REQUIRE(ld % 4 == 0 && ld > 0, "ld must be a positive multiple of 4");                 \
+  CCMPC_REQUIRE(dtype == CCMPC_F64 || dtype == CCMPC_F32, "bad dtype");                        \
+  CCMPC_REQUIRE(aligned(positions, 16), "positions must be 16-byte aligned");                  \
+  CCMPC_REQUIRE(workspace && aligned(workspace, 16), "workspace must be 16-byte aligned");     \
+  if (workspace_bytes < ccmpc_moments_workspace_bytes(T, n_cells, n_particles_bound)) {        \
+    set_error(std::string(__func__) + ": workspace too small");                                \
+    return CCMPC_ERR_WORKSPACE;                                                                \
+  }
 
 extern "C" int ccmpc_moments(const void *positions, int dtype, int64_t ld, int64_t T,
                              const double *origin, const int64_t *cell_off,
                              const int64_t *cell_cnt, int64_t n_cells,
                              int64_t n_particles_bound, void *workspace, size_t workspace_bytes,
                              double *out_mean, double *out_cov, ccmpc_stream_t stream) {
-  CCMPC_REQUIRE(T >= 1 && T <= kMaxT, "T must be in [1, 40]");
-  CCMPC_REQUIRE(n_cells >= 0 && n_cells < (1 << 30), "bad n_cells");
-  if (n_cells == 0) return CCMPC_OK;
-  CCMPC_REQUIRE(positions && cell_off && cell_cnt && out_mean && out_cov, "null pointer");
-  CCMPC_REQUIRE(ld % 4 == 0 && ld > 0, "ld must be a positive multiple of 4");
-  CCMPC_REQUIRE(dtype == CCMPC_F64 || dtype == CCMPC_F32, "dtype must be CCMPC_F64 or CCMPC_F32");
-  CCMPC_REQUIRE(aligned(positions, 16), "positions must be 16-byte aligned");
-  const size_t need = ccmpc_moments_workspace_bytes(T, n_cells, n_particles_bound);
-  if (workspace_bytes < need || (need && !workspace)) {
-    set_error("ccmpc_moments: workspace too small");
-    return CCMPC_ERR_WORKSPACE;
-  }
-  const int64_t chunk = pick_chunk(T, n_particles_bound);
-  const int64_t items = max_items(n_cells, n_particles_bound, chunk);
-  hipStream_t s = as_stream(stream);
-  int rc;
-  if (dtype == CCMPC_F64)
-    rc = dispatch_moments<double>(static_cast<const double *>(positions), ld, static_cast<int>(T),
-                                  origin, cell_off, cell_cnt, static_cast<int>(n_cells), chunk,
-                                  items, static_cast<double *>(workspace), out_mean, out_cov, s);
-  else
-    rc = dispatch_moments<float>(static_cast<const float *>(positions), ld, static_cast<int>(T),
-                                 origin, cell_off, cell_cnt, static_cast<int>(n_cells), chunk,
-                                 items, static_cast<double *>(workspace), out_mean, out_cov, s);
-  if (rc != CCMPC_OK) {
-    set_error("ccmpc_moments: unsupported T");
-    return rc;
-  }
-  CCMPC_LAUNCH_CHECK();
-  return CCMPC_OK;
+  CHECK_STORE_ARGS();
+  const MinkParams none{};
+  return run<false>(positions, dtype, ld, T, origin, cell_off, cell_cnt, n_cells,
+                    n_particles_bound, workspace, out_mean, out_cov, none, stream,
+                    "ccmpc_moments");
+}
+
+extern "C" int ccmpc_minkowski_cycle(const void *positions, int dtype, int64_t ld, int64_t T,
+                                     const double *origin, const int64_t *cell_off,
+                                     const int64_t *cell_cnt, int64_t n_cells,
+                                     int64_t n_particles_bound, void *workspace,
+                                     size_t workspace_bytes, const double *ref_traj,
+                                     const int32_t *cell_ref, const double *cell_risk, double R,
+                                     double tol, int32_t maxiter, double *out_mean,
+                                     double *out_cov, ccmpc_halfspace *out_rec,
+                                     double *out_prob_lower, ccmpc_stream_t stream) {
+  CHECK_STORE_ARGS();
+  CCMPC_REQUIRE(ref_traj && cell_risk && out_rec && out_prob_lower, "null pointer");
+  CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
+  const MinkParams mp{ref_traj, cell_ref, cell_risk, R, tol, maxiter, out_rec, out_prob_lower};
+  return run<true>(positions, dtype, ld, T, origin, cell_off, cell_cnt, n_cells,
+                   n_particles_bound, workspace, out_mean, out_cov, mp, stream,
+                   "ccmpc_minkowski_cycle");
 }

@@ -14,6 +14,7 @@
 //    the MFMA layout) and feeds the same f64 MFMA Gram reduction as ccmpc_moments.  The
 //    reference's only consumer of the 1e6-row ideal trajectories is np.cov (:886-907,
 //    :2586-2606), so this removes 32 * n * T bytes of HBM traffic per cell.
+#include "constraints.hpp"
 #include "gram.hpp"
 
 namespace ccmpc {
@@ -144,18 +145,21 @@ __global__ __launch_bounds__(256) void ideal_rollout_kernel(
 
 constexpr int kStageStride = 66;  // doubles per LDS row: bank-conflict-free both ways
 
-template <int RB>
+template <int RB, bool MINK>
 __global__ __launch_bounds__(64) void ideal_gram_kernel(
     const double *__restrict__ prev_mean, const double *__restrict__ prev_cov, int T_src,
     const int32_t *__restrict__ src_cell, int T, int64_t n, int64_t chunk, int64_t items_per_cell,
     const double *__restrict__ x0, uint64_t seed, const int32_t *__restrict__ rng_cell,
-    double *__restrict__ partial, double *__restrict__ shift_buf,
-    int32_t *__restrict__ out_status) {
+    double *__restrict__ partial, int32_t *__restrict__ counters, double *__restrict__ out_mean,
+    double *__restrict__ out_cov, int32_t *__restrict__ out_status, MinkParams mp) {
   constexpr int NT = n_tiles(RB);
   constexpr int D = 16 * RB;
+  constexpr int E = slab_doubles(RB);
   __shared__ StepPlan plan[40];
   __shared__ double stage[D * kStageStride];
   __shared__ double shift_s[D];
+  __shared__ double S_lds[D];
+  __shared__ double lb_s[MINK ? 40 * 39 / 2 : 1];
   __shared__ int status_s;
   const int lane = threadIdx.x;
   const int64_t item = blockIdx.x;
@@ -190,15 +194,11 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
     for (int R = rows; R < D; ++R) shift_s[R] = 0.0;
   }
   __syncthreads();
-  if (cidx == 0) {
-    for (int R = lane; R < rows; R += 64) shift_buf[static_cast<int64_t>(cell) * rows + R] = shift_s[R];
-    if (lane == 0 && out_status) out_status[cell] = status_s;
-  }
+  if (cidx == 0 && lane == 0 && out_status) out_status[cell] = status_s;
 
-  typedef double d4v __attribute__((ext_vector_type(4)));
-  d4v acc[NT];
+  d4 acc[1][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = d4v{0.0, 0.0, 0.0, 0.0};
+  for (int t = 0; t < NT; ++t) acc[0][t] = d4{0.0, 0.0, 0.0, 0.0};
   double s1[RB];
 #pragma unroll
   for (int b = 0; b < RB; ++b) s1[b] = 0.0;
@@ -233,25 +233,20 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
       for (int bi = 0; bi < RB; ++bi)
 #pragma unroll
         for (int bj = bi; bj < RB; ++bj) {
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[bi], v[bj], acc[t], 0, 0, 0);
+          acc[0][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[bi], v[bj], acc[0][t], 0, 0, 0);
           ++t;
         }
     }
     __syncthreads();
   }
 
-  double *slab = partial + item * slab_doubles(RB);
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) slab[t * 256 + k * 64 + lane] = acc[t][k];
-#pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    double x = s1[b];
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
-    if (lane < 16) slab[NT * 256 + b * 16 + lane] = x;
-  }
+  publish_slab<RB, 1>(partial + item * E, acc, s1);
+  if (!arrive_last(counters + cell, items_per_cell)) return;
+  double *mean = out_mean + static_cast<int64_t>(cell) * rows;
+  double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
+  reduce_cell<RB>(partial + cell * items_per_cell * E, items_per_cell, n, T, shift_s, S_lds, 0.0,
+                  0.0, mean, cov);
+  if (MINK) minkowski_cell(cov, mean, T, cell, mp, lb_s, lane, 64);
 }
 
 inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
@@ -262,21 +257,40 @@ inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
   return c;
 }
 
-template <int RB>
+template <int RB, bool MINK>
 static void launch_ideal_gram(const double *pm, const double *pc, int T_src, const int32_t *src,
                               int n_cells, int T, int64_t n, const double *x0, uint64_t seed,
-                              const int32_t *rng, double *partial, double *shift,
-                              double *out_mean, double *out_cov, int32_t *status, hipStream_t s) {
+                              const int32_t *rng, double *partial, int32_t *counters,
+                              double *out_mean, double *out_cov, int32_t *status,
+                              const MinkParams &mp, hipStream_t s) {
   const int64_t chunk = ideal_chunk(n_cells, n);
   const int64_t ipc = (n + chunk - 1) / chunk;
-  hipLaunchKernelGGL((ideal_gram_kernel<RB>), dim3(static_cast<unsigned>(ipc * n_cells)), dim3(64),
-                     0, s, pm, pc, T_src, src, T, n, chunk, ipc, x0, seed, rng, partial, shift,
-                     status);
-  hipLaunchKernelGGL((gram_finalize_kernel<double, RB>), dim3(n_cells), dim3(256), 0, s,
-                     static_cast<const double *>(nullptr), int64_t(0), T,
-                     static_cast<const double *>(shift), static_cast<const double *>(nullptr),
-                     static_cast<const int64_t *>(nullptr), static_cast<const int64_t *>(nullptr),
-                     n, chunk, static_cast<const double *>(partial), out_mean, out_cov);
+  hipLaunchKernelGGL((ideal_gram_kernel<RB, MINK>), dim3(static_cast<unsigned>(ipc * n_cells)),
+                     dim3(64), 0, s, pm, pc, T_src, src, T, n, chunk, ipc, x0, seed, rng, partial,
+                     counters, out_mean, out_cov, status, mp);
+}
+
+template <bool MINK>
+static int run_ideal(const double *prev_mean, const double *prev_cov, int64_t T_src,
+                     const int32_t *src_cell, int64_t n_cells, int64_t T, int64_t n_samples,
+                     const double *x0, uint64_t seed, const int32_t *rng_cell, void *workspace,
+                     double *out_mean, double *out_cov, int32_t *out_status, const MinkParams &mp,
+                     ccmpc_stream_t stream) {
+  int32_t *counters = static_cast<int32_t *>(workspace);
+  double *partial = reinterpret_cast<double *>(static_cast<char *>(workspace) +
+                                               counter_bytes(n_cells));
+  hipStream_t s = as_stream(stream);
+  const int nc = static_cast<int>(n_cells), Ti = static_cast<int>(T), Ts = static_cast<int>(T_src);
+  switch (row_blocks(T)) {
+    case 1: launch_ideal_gram<1, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
+    case 2: launch_ideal_gram<2, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
+    case 3: launch_ideal_gram<3, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
+    case 4: launch_ideal_gram<4, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
+    case 5: launch_ideal_gram<5, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
+    default: set_error("ideal moments: unsupported T"); return CCMPC_ERR_UNSUPPORTED;
+  }
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
 }
 
 }  // namespace ccmpc
@@ -311,9 +325,22 @@ extern "C" size_t ccmpc_ideal_moments_workspace_bytes(int64_t T, int64_t n_cells
   if (T < 1 || T > kMaxT || n_cells < 0 || n_samples < 1) return 0;
   const int64_t chunk = ideal_chunk(n_cells, n_samples);
   const int64_t items = ((n_samples + chunk - 1) / chunk) * n_cells;
-  const int rb = row_blocks(T);
-  return static_cast<size_t>(items * slab_doubles(rb) + n_cells * 2 * T) * sizeof(double);
+  return counter_bytes(n_cells) +
+         static_cast<size_t>(items) * slab_doubles(row_blocks(T)) * sizeof(double);
 }
+
+#define CHECK_IDEAL_ARGS()                                                                     \
+  CCMPC_REQUIRE(T_src >= 2 && T_src <= kMaxT, "T_src must be in [2, 40]");                     \
+  CCMPC_REQUIRE(T >= 1 && T <= T_src - 1, "T must be in [1, T_src - 1]");                      \
+  CCMPC_REQUIRE(n_cells >= 0 && n_cells < 65536, "bad n_cells");                               \
+  CCMPC_REQUIRE(n_samples >= 2 && n_samples < (int64_t(1) << 32), "bad n_samples");            \
+  if (n_cells == 0) return CCMPC_OK;                                                           \
+  CCMPC_REQUIRE(prev_mean && prev_cov && out_mean && out_cov, "null pointer");                 \
+  CCMPC_REQUIRE(workspace && aligned(workspace, 16), "workspace must be 16-byte aligned");     \
+  if (workspace_bytes < ccmpc_ideal_moments_workspace_bytes(T, n_cells, n_samples)) {          \
+    set_error(std::string(__func__) + ": workspace too small");                                \
+    return CCMPC_ERR_WORKSPACE;                                                                \
+  }
 
 extern "C" int ccmpc_ideal_moments(const double *prev_mean, const double *prev_cov,
                                    int64_t T_src, const int32_t *src_cell, int64_t n_cells,
@@ -321,32 +348,23 @@ extern "C" int ccmpc_ideal_moments(const double *prev_mean, const double *prev_c
                                    const int32_t *rng_cell, void *workspace,
                                    size_t workspace_bytes, double *out_mean, double *out_cov,
                                    int32_t *out_status, ccmpc_stream_t stream) {
-  CCMPC_REQUIRE(T_src >= 2 && T_src <= kMaxT, "T_src must be in [2, 40]");
-  CCMPC_REQUIRE(T >= 1 && T <= T_src - 1, "T must be in [1, T_src - 1]");
-  CCMPC_REQUIRE(n_cells >= 0 && n_cells < 65536, "bad n_cells");
-  CCMPC_REQUIRE(n_samples >= 2 && n_samples < (int64_t(1) << 32), "bad n_samples");
-  if (n_cells == 0) return CCMPC_OK;
-  CCMPC_REQUIRE(prev_mean && prev_cov && out_mean && out_cov, "null pointer");
-  const size_t need = ccmpc_ideal_moments_workspace_bytes(T, n_cells, n_samples);
-  if (workspace_bytes < need || !workspace) {
-    set_error("ccmpc_ideal_moments: workspace too small");
-    return CCMPC_ERR_WORKSPACE;
-  }
-  const int64_t chunk = ideal_chunk(n_cells, n_samples);
-  const int64_t items = ((n_samples + chunk - 1) / chunk) * n_cells;
-  const int rb = row_blocks(T);
-  double *partial = static_cast<double *>(workspace);
-  double *shift = partial + items * slab_doubles(rb);
-  hipStream_t s = as_stream(stream);
-  const int nc = static_cast<int>(n_cells), Ti = static_cast<int>(T), Ts = static_cast<int>(T_src);
-  switch (rb) {
-    case 1: launch_ideal_gram<1>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, shift, out_mean, out_cov, out_status, s); break;
-    case 2: launch_ideal_gram<2>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, shift, out_mean, out_cov, out_status, s); break;
-    case 3: launch_ideal_gram<3>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, shift, out_mean, out_cov, out_status, s); break;
-    case 4: launch_ideal_gram<4>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, shift, out_mean, out_cov, out_status, s); break;
-    case 5: launch_ideal_gram<5>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, shift, out_mean, out_cov, out_status, s); break;
-    default: set_error("ccmpc_ideal_moments: unsupported T"); return CCMPC_ERR_UNSUPPORTED;
-  }
-  CCMPC_LAUNCH_CHECK();
-  return CCMPC_OK;
+  CHECK_IDEAL_ARGS();
+  const MinkParams none{};
+  return run_ideal<false>(prev_mean, prev_cov, T_src, src_cell, n_cells, T, n_samples, x0, seed,
+                          rng_cell, workspace, out_mean, out_cov, out_status, none, stream);
+}
+
+extern "C" int ccmpc_ideal_minkowski_cycle(
+    const double *prev_mean, const double *prev_cov, int64_t T_src, const int32_t *src_cell,
+    int64_t n_cells, int64_t T, int64_t n_samples, const double *x0, uint64_t seed,
+    const int32_t *rng_cell, void *workspace, size_t workspace_bytes, const double *ref_traj,
+    const int32_t *cell_ref, const double *cell_risk, double R, double tol, int32_t maxiter,
+    double *out_mean, double *out_cov, int32_t *out_status, ccmpc_halfspace *out_rec,
+    double *out_prob_lower, ccmpc_stream_t stream) {
+  CHECK_IDEAL_ARGS();
+  CCMPC_REQUIRE(ref_traj && cell_risk && out_rec && out_prob_lower, "null pointer");
+  CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
+  const MinkParams mp{ref_traj, cell_ref, cell_risk, R, tol, maxiter, out_rec, out_prob_lower};
+  return run_ideal<true>(prev_mean, prev_cov, T_src, src_cell, n_cells, T, n_samples, x0, seed,
+                         rng_cell, workspace, out_mean, out_cov, out_status, mp, stream);
 }

@@ -105,7 +105,13 @@ const char *ccmpc_status_string(int status);
  *   cross_cov[t][tau] = block (t, tau)).
  * out_mean[c][t][2] (origin added back for F32), out_cov[c][2T][2T] (ddof = 1, symmetric).
  * n_particles_bound >= sum(cell_cnt) sizes the grid, so counts may be produced on the device.
- * T <= 40.  Deterministic: partial sums are combined in a fixed order.
+ * T <= 40.  ONE kernel launch: per-chunk partial Gram sums are combined by the last-arriving
+ * workgroup of each cell in a fixed order (deterministic, no float atomics).
+ *
+ * Workspace contract (every *_workspace_bytes-sized workspace): its first
+ * round_up(4 * n_cells, 256) bytes are per-cell arrival counters.  They must be ZERO before
+ * the first call on a fresh workspace (hipMemset once after allocating); every call leaves
+ * them zero again.  Do not share one workspace between concurrently running streams.
  * ------------------------------------------------------------------------------------- */
 size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_particles_bound);
 int ccmpc_moments(const void *positions, int dtype, int64_t ld, int64_t T,
@@ -131,6 +137,21 @@ int ccmpc_minkowski(const double *mean, const double *cov, int64_t T, int64_t n_
                     const double *ref_traj, const int32_t *cell_ref, const double *cell_risk,
                     double R, double tol, int32_t maxiter, ccmpc_halfspace *out_rec,
                     double *out_prob_lower, ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * One-launch Minkowski constraint-generation cycle: ccmpc_moments + ccmpc_minkowski fused.
+ * The last-arriving workgroup of each cell finalises its moments and immediately assembles the
+ * cell's T(T-1)/2 half-spaces, so one planning step's obstacle constraints cost one kernel
+ * (v8ideal/__init__.py:881-947 and the save_moments statistics :2575-2606).
+ * Same arguments and outputs as the two calls it replaces; same workspace contract.
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_minkowski_cycle(const void *positions, int dtype, int64_t ld, int64_t T,
+                          const double *origin, const int64_t *cell_off, const int64_t *cell_cnt,
+                          int64_t n_cells, int64_t n_particles_bound, void *workspace,
+                          size_t workspace_bytes, const double *ref_traj, const int32_t *cell_ref,
+                          const double *cell_risk, double R, double tol, int32_t maxiter,
+                          double *out_mean, double *out_cov, ccmpc_halfspace *out_rec,
+                          double *out_prob_lower, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * GMM-affine half-spaces for every (cell, t).  Replaces v8ideal/__init__.py:1470-1515.
@@ -163,13 +184,45 @@ int ccmpc_ideal_rollout(const double *prev_mean, const double *prev_cov, int64_t
 
 /* Same rollout fused with the moment reduction: particles are generated in registers and
  * reduced without ever being written to HBM (the reference's only consumer of the 1e6-row
- * ideal trajectories is np.cov, :886-907 and :2586-2606).  Z must be NULL (Philox). */
+ * ideal trajectories is np.cov, :886-907 and :2586-2606).  Noise from Philox only.  Same
+ * workspace contract as ccmpc_moments.  out_mean / out_cov as ccmpc_moments for T steps. */
 size_t ccmpc_ideal_moments_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_samples);
 int ccmpc_ideal_moments(const double *prev_mean, const double *prev_cov, int64_t T_src,
                         const int32_t *src_cell, int64_t n_cells, int64_t T, int64_t n_samples,
                         const double *x0, uint64_t seed, const int32_t *rng_cell,
                         void *workspace, size_t workspace_bytes, double *out_mean,
                         double *out_cov, int32_t *out_status, ccmpc_stream_t stream);
+
+/* The shrinking-horizon step (T < ph) in one launch: ideal rollout -> moments -> half-spaces
+ * (v8ideal/__init__.py:824-825 + :881-947).  Arguments as ccmpc_ideal_moments plus the
+ * ccmpc_minkowski ones. */
+int ccmpc_ideal_minkowski_cycle(const double *prev_mean, const double *prev_cov, int64_t T_src,
+                                const int32_t *src_cell, int64_t n_cells, int64_t T,
+                                int64_t n_samples, const double *x0, uint64_t seed,
+                                const int32_t *rng_cell, void *workspace, size_t workspace_bytes,
+                                const double *ref_traj, const int32_t *cell_ref,
+                                const double *cell_risk, double R, double tol, int32_t maxiter,
+                                double *out_mean, double *out_cov, int32_t *out_status,
+                                ccmpc_halfspace *out_rec, double *out_prob_lower,
+                                ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GMM-latent particle sampler (Trajectron++ predict tail behind prediction.py:81-86):
+ * z ~ Categorical(p(z|x)) by inverse CDF, per step a = mu + L eps (GMM2D.rsample, one
+ * component, L = [[s0, 0], [s1 rho, s1 sqrt(1 - rho^2)]]), Unicycle integration (exact at
+ * constant turn rate and acceleration; straight when |dphi| <= 1e-2), float32 as torch runs it.
+ *  init_state[o][4]   x, y, heading, speed (scene-relative)
+ *  latent_cdf[o][L]   cumulative p(z|x) (host), L <= 64
+ *  gmm[o][L][T][5]    mu_dphi, mu_a, log sigma_dphi, log sigma_a, rho   (float32)
+ *  out_z[o][N]        latent id per particle (the reference's argmax z, prediction.py:103)
+ *  out_pos            F32 store in SAMPLE order: OV o occupies [o*S, o*S + N), S = round_up(N, 4)
+ * Noise: z uses Philox (i, 0, o, STREAM_SAMPLER_Z), eps uses (i, t, o, STREAM_SAMPLER_EPS).
+ * PARITY UNPINNED upstream (absent submodule): checked against the repo's own restatement.
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf, int64_t n_latent,
+                          const float *gmm, int64_t n_ov, int64_t N, int64_t T, double dt,
+                          uint64_t seed, int32_t *out_z, float *out_pos, int64_t ld,
+                          ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Headings, bounding-box vertices and L4 outer approximation for every (cell, t).

@@ -1,0 +1,163 @@
+"""GPU tests of the one-launch cycles, the L4 / heading kernel and the GMM sampler."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ccmpc_oracle as orc
+
+from _cycle_inputs import cells_from_fixture, ovehicles_from_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+def eng():
+    import ccmpc.engine as e
+    return e
+
+
+def test_fused_cycle_bitwise_equals_two_calls(gpu, golden):
+    from ccmpc import cycle
+    g = golden("cycle_o2_t8")
+    T = int(g["T"])
+    store = eng().ParticleStore.from_cells(cells_from_fixture(g), device=gpu)
+    cyc = cycle.MinkowskiCycle(store, [int(k) for k in g["K"]], g["ref_traj"])
+    cyc.run_unfused()
+    a = (cyc.mean.clone(), cyc.cov.clone(), cyc.rec.clone(), cyc.prob_lower.clone())
+    for _ in range(3):                     # counters must come back to zero every launch
+        cyc.rec.zero_()
+        cyc.run()
+    assert torch.equal(a[0], cyc.mean) and torch.equal(a[1], cyc.cov)
+    assert torch.equal(a[2], cyc.rec) and torch.equal(a[3], cyc.prob_lower)
+    h = cyc.records().reshape(-1)
+    np.testing.assert_array_equal(h["which"], g["rec_which"])
+    assert len(h) == T * (T - 1) // 2 * store.n_cells
+
+
+def test_graph_replay_is_stable(gpu):
+    from ccmpc import cycle, synthetic
+    ovs, ref, _ = synthetic.scene(3, O=4, N=5000, T=8)
+    store = eng().ParticleStore.from_cells([c for o in ovs for c in o], device=gpu)
+    cyc = cycle.MinkowskiCycle(store, [len(o) for o in ovs], ref)
+    cyc.run()
+    first = cyc.rec.clone()
+    cyc.capture()
+    for _ in range(200):
+        cyc.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(first, cyc.rec)
+    assert np.all(cyc.records()["status"] == 0)
+
+
+def test_workspace_reused_across_shapes(gpu):
+    """One zero-initialised workspace serves calls of different cell counts back to back."""
+    e = eng()
+    ws = e.Workspace(gpu)
+    rng = np.random.default_rng(8)
+    for counts in ([5000, 3], [17], [100, 200, 300, 400], [70000]):
+        cells = [100 + np.cumsum(rng.normal(size=(n, 8, 2)), axis=1) for n in counts]
+        store = e.ParticleStore.from_cells(cells, device=gpu)
+        m, c = e.moments(store, workspace=ws)
+        for j, cl in enumerate(cells):
+            X = cl.transpose(1, 2, 0).reshape(16, -1)
+            np.testing.assert_allclose(c[j].cpu().numpy(), np.cov(X), rtol=1e-9, atol=1e-12)
+
+
+def test_empty_and_singleton_cells_give_nan_like_numpy(gpu):
+    e = eng()
+    store = e.ParticleStore(4, [0, 1, 6], device=gpu)
+    store.pos.normal_()
+    m, c = e.moments(store)
+    assert torch.isnan(c[0]).all() and torch.isnan(m[0]).all()   # np.cov of nothing
+    assert not torch.isfinite(c[1]).any()                         # ddof=1 with one sample
+    assert torch.isfinite(c[2]).all()
+
+
+def test_ideal_cycle_equals_ideal_moments_plus_minkowski(gpu):
+    from ccmpc import risk
+    e = eng()
+    rng = np.random.default_rng(4)
+    T_src = 8
+    cells = [190 + np.cumsum(rng.normal(0, 0.4, size=(n, T_src, 2)), axis=1) for n in (900, 1500)]
+    store = e.ParticleStore.from_cells(cells, device=gpu)
+    mean, cov = e.moments(store)
+    Tn, ns = T_src - 1, 50_000
+    src = torch.tensor([0, 1], dtype=torch.int32, device=gpu)
+    K = [2]
+    cr = torch.as_tensor(risk.cell_risk(risk.eps_ura(K), K, T_src), device=gpu)
+    ref = torch.as_tensor((np.array([170.0, 5.0]) + np.arange(1, Tn + 1)[:, None] * [4.0, 0.5])
+                          [None], device=gpu)
+    m1, c1, st1 = e.ideal_moments(mean, cov, src, Tn, ns, seed=5)
+    r1, pl1 = e.minkowski(m1, c1, ref, cr)
+    m2, c2, st2, r2, pl2 = e.ideal_minkowski_cycle(mean, cov, src, Tn, ns, ref, cr, seed=5)
+    assert torch.equal(m1, m2) and torch.equal(c1, c2)
+    assert torch.equal(r1, r2) and torch.equal(pl1, pl2)
+    assert st2.cpu().tolist() == [0, 0]
+
+
+@pytest.mark.parametrize("name", ["cycle_o2_t8", "cycle_o1_t12"])
+def test_l4_matches_reference_golden(gpu, golden, name):
+    e = eng()
+    g = golden(name)
+    T = int(g["T"])
+    K = [int(k) for k in g["K"]]
+    store = e.ParticleStore.from_cells(cells_from_fixture(g), device=gpu)
+    past = np.concatenate([[g["past"][o]] * K[o] for o in range(len(K))])
+    bbox = np.tile([4.5, 2.5], (store.n_cells, 1))
+    out = e.l4(store, past, bbox, with_yaw=True, with_vertices=True)
+    np.testing.assert_allclose(out["A"].cpu().numpy(), g["A_union"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(out["b"].cpu().numpy(), g["b_union"], rtol=1e-12)
+    # yaw statistics of ovStateMean/Cov_tau_1 (v8ideal/__init__.py:872, :875)
+    np.testing.assert_allclose(out["yaw_mean"].cpu().numpy()[:, 0], g["state_mean"][:, 2],
+                               rtol=1e-12)
+    np.testing.assert_allclose(out["yaw0_var"].cpu().numpy(), g["state_cov"][:, 2], rtol=1e-9)
+    # per-particle yaws and vertices against the oracle restatement
+    ovs = ovehicles_from_fixture(g)
+    yaw = out["yaw"].cpu().numpy()
+    vert = out["vertices"].cpu().numpy()
+    j = 0
+    for ov in ovs:
+        for k in range(ov.n_states):
+            o, n = store.offsets[j], store.counts[j]
+            np.testing.assert_allclose(yaw[:, o:o + n].T, ov.pred_yaws[k], rtol=1e-13, atol=1e-14)
+            t = T - 1
+            want = orc.vertices_of_bboxes(ov.pred_positions[k][:, t], ov.pred_yaws[k][:, t],
+                                          ov.bbox)
+            got = vert[8 * t:8 * t + 8, o:o + n].T.reshape(n, 4, 2)
+            np.testing.assert_allclose(got, want, rtol=1e-13)
+            j += 1
+
+
+def _sampler_inputs(O=3, L=25, T=8, seed=0):
+    rng = np.random.default_rng(seed)
+    init = np.stack([rng.uniform(20, 60, O), rng.uniform(20, 60, O),
+                     rng.uniform(-np.pi, np.pi, O), rng.uniform(3, 10, O)], axis=1)
+    pmf = np.stack([np.exp(rng.normal(0, 2.0, L)) for _ in range(O)])
+    pmf /= pmf.sum(1, keepdims=True)
+    gmm = np.zeros((O, L, T, 5), np.float32)
+    gmm[..., 0] = rng.normal(0, 0.15, size=(O, L, 1))
+    gmm[..., 1] = rng.normal(0, 1.0, size=(O, L, 1))
+    gmm[..., 2] = rng.uniform(np.log(0.05), np.log(0.5), size=(O, L, T))
+    gmm[..., 3] = rng.uniform(np.log(0.05), np.log(0.5), size=(O, L, T))
+    gmm[..., 4] = rng.uniform(-0.5, 0.5, size=(O, L, T))
+    gmm[:, 0, :, 0] = 0.0                      # one mode drives straight (|dphi| small branch)
+    gmm[:, 0, :, 2] = np.log(1e-4)
+    return init, pmf, gmm
+
+
+def test_sampler_matches_restatement(gpu):
+    """PARITY UNPINNED upstream (Trajectron++ absent): GPU sampler vs the repo's float32
+    restatement of DiscreteLatent.sample_p + GMM2D.rsample + Unicycle.integrate_samples."""
+    e = eng()
+    O, L, T, N, seed = 3, 25, 8, 20_000, 99
+    init, pmf, gmm = _sampler_inputs(O, L, T)
+    z, store = e.sample_unicycle(init, pmf, gmm, N, T, dt=0.5, seed=seed, device=gpu)
+    zc = z.cpu().numpy()
+    for o in range(O):
+        cdf = np.cumsum(pmf[o])
+        zo, pos = orc.sample_unicycle(init[o], cdf, gmm[o], N, T, 0.5, seed, ov=o)
+        np.testing.assert_array_equal(zc[o], zo)
+        got = store.cell_positions(o)
+        np.testing.assert_allclose(got, pos, rtol=0, atol=2e-4)   # float32 transcendentals
+    # empirical latent frequencies follow p(z|x)
+    freq = np.bincount(zc[0], minlength=L) / N
+    assert np.max(np.abs(freq - pmf[0])) < 5 * np.sqrt(pmf[0].max() / N) + 1e-3
