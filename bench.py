@@ -42,7 +42,52 @@ def parse():
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-cycles", type=int, default=40)
+    ap.add_argument("--sweep", action="store_true",
+                    help="also time the same kernel at the larger BASELINE configs (C3/C4/C5, "
+                         "ideal rollout) and report their roofline in 'roofline_sweep'")
     return ap.parse_args()
+
+
+def sweep(dev, seed):
+    """Kernel time and algorithmic HBM rate of the one-launch cycle at the configs where the
+    path is bandwidth-bound.  Not part of `value`."""
+    from ccmpc import cycle, engine, risk, synthetic
+    rows = []
+    configs = [("C3 np=1000 O=1 T=8", 1, 1000, 8, 1), ("C3 np=5000 O=1 T=8", 1, 5000, 8, 1),
+               ("C3 np=20000 O=1 T=8", 1, 20000, 8, 1), ("C3 np=100000 O=1 T=8", 1, 100000, 8, 1),
+               ("C4/GPU@8: 8 scenes x 4 OVs np=20000 T=12", 4, 20000, 12, 8),
+               ("C5 O=8 np=50000 T=40", 8, 50000, 40, 1)]
+    for name, O, N, T, scenes in configs:
+        cells, K, refs = [], [], []
+        for sc in range(scenes):
+            ovs, ref, _ = synthetic.scene(seed + 1000 + sc, O=O, N=N, T=T)
+            cells += [c for o in ovs for c in o]
+            K += [len(o) for o in ovs]
+            refs.append(ref)
+        store = engine.ParticleStore.from_cells(cells, device=dev)
+        cyc = cycle.MinkowskiCycle(store, K, refs[0])
+        t = time_kernel_live(cyc.run, dev, per_graph=10, replays=5)
+        b = int(sum(store.counts)) * 2 * T * 8
+        rows.append({"config": name, "particles": int(sum(store.counts)), "T": T,
+                     "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
+                     "alg_GBps": round(b / t / 1e9, 1), "frac": round(b / t / HBM_PEAK, 4)})
+        del store, cyc
+    # shrinking-horizon step: 1e6-sample ideal rollout fused with moments + half-spaces
+    ovs, ref, _ = synthetic.scene(seed + 7, O=1, N=100000, T=8, K=2)
+    store = engine.ParticleStore.from_cells(ovs[0], device=dev)
+    mean, cov = engine.moments(store)
+    src = torch.tensor([0, 1], dtype=torch.int32, device=dev)
+    cr = torch.as_tensor(risk.cell_risk(risk.eps_ura([2]), [2], 8), device=dev)
+    reft = torch.as_tensor(ref[None, :7], device=dev)
+    ws = engine.Workspace(dev)
+    fn = lambda: engine.ideal_minkowski_cycle(mean, cov, src, 7, 1_000_000, reft, cr, seed=3,
+                                              workspace=ws)
+    t = time_kernel_live(fn, dev, per_graph=4, replays=3)
+    rows.append({"config": "ideal rollout 2 cells x 1e6 samples T=7 (fused rollout+moments+"
+                           "half-spaces; 0 HBM bytes for trajectories)",
+                 "particles": 2_000_000, "T": 7, "kernel_us": round(t * 1e6, 2),
+                 "samples_per_s": round(2e6 * 7 / t, 1)})
+    return rows
 
 
 def init_dist(args):
@@ -213,6 +258,8 @@ def main():
                       "v8ideal/__init__.py:881-947 (numpy/scipy)",
         }
         out["speedup_vs_cpu"] = round(value / (1.0 / med), 1)
+    if args.sweep and rank == 0:
+        out["roofline_sweep"] = sweep(dev, args.seed)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -70,7 +70,7 @@ class ParticleStore:
 
     @property
     def n_cells(self):
-        return len(self.counts)
+        return int(self.cell_cnt.shape[0])
 
     @property
     def ccmpc_dtype(self):
@@ -94,8 +94,16 @@ class ParticleStore:
         store.pos.copy_(torch.from_numpy(host))
         return store
 
+    def sync_counts(self):
+        """Fetch device-side cell offsets/counts (after ccmpc_bucket); synchronises."""
+        self.counts = [int(c) for c in self.cell_cnt.cpu().tolist()]
+        self.offsets = [int(c) for c in self.cell_off.cpu().tolist()]
+        return self.counts
+
     def cell_positions(self, j):
         """(N_j, T, 2) float64 host copy of one cell (world frame)."""
+        if self.counts is None:
+            self.sync_counts()
         n, o = self.counts[j], self.offsets[j]
         x = self.pos[:, o:o + n].double().cpu().numpy().reshape(self.T, 2, n).transpose(2, 0, 1)
         if self.origin is not None:
@@ -310,3 +318,55 @@ def halfspaces(rec_bytes):
 def affine_records(rec_bytes):
     return rec_bytes.cpu().numpy().reshape(-1).view(_lib.AFFINE_DTYPE).reshape(
         rec_bytes.shape[:-1])
+
+
+def bucket(z, sample_store, latent_pmf, minpos, filter_pmf=0.1, max_k=None):
+    """GPU bucketing (ccmpc_bucket) of a sampler output (z [O,N], sample-order F32 store with
+    one cell per OV) into kept-mode cells.  latent_pmf (O, L) is host data, as in the reference
+    (latent_probs come back to the host in prediction.py:77-79).
+
+    Returns (bucketed F32 ParticleStore with origin = minpos per cell, K per OV, cell_pmf
+    [n_cells] device, init_center [n_cells, 2] device).  Device-side counts: store.counts holds
+    capacity bounds until ``store.sync_counts()``.
+    """
+    lib = _lib.load()
+    dev = sample_store.device
+    pmf = np.asarray(latent_pmf, np.float64)
+    O, L = pmf.shape
+    N = int(z.shape[1])
+    T = sample_store.T
+    keep = [np.argwhere(pmf[o] > filter_pmf).ravel() for o in range(O)]
+    K = [int(k.size) for k in keep]
+    if min(K) == 0:
+        raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent mode "
+                         f"with p(z|x) > {filter_pmf} (ovehicle.py:96-97 fails the same way)")
+    max_k = max(K) if max_k is None else max_k
+    keep_map = -np.ones((O, L), np.int32)
+    for o in range(O):
+        keep_map[o, keep[o]] = np.arange(K[o], dtype=np.int32)
+    cell_base = np.concatenate([[0], np.cumsum(K)[:-1]]).astype(np.int32)
+    region, cur = [], 0
+    for o in range(O):
+        region.append(cur)
+        cur = _round4(cur + N + 4 * K[o])
+    n_cells = int(sum(K))
+    origin = np.repeat(np.asarray(minpos, np.float64).reshape(-1, 2), K, axis=0)
+    out = ParticleStore(T, [0] * n_cells, dtype=torch.float32, device=dev, origin=origin,
+                        capacity=cur)
+    out.counts = None                                   # device-side until sync_counts()
+    out.n_bound = cur
+    t = lambda a, dt=None: torch.as_tensor(np.ascontiguousarray(a), device=dev)
+    t_keep, t_nk, t_base = t(keep_map), t(np.asarray(K, np.int32)), t(cell_base)
+    t_min = t(np.asarray(minpos, np.float64).reshape(-1, 2))
+    t_reg = t(np.asarray(region, np.int64))
+    pmf_out = torch.empty(n_cells, dtype=torch.float64, device=dev)
+    centre = torch.empty((n_cells, 2), dtype=torch.float64, device=dev)
+    need = lib.ccmpc_bucket_workspace_bytes(O, N, L, max_k)
+    ws = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
+    _lib.check(lib.ccmpc_bucket(_p(z), _p(sample_store.pos), sample_store.ld, T, O, N, L,
+                                _p(t_keep), _p(t_nk), _p(t_base), max_k, _p(t_min), _p(t_reg),
+                                _p(ws), ws.numel(), _p(out.pos), out.ld, _p(out.cell_off),
+                                _p(out.cell_cnt), _p(pmf_out), _p(centre), _stream()),
+               "ccmpc_bucket")
+    out._keepalive = (t_keep, t_nk, t_base, t_min, t_reg, ws)
+    return out, K, pmf_out, centre

@@ -1,0 +1,157 @@
+"""Other-vehicle particle clouds, mirroring collect/in_simulation/midlevel/ovehicle.py.
+
+The reference keeps each OV's bucketed predictions as Python lists of NumPy arrays
+(pred_positions[k]: (N_k, T, 2) float64, pred_yaws[k]: (N_k, T)).  Here every OV of a planning
+step shares ONE device-resident plane-major store (ScenePredictions); the list-of-arrays fields
+the reference exposes are materialised on the host only when someone reads them.
+"""
+import numpy as np
+import torch
+
+from . import engine
+
+DEFAULT_BBOX = np.array([4.5, 2.5])   # ovehicle.py:19
+
+
+class ScenePredictions:
+    """Bucketed particle clouds of all OVs of one planning step (cells in (ov, k) order)."""
+
+    def __init__(self, store, K, past_last, bbox, cell_pmf=None, init_center=None):
+        self.store = store
+        self.K = [int(k) for k in K]
+        self.T = store.T
+        self.cell_of = []                       # (ov, k) per cell
+        for o, k in enumerate(self.K):
+            self.cell_of += [(o, j) for j in range(k)]
+        assert len(self.cell_of) == store.n_cells
+        self.past_last = np.asarray(past_last, np.float64).reshape(len(self.K), 2)
+        self.bbox = np.asarray(bbox, np.float64).reshape(len(self.K), 2)
+        self.cell_pmf = cell_pmf
+        self.init_center = init_center
+        self._l4 = None
+
+    @property
+    def O(self):
+        return len(self.K)
+
+    def first_cell(self, ov):
+        return int(sum(self.K[:ov]))
+
+    def cell_past_last(self):
+        return np.repeat(self.past_last, self.K, axis=0)
+
+    def cell_bbox(self):
+        return np.repeat(self.bbox, self.K, axis=0)
+
+    def l4(self, with_yaw=False, with_vertices=False):
+        """Headings / vertices / L4 over all ph steps (cached per scene)."""
+        need = (self._l4 is None or (with_yaw and self._l4["yaw"] is None)
+                or (with_vertices and self._l4["vertices"] is None))
+        if need:
+            self._l4 = engine.l4(self.store, self.cell_past_last(), self.cell_bbox(),
+                                 with_yaw=with_yaw, with_vertices=with_vertices)
+        return self._l4
+
+
+class OVehicle:
+    """Mirror of ovehicle.py:OVehicle (fields :119-131), backed by a ScenePredictions."""
+
+    def __init__(self, scene, ov, node=None, past=None, ground_truth=None):
+        self.scene = scene
+        self.ov = ov
+        self.node = node
+        self.T = scene.T
+        self.past = np.asarray(past if past is not None else scene.past_last[ov:ov + 1])
+        self.ground_truth = ground_truth
+        self.bbox = scene.bbox[ov]
+        self.n_states = scene.K[ov]
+        self._pos = None
+        self._yaw = None
+
+    @property
+    def cells(self):
+        c0 = self.scene.first_cell(self.ov)
+        return list(range(c0, c0 + self.n_states))
+
+    @property
+    def latent_pmf(self):
+        if self.scene.cell_pmf is None:
+            st = self.scene.store
+            st.sync_counts() if st.counts is None else None
+            n = np.array([st.counts[c] for c in self.cells], float)
+            return n / n.sum()
+        return self.scene.cell_pmf[self.cells[0]:self.cells[-1] + 1].cpu().numpy()
+
+    @property
+    def init_center(self):
+        if self.scene.init_center is None:
+            return np.array([self.pred_positions[k][:, self.T - 1].mean(0)
+                             for k in range(self.n_states)])
+        return self.scene.init_center[self.cells[0]:self.cells[-1] + 1].cpu().numpy()
+
+    @property
+    def n_predictions(self):
+        return int(sum(p.shape[0] for p in self.pred_positions))
+
+    @property
+    def pred_positions(self):
+        """list over modes of (N_k, T, 2) float64 world positions (host copy, cached)."""
+        if self._pos is None:
+            self._pos = [self.scene.store.cell_positions(c) for c in self.cells]
+        return self._pos
+
+    @property
+    def pred_yaws(self):
+        """list over modes of (N_k, T) headings (ovehicle.py:72-76), computed on the GPU."""
+        if self._yaw is None:
+            st = self.scene.store
+            if st.counts is None:
+                st.sync_counts()
+            yaw = self.scene.l4(with_yaw=True)["yaw"]
+            self._yaw = [yaw[:, st.offsets[c]:st.offsets[c] + st.counts[c]].T.cpu().numpy()
+                         for c in self.cells]
+        return self._yaw
+
+
+def scene_from_positions(ov_cells, pasts, bboxes=None, device="cuda", dtype=torch.float64):
+    """Reference-format input (per OV a list over kept modes of (N_k, T, 2) world positions,
+    i.e. ovehicle.pred_positions) -> list[OVehicle] sharing one device store."""
+    K = [len(c) for c in ov_cells]
+    flat = [c for cells in ov_cells for c in cells]
+    store = engine.ParticleStore.from_cells(flat, device=device, dtype=dtype)
+    bboxes = np.tile(DEFAULT_BBOX, (len(K), 1)) if bboxes is None else bboxes
+    pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
+    scene = ScenePredictions(store, K, [p[-1] for p in pasts], bboxes)
+    return [OVehicle(scene, o, past=pasts[o]) for o in range(len(K))]
+
+
+def make_ovehicles(predictions, z, latent_probs, minpos, pasts, bboxes=None, T=None,
+                   filter_pmf=0.1, device="cuda"):
+    """v8ideal/__init__.py:469-505 + OVehicle.from_trajectron (ovehicle.py:24-117) on the GPU.
+
+    predictions: either a sample-order F32 ParticleStore from engine.sample_unicycle (one cell
+    per OV) with z [O, N] int32 on the device, or host arrays (O, N, T, 2) float32 + (O, N).
+    latent_probs: (O, L) host p(z|x).  Returns list[OVehicle] sharing one ScenePredictions."""
+    dev = engine.require_device(device)
+    if isinstance(predictions, engine.ParticleStore):
+        store_in, z_dev = predictions, z
+    else:
+        pred = np.asarray(predictions, np.float32)
+        O, N, T_, _ = pred.shape
+        store_in = engine.ParticleStore(T_, [N] * O, dtype=torch.float32, device=dev,
+                                        origin=np.zeros((O, 2)))
+        host = np.zeros((2 * T_, store_in.ld), np.float32)
+        for o in range(O):
+            host[:, store_in.offsets[o]:store_in.offsets[o] + N] = pred[o].transpose(1, 2, 0).reshape(2 * T_, N)
+        store_in.pos.copy_(torch.from_numpy(host))
+        z_dev = torch.as_tensor(np.asarray(z, np.int32), device=dev)
+    O = z_dev.shape[0]
+    mp = np.asarray(minpos, np.float64)
+    mp = np.tile(mp.reshape(2), (O, 1)) if mp.size == 2 else mp.reshape(O, 2)
+    store, K, pmf, centre = engine.bucket(z_dev, store_in, latent_probs, mp,
+                                          filter_pmf=filter_pmf)
+    store.sync_counts()
+    pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
+    bboxes = np.tile(DEFAULT_BBOX, (O, 1)) if bboxes is None else np.asarray(bboxes)
+    scene = ScenePredictions(store, K, [p[-1] for p in pasts], bboxes, pmf, centre)
+    return [OVehicle(scene, o, past=pasts[o]) for o in range(O)]

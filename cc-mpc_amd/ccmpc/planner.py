@@ -1,0 +1,369 @@
+"""Drop-in constraint-generation surface of the v8ideal planner
+(collect/in_simulation/midlevel/v8ideal/__init__.py, class MidlevelAgent).
+
+The reference planner couples CARLA, Trajectron++, cvxpy and CPLEX; only its chance-constraint
+path is in scope here.  This class keeps that path's Python call surface --
+the two generator methods with their argument lists and 9-tuple results, save_moments and
+predict_ideal -- and runs every numeric step on the GPU through libccmpc.so:
+
+  compute_obstacle_constraints_GMM_Minkowski_idealprediction   v8ideal/__init__.py:781-964
+      T == ph : ONE launch  (ccmpc_minkowski_cycle)        particles -> moments -> half-spaces
+      T <  ph : ONE launch  (ccmpc_ideal_minkowski_cycle)  previous moments -> 1e6-sample
+                                                            rollout -> moments -> half-spaces
+      + ccmpc_l4 for vertices / A_union / b_union / yaw statistics
+  compute_obstacle_constraints_GMM_affine                       v8ideal/__init__.py:1378-1539
+  save_moments / predict_ideal                                  v8ideal/__init__.py:2575-2711
+
+Differences from the reference, all at the boundary:
+  * constraints are HalfSpace records (cvxpy is not part of the compute path and is not
+    installed here); HalfSpace.expr(temp_x) builds the reference's cvxpy constraint when cvxpy
+    is importable, HalfSpace.holds(x) evaluates it numerically;
+  * the moments pickle (out/data/agent{id}_frame{f}_moments) is replaced by device-resident
+    state keyed by frame (save_moments_npz / load_moments_npz keep the file format's keys);
+  * the unseeded RNG of predict_ideal (:2664, :2699) is a Philox stream keyed by
+    (seed, frame, cell), so runs are reproducible.
+"""
+import numpy as np
+import scipy.stats
+import torch
+
+from . import engine, risk
+from .ovehicle import OVehicle, ScenePredictions
+
+
+class HalfSpace:
+    """One chance constraint on the ego position x_t (t = planning step):
+    side = +1:  n . x_t >= rhs      side = -1:  n . x_t <= rhs
+    Minkowski records have rhs = d (v8ideal/__init__.py:926-939); affine records have
+    rhs = d +/- Gamma ||sqrtm(cov) [m, -1]|| (:1504-1515)."""
+
+    __slots__ = ("ov", "k", "t", "tau", "n", "d", "rhs", "side", "which", "margin", "status")
+
+    def __init__(self, ov, k, t, tau, n, d, rhs, side, which, margin=0.0, status=0):
+        self.ov, self.k, self.t, self.tau = ov, k, t, tau
+        self.n = n
+        self.d, self.rhs, self.side, self.which = d, rhs, side, which
+        self.margin, self.status = margin, status
+
+    @property
+    def A(self):
+        """(A, b) of the reference's half-space bookkeeping (:931-939): A x <= b."""
+        return -self.n if self.side > 0 else self.n
+
+    @property
+    def b(self):
+        return -self.rhs if self.side > 0 else self.rhs
+
+    def holds(self, xy, tol=0.0):
+        v = float(self.n @ np.asarray(xy, float)[:2])
+        return v >= self.rhs - tol if self.side > 0 else v <= self.rhs + tol
+
+    def expr(self, temp_x):
+        """The reference's cvxpy constraint n^T [x_t, y_t] >= / <= rhs."""
+        import cvxpy as cp  # noqa: F401  (not installed in this image)
+        lhs = self.n.T @ cp.vstack([temp_x[self.t][0], temp_x[self.t][1]])
+        return lhs >= self.rhs if self.side > 0 else lhs <= self.rhs
+
+    def __repr__(self):
+        op = ">=" if self.side > 0 else "<="
+        return (f"HalfSpace(ov={self.ov}, k={self.k}, t={self.t}, tau={self.tau}: "
+                f"[{self.n[0]:.6g}, {self.n[1]:.6g}] . x {op} {self.rhs:.9g})")
+
+
+class LazyVertices:
+    """vertices[t][k][ov] -> (N_k, 4, 2) corners (v8ideal/__init__.py:627-640), copied from the
+    device on first access only (100k particles x 8 corners is tens of MB per OV)."""
+
+    def __init__(self, scene, ph):
+        self.scene, self.ph = scene, ph
+
+    def __len__(self):
+        return self.ph
+
+    def __getitem__(self, t):
+        return _VertT(self, t)
+
+
+class _VertT:
+    def __init__(self, lv, t):
+        self.lv, self.t = lv, t
+
+    def __getitem__(self, k):
+        return _VertTK(self.lv, self.t, k)
+
+
+class _VertTK:
+    def __init__(self, lv, t, k):
+        self.lv, self.t, self.k = lv, t, k
+
+    def __getitem__(self, ov):
+        sc = self.lv.scene
+        if self.k >= sc.K[ov]:
+            return None
+        v = sc.l4(with_yaw=True, with_vertices=True)["vertices"]
+        st = sc.store
+        c = sc.first_cell(ov) + self.k
+        o, n = st.offsets[c], st.counts[c]
+        return v[8 * self.t:8 * self.t + 8, o:o + n].T.cpu().numpy().reshape(n, 4, 2)
+
+
+def _object_grid(*shape):
+    return np.empty(shape, dtype=object).tolist()
+
+
+class MidlevelAgent:
+    """Constraint-generation surface of v8ideal.MidlevelAgent (v8ideal/__init__.py:202-235).
+
+    Only the arguments the chance-constraint path reads are kept; the CARLA/Trajectron/QP
+    arguments of the reference constructor are accepted and ignored (**kwargs, as :234)."""
+
+    def __init__(self, prediction_horizon=8, control_horizon=None, n_predictions=100,
+                 ego_vehicle_id=0, n_ideal=1_000_000, record_interval=10, seed=0,
+                 road_boundary_constraints=False, device="cuda", **kwargs):
+        self.device = engine.require_device(device)
+        self.prediction_horizon = int(prediction_horizon)
+        self.control_horizon = int(control_horizon or prediction_horizon)
+        self.n_predictions = int(n_predictions)
+        self.n_ideal = int(n_ideal)
+        self.record_interval = int(record_interval)
+        self.ego_vehicle_id = ego_vehicle_id
+        self.seed = int(seed)
+        self.road_boundary_constraints = road_boundary_constraints
+        self.R = risk.R_COLLISION
+        self._moments = {}                 # frame -> (mean [C,T,2], cov [C,2T,2T], K, T)
+        self._ws = engine.Workspace(self.device)
+        self.prob_lower_save = None
+        self.last_records = None
+
+    # ------------------------------------------------------------------------------------
+    def _scene(self, ovehicles):
+        """All OVs must share one ScenePredictions (the fast path); otherwise pack them."""
+        scenes = {id(ov.scene) for ov in ovehicles}
+        if len(scenes) == 1 and [ov.ov for ov in ovehicles] == list(range(ovehicles[0].scene.O)):
+            return ovehicles[0].scene
+        cells = [[np.asarray(p) for p in ov.pred_positions] for ov in ovehicles]
+        flat = [c for cs in cells for c in cs]
+        store = engine.ParticleStore.from_cells(flat, device=self.device)
+        return ScenePredictions(store, [len(c) for c in cells],
+                                [ov.past[-1] for ov in ovehicles], [ov.bbox for ov in ovehicles])
+
+    def _cell_risk(self, eps_ura, K):
+        """Per-cell (chi_r, chi_p, gamma) from the caller's eps_ura (:910-913)."""
+        ph = self.prediction_horizon
+        chi_p = scipy.stats.chi2.ppf(risk.TARGET_P, df=2)
+        rows = []
+        for o, k_o in enumerate(K):
+            for k in range(k_o):
+                e = eps_ura[o, k] / ph
+                rows.append((scipy.stats.chi2.ppf(1 - e, df=2), chi_p, scipy.stats.norm.ppf(1 - e)))
+        return torch.as_tensor(np.asarray(rows, np.float64).reshape(-1, 3), device=self.device)
+
+    def _ref(self, ref_traj, T):
+        ref = np.asarray([[ref_traj[t][0], ref_traj[t][1]] for t in range(T)], np.float64)
+        return torch.as_tensor(ref.reshape(1, T, 2), device=self.device)
+
+    def _state_stats(self, scene, mean0, cov0):
+        """ovStateMean/Cov_tau_1 (:864-875): t = 0 mean / variance of x, y, yaw per (ov, k)."""
+        O, K = scene.O, scene.K
+        maxK = max(K)
+        l4 = scene.l4()
+        ym, yv = l4["yaw_mean"][:, 0].cpu().numpy(), l4["yaw0_var"].cpu().numpy()
+        mx, my, myaw, vx, vy, vyaw = (_object_grid(O, maxK) for _ in range(6))
+        c = 0
+        for o in range(O):
+            for k in range(K[o]):
+                mx[o][k], my[o][k], myaw[o][k] = mean0[c, 0], mean0[c, 1], ym[c]
+                vx[o][k], vy[o][k], vyaw[o][k] = cov0[c, 0, 0], cov0[c, 1, 1], yv[c]
+                c += 1
+        return (mx, my, myaw), (vx, vy, vyaw)
+
+    def _l4_lists(self, scene):
+        ph = self.prediction_horizon
+        l4 = scene.l4()
+        A, b = l4["A"].cpu().numpy(), l4["b"].cpu().numpy()
+        A_union = _object_grid(ph, max(scene.K), scene.O)
+        b_union = _object_grid(ph, max(scene.K), scene.O)
+        for c, (o, k) in enumerate(scene.cell_of):
+            for t in range(ph):
+                A_union[t][k][o] = A[c, t]
+                b_union[t][k][o] = b[c, t]
+        return LazyVertices(scene, ph), A_union, b_union
+
+    def _ov_in_junction(self, scene, mean0):
+        """OVconstraint (:831-851): the Town03 scene-4 T-intersection test, last mode wins."""
+        flag = False
+        c = 0
+        for o in range(scene.O):
+            inj = None
+            for k in range(scene.K[o]):
+                inj = not (mean0[c, 0] >= 190 or mean0[c, 1] <= -80)
+                c += 1
+            flag = flag or bool(inj)
+        return flag
+
+    def _src_cells(self, prev_K, K):
+        """data_idx fallback (:2648-2656): mode k reads saved mode k, or the last saved slot."""
+        maxK_prev = max(prev_K)
+        src, c0 = [], 0
+        starts = np.concatenate([[0], np.cumsum(prev_K)[:-1]])
+        for o, k_o in enumerate(K):
+            for k in range(k_o):
+                d = k if k < maxK_prev else max(maxK_prev - 1, 0)
+                if d >= prev_K[o]:
+                    raise ValueError(f"saved moments of OV {o} have no mode {d} (the reference "
+                                     "reads None there and fails)")
+                src.append(int(starts[o] + d))
+        return torch.as_tensor(np.asarray(src, np.int32), device=self.device)
+
+    def _records_to_halfspaces(self, h, scene, T):
+        cons = []
+        P = T * (T - 1) // 2
+        for c, (o, k) in enumerate(scene.cell_of):
+            for p in range(P):
+                r = h[c, p]
+                if r["status"] != 0:
+                    raise FloatingPointError(
+                        f"constraint (ov={o}, k={k}, t={r['t_tau'] >> 16}, tau="
+                        f"{r['t_tau'] & 0xFFFF}) failed: {engine._lib.STATUS.get(int(r['status']))}")
+                n = np.array([r["n0"], r["n1"]])
+                cons.append(HalfSpace(o, k, int(r["t_tau"] >> 16), int(r["t_tau"] & 0xFFFF), n,
+                                      float(r["d"]), float(r["d"]), int(r["side"]),
+                                      int(r["which"])))
+        return cons
+
+    # ------------------------------------------------------------------------------------
+    def compute_obstacle_constraints_GMM_Minkowski_idealprediction(
+            self, params, ovehicles, Delta2, Omicron, temp_x, eps_ura, segments, Tsh, ref_traj):
+        """v8ideal/__init__.py:781-964.  Returns the reference's 9-tuple
+        (constraints, vertices, A_union, b_union, OVconstraint, direct, ovStateMean_tau_1,
+        ovStateCov_tau_1, 0)."""
+        if self.road_boundary_constraints:
+            raise NotImplementedError("road-boundary QP variables are outside the GPU path")
+        T, ph = int(Tsh), self.prediction_horizon
+        scene = self._scene(ovehicles)
+        K = scene.K
+        cr = self._cell_risk(np.asarray(eps_ura), K)
+        ref = self._ref(ref_traj, T)
+        m_scene, c_scene = engine.moments(scene.store, workspace=self._ws) if T < ph else (None, None)
+        if T < ph:
+            prev = self._moments.get(params.frame - self.record_interval)
+            if prev is None:
+                raise KeyError(f"no moments saved for frame {params.frame - self.record_interval}"
+                               " (the reference fails to load its pickle here)")
+            src = self._src_cells(prev[2], K)
+            seed = (self.seed * 1_000_003 + int(params.frame)) & (2**63 - 1)
+            mean, cov, status, rec, pl = engine.ideal_minkowski_cycle(
+                prev[0], prev[1], src, T, self.n_ideal, ref, cr, seed=seed, R=self.R,
+                workspace=self._ws)
+            st = status.cpu().numpy()
+            if np.any(st != 0):
+                raise np.linalg.LinAlgError(f"predict_ideal: conditional covariance not PD in "
+                                            f"cells {np.nonzero(st)[0].tolist()}")
+        else:
+            mean, cov, rec, pl = engine.minkowski_cycle(scene.store, ref, cr, R=self.R,
+                                                        workspace=self._ws)
+            m_scene, c_scene = mean, cov
+        # save_moments (:960): the moments of exactly the particles this step reduced
+        self._moments[params.frame] = (mean, cov, list(K), T)
+        h = engine.halfspaces(rec)
+        self.last_records = h
+        constraints = self._records_to_halfspaces(h, scene, T)
+        pl_h = pl.cpu().numpy()
+        if T == ph:
+            self.prob_lower_save = list(pl_h[-1])          # last cell wins (:947, :961-962)
+        mean0 = m_scene[:, 0, :].cpu().numpy()
+        cov0 = c_scene[:, 0:2, 0:2].cpu().numpy()
+        st_mean, st_cov = self._state_stats(scene, mean0, cov0)
+        vertices, A_union, b_union = self._l4_lists(scene)
+        direct = _object_grid(scene.O)
+        return (constraints, vertices, A_union, b_union, self._ov_in_junction(scene, mean0),
+                direct, st_mean, st_cov, 0)
+
+    def compute_obstacle_constraints_GMM_affine(
+            self, params, ovehicles, Delta2, Omicron, temp_x, eps_ura, segments, Tsh, ref_traj):
+        """v8ideal/__init__.py:1378-1539 (the S_big_repeated term is a QP variable, zero when
+        road-boundary constraints are off, and is left to the caller)."""
+        if self.road_boundary_constraints:
+            raise NotImplementedError("road-boundary QP variables are outside the GPU path")
+        T = int(Tsh)
+        scene = self._scene(ovehicles)
+        K = scene.K
+        gamma = self._cell_risk(np.asarray(eps_ura), K)[:, 2].contiguous()
+        ref = self._ref(ref_traj, T)
+        mean, cov = engine.moments(scene.store, workspace=self._ws)
+        if T != scene.T:
+            raise ValueError("the affine generator runs on the prediction horizon's particles")
+        h = engine.affine_records(engine.affine(mean, cov, ref, gamma, R=self.R))
+        self.last_records = h
+        cons = []
+        for c, (o, k) in enumerate(scene.cell_of):
+            for t in range(T):
+                r = h[c, t]
+                if r["status"] != 0:
+                    raise FloatingPointError(f"affine constraint (ov={o}, k={k}, t={t}) failed:"
+                                             f" {engine._lib.STATUS.get(int(r['status']))}")
+                cons.append(HalfSpace(o, k, t, -1, np.array([r["n0"], r["n1"]]), float(r["d"]),
+                                      float(r["rhs"]), int(r["side"]), int(r["which"]),
+                                      float(r["margin"])))
+        mean0 = mean[:, 0, :].cpu().numpy()
+        cov0 = cov[:, 0:2, 0:2].cpu().numpy()
+        st_mean, st_cov = self._state_stats(scene, mean0, cov0)
+        vertices, A_union, b_union = self._l4_lists(scene)
+        return (cons, vertices, A_union, b_union, False, _object_grid(scene.O), st_mean, st_cov,
+                0)
+
+    # ------------------------------------------------------------------------------------
+    def save_moments(self, ovehicles, O, K, T, Tpred, ego_vehicle_id, params):
+        """v8ideal/__init__.py:2575-2618: moments of the given OVs' first T steps, kept on the
+        device under params.frame (the generator calls this implicitly)."""
+        scene = self._scene(ovehicles)
+        mean, cov = engine.moments(scene.store, workspace=self._ws)
+        self._moments[params.frame] = (mean[:, :T].contiguous(),
+                                       cov[:, :2 * T, :2 * T].contiguous(), list(scene.K), T)
+
+    def saved_moments(self, frame):
+        """The reference's pickle content for `frame`: dict(mean_p0p1, cov_p0p1, cross_cov)
+        as nested lists [ov][k][t] (and [ov][k][t][tau])."""
+        mean, cov, K, T = self._moments[frame]
+        mean, cov = mean.cpu().numpy(), cov.cpu().numpy()
+        O, maxK = len(K), max(K)
+        mp, cp_, xc = _object_grid(O, maxK, T), _object_grid(O, maxK, T), _object_grid(O, maxK, T, T - 1)
+        c = 0
+        for o in range(O):
+            for k in range(K[o]):
+                for t in range(T):
+                    mp[o][k][t] = mean[c, t]
+                    cp_[o][k][t] = cov[c, 2 * t:2 * t + 2, 2 * t:2 * t + 2]
+                    for tau in range(t):
+                        xc[o][k][t][tau] = cov[c, 2 * t:2 * t + 2, 2 * tau:2 * tau + 2]
+                c += 1
+        return dict(mean_p0p1=mp, cov_p0p1=cp_, cross_cov=xc)
+
+    def save_moments_npz(self, frame, path):
+        """Write the saved moments of `frame` with the reference pickle's keys (flattened)."""
+        mean, cov, K, T = self._moments[frame]
+        np.savez(path, mean=mean.cpu().numpy(), cov=cov.cpu().numpy(), K=np.asarray(K), T=T)
+
+    def load_moments_npz(self, frame, path):
+        d = np.load(path, allow_pickle=False)
+        self._moments[frame] = (torch.as_tensor(d["mean"], device=self.device),
+                                torch.as_tensor(d["cov"], device=self.device),
+                                [int(k) for k in d["K"]], int(d["T"]))
+
+    def predict_ideal(self, ovehicles, T, ego_vehicle_id, params):
+        """v8ideal/__init__.py:2620-2711, materialised: traj_all[ov][k] = (n_ideal, T, 2).
+        (The generator never materialises these; it fuses the rollout with the moments.)"""
+        prev = self._moments[params.frame - self.record_interval]
+        K = [ov.n_states for ov in ovehicles]
+        src = self._src_cells(prev[2], K)
+        seed = (self.seed * 1_000_003 + int(params.frame)) & (2**63 - 1)
+        store, status = engine.ideal_rollout(prev[0], prev[1], src, T, self.n_ideal, seed=seed)
+        if np.any(status.cpu().numpy() != 0):
+            raise np.linalg.LinAlgError("predict_ideal: conditional covariance not PD")
+        out, c = {}, 0
+        for o, k_o in enumerate(K):
+            out[o] = {}
+            for k in range(k_o):
+                out[o][k] = store.cell_positions(c)
+                c += 1
+        return out

@@ -1,17 +1,17 @@
 // Segmented Gram reduction shared by moments.hip (particle stores) and rollout.hip (fused
-// ideal rollout): MFMA accumulation, partial-slab publication and the in-launch per-cell
-// combine by the last-arriving work item.
+// ideal rollout): workgroup geometry, MFMA load groups, the cross-wave combine, the in-launch
+// combine tree across workgroups, and the per-cell finalisation.
 //
-// Slab layout per work item: NT = RB(RB+1)/2 tiles of the f64 16x16x4 MFMA C layout
-// (entry (tile, reg, lane) <-> row (lane>>4) + 4 reg, col lane&15 of tile (bi, bj)), then
-// RB*16 shifted row sums.
+// Slab layout (one per work item / tree node): NT = RB(RB+1)/2 tiles of the f64 16x16x4 MFMA
+// C layout (entry (tile, reg, lane) <-> row (lane>>4) + 4 reg, col lane&15 of tile (bi, bj)),
+// then RB*16 shifted row sums.
 //
 // Cross-workgroup hand-off (MI355X_MICROARCH.md "Valid forms", first table row; guide §6 G16):
-// every slab store is an agent-scope write-through (sc1) store, the wave drains with
-// s_waitcnt vmcnt(0), then ONE lane adds to the cell's arrival counter (agent scope).  The item
-// that draws ticket nit-1 is the reducer: it reads every slab of the cell with sc1 loads (no L1,
-// so no acquire fence is needed) in a fixed item order -- bitwise reproducible, no float
-// atomics -- and resets the counter to 0 for the next launch.
+// every slab store is an agent-scope write-through (sc1) store, every storing wave drains with
+// s_waitcnt vmcnt(0) before the workgroup barrier, then ONE lane adds to the group's arrival
+// counter (agent scope).  The last arriver reads the slabs with sc1 loads (no L1 involved, so
+// no acquire fence is needed) in a fixed order -- bitwise reproducible, no float atomics -- and
+// resets the counter to 0 for the next launch.
 #pragma once
 #include "ccmpc_common.hpp"
 
@@ -20,66 +20,114 @@ namespace ccmpc {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxT = 40;
-constexpr int kCounterAlign = 256;  // bytes reserved at the head of every workspace
+constexpr int kCounterAlign = 256;
 
 __host__ __device__ constexpr int n_tiles(int rb) { return rb * (rb + 1) / 2; }
 __host__ __device__ constexpr int slab_doubles(int rb) { return n_tiles(rb) * 256 + rb * 16; }
 
 inline int row_blocks(int64_t T) { return static_cast<int>((2 * T + 15) / 16); }
 
-inline size_t counter_bytes(int64_t n_cells) {
-  const size_t b = static_cast<size_t>(n_cells) * sizeof(int32_t);
-  return (b + kCounterAlign - 1) / kCounterAlign * kCounterAlign;
-}
+// ---- work-item geometry of the particle-store kernel ----------------------------------------
+// One work item = one workgroup of NW waves; each wave owns WQ consecutive particles and loads
+// S 16-particle steps per group, double-buffered, so ~2 groups of 16-byte loads are in flight.
+// WQ is picked per launch: the f64 MFMA work of a small problem must be spread over many CUs
+// (one CU's 4 matrix pipes need ~4 us for a 2000-particle T=8 cell), so latency-bound sizes
+// use WQ = 64 (one load group per wave, one tree level); bandwidth-bound sizes use WQ = 256
+// (fewer slabs, shallower tree).  A cell that fits one item never leaves its workgroup.
+template <int RB>
+struct Geo {
+  static constexpr int NW = RB <= 2 ? 4 : 8;
+  static constexpr int S = RB == 1 ? 4 : (RB == 2 ? 2 : 1);
+  static constexpr int NACC = (n_tiles(RB) == 1) ? 2 : 1;  // 2 chains when there is one tile
+  static constexpr int MIN_WAVES_PER_SIMD = RB == 1 ? 4 : 2;
+};
 
-// particles per work item (one wavefront): ~8 items for a 2000-particle cell keeps the combine
-// short; large inputs get >= 2048 items to fill 256 CUs
-inline int64_t pick_chunk(int64_t n_bound) {
-  int64_t c = (n_bound + 2047) / 2048;
-  c = ((c + 63) / 64) * 64;
-  if (c < 256) c = 256;
-  if (c > 8192) c = 8192;
-  return c;
+inline int waves_per_item(int rb) { return rb <= 2 ? 4 : 8; }
+
+// particles per wave: 64 while the whole input is small enough to be latency-bound
+inline int64_t store_wave_quota(int64_t n_bound) { return n_bound <= (int64_t(1) << 18) ? 64 : 256; }
+
+inline int64_t store_chunk(int rb, int64_t n_bound) {
+  return waves_per_item(rb) * store_wave_quota(n_bound);
 }
 
 inline int64_t max_items(int64_t n_cells, int64_t n_bound, int64_t chunk) {
   return (n_bound + chunk - 1) / chunk + n_cells;
 }
 
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
 // items of a cell: at least one, so an empty cell is still finalised (to NaN, as np.cov does)
 __device__ __forceinline__ int64_t items_of(int64_t n, int64_t chunk) {
-  return n > 0 ? (n + chunk - 1) / chunk : 1;
+  return n > 0 ? ceil_div(n, chunk) : 1;
 }
 
-// Item id -> (cell, chunk index, first item of the cell), wave-parallel scan.
-// False for ids past the last item (the grid is sized by an upper bound).
+constexpr int kFanIn = 16;
+constexpr int kMaxLevels = 6;  // combine-tree depth bound: 16^6 items per cell
+
+struct ItemLoc {
+  int cell;
+  int64_t chunk_idx, first, cnt, off;
+  int64_t level_first[kMaxLevels + 1];  // index of the cell's first node at each tree level
+};
+
+// Item id -> (cell, chunk index, cell count, cell offset, and the cell's first node at every
+// level of the combine tree): one wave-parallel scan over the cells, so everything the item
+// needs arrives with a single memory round trip.  False for ids past the last item (the grid
+// is sized by an upper bound).
 __device__ __forceinline__ bool locate_item(int64_t item, const int64_t *__restrict__ cnt,
-                                            int n_cells, int64_t chunk, int &cell,
-                                            int64_t &chunk_idx, int64_t &first) {
+                                            const int64_t *__restrict__ off, int n_cells,
+                                            int64_t chunk, ItemLoc &loc) {
   const int lane = threadIdx.x & 63;
-  int64_t before = 0;
+  int64_t before[kMaxLevels + 1];
+#pragma unroll
+  for (int l = 0; l <= kMaxLevels; ++l) before[l] = 0;
   for (int base = 0; base < n_cells; base += 64) {
     const int c = base + lane;
-    const int64_t my = (c < n_cells) ? items_of(cnt[c], chunk) : 0;
-    int64_t incl = my;
+    const int64_t n = (c < n_cells) ? cnt[c] : 0;
+    const int64_t o = (c < n_cells) ? off[c] : 0;
+    int64_t my = (c < n_cells) ? items_of(n, chunk) : 0;
+    int64_t incl[kMaxLevels + 1], mine[kMaxLevels + 1];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
+    for (int l = 0; l <= kMaxLevels; ++l) {
+      mine[l] = my;
+      incl[l] = my;
+#pragma unroll
+      for (int s = 1; s < 64; s <<= 1) {
+        const int64_t y = __shfl_up(incl[l], s, 64);
+        if (lane >= s) incl[l] += y;
+      }
+      my = ceil_div(my, kFanIn);
     }
-    const int64_t total = __shfl(incl, 63, 64);
-    if (item < before + total) {
-      const unsigned long long m = __ballot(before + incl > item);
+    const int64_t total = __shfl(incl[0], 63, 64);
+    if (item < before[0] + total) {
+      const unsigned long long m = __ballot(before[0] + incl[0] > item);
       const int l = __ffsll(static_cast<long long>(m)) - 1;
-      const int64_t excl = __shfl(incl - my, l, 64);
-      cell = base + l;
-      first = before + excl;
-      chunk_idx = item - first;
+      loc.cell = base + l;
+#pragma unroll
+      for (int k = 0; k <= kMaxLevels; ++k)
+        loc.level_first[k] = before[k] + __shfl(incl[k] - mine[k], l, 64);
+      loc.first = loc.level_first[0];
+      loc.chunk_idx = item - loc.first;
+      loc.cnt = __shfl(n, l, 64);
+      loc.off = __shfl(o, l, 64);
       return true;
     }
-    before += total;
+#pragma unroll
+    for (int k = 0; k <= kMaxLevels; ++k) before[k] += __shfl(incl[k], 63, 64);
   }
   return false;
+}
+
+// Sum over cells c < cell of f(c), wave-parallel (every wave computes it redundantly).
+template <typename F>
+__device__ __forceinline__ int64_t wave_prefix(int cell, F f) {
+  const int lane = threadIdx.x & 63;
+  int64_t s = 0;
+  for (int c = lane; c < cell; c += 64) s += f(c);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  return s;
 }
 
 template <typename P>
@@ -116,78 +164,199 @@ __device__ __forceinline__ double ld_sc1(const double *p) {
       __HIP_MEMORY_SCOPE_AGENT)));
 }
 
-// Write one item's accumulators (tiles + row sums) write-through.
-template <int RB, int NACC>
-__device__ __forceinline__ void publish_slab(double *slab, const d4 (&acc)[NACC][n_tiles(RB)],
-                                             const double (&s1)[RB]) {
+// Combine the NW waves' accumulators in a fixed order (wave 0 + 1 + ... + NW-1), tile by tile
+// through `xch` ((NW-1) x 256 doubles, >= 16 NW), and let wave 0 write the item's slab: to
+// global memory write-through (to_lds = false) or to the LDS slab `dst` (to_lds = true).
+// Every thread of the workgroup must call it.
+template <int RB, int NACC, int NW>
+__device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)],
+                                              const double (&s1)[RB], double *xch, double *dst,
+                                              bool to_lds) {
   constexpr int NT = n_tiles(RB);
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     d4 s = acc[0][t];
     if (NACC == 2) s += acc[NACC - 1][t];
+    if (NW > 1) {
+      if (w > 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) st_sc1(slab + t * 256 + k * 64 + lane, s[k]);
+        for (int k = 0; k < 4; ++k) xch[(w - 1) * 256 + k * 64 + lane] = s[k];
+      }
+      __syncthreads();
+    }
+    if (w == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double v = s[k];
+#pragma unroll
+        for (int o = 0; o < NW - 1; ++o) v += xch[o * 256 + k * 64 + lane];
+        if (to_lds)
+          dst[t * 256 + k * 64 + lane] = v;
+        else
+          st_sc1(dst + t * 256 + k * 64 + lane, v);
+      }
+    }
+    if (NW > 1) __syncthreads();
   }
 #pragma unroll
   for (int b = 0; b < RB; ++b) {
     double x = s1[b];
     x += __shfl_xor(x, 16, 64);
     x += __shfl_xor(x, 32, 64);
-    if (lane < 16) st_sc1(slab + NT * 256 + b * 16 + lane, x);
+    if (lane < 16) xch[w * 16 + lane] = x;
+    __syncthreads();
+    if (w == 0 && lane < 16) {
+      double v = xch[lane];
+#pragma unroll
+      for (int o = 1; o < NW; ++o) v += xch[o * 16 + lane];
+      if (to_lds)
+        dst[NT * 256 + b * 16 + lane] = v;
+      else
+        st_sc1(dst + NT * 256 + b * 16 + lane, v);
+    }
+    __syncthreads();
   }
 }
 
-// Drain this wave's slab stores, take a ticket; true for the last of `nit` arrivals (which
-// also resets the counter for the next launch).  One-wave workgroups only.
-__device__ __forceinline__ bool arrive_last(int32_t *counter, int64_t nit) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int ticket = 0;
-  if ((threadIdx.x & 63) == 0)
-    ticket = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0, 64);
-  const bool last = static_cast<int64_t>(ticket) == nit - 1;
-  if (last && (threadIdx.x & 63) == 0)
-    __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep slab loads below the ticket
+// Drain the workgroup's slab stores, take a ticket; true (in every thread) for the last of
+// `nit` arrivals, which also resets the counter for the next launch.
+__device__ __forceinline__ bool arrive_last(int32_t *counter, int64_t nit, int *flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int ticket =
+        __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = static_cast<int64_t>(ticket) == nit - 1;
+    if (last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = last ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = *flag_lds != 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keep slab loads below the ticket
   return last;
 }
 
-// Sum entry e over the cell's nit slabs (sc1 loads, 4 independent chains, fixed order).
-__device__ __forceinline__ double sum_items(const double *__restrict__ slab0, int64_t nit, int E,
-                                            int e) {
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int64_t i = 0;
-  for (; i + 4 <= nit; i += 4) {
-    a0 += ld_sc1(slab0 + (i + 0) * E + e);
-    a1 += ld_sc1(slab0 + (i + 1) * E + e);
-    a2 += ld_sc1(slab0 + (i + 2) * E + e);
-    a3 += ld_sc1(slab0 + (i + 3) * E + e);
-  }
-  for (; i < nit; ++i) a0 += ld_sc1(slab0 + i * E + e);
-  return (a0 + a1) + (a2 + a3);
+// ---- fixed fan-in combine tree ------------------------------------------------------------
+// Items of a cell are the leaves (level 0).  Each group of up to kFanIn consecutive level-l
+// nodes has an arrival counter; its last arriver sums the group's slabs into one level-(l+1)
+// slab.  When a level has <= kFanIn nodes, the last arriver of that single group is the cell's
+// reducer.  Depth = ceil(log16(items)), every combine reads <= 16 slabs with all loads in
+// flight at once, and the summation order is fixed by the tree: bitwise reproducible.
+struct TreeLayout {
+  int32_t *counters[kMaxLevels];  // level l: one counter per group of level-l nodes
+  double *slabs[kMaxLevels];      // level l: node slabs (level 0 = work items)
+};
+
+// nodes of a cell with `nit` items at level l
+__device__ __forceinline__ int64_t nodes_at(int64_t nit, int l) {
+  int64_t n = nit;
+  for (int i = 0; i < l; ++i) n = ceil_div(n, kFanIn);
+  return n;
 }
 
-// The reducer: slabs of one cell -> mean[T][2] (+ origin) and cov[2T][2T] (ddof = 1),
-// cov = (G - S S^T / n) / (n - 1) on data shifted by shift_lds (LDS, D entries).
-// Uses S_lds (LDS, D entries) as scratch.  One wavefront; ends with a barrier so the caller can
-// read mean/cov back.
-template <int RB>
-__device__ void reduce_cell(const double *__restrict__ slab0, int64_t nit, int64_t cnt, int T,
-                            const double *shift_lds, double *S_lds, double o0, double o1,
-                            double *__restrict__ mean, double *__restrict__ cov) {
+// Host: capacity of level l (nodes) for n_cells cells holding <= max_items items in total.
+inline int64_t level_capacity(int64_t max_items, int64_t n_cells, int l) {
+  int64_t c = max_items;
+  for (int i = 0; i < l; ++i) c = c / kFanIn + n_cells;  // sum of ceils <= sum/16 + cells
+  return c + 1;
+}
+
+inline size_t tree_counter_bytes(int64_t max_items, int64_t n_cells) {
+  size_t ctr = 0;
+  for (int l = 0; l < kMaxLevels; ++l)
+    ctr += static_cast<size_t>(level_capacity(max_items, n_cells, l + 1)) * sizeof(int32_t);
+  return (ctr + kCounterAlign - 1) / kCounterAlign * kCounterAlign;
+}
+
+inline size_t tree_bytes(int64_t max_items, int64_t n_cells, int E) {
+  size_t slab = 0;
+  for (int l = 0; l < kMaxLevels; ++l)
+    slab += static_cast<size_t>(level_capacity(max_items, n_cells, l)) * E * sizeof(double);
+  return tree_counter_bytes(max_items, n_cells) + slab;
+}
+
+inline TreeLayout tree_layout(void *ws, int64_t max_items, int64_t n_cells, int E) {
+  TreeLayout L;
+  int32_t *c = static_cast<int32_t *>(ws);
+  for (int l = 0; l < kMaxLevels; ++l) {
+    L.counters[l] = c;
+    c += level_capacity(max_items, n_cells, l + 1);
+  }
+  double *s = reinterpret_cast<double *>(static_cast<char *>(ws) +
+                                         tree_counter_bytes(max_items, n_cells));
+  for (int l = 0; l < kMaxLevels; ++l) {
+    L.slabs[l] = s;
+    s += level_capacity(max_items, n_cells, l) * E;
+  }
+  return L;
+}
+
+// Sum entry e over n <= kFanIn consecutive slabs: all loads issued first (indices clamped, no
+// per-load branch), then a fixed-order sum.
+__device__ __forceinline__ double sum_group(const double *__restrict__ slab0, int64_t n, int E,
+                                            int e) {
+  double v[kFanIn];
+#pragma unroll
+  for (int i = 0; i < kFanIn; ++i) {
+    const int64_t j = i < n ? i : n - 1;
+    v[i] = ld_sc1(slab0 + j * E + e);
+  }
+  double s = v[0];
+#pragma unroll
+  for (int i = 1; i < kFanIn; ++i) s += (i < n) ? v[i] : 0.0;
+  return s;
+}
+
+// Climb the tree from a published leaf.  Returns true in the workgroup that must finalise the
+// cell; then *root points at the last level's first slab and *root_n is its node count (<= 16).
+// node_prefix(l) must return the index of the cell's first level-l node within level l.
+template <int E, typename Prefix>
+__device__ bool tree_climb(const TreeLayout &L, int64_t idx, int64_t nit, Prefix node_prefix,
+                           int *flag, const double **root, int64_t *root_n) {
+  int64_t n_l = nit;
+  for (int l = 0; l < kMaxLevels; ++l) {
+    const int64_t grp = idx / kFanIn;
+    const int64_t gsize = (n_l - grp * kFanIn) < kFanIn ? (n_l - grp * kFanIn) : kFanIn;
+    const int64_t pre_l = node_prefix(l), pre_up = node_prefix(l + 1);
+    if (!arrive_last(L.counters[l] + pre_up + grp, gsize, flag)) return false;
+    const double *children = L.slabs[l] + (pre_l + grp * kFanIn) * E;
+    if (n_l <= kFanIn || l + 1 == kMaxLevels) {
+      *root = children;
+      *root_n = gsize;
+      return true;
+    }
+    double *parent = L.slabs[l + 1] + (pre_up + grp) * E;
+    for (int e = threadIdx.x; e < E; e += blockDim.x)
+      st_sc1(parent + e, sum_group(children, gsize, E, e));
+    idx = grp;
+    n_l = ceil_div(n_l, kFanIn);
+  }
+  return false;
+}
+
+// The per-cell finalisation: summed slab entries (read through `rd(e)`) -> mean[T][2]
+// (+ origin) and cov[2T][2T] (ddof = 1), cov = (G - S S^T / n) / (n - 1) on data shifted by
+// shift_lds.  Writes cov to global memory and, when cov_lds != nullptr, to LDS as well (row
+// stride 2T) for the fused half-space tail.  Called by every thread of the workgroup; ends
+// with a barrier.
+template <int RB, typename Reader>
+__device__ void finalize_cell(Reader rd, int64_t cnt, int T, const double *shift_lds,
+                              double *S_lds, double o0, double o1, double *__restrict__ mean,
+                              double *__restrict__ cov, double *mean_lds, double *cov_lds) {
   constexpr int NT = n_tiles(RB);
-  constexpr int E = slab_doubles(RB);
   constexpr int D = 16 * RB;
-  const int lane = threadIdx.x & 63;
+  const int tid = threadIdx.x, nth = blockDim.x;
   const int rows = 2 * T;
   const double n = static_cast<double>(cnt);
-  for (int r = lane; r < D; r += 64)
-    S_lds[r] = r < rows ? sum_items(slab0, nit, E, NT * 256 + r) : 0.0;
+  for (int r = tid; r < D; r += nth) S_lds[r] = r < rows ? rd(NT * 256 + r) : 0.0;
   __syncthreads();
-  for (int r = lane; r < rows; r += 64)
-    mean[r] = (shift_lds[r] + S_lds[r] / n) + ((r & 1) ? o1 : o0);
-  for (int e = lane; e < NT * 256; e += 64) {
+  for (int r = tid; r < rows; r += nth) {
+    const double m = (shift_lds[r] + S_lds[r] / n) + ((r & 1) ? o1 : o0);
+    mean[r] = m;
+    if (mean_lds) mean_lds[r] = m;
+  }
+  for (int e = tid; e < NT * 256; e += nth) {
     const int tile = e >> 8, k = (e >> 6) & 3, l = e & 63;
     const int row = (l >> 4) + 4 * k, col = l & 15;
     int bi = 0, t = tile;
@@ -198,10 +367,13 @@ __device__ void reduce_cell(const double *__restrict__ slab0, int64_t nit, int64
     const int bj = bi + t;
     const int i = 16 * bi + row, j = 16 * bj + col;
     if (i >= rows || j >= rows || i > j) continue;  // one value per symmetric pair
-    const double g = sum_items(slab0, nit, E, e);
-    const double c = (g - S_lds[i] * S_lds[j] / n) / (n - 1.0);
+    const double c = (rd(e) - S_lds[i] * S_lds[j] / n) / (n - 1.0);
     cov[i * rows + j] = c;
     cov[j * rows + i] = c;
+    if (cov_lds) {
+      cov_lds[i * rows + j] = c;
+      cov_lds[j * rows + i] = c;
+    }
   }
   __syncthreads();
 }

@@ -8,7 +8,6 @@
 // particle cloud is read exactly once.
 //
 // Design (gfx950), ONE launch per call:
-//  * Work item = (cell, chunk of `chunk` particles), one wavefront per workgroup.
 //  * The Gram matrix G = X X^T of the shifted data X[r][p] = pos[r][p] - pos[r][first]
 //    (r = 2t + xy) runs on the f64 matrix core: v_mfma_f64_16x16x4_f64 takes A[i][k] from lane
 //    (i + 16k) and B[k][j] from lane (j + 16k), so a lane holding X[16b + (lane&15)][p_k]
@@ -20,39 +19,100 @@
 //    group k -- summation order is irrelevant for a Gram sum.
 //  * Shift by the cell's first particle (shifted one-pass formula): positions sit around
 //    x ~ 200 m with sub-metre spread, and the un-shifted one-pass form loses every digit.
-//  * Each item publishes its partial slab write-through and takes a per-cell ticket; the last
-//    arriver combines the cell (gram.hpp) and, in the cycle variant, immediately builds the
-//    cell's T(T-1)/2 half-spaces -- no kernel boundary between moments and constraints.
+//  * Work item = one workgroup of Geo<RB>::NW waves over CHUNK particles of one cell (gram.hpp).
+//    A cell that fits one item is combined entirely in LDS; larger cells publish per-item
+//    slabs write-through and meet in the fixed fan-in-16 tree.  The cell's finaliser then
+//    (cycle variant) builds its T(T-1)/2 half-spaces from the covariance it just produced in
+//    LDS -- no kernel boundary between moments and constraints.
 #include "constraints.hpp"
 #include "gram.hpp"
 
 namespace ccmpc {
 
+template <typename P, int RB, int S>
+__device__ __forceinline__ void load_group(double (&v)[S][RB][4], const P *const (&rowp)[RB],
+                                           const bool (&live)[RB], const double (&sh)[RB],
+                                           int64_t gbase, int64_t p1, int g) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t q = gbase + 16 * s + 4 * g;
+#pragma unroll
+    for (int b = 0; b < RB; ++b) {
+      if (live[b] && q + 3 < p1) {
+        load4<P>(rowp[b] + q, v[s][b]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[s][b][j] = (live[b] && q + j < p1) ? static_cast<double>(rowp[b][q + j]) : sh[b];
+      }
+    }
+  }
+}
+
+template <int RB, int S, int NACC>
+__device__ __forceinline__ void mfma_group(double (&v)[S][RB][4], const double (&sh)[RB],
+                                           d4 (&acc)[NACC][n_tiles(RB)], double (&s1)[RB]) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+#pragma unroll
+    for (int b = 0; b < RB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[s][b][j] -= sh[b];  // out-of-range slots become 0
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int a = (NACC == 2) ? (j & 1) : 0;
+      int t = 0;
+#pragma unroll
+      for (int bi = 0; bi < RB; ++bi)
+#pragma unroll
+        for (int bj = bi; bj < RB; ++bj) {
+          acc[a][t] =
+              __builtin_amdgcn_mfma_f64_16x16x4f64(v[s][bi][j], v[s][bj][j], acc[a][t], 0, 0, 0);
+          ++t;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < RB; ++b) s1[b] += (v[s][b][0] + v[s][b][1]) + (v[s][b][2] + v[s][b][3]);
+  }
+}
+
 template <typename P, int RB, bool MINK>
-__global__ __launch_bounds__(64) void moments_kernel(
+__global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void moments_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
-    int64_t chunk, double *__restrict__ partial, int32_t *__restrict__ counters,
-    double *__restrict__ out_mean, double *__restrict__ out_cov, MinkParams mp) {
+    int64_t wq, TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
+    MinkParams mp) {
+  using G = Geo<RB>;
   constexpr int NT = n_tiles(RB);
-  constexpr int NACC = (NT == 1) ? 2 : 1;  // two chains hide MFMA latency when there is one tile
+  constexpr int NACC = G::NACC;
   constexpr int D = 16 * RB;
+  constexpr int S = G::S;
+  constexpr int E = slab_doubles(RB);
+  constexpr bool COV_IN_LDS = MINK && RB <= 2;
+  __shared__ double xch[(G::NW - 1) * 256];
+  __shared__ double slab_lds[E];
   __shared__ double shift_lds[D];
   __shared__ double S_lds[D];
+  __shared__ double mean_lds[D];
+  __shared__ double cov_lds[COV_IN_LDS ? D * D : 1];
   __shared__ double lb_s[MINK ? 40 * 39 / 2 : 1];
-  int cell;
-  int64_t cidx, first;
-  const int64_t item = blockIdx.x;
-  if (!locate_item(item, cell_cnt, n_cells, chunk, cell, cidx, first)) return;
+  __shared__ int flag;
 
-  const int lane = threadIdx.x;
+  ItemLoc loc;
+  const int64_t chunk = G::NW * wq;
+  if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, chunk, loc)) return;  // uniform
+  const int cell = loc.cell;
+  const int64_t cnt = loc.cnt;
+
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
   const int r = lane & 15;
   const int g = lane >> 4;
   const int rows = 2 * T;
-  const int64_t off = cell_off[cell];
-  const int64_t cnt = cell_cnt[cell];
-  const int64_t p0 = cidx * chunk;
-  const int64_t p1 = (p0 + chunk < cnt) ? p0 + chunk : cnt;
+  const int64_t i0 = loc.chunk_idx * chunk;
+  const int64_t i1 = (i0 + chunk < cnt) ? i0 + chunk : cnt;
+  const int64_t p0 = i0 + static_cast<int64_t>(w) * wq;
+  const int64_t p1 = (p0 + wq < i1) ? p0 + wq : i1;
 
   double sh[RB];
   const P *rowp[RB];
@@ -61,7 +121,7 @@ __global__ __launch_bounds__(64) void moments_kernel(
   for (int b = 0; b < RB; ++b) {
     const int R = 16 * b + r;
     live[b] = R < rows;
-    rowp[b] = pos + static_cast<int64_t>(live[b] ? R : 0) * ld + off;
+    rowp[b] = pos + static_cast<int64_t>(live[b] ? R : 0) * ld + loc.off;
     sh[b] = (live[b] && cnt > 0) ? static_cast<double>(rowp[b][0]) : 0.0;
   }
 
@@ -74,76 +134,70 @@ __global__ __launch_bounds__(64) void moments_kernel(
 #pragma unroll
   for (int b = 0; b < RB; ++b) s1[b] = 0.0;
 
-  for (int64_t base = p0; base < p1; base += 16) {
-    const int64_t q = base + 4 * g;
-    double v[RB][4];
-#pragma unroll
-    for (int b = 0; b < RB; ++b) {
-      if (live[b] && q + 3 < p1) {
-        load4<P>(rowp[b] + q, v[b]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[b][j] -= sh[b];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          v[b][j] = (live[b] && q + j < p1) ? static_cast<double>(rowp[b][q + j]) - sh[b] : 0.0;
-      }
+  // double-buffered load groups: the next group's loads are in flight during this group's MFMAs
+  const int64_t ngroups = p1 > p0 ? ceil_div(p1 - p0, 16 * S) : 0;
+  double va[S][RB][4], vb[S][RB][4];
+  if (ngroups > 0) load_group<P, RB, S>(va, rowp, live, sh, p0, p1, g);
+  for (int64_t gi = 0; gi < ngroups; gi += 2) {
+    if (gi + 1 < ngroups) load_group<P, RB, S>(vb, rowp, live, sh, p0 + (gi + 1) * 16 * S, p1, g);
+    mfma_group<RB, S, NACC>(va, sh, acc, s1);
+    if (gi + 1 < ngroups) {
+      if (gi + 2 < ngroups)
+        load_group<P, RB, S>(va, rowp, live, sh, p0 + (gi + 2) * 16 * S, p1, g);
+      mfma_group<RB, S, NACC>(vb, sh, acc, s1);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int a = (NACC == 2) ? (j & 1) : 0;
-      int t = 0;
-#pragma unroll
-      for (int bi = 0; bi < RB; ++bi)
-#pragma unroll
-        for (int bj = bi; bj < RB; ++bj) {
-          acc[a][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[bi][j], v[bj][j], acc[a][t], 0, 0, 0);
-          ++t;
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < RB; ++b) s1[b] += (v[b][0] + v[b][1]) + (v[b][2] + v[b][3]);
   }
 
-  constexpr int E = slab_doubles(RB);
-  publish_slab<RB, NACC>(partial + item * E, acc, s1);
   const int64_t nit = items_of(cnt, chunk);
-  if (!arrive_last(counters + cell, nit)) return;
-
-  // ---- last arriver of this cell: combine, then (cycle variant) the half-spaces ----------
 #pragma unroll
   for (int b = 0; b < RB; ++b) {
-    if (g == 0) shift_lds[16 * b + r] = sh[b];
+    if (w == 0 && g == 0) shift_lds[16 * b + r] = sh[b];
   }
-  __syncthreads();
   const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
   double *mean = out_mean + static_cast<int64_t>(cell) * rows;
   double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
-  reduce_cell<RB>(partial + first * E, nit, cnt, T, shift_lds, S_lds, o0, o1, mean, cov);
-  if (MINK) minkowski_cell(cov, mean, T, cell, mp, lb_s, lane, 64);
+
+  if (nit == 1) {
+    // the whole cell lives in this workgroup: combine in LDS, no global round trip
+    combine_waves<RB, NACC, G::NW>(acc, s1, xch, slab_lds, true);
+    finalize_cell<RB>([&](int e) { return slab_lds[e]; }, cnt, T, shift_lds, S_lds, o0, o1, mean,
+                      cov, mean_lds, COV_IN_LDS ? cov_lds : nullptr);
+  } else {
+    combine_waves<RB, NACC, G::NW>(acc, s1, xch, tree.slabs[0] + blockIdx.x * E, false);
+    auto prefix = [&](int l) -> int64_t { return loc.level_first[l]; };
+    const double *root;
+    int64_t root_n;
+    if (!tree_climb<E>(tree, loc.chunk_idx, nit, prefix, &flag, &root, &root_n)) return;
+    finalize_cell<RB>([&](int e) { return sum_group(root, root_n, E, e); }, cnt, T, shift_lds,
+                      S_lds, o0, o1, mean, cov, mean_lds, COV_IN_LDS ? cov_lds : nullptr);
+  }
+  if (MINK)
+    minkowski_cell(COV_IN_LDS ? cov_lds : cov, mean_lds, T, cell, mp, lb_s, threadIdx.x,
+                   blockDim.x);
 }
 
 template <typename P, int RB, bool MINK>
 static void launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
-                   const int64_t *cnt, int n_cells, int64_t chunk, int64_t items, double *partial,
-                   int32_t *counters, double *mean, double *cov, const MinkParams &mp,
-                   hipStream_t s) {
-  hipLaunchKernelGGL((moments_kernel<P, RB, MINK>), dim3(static_cast<unsigned>(items)), dim3(64),
-                     0, s, pos, ld, T, origin, off, cnt, n_cells, chunk, partial, counters, mean,
-                     cov, mp);
+                   const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
+                   double *cov, const MinkParams &mp, hipStream_t s) {
+  const int64_t wq = store_wave_quota(n_bound);
+  const int64_t items = max_items(n_cells, n_bound, Geo<RB>::NW * wq);
+  const TreeLayout tree = tree_layout(ws, items, n_cells, slab_doubles(RB));
+  hipLaunchKernelGGL((moments_kernel<P, RB, MINK>), dim3(static_cast<unsigned>(items)),
+                     dim3(Geo<RB>::NW * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, wq,
+                     tree, mean, cov, mp);
 }
 
 template <typename P, bool MINK>
 static int dispatch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
-                    const int64_t *cnt, int n_cells, int64_t chunk, int64_t items,
-                    double *partial, int32_t *counters, double *mean, double *cov,
-                    const MinkParams &mp, hipStream_t s) {
+                    const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
+                    double *cov, const MinkParams &mp, hipStream_t s) {
   switch (row_blocks(T)) {
-    case 1: launch<P, 1, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
-    case 2: launch<P, 2, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
-    case 3: launch<P, 3, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
-    case 4: launch<P, 4, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
-    case 5: launch<P, 5, MINK>(pos, ld, T, origin, off, cnt, n_cells, chunk, items, partial, counters, mean, cov, mp, s); break;
+    case 1: launch<P, 1, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
+    case 2: launch<P, 2, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
+    case 3: launch<P, 3, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
+    case 4: launch<P, 4, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
+    case 5: launch<P, 5, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
     default: return CCMPC_ERR_UNSUPPORTED;
   }
   return CCMPC_OK;
@@ -154,22 +208,15 @@ static int run(const void *positions, int dtype, int64_t ld, int64_t T, const do
                const int64_t *cell_off, const int64_t *cell_cnt, int64_t n_cells,
                int64_t n_bound, void *workspace, double *out_mean, double *out_cov,
                const MinkParams &mp, ccmpc_stream_t stream, const char *who) {
-  const int64_t chunk = pick_chunk(n_bound);
-  const int64_t items = max_items(n_cells, n_bound, chunk);
-  int32_t *counters = static_cast<int32_t *>(workspace);
-  double *partial = reinterpret_cast<double *>(static_cast<char *>(workspace) +
-                                               counter_bytes(n_cells));
   hipStream_t s = as_stream(stream);
   const int Ti = static_cast<int>(T), nc = static_cast<int>(n_cells);
   int rc;
   if (dtype == CCMPC_F64)
     rc = dispatch<double, MINK>(static_cast<const double *>(positions), ld, Ti, origin, cell_off,
-                                cell_cnt, nc, chunk, items, partial, counters, out_mean, out_cov,
-                                mp, s);
+                                cell_cnt, nc, n_bound, workspace, out_mean, out_cov, mp, s);
   else
     rc = dispatch<float, MINK>(static_cast<const float *>(positions), ld, Ti, origin, cell_off,
-                               cell_cnt, nc, chunk, items, partial, counters, out_mean, out_cov,
-                               mp, s);
+                               cell_cnt, nc, n_bound, workspace, out_mean, out_cov, mp, s);
   if (rc != CCMPC_OK) {
     set_error(std::string(who) + ": unsupported T");
     return rc;
@@ -189,10 +236,9 @@ using namespace ccmpc;
 extern "C" size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells,
                                                 int64_t n_particles_bound) {
   if (T < 1 || T > kMaxT || n_cells < 0 || n_particles_bound < 0) return 0;
-  const int64_t chunk = pick_chunk(n_particles_bound);
-  const int64_t items = max_items(n_cells, n_particles_bound, chunk);
-  return counter_bytes(n_cells) +
-         static_cast<size_t>(items) * slab_doubles(row_blocks(T)) * sizeof(double);
+  const int rb = row_blocks(T);
+  const int64_t items = max_items(n_cells, n_particles_bound, store_chunk(rb, n_particles_bound));
+  return tree_bytes(items, n_cells, slab_doubles(rb));
 }
 
 #define CHECK_STORE_ARGS()                                                                     \

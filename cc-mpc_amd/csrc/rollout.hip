@@ -145,23 +145,31 @@ __global__ __launch_bounds__(256) void ideal_rollout_kernel(
 
 constexpr int kStageStride = 66;  // doubles per LDS row: bank-conflict-free both ways
 
+__host__ __device__ constexpr int ideal_waves(int rb) { return rb <= 2 ? 4 : 2; }
+
 template <int RB, bool MINK>
-__global__ __launch_bounds__(64) void ideal_gram_kernel(
+__global__ __launch_bounds__(256) void ideal_gram_kernel(
     const double *__restrict__ prev_mean, const double *__restrict__ prev_cov, int T_src,
     const int32_t *__restrict__ src_cell, int T, int64_t n, int64_t chunk, int64_t items_per_cell,
     const double *__restrict__ x0, uint64_t seed, const int32_t *__restrict__ rng_cell,
-    double *__restrict__ partial, int32_t *__restrict__ counters, double *__restrict__ out_mean,
-    double *__restrict__ out_cov, int32_t *__restrict__ out_status, MinkParams mp) {
+    TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
+    int32_t *__restrict__ out_status, MinkParams mp) {
   constexpr int NT = n_tiles(RB);
   constexpr int D = 16 * RB;
   constexpr int E = slab_doubles(RB);
+  constexpr int NW = ideal_waves(RB);
   __shared__ StepPlan plan[40];
-  __shared__ double stage[D * kStageStride];
+  __shared__ double stage_all[NW * D * kStageStride];
+  __shared__ double xch[(NW - 1) * 256 > 64 ? (NW - 1) * 256 : 64];
   __shared__ double shift_s[D];
   __shared__ double S_lds[D];
+  __shared__ double mean_lds[D];
   __shared__ double lb_s[MINK ? 40 * 39 / 2 : 1];
   __shared__ int status_s;
-  const int lane = threadIdx.x;
+  __shared__ int flag;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  double *stage = stage_all + w * D * kStageStride;
   const int64_t item = blockIdx.x;
   const int cell = static_cast<int>(item / items_per_cell);
   const int64_t cidx = item % items_per_cell;
@@ -170,9 +178,9 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
   const double *mu = prev_mean + static_cast<int64_t>(src) * rows_src;
   const double *cv = prev_cov + static_cast<int64_t>(src) * rows_src * rows_src;
   const uint32_t rng = rng_cell ? static_cast<uint32_t>(rng_cell[cell]) : static_cast<uint32_t>(cell);
-  if (lane == 0) status_s = 0;
+  if (threadIdx.x == 0) status_s = 0;
   __syncthreads();
-  for (int t = lane; t < T; t += 64) {
+  for (int t = threadIdx.x; t < T; t += blockDim.x) {
     const int st = build_step(mu, cv, rows_src, t, plan[t]);
     if (st) atomicMin(&status_s, st);
   }
@@ -181,10 +189,10 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
   {
     int st = 0;
     initial_draw(mu, cv, rows_src, x0, cell, rng, seed, x0x, x0y, st);
-    if (st && lane == 0) atomicMin(&status_s, st);
+    if (st && threadIdx.x == 0) atomicMin(&status_s, st);
   }
   // shift = the noise-free path (the rollout's exact mean given x0): same for every item
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     double x = x0x, y = x0y;
     for (int t = 0; t < T; ++t) {
       advance(plan[t], 0.0, 0.0, x, y);
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
     for (int R = rows; R < D; ++R) shift_s[R] = 0.0;
   }
   __syncthreads();
-  if (cidx == 0 && lane == 0 && out_status) out_status[cell] = status_s;
+  if (cidx == 0 && threadIdx.x == 0 && out_status) out_status[cell] = status_s;
 
   d4 acc[1][NT];
 #pragma unroll
@@ -203,9 +211,13 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
 #pragma unroll
   for (int b = 0; b < RB; ++b) s1[b] = 0.0;
   const int r = lane & 15, g = lane >> 4;
-  const int64_t p0 = cidx * chunk;
-  const int64_t p1 = (p0 + chunk < n) ? p0 + chunk : n;
+  const int64_t wq = chunk / NW;  // samples per wave (multiple of 64)
+  const int64_t i0 = cidx * chunk;
+  const int64_t i1 = (i0 + chunk < n) ? i0 + chunk : n;
+  const int64_t p0 = i0 + w * wq;
+  const int64_t p1 = (p0 + wq < i1) ? p0 + wq : i1;
 
+  // the trip count differs between waves only at the tail: keep barriers wave-local
   for (int64_t base = p0; base < p1; base += 64) {
     const int64_t i = base + lane;
     const bool valid = i < p1;
@@ -218,7 +230,8 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
       stage[(2 * t) * kStageStride + lane] = valid ? x - shift_s[2 * t] : 0.0;
       stage[(2 * t + 1) * kStageStride + lane] = valid ? y - shift_s[2 * t + 1] : 0.0;
     }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll 4
     for (int j = 0; j < 16; ++j) {
       double v[RB];
@@ -237,21 +250,26 @@ __global__ __launch_bounds__(64) void ideal_gram_kernel(
           ++t;
         }
     }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // reads done before the next batch overwrites
+    __builtin_amdgcn_wave_barrier();
   }
 
-  publish_slab<RB, 1>(partial + item * E, acc, s1);
-  if (!arrive_last(counters + cell, items_per_cell)) return;
+  combine_waves<RB, 1, NW>(acc, s1, xch, tree.slabs[0] + item * E, false);
+  auto prefix = [&](int l) -> int64_t { return cell * nodes_at(items_per_cell, l); };
+  const double *root;
+  int64_t root_n;
+  if (!tree_climb<E>(tree, cidx, items_per_cell, prefix, &flag, &root, &root_n)) return;
   double *mean = out_mean + static_cast<int64_t>(cell) * rows;
   double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
-  reduce_cell<RB>(partial + cell * items_per_cell * E, items_per_cell, n, T, shift_s, S_lds, 0.0,
-                  0.0, mean, cov);
-  if (MINK) minkowski_cell(cov, mean, T, cell, mp, lb_s, lane, 64);
+  finalize_cell<RB>([&](int e) { return sum_group(root, root_n, E, e); }, n, T, shift_s, S_lds,
+                    0.0, 0.0, mean, cov, mean_lds, nullptr);
+  if (MINK) minkowski_cell(cov, mean_lds, T, cell, mp, lb_s, threadIdx.x, blockDim.x);
 }
 
+// samples per work item (multiple of 256 = 4 waves x 64): >= ~1024 items for 1e6-sample cells
 inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
-  int64_t c = (n_cells * n + 2047) / 2048;
-  c = ((c + 63) / 64) * 64;
+  int64_t c = (n_cells * n + 1023) / 1024;
+  c = ((c + 255) / 256) * 256;
   if (c < 256) c = 256;
   if (c > 16384) c = 16384;
   return c;
@@ -260,14 +278,14 @@ inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
 template <int RB, bool MINK>
 static void launch_ideal_gram(const double *pm, const double *pc, int T_src, const int32_t *src,
                               int n_cells, int T, int64_t n, const double *x0, uint64_t seed,
-                              const int32_t *rng, double *partial, int32_t *counters,
-                              double *out_mean, double *out_cov, int32_t *status,
-                              const MinkParams &mp, hipStream_t s) {
+                              const int32_t *rng, void *ws, double *out_mean, double *out_cov,
+                              int32_t *status, const MinkParams &mp, hipStream_t s) {
   const int64_t chunk = ideal_chunk(n_cells, n);
   const int64_t ipc = (n + chunk - 1) / chunk;
+  const TreeLayout tree = tree_layout(ws, ipc * n_cells, n_cells, slab_doubles(RB));
   hipLaunchKernelGGL((ideal_gram_kernel<RB, MINK>), dim3(static_cast<unsigned>(ipc * n_cells)),
-                     dim3(64), 0, s, pm, pc, T_src, src, T, n, chunk, ipc, x0, seed, rng, partial,
-                     counters, out_mean, out_cov, status, mp);
+                     dim3(64 * ideal_waves(RB)), 0, s, pm, pc, T_src, src, T, n, chunk, ipc, x0,
+                     seed, rng, tree, out_mean, out_cov, status, mp);
 }
 
 template <bool MINK>
@@ -276,17 +294,14 @@ static int run_ideal(const double *prev_mean, const double *prev_cov, int64_t T_
                      const double *x0, uint64_t seed, const int32_t *rng_cell, void *workspace,
                      double *out_mean, double *out_cov, int32_t *out_status, const MinkParams &mp,
                      ccmpc_stream_t stream) {
-  int32_t *counters = static_cast<int32_t *>(workspace);
-  double *partial = reinterpret_cast<double *>(static_cast<char *>(workspace) +
-                                               counter_bytes(n_cells));
   hipStream_t s = as_stream(stream);
   const int nc = static_cast<int>(n_cells), Ti = static_cast<int>(T), Ts = static_cast<int>(T_src);
   switch (row_blocks(T)) {
-    case 1: launch_ideal_gram<1, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
-    case 2: launch_ideal_gram<2, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
-    case 3: launch_ideal_gram<3, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
-    case 4: launch_ideal_gram<4, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
-    case 5: launch_ideal_gram<5, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, partial, counters, out_mean, out_cov, out_status, mp, s); break;
+    case 1: launch_ideal_gram<1, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
+    case 2: launch_ideal_gram<2, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
+    case 3: launch_ideal_gram<3, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
+    case 4: launch_ideal_gram<4, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
+    case 5: launch_ideal_gram<5, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
     default: set_error("ideal moments: unsupported T"); return CCMPC_ERR_UNSUPPORTED;
   }
   CCMPC_LAUNCH_CHECK();
@@ -325,8 +340,7 @@ extern "C" size_t ccmpc_ideal_moments_workspace_bytes(int64_t T, int64_t n_cells
   if (T < 1 || T > kMaxT || n_cells < 0 || n_samples < 1) return 0;
   const int64_t chunk = ideal_chunk(n_cells, n_samples);
   const int64_t items = ((n_samples + chunk - 1) / chunk) * n_cells;
-  return counter_bytes(n_cells) +
-         static_cast<size_t>(items) * slab_doubles(row_blocks(T)) * sizeof(double);
+  return tree_bytes(items, n_cells, slab_doubles(row_blocks(T)));
 }
 
 #define CHECK_IDEAL_ARGS()                                                                     \

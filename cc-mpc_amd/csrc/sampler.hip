@@ -13,10 +13,25 @@
 //
 // The GMM parameters are per (OV, latent, step) -- the decoder's output; the learned encoder /
 // GRU decoder that produce them are upstream of this boundary (absent submodule).
-// Float32 arithmetic throughout, as torch runs it; the noise is drawn in float64 and rounded.
+// Float32 arithmetic throughout, as torch runs it; the noise and the transcendentals are
+// evaluated in float64 and rounded to float32.
 #include "ccmpc_common.hpp"
 
 namespace ccmpc {
+
+// float32 sin/cos/exp evaluated in float64 and rounded once: correctly rounded in practice, so
+// the result does not depend on which libm computes it (the oracle does the same), and the
+// (sin(phi + w dt) - sin(phi)) / w cancellation cannot amplify a 1-ulp libm difference.
+__device__ __forceinline__ void sincos_rn(float a, float &s, float &c) {
+  double sd, cd;
+  sincos(static_cast<double>(a), &sd, &cd);
+  s = static_cast<float>(sd);
+  c = static_cast<float>(cd);
+}
+
+__device__ __forceinline__ float exp_rn(float a) {
+  return static_cast<float>(exp(static_cast<double>(a)));
+}
 
 __device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, float &v, float dphi,
                                               float a, float dt) {
@@ -24,8 +39,8 @@ __device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, fl
   const float w = straight ? 1.0f : dphi;
   const float phi1 = phi + w * dt;
   float s0, c0, s1, c1;
-  sincosf(phi, &s0, &c0);
-  sincosf(phi1, &s1, &c1);
+  sincos_rn(phi, s0, c0);
+  sincos_rn(phi1, s1, c1);
   if (straight) {
     x = x + v * c0 * dt + (a / 2.0f) * c0 * dt * dt;
     y = y + v * s0 * dt + (a / 2.0f) * s0 * dt * dt;
@@ -69,7 +84,7 @@ __global__ __launch_bounds__(256) void sample_unicycle_kernel(
                 STREAM_SAMPLER_EPS, seed, e0d, e1d);
     const float e0 = static_cast<float>(e0d), e1 = static_cast<float>(e1d);
     const float mu0 = g[5 * t], mu1 = g[5 * t + 1];
-    const float s0 = expf(g[5 * t + 2]), s1 = expf(g[5 * t + 3]), rho = g[5 * t + 4];
+    const float s0 = exp_rn(g[5 * t + 2]), s1 = exp_rn(g[5 * t + 3]), rho = g[5 * t + 4];
     const float dphi = mu0 + s0 * e0;
     const float acc = (mu1 + (s1 * rho) * e0) + (s1 * sqrtf(1.0f - rho * rho)) * e1;
     unicycle_step(x, y, phi, v, dphi, acc, dt);

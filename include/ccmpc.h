@@ -105,13 +105,13 @@ const char *ccmpc_status_string(int status);
  *   cross_cov[t][tau] = block (t, tau)).
  * out_mean[c][t][2] (origin added back for F32), out_cov[c][2T][2T] (ddof = 1, symmetric).
  * n_particles_bound >= sum(cell_cnt) sizes the grid, so counts may be produced on the device.
- * T <= 40.  ONE kernel launch: per-chunk partial Gram sums are combined by the last-arriving
- * workgroup of each cell in a fixed order (deterministic, no float atomics).
+ * T <= 40.  ONE kernel launch: per-chunk partial Gram sums are combined in-launch through a
+ * fixed fan-in-16 tree of arrival counters (the last arriver of each group combines it), so
+ * the result is deterministic and uses no float atomics.
  *
- * Workspace contract (every *_workspace_bytes-sized workspace): its first
- * round_up(4 * n_cells, 256) bytes are per-cell arrival counters.  They must be ZERO before
- * the first call on a fresh workspace (hipMemset once after allocating); every call leaves
- * them zero again.  Do not share one workspace between concurrently running streams.
+ * Workspace contract (every *_workspace_bytes-sized workspace): its head holds the tree's
+ * arrival counters.  Zero-fill a fresh workspace ONCE (hipMemset after allocating); every call
+ * leaves the counters zero again.  Do not share one workspace between concurrent streams.
  * ------------------------------------------------------------------------------------- */
 size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_particles_bound);
 int ccmpc_moments(const void *positions, int dtype, int64_t ld, int64_t T,
@@ -223,6 +223,30 @@ int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf, in
                           const float *gmm, int64_t n_ov, int64_t N, int64_t T, double dt,
                           uint64_t seed, int32_t *out_z, float *out_pos, int64_t ld,
                           ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Particle bucketing by latent mode: make_ovehicles (v8ideal/__init__.py:469-505) +
+ * OVehicle.from_trajectron (ovehicle.py:24-117) on the sampler's sample-order store.
+ *  keep_map[o][L]   kept-mode index of each latent value, -1 if p(z|x) <= filter (host decides;
+ *                   latent_probs are host data); n_kept[o] >= 1 (the reference cannot regroup
+ *                   into zero modes); cell_base[o] = first global cell of OV o
+ *  minpos[o][2]     scene origin added in float64 to the float32 predictions (:486)
+ *  region[o]        first slot of OV o's region in pos_out (4-aligned; each region needs
+ *                   N + 4 * n_kept[o] slots)
+ *  out: pos_out     F32 store (origin = minpos), cells in (ov, kept mode) order, each cell's
+ *                   particles in the reference's order (native mode in sample order, then the
+ *                   regrouped rare modes in ascending latent order, each in sample order)
+ *       cell_off/cell_cnt [n_cells], cell_pmf = N_k / N, init_center [n_cells][2] (world)
+ * Rare particles go to the kept mode whose centre (mean final position) is nearest, first
+ * index on ties (scipy.spatial.distance_matrix + np.argmin).  Deterministic.
+ * ------------------------------------------------------------------------------------- */
+size_t ccmpc_bucket_workspace_bytes(int64_t n_ov, int64_t N, int64_t n_latent, int64_t max_k);
+int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T, int64_t n_ov,
+                 int64_t N, int64_t n_latent, const int32_t *keep_map, const int32_t *n_kept,
+                 const int32_t *cell_base, int64_t max_k, const double *minpos,
+                 const int64_t *region, void *workspace, size_t workspace_bytes, float *pos_out,
+                 int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
+                 double *init_center, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Headings, bounding-box vertices and L4 outer approximation for every (cell, t).

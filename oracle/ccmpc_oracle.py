@@ -175,7 +175,7 @@ def from_trajectron(T, past, latent_pmf, predictions, filter_pmf=FILTER_PMF,
         yaws_list.append(_step_yaws(ps, pos_last, T))
         total += ps.shape[0]
         centres[j] = np.mean(ps[:, T - 1], axis=0)
-    rare = np.arange(n_states)[np.in1d(np.arange(n_states), keep, invert=True)]
+    rare = np.arange(n_states)[np.isin(np.arange(n_states), keep, invert=True)]
     for zv in rare:
         ps = predictions[zv]
         if ps.size == 0:
@@ -493,16 +493,22 @@ def predict_ideal(moments, n_states, T, n_samples, x0s=None, Zs=None, seed=0):
 # Trajectron++ GMM-latent sampler (absent submodule; restated from upstream semantics)
 # PARITY UNPINNED: no reference test or fixture covers these internals.
 # ----------------------------------------------------------------------------------------
+def _rn32(fn, x):
+    """float32 transcendental evaluated in float64 and rounded once (as the kernel does)."""
+    return fn(np.asarray(x, np.float64)).astype(np.float32)
+
+
 def unicycle_step(x, y, phi, v, dphi, a, dt):
     """Trajectron++ Unicycle.dynamic: exact integration at constant (dphi, a); straight-line
-    branch when |dphi| <= 1e-2 (float32 throughout, as torch runs it)."""
+    branch when |dphi| <= 1e-2 (float32 throughout, as torch runs it; sin/cos rounded from
+    float64)."""
     f = np.float32
     dt = f(dt)
     straight = np.abs(dphi) <= f(1e-2)
     w = np.where(straight, f(1.0), dphi).astype(f)
     phi1 = (phi + w * dt).astype(f)
-    s0, c0 = np.sin(phi).astype(f), np.cos(phi).astype(f)
-    s1, c1 = np.sin(phi1).astype(f), np.cos(phi1).astype(f)
+    s0, c0 = _rn32(np.sin, phi), _rn32(np.cos, phi)
+    s1, c1 = _rn32(np.sin, phi1), _rn32(np.cos, phi1)
     dsin = ((s1 - s0) / w).astype(f)
     dcos = ((c1 - c0) / w).astype(f)
     aw = (a / w).astype(f)
@@ -542,7 +548,7 @@ def sample_unicycle(init_state, latent_cdf, gmm, n, T, dt, seed, ov=0):
         e0, e1 = philox.normal_pair(idx, t, ov, philox.STREAM_SAMPLER_EPS, seed)
         e0, e1 = e0.astype(f), e1.astype(f)
         p = g[z, t]
-        s0, s1, rho = np.exp(p[:, 2]), np.exp(p[:, 3]), p[:, 4]
+        s0, s1, rho = _rn32(np.exp, p[:, 2]), _rn32(np.exp, p[:, 3]), p[:, 4]
         dphi = p[:, 0] + s0 * e0
         acc = p[:, 1] + (s1 * rho) * e0 + (s1 * np.sqrt(f(1) - rho * rho)) * e1
         x, y, phi, v = unicycle_step(x, y, phi, v, dphi.astype(f), acc.astype(f), dt)
