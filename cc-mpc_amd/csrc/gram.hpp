@@ -3,8 +3,8 @@
 // combine tree across workgroups, and the per-cell finalisation.
 //
 // Slab layout (one per work item / tree node): NT = RB(RB+1)/2 tiles of the f64 16x16x4 MFMA
-// C layout (entry (tile, reg, lane) <-> row (lane>>4) + 4 reg, col lane&15 of tile (bi, bj)),
-// then RB*16 shifted row sums.
+// C layout, lane-major (entry t*256 + 4 lane + reg <-> row (lane>>4) + 4 reg, col lane&15 of
+// tile (bi, bj)), then RB*16 shifted row sums; every access is a 16-byte pair.
 //
 // Cross-workgroup hand-off (MI355X_MICROARCH.md "Valid forms", first table row; guide §6 G16):
 // every slab store is an agent-scope write-through (sc1) store, every storing wave drains with
@@ -152,16 +152,37 @@ __device__ __forceinline__ void load4<float>(const float *__restrict__ p, double
   v[3] = a.w;
 }
 
-__device__ __forceinline__ void st_sc1(double *p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p),
-                     static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+// 16-byte write-through (sc1) buffer accesses: one dwordx4 transaction per lane instead of two
+// 8-byte atomic-typed ones.
+// aux = 16 selects sc1 on gfx950; word 3 = 0x00020000 is the raw-buffer format for gfx9.
+typedef unsigned int b128_t __attribute__((__vector_size__(16)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const double *base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-__device__ __forceinline__ double ld_sc1(const double *p) {
-  return __longlong_as_double(static_cast<long long>(__hip_atomic_load(
-      reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
-      __HIP_MEMORY_SCOPE_AGENT)));
+__device__ __forceinline__ void st2_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, double a,
+                                        double b) {
+  const double2 v = {a, b};
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128_t, v), r, byte_off, 0, 16);
+}
+
+__device__ __forceinline__ double2 ld2_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
+}
+
+// Slab entry order: tile t, lane l, register k at t*256 + 4 l + k (lane-major, so a lane's 4
+// accumulators are two 16-byte stores); then the RB*16 row sums.
+__device__ __forceinline__ void decode_entry(int e, int RB, int &i, int &j) {
+  const int tile = e >> 8, l = (e >> 2) & 63, k = e & 3;
+  const int row = (l >> 4) + 4 * k, col = l & 15;
+  int bi = 0, t = tile;
+  while (t >= RB - bi) {
+    t -= RB - bi;
+    ++bi;
+  }
+  i = 16 * bi + row;
+  j = 16 * (bi + t) + col;
 }
 
 // Combine the NW waves' accumulators in a fixed order (wave 0 + 1 + ... + NW-1), tile by tile
@@ -174,6 +195,7 @@ __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)]
                                               bool to_lds) {
   constexpr int NT = n_tiles(RB);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(dst);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     d4 s = acc[0][t];
@@ -186,15 +208,20 @@ __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)]
       __syncthreads();
     }
     if (w == 0) {
+      double v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        double v = s[k];
+        v[k] = s[k];
 #pragma unroll
-        for (int o = 0; o < NW - 1; ++o) v += xch[o * 256 + k * 64 + lane];
-        if (to_lds)
-          dst[t * 256 + k * 64 + lane] = v;
-        else
-          st_sc1(dst + t * 256 + k * 64 + lane, v);
+        for (int o = 0; o < NW - 1; ++o) v[k] += xch[o * 256 + k * 64 + lane];
+      }
+      const int e = t * 256 + 4 * lane;
+      if (to_lds) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[e + k] = v[k];
+      } else {
+        st2_sc1(rs, 8 * e, v[0], v[1]);
+        st2_sc1(rs, 8 * (e + 2), v[2], v[3]);
       }
     }
     if (NW > 1) __syncthreads();
@@ -206,14 +233,20 @@ __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)]
     x += __shfl_xor(x, 32, 64);
     if (lane < 16) xch[w * 16 + lane] = x;
     __syncthreads();
-    if (w == 0 && lane < 16) {
-      double v = xch[lane];
+    if (w == 0 && lane < 8) {
+      double v0 = xch[2 * lane], v1 = xch[2 * lane + 1];
 #pragma unroll
-      for (int o = 1; o < NW; ++o) v += xch[o * 16 + lane];
-      if (to_lds)
-        dst[NT * 256 + b * 16 + lane] = v;
-      else
-        st_sc1(dst + NT * 256 + b * 16 + lane, v);
+      for (int o = 1; o < NW; ++o) {
+        v0 += xch[o * 16 + 2 * lane];
+        v1 += xch[o * 16 + 2 * lane + 1];
+      }
+      const int e = NT * 256 + b * 16 + 2 * lane;
+      if (to_lds) {
+        dst[e] = v0;
+        dst[e + 1] = v1;
+      } else {
+        st2_sc1(rs, 8 * e, v0, v1);
+      }
     }
     __syncthreads();
   }
@@ -292,19 +325,23 @@ inline TreeLayout tree_layout(void *ws, int64_t max_items, int64_t n_cells, int 
   return L;
 }
 
-// Sum entry e over n <= kFanIn consecutive slabs: all loads issued first (indices clamped, no
-// per-load branch), then a fixed-order sum.
-__device__ __forceinline__ double sum_group(const double *__restrict__ slab0, int64_t n, int E,
-                                            int e) {
-  double v[kFanIn];
+// Sum the entry pair (e, e+1), e even, over n <= kFanIn consecutive slabs: all 16-byte sc1 loads
+// issued first (indices clamped, no per-load branch), then a fixed-order sum.
+__device__ __forceinline__ double2 sum_group2(const double *__restrict__ slab0, int64_t n, int E,
+                                              int e) {
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(slab0);
+  double2 v[kFanIn];
 #pragma unroll
   for (int i = 0; i < kFanIn; ++i) {
-    const int64_t j = i < n ? i : n - 1;
-    v[i] = ld_sc1(slab0 + j * E + e);
+    const int j = static_cast<int>(i < n ? i : n - 1);
+    v[i] = ld2_sc1(rs, 8 * (j * E + e));
   }
-  double s = v[0];
+  double2 s = v[0];
 #pragma unroll
-  for (int i = 1; i < kFanIn; ++i) s += (i < n) ? v[i] : 0.0;
+  for (int i = 1; i < kFanIn; ++i) {
+    s.x += (i < n) ? v[i].x : 0.0;
+    s.y += (i < n) ? v[i].y : 0.0;
+  }
   return s;
 }
 
@@ -327,8 +364,11 @@ __device__ bool tree_climb(const TreeLayout &L, int64_t idx, int64_t nit, Prefix
       return true;
     }
     double *parent = L.slabs[l + 1] + (pre_up + grp) * E;
-    for (int e = threadIdx.x; e < E; e += blockDim.x)
-      st_sc1(parent + e, sum_group(children, gsize, E, e));
+    const __amdgpu_buffer_rsrc_t rp = slab_rsrc(parent);
+    for (int e = 2 * threadIdx.x; e < E; e += 2 * blockDim.x) {
+      const double2 s = sum_group2(children, gsize, E, e);
+      st2_sc1(rp, 8 * e, s.x, s.y);
+    }
     idx = grp;
     n_l = ceil_div(n_l, kFanIn);
   }
@@ -349,30 +389,37 @@ __device__ void finalize_cell(Reader rd, int64_t cnt, int T, const double *shift
   const int tid = threadIdx.x, nth = blockDim.x;
   const int rows = 2 * T;
   const double n = static_cast<double>(cnt);
-  for (int r = tid; r < D; r += nth) S_lds[r] = r < rows ? rd(NT * 256 + r) : 0.0;
+  // rd(e) returns the summed entry pair (e, e+1), e even
+  for (int r = 2 * tid; r < D; r += 2 * nth) {
+    const double2 s = r < rows ? rd(NT * 256 + r) : double2{0.0, 0.0};
+    S_lds[r] = s.x;
+    S_lds[r + 1] = s.y;
+  }
   __syncthreads();
   for (int r = tid; r < rows; r += nth) {
     const double m = (shift_lds[r] + S_lds[r] / n) + ((r & 1) ? o1 : o0);
     mean[r] = m;
     if (mean_lds) mean_lds[r] = m;
   }
-  for (int e = tid; e < NT * 256; e += nth) {
-    const int tile = e >> 8, k = (e >> 6) & 3, l = e & 63;
-    const int row = (l >> 4) + 4 * k, col = l & 15;
-    int bi = 0, t = tile;
-    while (t >= RB - bi) {
-      t -= RB - bi;
-      ++bi;
-    }
-    const int bj = bi + t;
-    const int i = 16 * bi + row, j = 16 * bj + col;
-    if (i >= rows || j >= rows || i > j) continue;  // one value per symmetric pair
-    const double c = (rd(e) - S_lds[i] * S_lds[j] / n) / (n - 1.0);
-    cov[i * rows + j] = c;
-    cov[j * rows + i] = c;
-    if (cov_lds) {
-      cov_lds[i * rows + j] = c;
-      cov_lds[j * rows + i] = c;
+  for (int e = 2 * tid; e < NT * 256; e += 2 * nth) {
+    int i0, j0, i1, j1;
+    decode_entry(e, RB, i0, j0);
+    decode_entry(e + 1, RB, i1, j1);
+    const bool use0 = i0 < rows && j0 < rows && i0 <= j0;  // one value per symmetric pair
+    const bool use1 = i1 < rows && j1 < rows && i1 <= j1;
+    if (!use0 && !use1) continue;
+    const double2 g = rd(e);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!(h ? use1 : use0)) continue;
+      const int i = h ? i1 : i0, j = h ? j1 : j0;
+      const double c = ((h ? g.y : g.x) - S_lds[i] * S_lds[j] / n) / (n - 1.0);
+      cov[i * rows + j] = c;
+      cov[j * rows + i] = c;
+      if (cov_lds) {
+        cov_lds[i * rows + j] = c;
+        cov_lds[j * rows + i] = c;
+      }
     }
   }
   __syncthreads();

@@ -160,15 +160,16 @@ __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void
   if (nit == 1) {
     // the whole cell lives in this workgroup: combine in LDS, no global round trip
     combine_waves<RB, NACC, G::NW>(acc, s1, xch, slab_lds, true);
-    finalize_cell<RB>([&](int e) { return slab_lds[e]; }, cnt, T, shift_lds, S_lds, o0, o1, mean,
-                      cov, mean_lds, COV_IN_LDS ? cov_lds : nullptr);
+    finalize_cell<RB>([&](int e) { return double2{slab_lds[e], slab_lds[e + 1]}; }, cnt, T,
+                      shift_lds, S_lds, o0, o1, mean, cov, mean_lds,
+                      COV_IN_LDS ? cov_lds : nullptr);
   } else {
     combine_waves<RB, NACC, G::NW>(acc, s1, xch, tree.slabs[0] + blockIdx.x * E, false);
     auto prefix = [&](int l) -> int64_t { return loc.level_first[l]; };
     const double *root;
     int64_t root_n;
     if (!tree_climb<E>(tree, loc.chunk_idx, nit, prefix, &flag, &root, &root_n)) return;
-    finalize_cell<RB>([&](int e) { return sum_group(root, root_n, E, e); }, cnt, T, shift_lds,
+    finalize_cell<RB>([&](int e) { return sum_group2(root, root_n, E, e); }, cnt, T, shift_lds,
                       S_lds, o0, o1, mean, cov, mean_lds, COV_IN_LDS ? cov_lds : nullptr);
   }
   if (MINK)
