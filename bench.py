@@ -13,6 +13,7 @@ Multi-GPU (torchrun, one process per GPU): every rank plans its own independent 
 wall time.  Rank 0 prints ONE JSON line.
 """
 import argparse
+import glob
 import json
 import os
 import statistics
@@ -67,10 +68,14 @@ def sweep(dev, seed):
         store = engine.ParticleStore.from_cells(cells, device=dev)
         cyc = cycle.MinkowskiCycle(store, K, refs[0])
         t = time_kernel_live(cyc.run, dev, per_graph=10, replays=5)
+        tm = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev,
+                              per_graph=10, replays=5)
         b = int(sum(store.counts)) * 2 * T * 8
         rows.append({"config": name, "particles": int(sum(store.counts)), "T": T,
                      "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
-                     "alg_GBps": round(b / t / 1e9, 1), "frac": round(b / t / HBM_PEAK, 4)})
+                     "alg_GBps": round(b / t / 1e9, 1), "frac": round(b / t / HBM_PEAK, 4),
+                     "moments_only_us": round(tm * 1e6, 2),
+                     "moments_only_frac": round(b / tm / HBM_PEAK, 4)})
         del store, cyc
     # shrinking-horizon step: 1e6-sample ideal rollout fused with moments + half-spaces
     ovs, ref, _ = synthetic.scene(seed + 7, O=1, N=100000, T=8, K=2)
@@ -176,6 +181,44 @@ def cpu_baseline(ovs, ref, T, cycles):
     return best
 
 
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/<round>/summary.json, written by profiles/collect.sh on this same default
+    workload: FETCH_SIZE x2 (gfx950) + WRITE_SIZE).  None when no summary is committed."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")))
+    for path in reversed(paths):
+        with open(path) as f:
+            summ = json.load(f)
+        for name, d in summ.items():
+            if name.startswith(kernel_prefix) and "hbm_bytes_avg" in d:
+                return int(d["hbm_bytes_avg"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def pcie_inclusive(cyc, dev, iters=200):
+    """Cycles/s when the boundary is handed HOST particles: pinned H2D of the whole particle
+    store, the captured cycle, pinned D2H of every record; synchronised per cycle (the planner
+    needs the records before its QP).  Reported beside `value`, never as it."""
+    host_pos = torch.empty(cyc.store.pos.shape, dtype=cyc.store.pos.dtype, pin_memory=True)
+    host_pos.copy_(cyc.store.pos)
+    host_rec = torch.empty(cyc.rec.shape, dtype=cyc.rec.dtype, pin_memory=True)
+    for _ in range(5):
+        cyc.store.pos.copy_(host_pos, non_blocking=True)
+        cyc.replay()
+        host_rec.copy_(cyc.rec, non_blocking=True)
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        cyc.store.pos.copy_(host_pos, non_blocking=True)
+        cyc.replay()
+        host_rec.copy_(cyc.rec, non_blocking=True)
+        torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / iters
+    return {"cycles_per_s": round(1.0 / dt, 1), "us_per_cycle": round(dt * 1e6, 2),
+            "h2d_bytes": host_pos.numel() * host_pos.element_size(),
+            "d2h_bytes": host_rec.numel()}
+
+
 def main():
     args = parse()
     world, rank, local = init_dist(args)
@@ -213,6 +256,8 @@ def main():
     t_kernel = time_kernel_live(cyc.run, dev)
     t_mom = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev)
 
+    pcie = pcie_inclusive(cyc, dev)
+    traffic, traffic_src = pmc_traffic("void ccmpc::moments_kernel<double, 1, true>")
     value = world * args.steps / elapsed
     out = {
         "metric": METRIC,
@@ -235,6 +280,7 @@ def main():
             "cells": store.n_cells, "halfspaces_per_cycle": cyc.n_constraints,
         },
         "constraints_per_s": round(value * cyc.n_constraints, 1),
+        "pcie_inclusive": pcie,
         "roofline": {
             "bound": "hbm",
             "kernel": "moments_kernel<double,1,true> (ccmpc_minkowski_cycle: MFMA Gram + "
@@ -243,7 +289,8 @@ def main():
             "peak": HBM_PEAK / 1e9,
             "unit": "GB/s",
             "frac": round(alg_bytes / t_kernel / HBM_PEAK, 5),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "alg_bytes_per_launch": alg_bytes,
             "avg_launch_us": round(t_kernel * 1e6, 3),
             "moments_only_avg_launch_us": round(t_mom * 1e6, 3),

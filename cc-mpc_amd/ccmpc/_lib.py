@@ -67,8 +67,8 @@ SIGNATURES = {
     "ccmpc_ideal_minkowski_cycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _U64,
                                                    _P, _P, _SZ, _P, _P, _P, _D, _D, _I32, _P,
                                                    _P, _P, _P, _P, _P]),
-    "ccmpc_sample_unicycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _D, _U64, _P,
-                                             _P, _I64, _P]),
+    "ccmpc_sample_unicycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _D, _U64, _I64,
+                                             _P, _P, _I64, _P]),
     "ccmpc_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "ccmpc_bucket": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _I64, _P,
                                     _P, _P, _SZ, _P, _I64, _P, _P, _P, _P, _P]),

@@ -1,0 +1,59 @@
+"""Multi-GPU layout of the path: one process per GPU, scenes sharded.
+
+Cells (scene, OV, mode) are independent, so a node runs the path as weak-scaled shards:
+
+* ``scene_range`` gives each rank a contiguous block of scenes; particles are sampled, bucketed,
+  reduced and turned into half-spaces on the rank that owns the scene and never leave its HBM.
+* RNG streams are keyed by the GLOBAL cell id (``rng_cell`` of ccmpc_ideal_rollout /
+  ccmpc_ideal_moments, the sampler's OV index), so every cell's draws -- and therefore every
+  record -- are identical at 1, 2, 4 or 8 ranks.
+* The planner's QP for a scene stays on the owning rank (v8ideal/__init__.py:2934-2976 solves
+  one scene per agent), so the data path has NO collective.  ``gather_records`` is the one
+  optional exchange, for a consumer that wants every scene's fixed-size half-space records on
+  every rank (a fleet-level monitor, or a rank-0 logger): one all_gather of the padded record
+  block, which RCCL runs over xGMI on a GPU node and gloo runs on the CPU in the tests.
+"""
+import torch
+
+REC_BYTES = 128
+
+
+def scene_range(n_scenes, rank, world):
+    """[begin, end) of the scenes owned by `rank`: contiguous blocks, sizes differ by <= 1."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    base, extra = divmod(int(n_scenes), world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def global_cell_ids(cells_per_scene, begin, end):
+    """Global ids of the cells of scenes [begin, end), given every scene's cell count (the
+    cells of scene s are numbered after those of scenes < s)."""
+    first = sum(int(c) for c in cells_per_scene[:begin])
+    n = sum(int(c) for c in cells_per_scene[begin:end])
+    return list(range(first, first + n))
+
+
+def gather_records(rec, group=None):
+    """All-gather every rank's record block.
+
+    rec: uint8 tensor (n_local, P, 128) on this rank's device (CPU under gloo).  Ranks may hold
+    different numbers of cells; blocks are padded to the largest and trimmed after the
+    exchange.  Returns the (sum n, P, 128) block in rank order, i.e. the global cell order of
+    contiguous ``scene_range`` shards.
+    """
+    import torch.distributed as dist
+    if rec.dtype != torch.uint8 or rec.dim() != 3 or rec.shape[2] != REC_BYTES:
+        raise ValueError("rec must be a uint8 (cells, P, 128) record block")
+    world = dist.get_world_size(group)
+    n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=rec.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    counts = [int(x.item()) for x in ns]
+    cap = max(counts)
+    padded = rec.new_zeros((cap,) + tuple(rec.shape[1:]))
+    padded[: rec.shape[0]] = rec
+    out = [torch.empty_like(padded) for _ in range(world)]
+    dist.all_gather(out, padded.contiguous(), group=group)
+    return torch.cat([o[:c] for o, c in zip(out, counts)], dim=0)

@@ -235,8 +235,9 @@ def l4(store, past_last, bbox, with_yaw=False, with_vertices=False):
     return out
 
 
-def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="cuda"):
+def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="cuda", ov_base=0):
     """GMM-latent particle sampler.  init_state (O,4), latent_pmf (O,L), gmm (O,L,T,5).
+    ov_base = global id of the first OV (keys the RNG streams; see ccmpc.dist).
     Returns (z [O,N] int32, F32 ParticleStore in sample order: one cell per OV)."""
     lib = _lib.load()
     dev = require_device(device)
@@ -252,7 +253,8 @@ def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="c
     t_cdf = torch.as_tensor(cdf, device=dev)
     t_gmm = torch.as_tensor(gmm, device=dev)
     _lib.check(lib.ccmpc_sample_unicycle(_p(t_init), _p(t_cdf), L, _p(t_gmm), O, N, T, float(dt),
-                                         int(seed) & (2**64 - 1), _p(z), _p(store.pos), store.ld,
+                                         int(seed) & (2**64 - 1), int(ov_base), _p(z),
+                                         _p(store.pos), store.ld,
                                          _stream()), "ccmpc_sample_unicycle")
     store._keepalive = (t_init, t_cdf, t_gmm)
     return z, store

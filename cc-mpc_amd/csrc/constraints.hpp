@@ -79,12 +79,14 @@ __device__ bool compute_mvoe(const M2 &S1, const M2 &S2, double tol, int maxiter
     l1 = half_tr;
     l2 = half_tr;
   }
+  // beta' = sqrt(sum 1/w / sum l/w), w = 1 + beta l  ==  sqrt((w1 + w2) / (l1 w2 + l2 w1)):
+  // the same fixed point with one division per iteration instead of five (the iteration is a
+  // serial chain per record, so the division latency is the tail's critical path).  Rounding
+  // differs from the reference's order by ~1 ulp per step; the contraction damps it.
   double b = 1.0;
   for (int it = 0; it < maxiter; ++it) {
     const double w1 = 1.0 + b * l1, w2 = 1.0 + b * l2;
-    const double num = 1.0 / w1 + 1.0 / w2;
-    const double den = l1 / w1 + l2 / w2;
-    const double bn = sqrt(num / den);
+    const double bn = sqrt((w1 + w2) / (l1 * w2 + l2 * w1));
     const bool done = fabs(bn - b) < tol;
     b = bn;
     if (done) break;
@@ -138,6 +140,13 @@ __device__ double minkowski_pair(const double *C, const double *mu, const double
   bool ok = inv2(c_tau, inv_tau);
   const M2 cov_mu = mul(mul(c_x, inv_tau), c_xT);
   const M2 cov_infer = sub(c_t, cov_mu);
+  // compute_lower_bound (makeconstraint.py:282-303): independent of the MVOE chain, so it is
+  // issued first and its sqrt/div latency overlaps the setup of the first MVOE
+  const double root_t = sqrt(fro(c_t));
+  const double al = sqrt(fro(cov_infer)) / root_t;
+  const double be = sqrt(fro(cov_mu)) / root_t;
+  const double x = gamma * (1.0 - al) / be;
+  const double lb = -expm1(-0.5 * (x * x));
   // two MVOE calls (:915, :917-918)
   double b1 = NAN, b2 = NAN;
   M2 Q = {NAN, NAN, NAN, NAN}, QR = {NAN, NAN, NAN, NAN};
@@ -168,12 +177,6 @@ __device__ double minkowski_pair(const double *C, const double *mu, const double
     d = which ? d2 : d1;
     side = (n0 * m0 + n1 * m1 <= d) ? 1 : -1;  // (:926) n.mean <= d  ->  n.x >= d
   }
-  // compute_lower_bound (makeconstraint.py:282-303)
-  const double root_t = sqrt(fro(c_t));
-  const double al = sqrt(fro(cov_infer)) / root_t;
-  const double be = sqrt(fro(cov_mu)) / root_t;
-  const double x = gamma * (1.0 - al) / be;
-  const double lb = -expm1(-0.5 * (x * x));
   if (h.status == 0 && !(isfinite(d) && isfinite(Q.a) && isfinite(QR.a) && isfinite(m0)))
     h.status = CCMPC_REC_NONFINITE;
   h.n0 = n0;
@@ -195,17 +198,14 @@ __device__ double minkowski_pair(const double *C, const double *mu, const double
   return lb;
 }
 
-// All pairs of one cell by the threads [0, nthreads) of the calling group; lb_s has room for
+// All pairs of one cell by the threads [0, nthreads) of the calling group, with the cell's
+// reference trajectory `ref` ([T][2]) and risk constants already at hand; lb_s has room for
 // T(T-1)/2 doubles.  Includes the barrier needed before the per-t minimum.
 __device__ void minkowski_cell(const double *C, const double *mu, int T, int cell,
+                               const double *ref, double chi_r, double chi_p, double gamma,
                                const MinkParams &mp, double *lb_s, int tid, int nthreads) {
   const int rows = 2 * T;
   const int P = T * (T - 1) / 2;
-  const int rsel = mp.cell_ref ? mp.cell_ref[cell] : 0;
-  const double *ref = mp.ref_traj + static_cast<int64_t>(rsel) * rows;
-  const double chi_r = mp.cell_risk[3 * cell + 0];
-  const double chi_p = mp.cell_risk[3 * cell + 1];
-  const double gamma = mp.cell_risk[3 * cell + 2];
   for (int p = tid; p < P; p += nthreads) {
     int t, tau;
     pair_of(p, t, tau);
@@ -220,6 +220,15 @@ __device__ void minkowski_cell(const double *C, const double *mu, int T, int cel
     for (int tau = 0; tau < t; ++tau) v = fmin(v, lb_s[t * (t - 1) / 2 + tau]);
     mp.out_prob_lower[static_cast<int64_t>(cell) * T + t] = v;
   }
+}
+
+// Same, reading the reference trajectory and risk constants from global memory.
+__device__ void minkowski_cell(const double *C, const double *mu, int T, int cell,
+                               const MinkParams &mp, double *lb_s, int tid, int nthreads) {
+  const int rsel = mp.cell_ref ? mp.cell_ref[cell] : 0;
+  const double *ref = mp.ref_traj + static_cast<int64_t>(rsel) * (2 * T);
+  minkowski_cell(C, mu, T, cell, ref, mp.cell_risk[3 * cell + 0], mp.cell_risk[3 * cell + 1],
+                 mp.cell_risk[3 * cell + 2], mp, lb_s, tid, nthreads);
 }
 
 }  // namespace ccmpc

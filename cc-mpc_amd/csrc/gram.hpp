@@ -42,13 +42,18 @@ struct Geo {
   static constexpr int MIN_WAVES_PER_SIMD = RB == 1 ? 4 : 2;
 };
 
-inline int waves_per_item(int rb) { return rb <= 2 ? 4 : 8; }
+// log2 of the particles per wave.  Small inputs are latency-bound: 64 per wave spreads the
+// MFMA work over many CUs.  Large inputs are bandwidth-bound: 256 per wave means fewer slabs
+// and a shallower tree.  (64 at RB >= 3 balances the f64 matrix pipes better per wave but
+// pays the per-workgroup combine ~3x more often: C5 went from 94 to 134 us.)
+inline int store_lg_wave_quota(int /*rb*/, int64_t n_bound) {
+  return n_bound <= (int64_t(1) << 18) ? 6 : 8;
+}
 
-// particles per wave: 64 while the whole input is small enough to be latency-bound
-inline int64_t store_wave_quota(int64_t n_bound) { return n_bound <= (int64_t(1) << 18) ? 64 : 256; }
+inline int lg_waves_per_item(int rb) { return rb <= 2 ? 2 : 3; }
 
-inline int64_t store_chunk(int rb, int64_t n_bound) {
-  return waves_per_item(rb) * store_wave_quota(n_bound);
+inline int store_lg_chunk(int rb, int64_t n_bound) {
+  return lg_waves_per_item(rb) + store_lg_wave_quota(rb, n_bound);
 }
 
 inline int64_t max_items(int64_t n_cells, int64_t n_bound, int64_t chunk) {
@@ -57,49 +62,57 @@ inline int64_t max_items(int64_t n_cells, int64_t n_bound, int64_t chunk) {
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// items of a cell: at least one, so an empty cell is still finalised (to NaN, as np.cov does)
-__device__ __forceinline__ int64_t items_of(int64_t n, int64_t chunk) {
-  return n > 0 ? ceil_div(n, chunk) : 1;
+// items of a cell: at least one, so an empty cell is still finalised (to NaN, as np.cov does).
+// Chunks are powers of two, so this is a shift (a 64-bit division by a runtime value costs
+// ~100 instructions, and locate_item ran it per tree level).
+__device__ __forceinline__ int32_t items_of(int64_t n, int lg_chunk) {
+  return n > 0 ? static_cast<int32_t>((n + (int64_t(1) << lg_chunk) - 1) >> lg_chunk) : 1;
 }
 
 constexpr int kFanIn = 16;
+constexpr int kLgFanIn = 4;
 constexpr int kMaxLevels = 6;  // combine-tree depth bound: 16^6 items per cell
 
 struct ItemLoc {
   int cell;
-  int64_t chunk_idx, first, cnt, off;
-  int64_t level_first[kMaxLevels + 1];  // index of the cell's first node at each tree level
+  int32_t ref_sel;  // cell_ref[cell] (0 when no table is given)
+  int32_t chunk_idx;
+  int64_t cnt, off;
+  int32_t level_first[kMaxLevels + 1];  // index of the cell's first node at each tree level
 };
 
 // Item id -> (cell, chunk index, cell count, cell offset, and the cell's first node at every
-// level of the combine tree): one wave-parallel scan over the cells, so everything the item
-// needs arrives with a single memory round trip.  False for ids past the last item (the grid
-// is sized by an upper bound).
-__device__ __forceinline__ bool locate_item(int64_t item, const int64_t *__restrict__ cnt,
+// level of the combine tree): one wave-parallel scan over the cells in 32-bit item arithmetic
+// (items and nodes < 2^31: the grid is sized by them), so everything the item needs arrives
+// with a single memory round trip.  False for ids past the last item (the grid is sized by an
+// upper bound).
+__device__ __forceinline__ bool locate_item(int32_t item, const int64_t *__restrict__ cnt,
                                             const int64_t *__restrict__ off, int n_cells,
-                                            int64_t chunk, ItemLoc &loc) {
+                                            int lg_chunk, ItemLoc &loc,
+                                            const int32_t *__restrict__ cell_ref = nullptr) {
   const int lane = threadIdx.x & 63;
-  int64_t before[kMaxLevels + 1];
+  int32_t before[kMaxLevels + 1];
 #pragma unroll
   for (int l = 0; l <= kMaxLevels; ++l) before[l] = 0;
   for (int base = 0; base < n_cells; base += 64) {
     const int c = base + lane;
     const int64_t n = (c < n_cells) ? cnt[c] : 0;
     const int64_t o = (c < n_cells) ? off[c] : 0;
-    int64_t my = (c < n_cells) ? items_of(n, chunk) : 0;
-    int64_t incl[kMaxLevels + 1], mine[kMaxLevels + 1];
+    const int32_t rs = (cell_ref && c < n_cells) ? cell_ref[c] : 0;  // same round trip
+    int32_t my = (c < n_cells) ? items_of(n, lg_chunk) : 0;
+    int32_t incl[kMaxLevels + 1], mine[kMaxLevels + 1];
 #pragma unroll
     for (int l = 0; l <= kMaxLevels; ++l) {
       mine[l] = my;
       incl[l] = my;
 #pragma unroll
       for (int s = 1; s < 64; s <<= 1) {
-        const int64_t y = __shfl_up(incl[l], s, 64);
+        const int32_t y = __shfl_up(incl[l], s, 64);
         if (lane >= s) incl[l] += y;
       }
-      my = ceil_div(my, kFanIn);
+      my = (my + kFanIn - 1) >> kLgFanIn;
     }
-    const int64_t total = __shfl(incl[0], 63, 64);
+    const int32_t total = __shfl(incl[0], 63, 64);
     if (item < before[0] + total) {
       const unsigned long long m = __ballot(before[0] + incl[0] > item);
       const int l = __ffsll(static_cast<long long>(m)) - 1;
@@ -107,10 +120,10 @@ __device__ __forceinline__ bool locate_item(int64_t item, const int64_t *__restr
 #pragma unroll
       for (int k = 0; k <= kMaxLevels; ++k)
         loc.level_first[k] = before[k] + __shfl(incl[k] - mine[k], l, 64);
-      loc.first = loc.level_first[0];
-      loc.chunk_idx = item - loc.first;
+      loc.chunk_idx = item - loc.level_first[0];
       loc.cnt = __shfl(n, l, 64);
       loc.off = __shfl(o, l, 64);
+      loc.ref_sel = __shfl(rs, l, 64);
       return true;
     }
 #pragma unroll
@@ -373,6 +386,21 @@ __device__ bool tree_climb(const TreeLayout &L, int64_t idx, int64_t nit, Prefix
     n_l = ceil_div(n_l, kFanIn);
   }
   return false;
+}
+
+// The last arriver's root combine: every summed entry pair of the n <= 16 root slabs into LDS
+// in ONE round of 16-byte sc1 loads (the finaliser then reads LDS only, instead of paying a
+// second dependent global round trip for the Gram tiles after the row sums).  Ends with a
+// barrier.
+template <int E>
+__device__ __forceinline__ void gather_root(const double *__restrict__ root, int64_t root_n,
+                                            double *dst_lds) {
+  for (int e = 2 * threadIdx.x; e < E; e += 2 * blockDim.x) {
+    const double2 s = sum_group2(root, root_n, E, e);
+    dst_lds[e] = s.x;
+    dst_lds[e + 1] = s.y;
+  }
+  __syncthreads();
 }
 
 // The per-cell finalisation: summed slab entries (read through `rd(e)`) -> mean[T][2]

@@ -27,37 +27,66 @@
 #include "constraints.hpp"
 #include "gram.hpp"
 
+#ifndef CCMPC_PROBE
+#define CCMPC_PROBE 0
+#endif
+
+// CCMPC_PROBE & 4 (diagnostic build only): per-workgroup phase timestamps (s_memrealtime,
+// 100 MHz) into a device table read back by ccmpc_probe_timestamps.
+#if CCMPC_PROBE & 4
+constexpr int kProbeSlots = 8, kProbeMaxWG = 8192;
+__device__ unsigned long long g_probe_ts[kProbeMaxWG * kProbeSlots];
+#define PROBE_TS(k)                                                                            \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kProbeMaxWG)                                          \
+      g_probe_ts[blockIdx.x * kProbeSlots + (k)] = __builtin_amdgcn_s_memrealtime();           \
+  } while (0)
+#else
+#define PROBE_TS(k) \
+  do {              \
+  } while (0)
+#endif
+
 namespace ccmpc {
 
+// Loads are pure loads, branch-free: every lane always issues its 16-byte loads, the address
+// clamped to the wave's last aligned quad (addressable because cell offsets and ld are
+// multiples of 4).  Masking (out-of-range particles, dead rows) happens in mfma_group, so a
+// group's loads have no consumer until its MFMAs run.  A guarded scalar fallback here turned
+// the loop into branches, and the waitcnt pass then drained vmcnt(0) before every MFMA group --
+// waiting on the NEXT group's loads too, which serialised the double buffer.
 template <typename P, int RB, int S>
 __device__ __forceinline__ void load_group(double (&v)[S][RB][4], const P *const (&rowp)[RB],
-                                           const bool (&live)[RB], const double (&sh)[RB],
                                            int64_t gbase, int64_t p1, int g) {
+  const int64_t qlast = (p1 - 1) & ~int64_t(3);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int64_t q = gbase + 16 * s + 4 * g;
+    const int64_t qc = q < qlast ? q : qlast;
 #pragma unroll
     for (int b = 0; b < RB; ++b) {
-      if (live[b] && q + 3 < p1) {
-        load4<P>(rowp[b] + q, v[s][b]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          v[s][b][j] = (live[b] && q + j < p1) ? static_cast<double>(rowp[b][q + j]) : sh[b];
-      }
+#if CCMPC_PROBE & 2  // diagnostic build only: no memory traffic
+      for (int j = 0; j < 4; ++j) v[s][b][j] = static_cast<double>(qc + j + b) * 1e-3;
+#else
+      load4<P>(rowp[b] + qc, v[s][b]);
+#endif
     }
   }
 }
 
 template <int RB, int S, int NACC>
 __device__ __forceinline__ void mfma_group(double (&v)[S][RB][4], const double (&sh)[RB],
-                                           d4 (&acc)[NACC][n_tiles(RB)], double (&s1)[RB]) {
+                                           const bool (&live)[RB], int64_t gbase, int64_t p1,
+                                           int g, d4 (&acc)[NACC][n_tiles(RB)],
+                                           double (&s1)[RB]) {
 #pragma unroll
   for (int s = 0; s < S; ++s) {
+    const int64_t q = gbase + 16 * s + 4 * g;
 #pragma unroll
     for (int b = 0; b < RB; ++b)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[s][b][j] -= sh[b];  // out-of-range slots become 0
+      for (int j = 0; j < 4; ++j)  // shifted; out-of-range slots and dead rows become 0
+        v[s][b][j] = (live[b] && q + j < p1) ? v[s][b][j] - sh[b] : 0.0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int a = (NACC == 2) ? (j & 1) : 0;
@@ -66,8 +95,12 @@ __device__ __forceinline__ void mfma_group(double (&v)[S][RB][4], const double (
       for (int bi = 0; bi < RB; ++bi)
 #pragma unroll
         for (int bj = bi; bj < RB; ++bj) {
+#if CCMPC_PROBE & 1  // diagnostic build only: no matrix-core work
+          acc[a][t][0] += v[s][bi][j] * v[s][bj][j];
+#else
           acc[a][t] =
               __builtin_amdgcn_mfma_f64_16x16x4f64(v[s][bi][j], v[s][bj][j], acc[a][t], 0, 0, 0);
+#endif
           ++t;
         }
     }
@@ -80,7 +113,7 @@ template <typename P, int RB, bool MINK>
 __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void moments_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
-    int64_t wq, TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
+    int lg_wq, TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
     MinkParams mp) {
   using G = Geo<RB>;
   constexpr int NT = n_tiles(RB);
@@ -96,20 +129,34 @@ __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void
   __shared__ double mean_lds[D];
   __shared__ double cov_lds[COV_IN_LDS ? D * D : 1];
   __shared__ double lb_s[MINK ? 40 * 39 / 2 : 1];
+  __shared__ double ref_lds[MINK ? D + 3 : 1];  // reference trajectory [T][2], then risk[3]
   __shared__ int flag;
 
   ItemLoc loc;
-  const int64_t chunk = G::NW * wq;
-  if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, chunk, loc)) return;  // uniform
+  const int lg_chunk = lg_wq + (G::NW == 4 ? 2 : 3);
+  const int64_t wq = int64_t(1) << lg_wq, chunk = int64_t(1) << lg_chunk;
+  PROBE_TS(0);
+  if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc,
+                   MINK ? mp.cell_ref : nullptr))
+    return;  // uniform
+  PROBE_TS(1);
   const int cell = loc.cell;
   const int64_t cnt = loc.cnt;
 
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int r = lane & 15;
   const int g = lane >> 4;
   const int rows = 2 * T;
-  const int64_t i0 = loc.chunk_idx * chunk;
+  const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
+  // the half-space tail's per-cell inputs: loads issued now, landing behind the stream loop
+  double pre = 0.0;
+  if (MINK) {
+    if (threadIdx.x < rows)
+      pre = mp.ref_traj[static_cast<int64_t>(loc.ref_sel) * rows + threadIdx.x];
+    else if (threadIdx.x < rows + 3)
+      pre = mp.cell_risk[3 * loc.cell + (threadIdx.x - rows)];
+  }
   const int64_t i1 = (i0 + chunk < cnt) ? i0 + chunk : cnt;
   const int64_t p0 = i0 + static_cast<int64_t>(w) * wq;
   const int64_t p1 = (p0 + wq < i1) ? p0 + wq : i1;
@@ -134,21 +181,33 @@ __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void
 #pragma unroll
   for (int b = 0; b < RB; ++b) s1[b] = 0.0;
 
-  // double-buffered load groups: the next group's loads are in flight during this group's MFMAs
+  // double-buffered load groups: the next group's loads are in flight during this group's
+  // MFMAs.  The prefetch is unconditional (a group past the end is clamped + masked and
+  // never multiplied) so there is no divergent join for the waitcnt pass to merge.
   const int64_t ngroups = p1 > p0 ? ceil_div(p1 - p0, 16 * S) : 0;
   double va[S][RB][4], vb[S][RB][4];
-  if (ngroups > 0) load_group<P, RB, S>(va, rowp, live, sh, p0, p1, g);
-  for (int64_t gi = 0; gi < ngroups; gi += 2) {
-    if (gi + 1 < ngroups) load_group<P, RB, S>(vb, rowp, live, sh, p0 + (gi + 1) * 16 * S, p1, g);
-    mfma_group<RB, S, NACC>(va, sh, acc, s1);
-    if (gi + 1 < ngroups) {
-      if (gi + 2 < ngroups)
-        load_group<P, RB, S>(va, rowp, live, sh, p0 + (gi + 2) * 16 * S, p1, g);
-      mfma_group<RB, S, NACC>(vb, sh, acc, s1);
+  // sched_barrier(0) fences keep the four phases in program order, so each MFMA group waits
+  // (vmcnt) only for its own buffer while the other buffer's loads stay in flight.
+  if (ngroups > 0) {
+    load_group<P, RB, S>(va, rowp, p0, p1, g);
+    int64_t gi = 0;
+    for (; gi + 2 <= ngroups; gi += 2) {
+      const int64_t ga = p0 + gi * 16 * S, gb = ga + 16 * S;
+      load_group<P, RB, S>(vb, rowp, gb, p1, g);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_group<RB, S, NACC>(va, sh, live, ga, p1, g, acc, s1);
+      __builtin_amdgcn_sched_barrier(0);
+      load_group<P, RB, S>(va, rowp, gb + 16 * S, p1, g);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_group<RB, S, NACC>(vb, sh, live, gb, p1, g, acc, s1);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if (gi < ngroups) mfma_group<RB, S, NACC>(va, sh, live, p0 + gi * 16 * S, p1, g, acc, s1);
   }
+  PROBE_TS(2);
 
-  const int64_t nit = items_of(cnt, chunk);
+  const int32_t nit = items_of(cnt, lg_chunk);
+  if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
 #pragma unroll
   for (int b = 0; b < RB; ++b) {
     if (w == 0 && g == 0) shift_lds[16 * b + r] = sh[b];
@@ -160,32 +219,41 @@ __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void
   if (nit == 1) {
     // the whole cell lives in this workgroup: combine in LDS, no global round trip
     combine_waves<RB, NACC, G::NW>(acc, s1, xch, slab_lds, true);
+    PROBE_TS(3);
+    PROBE_TS(4);
     finalize_cell<RB>([&](int e) { return double2{slab_lds[e], slab_lds[e + 1]}; }, cnt, T,
                       shift_lds, S_lds, o0, o1, mean, cov, mean_lds,
                       COV_IN_LDS ? cov_lds : nullptr);
   } else {
     combine_waves<RB, NACC, G::NW>(acc, s1, xch, tree.slabs[0] + blockIdx.x * E, false);
+    PROBE_TS(3);
     auto prefix = [&](int l) -> int64_t { return loc.level_first[l]; };
     const double *root;
     int64_t root_n;
-    if (!tree_climb<E>(tree, loc.chunk_idx, nit, prefix, &flag, &root, &root_n)) return;
-    finalize_cell<RB>([&](int e) { return sum_group2(root, root_n, E, e); }, cnt, T, shift_lds,
-                      S_lds, o0, o1, mean, cov, mean_lds, COV_IN_LDS ? cov_lds : nullptr);
+    const bool last = tree_climb<E>(tree, loc.chunk_idx, nit, prefix, &flag, &root, &root_n);
+    PROBE_TS(4);
+    if (!last) return;
+    gather_root<E>(root, root_n, slab_lds);
+    finalize_cell<RB>([&](int e) { return double2{slab_lds[e], slab_lds[e + 1]}; }, cnt, T,
+                      shift_lds, S_lds, o0, o1, mean, cov, mean_lds,
+                      COV_IN_LDS ? cov_lds : nullptr);
   }
+  PROBE_TS(5);
   if (MINK)
-    minkowski_cell(COV_IN_LDS ? cov_lds : cov, mean_lds, T, cell, mp, lb_s, threadIdx.x,
-                   blockDim.x);
+    minkowski_cell(COV_IN_LDS ? cov_lds : cov, mean_lds, T, cell, ref_lds, ref_lds[rows],
+                   ref_lds[rows + 1], ref_lds[rows + 2], mp, lb_s, threadIdx.x, blockDim.x);
+  PROBE_TS(6);
 }
 
 template <typename P, int RB, bool MINK>
 static void launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
                    const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
                    double *cov, const MinkParams &mp, hipStream_t s) {
-  const int64_t wq = store_wave_quota(n_bound);
-  const int64_t items = max_items(n_cells, n_bound, Geo<RB>::NW * wq);
+  const int lg_wq = store_lg_wave_quota(RB, n_bound);
+  const int64_t items = max_items(n_cells, n_bound, int64_t(1) << store_lg_chunk(RB, n_bound));
   const TreeLayout tree = tree_layout(ws, items, n_cells, slab_doubles(RB));
   hipLaunchKernelGGL((moments_kernel<P, RB, MINK>), dim3(static_cast<unsigned>(items)),
-                     dim3(Geo<RB>::NW * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, wq,
+                     dim3(Geo<RB>::NW * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq,
                      tree, mean, cov, mp);
 }
 
@@ -234,11 +302,23 @@ static int run(const void *positions, int dtype, int64_t ld, int64_t T, const do
 
 using namespace ccmpc;
 
+#if CCMPC_PROBE & 4
+extern "C" int ccmpc_probe_timestamps(void *host, int reset) {
+  const size_t bytes = sizeof(g_probe_ts);
+  if (reset) {
+    static unsigned long long zeros[kProbeMaxWG * kProbeSlots];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_probe_ts), zeros, bytes) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe_ts), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells,
                                                 int64_t n_particles_bound) {
   if (T < 1 || T > kMaxT || n_cells < 0 || n_particles_bound < 0) return 0;
   const int rb = row_blocks(T);
-  const int64_t items = max_items(n_cells, n_particles_bound, store_chunk(rb, n_particles_bound));
+  const int64_t items =
+      max_items(n_cells, n_particles_bound, int64_t(1) << store_lg_chunk(rb, n_particles_bound));
   return tree_bytes(items, n_cells, slab_doubles(rb));
 }
 

@@ -261,8 +261,10 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
   if (!tree_climb<E>(tree, cidx, items_per_cell, prefix, &flag, &root, &root_n)) return;
   double *mean = out_mean + static_cast<int64_t>(cell) * rows;
   double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
-  finalize_cell<RB>([&](int e) { return sum_group2(root, root_n, E, e); }, n, T, shift_s, S_lds,
-                    0.0, 0.0, mean, cov, mean_lds, nullptr);
+  static_assert(NW * D * kStageStride >= E, "root staging reuses the sample stage");
+  gather_root<E>(root, root_n, stage_all);  // the sample stage is free after combine_waves
+  finalize_cell<RB>([&](int e) { return double2{stage_all[e], stage_all[e + 1]}; }, n, T,
+                    shift_s, S_lds, 0.0, 0.0, mean, cov, mean_lds, nullptr);
   if (MINK) minkowski_cell(cov, mean_lds, T, cell, mp, lb_s, threadIdx.x, blockDim.x);
 }
 

@@ -56,14 +56,14 @@ __device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, fl
 
 __global__ __launch_bounds__(256) void sample_unicycle_kernel(
     const double *__restrict__ init_state, const double *__restrict__ latent_cdf, int n_latent,
-    const float *__restrict__ gmm, int64_t N, int T, float dt, uint64_t seed,
+    const float *__restrict__ gmm, int64_t N, int T, float dt, uint64_t seed, uint32_t ov_base,
     int32_t *__restrict__ out_z, float *__restrict__ out_pos, int64_t ld) {
   const int ov = blockIdx.y;
+  const uint32_t key = ov_base + static_cast<uint32_t>(ov);  // global OV id keys the streams
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const double *cdf = latent_cdf + static_cast<int64_t>(ov) * n_latent;
-  const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, static_cast<uint32_t>(ov),
-                             STREAM_SAMPLER_Z, seed);
+  const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, key, STREAM_SAMPLER_Z, seed);
   const double u = uniform53(w.x, w.y);
   int z = n_latent - 1;
   for (int k = 0; k < n_latent; ++k) {
@@ -80,8 +80,8 @@ __global__ __launch_bounds__(256) void sample_unicycle_kernel(
   float *o = out_pos + static_cast<int64_t>(ov) * ((N + 3) & ~int64_t(3)) + i;
   for (int t = 0; t < T; ++t) {
     double e0d, e1d;
-    normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), static_cast<uint32_t>(ov),
-                STREAM_SAMPLER_EPS, seed, e0d, e1d);
+    normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), key, STREAM_SAMPLER_EPS, seed,
+                e0d, e1d);
     const float e0 = static_cast<float>(e0d), e1 = static_cast<float>(e1d);
     const float mu0 = g[5 * t], mu1 = g[5 * t + 1];
     const float s0 = exp_rn(g[5 * t + 2]), s1 = exp_rn(g[5 * t + 3]), rho = g[5 * t + 4];
@@ -99,19 +99,22 @@ using namespace ccmpc;
 
 extern "C" int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf,
                                      int64_t n_latent, const float *gmm, int64_t n_ov, int64_t N,
-                                     int64_t T, double dt, uint64_t seed, int32_t *out_z,
-                                     float *out_pos, int64_t ld, ccmpc_stream_t stream) {
+                                     int64_t T, double dt, uint64_t seed, int64_t ov_base,
+                                     int32_t *out_z, float *out_pos, int64_t ld,
+                                     ccmpc_stream_t stream) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
   CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536, "bad n_ov");
   CCMPC_REQUIRE(N >= 1 && N < (int64_t(1) << 32), "bad N");
+  CCMPC_REQUIRE(ov_base >= 0 && ov_base + n_ov <= (int64_t(1) << 32), "bad ov_base");
   if (n_ov == 0) return CCMPC_OK;
   CCMPC_REQUIRE(init_state && latent_cdf && gmm && out_z && out_pos, "null pointer");
   CCMPC_REQUIRE(ld >= n_ov * ((N + 3) & ~int64_t(3)), "ld too small");
   const dim3 grid(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(n_ov));
   hipLaunchKernelGGL(sample_unicycle_kernel, grid, dim3(256), 0, as_stream(stream), init_state,
                      latent_cdf, static_cast<int>(n_latent), gmm, N, static_cast<int>(T),
-                     static_cast<float>(dt), seed, out_z, out_pos, ld);
+                     static_cast<float>(dt), seed, static_cast<uint32_t>(ov_base), out_z, out_pos,
+                     ld);
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

@@ -18,4 +18,6 @@ BENCH="python3 $ROOT/bench.py --no-cpu --steps 300 --warmup 30"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- $BENCH > "$OUT/trace_bench.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/fetch" -o run --output-format csv -- $BENCH > "$OUT/fetch_bench.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/write" -o run --output-format csv -- $BENCH > "$OUT/write_bench.log" 2>&1
-python3 "$ROOT/profiles/summarize.py" "$OUT" "$ROOT/profiles/$ROUND"
+# summary lands under gpurun_out/ (merged back); copy into profiles/<round>/ afterwards with
+#   python profiles/summarize.py gpurun_out/prof_<round> profiles/<round>
+python3 "$ROOT/profiles/summarize.py" "$OUT" "$OUT/summary"

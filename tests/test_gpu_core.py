@@ -234,13 +234,33 @@ def test_ideal_moments_full_size_properties(gpu):
     m2, c2, _ = eng.ideal_moments(mean, cov, src, Tn, ns, seed=9)
     assert torch.equal(m1, m2) and torch.equal(c1, c2)
     assert st.cpu().numpy().tolist() == [0, 0]
-    # the last step's variance is bounded by the source covariance (conditioning shrinks it)
-    c1 = c1.cpu().numpy()
-    src_cov = cov.cpu().numpy()
+    # the sample moments reproduce the Gaussian the rollout propagates analytically
+    # (v8ideal/__init__.py:2671-2700): slot t holds x_{t+1} = mu_{t+1} + A_t (x_t - mu_t) + L_t z,
+    # so m_t = mu_{t+1} + A_t (m_{t-1} - mu_t), C_t = A_t C_{t-1} A_t^T + L_t L_t^T, C_{-1} = 0,
+    # m_{-1} = x0 (the one shared draw); the lag-1 cross block is A_t C_{t-1}.
+    c1, m1 = c1.cpu().numpy(), m1.cpu().numpy()
+    mu, src_cov = mean.cpu().numpy(), cov.cpu().numpy()
     for k in range(2):
+        blk = lambda M, i, j: M[2 * i:2 * i + 2, 2 * j:2 * j + 2]
+        x0 = orc.ideal_x0(mu[k, 0], blk(src_cov[k], 0, 0), k, 9)
+        m_prev, C_prev = x0, np.zeros((2, 2))
         for t in range(Tn):
-            v = np.trace(c1[k, 2 * t:2 * t + 2, 2 * t:2 * t + 2])
-            assert 0 < v <= np.trace(src_cov[k, 2 * t + 2:2 * t + 4, 2 * t + 2:2 * t + 4]) * 1.01
+            S_t, X = blk(src_cov[k], t, t), blk(src_cov[k], t + 1, t)
+            A = X @ np.linalg.inv(S_t)
+            LLt = blk(src_cov[k], t + 1, t + 1) - A @ X.T
+            m = mu[k, t + 1] + A @ (m_prev - mu[k, t])
+            C = A @ C_prev @ A.T + LLt
+            got_C = blk(c1[k], t, t)
+            # 1e6 samples: ~5 sigma of the sampling error of a mean / a covariance entry
+            sd = np.sqrt(np.diag(C))
+            assert np.all(np.abs(m1[k, t] - m) <= 5 * sd / np.sqrt(ns)), (k, t)
+            assert np.all(np.abs(got_C - C) <= 5 * np.outer(sd, sd) * np.sqrt(2.0 / ns)), (k, t)
+            if t > 0:
+                got_X = blk(c1[k], t, t - 1)
+                sdp = np.sqrt(np.diag(C_prev))
+                assert np.all(np.abs(got_X - A @ C_prev) <=
+                              5 * np.outer(sd, sdp) * np.sqrt(2.0 / ns)), (k, t)
+            m_prev, C_prev = m, C
 
 
 def test_moments_deterministic(gpu):

@@ -161,6 +161,12 @@ def test_sampler_matches_restatement(gpu):
         mism = np.mean(got != pos)
         assert mism < 1e-4, mism
         np.testing.assert_allclose(got, pos, rtol=0, atol=1e-3)
+    # sharded launch: OVs 1..2 alone with ov_base=1 draw exactly what the batched call drew
+    z2, store2 = e.sample_unicycle(init[1:], pmf[1:], gmm[1:], N, T, dt=0.5, seed=seed,
+                                   device=gpu, ov_base=1)
+    np.testing.assert_array_equal(z2.cpu().numpy(), zc[1:])
+    for o in range(2):
+        np.testing.assert_array_equal(store2.cell_positions(o), store.cell_positions(o + 1))
     # empirical latent frequencies follow p(z|x)
     freq = np.bincount(zc[0], minlength=L) / N
     assert np.max(np.abs(freq - pmf[0])) < 5 * np.sqrt(pmf[0].max() / N) + 1e-3

@@ -1,0 +1,68 @@
+"""Run one bench configuration's moments kernel (or full cycle) in a loop, for rocprofv3.
+
+    python tools/probe_moments.py C4 moments 200
+    python tools/probe_moments.py C5 cycle 100
+    python tools/probe_moments.py ALL time 0      (graph-timed us per launch, every config)
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "cc-mpc_amd")]
+
+import torch  # noqa: E402
+
+from ccmpc import cycle, engine, synthetic  # noqa: E402
+
+CONFIGS = {"C2": (4, 5000, 8, 1), "C3": (1, 100000, 8, 1), "C4": (4, 20000, 12, 8),
+           "C5": (8, 50000, 40, 1)}
+
+
+def build(name, dev):
+    O, N, T, scenes = CONFIGS[name]
+    cells, K, refs = [], [], []
+    for sc in range(scenes):
+        ovs, ref, _ = synthetic.scene(1000 + sc, O=O, N=N, T=T)
+        cells += [c for o in ovs for c in o]
+        K += [len(o) for o in ovs]
+        refs.append(ref)
+    store = engine.ParticleStore.from_cells(cells, device=dev)
+    return store, cycle.MinkowskiCycle(store, K, refs[0])
+
+
+def time_all(dev):
+    sys.path.insert(0, ROOT)
+    from bench import time_kernel_live
+    for name in CONFIGS:
+        store, cyc = build(name, dev)
+        tm = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev,
+                              per_graph=10, replays=5)
+        tc = time_kernel_live(cyc.run, dev, per_graph=10, replays=5)
+        print(f"{name}: moments {tm * 1e6:8.2f} us   cycle {tc * 1e6:8.2f} us", flush=True)
+
+
+def main():
+    name, what, iters = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    if what == "time":
+        time_all(torch.device("cuda:0"))
+        return
+    O, N, T, scenes = CONFIGS[name]
+    dev = torch.device("cuda:0")
+    cells, K, refs = [], [], []
+    for sc in range(scenes):
+        ovs, ref, _ = synthetic.scene(1000 + sc, O=O, N=N, T=T)
+        cells += [c for o in ovs for c in o]
+        K += [len(o) for o in ovs]
+        refs.append(ref)
+    store = engine.ParticleStore.from_cells(cells, device=dev)
+    cyc = cycle.MinkowskiCycle(store, K, refs[0])
+    fn = cyc.run if what == "cycle" else (
+        lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws))
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    print(f"{name} {what} x{iters}: {sum(store.counts)} particles, {store.n_cells} cells")
+
+
+if __name__ == "__main__":
+    main()
