@@ -216,13 +216,15 @@ int ccmpc_ideal_minkowski_cycle(const double *prev_mean, const double *prev_cov,
  *  gmm[o][L][T][5]    mu_dphi, mu_a, log sigma_dphi, log sigma_a, rho   (float32)
  *  out_z[o][N]        latent id per particle (the reference's argmax z, prediction.py:103)
  *  out_pos            F32 store in SAMPLE order: OV o occupies [o*S, o*S + N), S = round_up(N, 4)
- * Noise: z uses Philox (i, 0, o, STREAM_SAMPLER_Z), eps uses (i, t, o, STREAM_SAMPLER_EPS).
+ * Noise: z uses Philox (i, 0, g, STREAM_SAMPLER_Z), eps uses (i, t, g, STREAM_SAMPLER_EPS) with
+ * g = ov_base + o the GLOBAL OV id, so a scene's draws do not depend on how scenes are sharded
+ * over ranks or batched into calls.
  * PARITY UNPINNED upstream (absent submodule): checked against the repo's own restatement.
  * ------------------------------------------------------------------------------------- */
 int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf, int64_t n_latent,
                           const float *gmm, int64_t n_ov, int64_t N, int64_t T, double dt,
-                          uint64_t seed, int32_t *out_z, float *out_pos, int64_t ld,
-                          ccmpc_stream_t stream);
+                          uint64_t seed, int64_t ov_base, int32_t *out_z, float *out_pos,
+                          int64_t ld, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Particle bucketing by latent mode: make_ovehicles (v8ideal/__init__.py:469-505) +
