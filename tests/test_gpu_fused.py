@@ -48,6 +48,21 @@ def test_graph_replay_is_stable(gpu):
     assert np.all(cyc.records()["status"] == 0)
 
 
+def test_bound_launch_equals_run(gpu):
+    """The pre-bound one-call path bench.py times is the same launch as the engine path."""
+    from ccmpc import cycle, synthetic
+    ovs, ref, _ = synthetic.scene(4, O=4, N=5000, T=8)
+    store = eng().ParticleStore.from_cells([c for o in ovs for c in o], device=gpu)
+    a = cycle.MinkowskiCycle(store, [len(o) for o in ovs], ref)
+    a.run()
+    b = cycle.MinkowskiCycle(store, [len(o) for o in ovs], ref).bind()
+    for _ in range(100):
+        b.launch()
+    torch.cuda.synchronize()
+    assert torch.equal(a.rec, b.rec) and torch.equal(a.cov, b.cov)
+    assert torch.equal(a.prob_lower, b.prob_lower)
+
+
 def test_workspace_reused_across_shapes(gpu):
     """One zero-initialised workspace serves calls of different cell counts back to back."""
     e = eng()
