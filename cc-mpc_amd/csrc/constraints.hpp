@@ -29,29 +29,50 @@ __device__ __forceinline__ M2 add(const M2 &x, const M2 &y) {
 }
 __device__ __forceinline__ M2 transpose(const M2 &x) { return {x.a, x.c, x.b, x.d}; }
 
-// Inverse by LU with partial pivoting, as LAPACK getrf/getri does it for 2x2.
+// Latency-lean f64 reciprocal and square root for the MVOE chain (a serial dependency chain per
+// record, so each IEEE div / sqrt fix-up sequence is pure latency): hardware estimate + Newton /
+// Goldschmidt refinement, <= ~2 ulp on the well-scaled values here (covariances, beta ~ 1),
+// against the 1e-5 relative Frobenius parity bar on Q.  The tangent choice and side test keep
+// IEEE division, so which / side stay decided exactly as the reference decides them.
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return r;
+}
+
+__device__ __forceinline__ double div_nr(double a, double b) {
+  const double r = rcp_nr(b);
+  const double q = a * r;
+  return fma(fma(-b, q, a), r, q);  // one residual correction
+}
+
+__device__ __forceinline__ double sqrt_gs(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-g, h, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  const double d = fma(-g, g, x);
+  return x > 0.0 ? fma(d, h, g) : (x == 0.0 ? 0.0 : NAN);
+}
+
+// Inverse by LU with partial pivoting, as LAPACK getrf/getri does it for 2x2.  Branch-free:
+// the pivot row is selected, not branched on (lanes of a wave pick different pivots, and a
+// branch would run both LU paths back to back); the arithmetic per pivot choice is unchanged.
 __device__ __forceinline__ bool inv2(const M2 &m, M2 &out) {
-  if (fabs(m.c) > fabs(m.a)) {
-    // pivot rows: P m = [[c, d], [a, b]]
-    const double l = m.a / m.c;
-    const double u22 = m.b - l * m.d;
-    if (m.c == 0.0 || u22 == 0.0) return false;
-    // inverse of P m, then columns swapped back
-    const double i11 = 1.0 / m.c, i22 = 1.0 / u22;
-    const double i12 = -m.d * i11 * i22;
-    // inv(U) = [[i11, i12], [0, i22]]; inv(L) = [[1, 0], [-l, 1]]; inv(Pm) = inv(U) inv(L)
-    const double x11 = i11 - i12 * l, x12 = i12, x21 = -i22 * l, x22 = i22;
-    out = {x12, x11, x22, x21};  // inv(m) = inv(Pm) P
-    return true;
-  }
-  if (m.a == 0.0) return false;
-  const double l = m.c / m.a;
-  const double u22 = m.d - l * m.b;
-  if (u22 == 0.0) return false;
-  const double i11 = 1.0 / m.a, i22 = 1.0 / u22;
-  const double i12 = -m.b * i11 * i22;
-  out = {i11 - i12 * l, i12, -i22 * l, i22};
-  return true;
+  const bool piv = fabs(m.c) > fabs(m.a);
+  const double p0 = piv ? m.c : m.a, p1 = piv ? m.d : m.b;  // pivot row of P m
+  const double q0 = piv ? m.a : m.c, q1 = piv ? m.b : m.d;  // other row
+  const double i11 = rcp_nr(p0);
+  const double l = q0 * i11;
+  const double u22 = q1 - l * p1;
+  const double i22 = rcp_nr(u22);
+  const double i12 = -p1 * i11 * i22;
+  // inv(U) = [[i11, i12], [0, i22]]; inv(L) = [[1, 0], [-l, 1]]; inv(P m) = inv(U) inv(L)
+  const double x11 = i11 - i12 * l, x12 = i12, x21 = -i22 * l, x22 = i22;
+  out = piv ? M2{x12, x11, x22, x21} : M2{x11, x12, x21, x22};  // inv(m) = inv(P m) P
+  return p0 != 0.0 && u22 != 0.0;
 }
 
 // solve(S1, S2) = S1^{-1} S2 by the same LU (scipy.linalg.solve -> gesv)
@@ -70,15 +91,9 @@ __device__ bool compute_mvoe(const M2 &S1, const M2 &S2, double tol, int maxiter
   const double half_tr = 0.5 * (M.a + M.d);
   const double hd = 0.5 * (M.a - M.d);
   const double disc = hd * hd + M.b * M.c;
-  double l1, l2;
-  if (disc >= 0.0) {
-    const double s = sqrt(disc);
-    l1 = half_tr + s;
-    l2 = half_tr - s;
-  } else {  // complex pair: .real keeps the real part of both
-    l1 = half_tr;
-    l2 = half_tr;
-  }
+  // complex pair (disc < 0): .real keeps the real part of both
+  const double sd = disc >= 0.0 ? sqrt_gs(disc) : 0.0;
+  const double l1 = half_tr + sd, l2 = half_tr - sd;
   // beta' = sqrt(sum 1/w / sum l/w), w = 1 + beta l  ==  sqrt((w1 + w2) / (l1 w2 + l2 w1)):
   // the same fixed point with one division per iteration instead of five (the iteration is a
   // serial chain per record, so the division latency is the tail's critical path).  Rounding
@@ -86,13 +101,13 @@ __device__ bool compute_mvoe(const M2 &S1, const M2 &S2, double tol, int maxiter
   double b = 1.0;
   for (int it = 0; it < maxiter; ++it) {
     const double w1 = 1.0 + b * l1, w2 = 1.0 + b * l2;
-    const double bn = sqrt((w1 + w2) / (l1 * w2 + l2 * w1));
+    const double bn = sqrt_gs(div_nr(w1 + w2, l1 * w2 + l2 * w1));
     const bool done = fabs(bn - b) < tol;
     b = bn;
     if (done) break;
   }
   beta = b;
-  Q = add(scale(S1, 1.0 + 1.0 / b), scale(S2, 1.0 + b));
+  Q = add(scale(S1, 1.0 + rcp_nr(b)), scale(S2, 1.0 + b));
   return true;
 }
 
@@ -106,7 +121,7 @@ __device__ __forceinline__ M2 block(const double *cov, int rows, int i, int j) {
 }
 
 __device__ __forceinline__ void pair_of(int p, int &t, int &tau) {
-  int tt = static_cast<int>((1.0 + sqrt(1.0 + 8.0 * p)) * 0.5);
+  int tt = static_cast<int>((1.0f + sqrtf(1.0f + 8.0f * static_cast<float>(p))) * 0.5f);
   while (tt * (tt - 1) / 2 > p) --tt;
   while ((tt + 1) * tt / 2 <= p) ++tt;
   t = tt;
@@ -124,35 +139,51 @@ struct MinkParams {
   double *out_prob_lower;    // [n_cells][T]
 };
 
-// One (cell, t, tau) record from the cell's 2T x 2T covariance C (row stride `rows`) and mean mu
-// (v8ideal/__init__.py:893-943).  Returns the lower bound (for the per-t minimum).
-__device__ double minkowski_pair(const double *C, const double *mu, const double *ref, int rows,
-                                 int t, int tau, double chi_r, double chi_p, double gamma,
-                                 double R, double tol, int maxiter, ccmpc_halfspace &h) {
-  h.status = 0;
-  h.t_tau = (t << 16) | tau;
-  // predict_moments (makeconstraint.py:41-70): blocks of the 2T x 2T covariance
-  const M2 c_t = block(C, rows, t, t);
+// predict_moments (makeconstraint.py:41-70) from blocks of the 2T x 2T covariance:
+// cov_mu = C_t,tau C_tau^-1 C_tau,t and cov_infer = C_t - cov_mu.
+struct PairMoments {
+  M2 c_t, cov_mu, cov_infer;
+  bool ok;
+};
+
+__device__ __forceinline__ PairMoments pair_moments(const double *C, int rows, int t, int tau) {
+  PairMoments pm;
+  pm.c_t = block(C, rows, t, t);
   const M2 c_x = block(C, rows, t, tau);
   const M2 c_xT = block(C, rows, tau, t);
-  const M2 c_tau = block(C, rows, tau, tau);
   M2 inv_tau;
-  bool ok = inv2(c_tau, inv_tau);
-  const M2 cov_mu = mul(mul(c_x, inv_tau), c_xT);
-  const M2 cov_infer = sub(c_t, cov_mu);
-  // compute_lower_bound (makeconstraint.py:282-303): independent of the MVOE chain, so it is
-  // issued first and its sqrt/div latency overlaps the setup of the first MVOE
-  const double root_t = sqrt(fro(c_t));
-  const double al = sqrt(fro(cov_infer)) / root_t;
-  const double be = sqrt(fro(cov_mu)) / root_t;
+  pm.ok = inv2(block(C, rows, tau, tau), inv_tau);
+  pm.cov_mu = mul(mul(c_x, inv_tau), c_xT);
+  pm.cov_infer = sub(pm.c_t, pm.cov_mu);
+  return pm;
+}
+
+// compute_lower_bound (makeconstraint.py:282-303):
+// alpha = sqrt|cov_infer|_F / sqrt|C_t|_F, beta likewise with cov_mu, p = chi2_2 cdf
+// ((Gamma (1 - alpha) / beta)^2) = 1 - exp(-x / 2).
+__device__ __forceinline__ double pair_lower_bound(const PairMoments &pm, double gamma) {
+  const double root_t = sqrt(fro(pm.c_t));
+  const double al = sqrt(fro(pm.cov_infer)) / root_t;
+  const double be = sqrt(fro(pm.cov_mu)) / root_t;
   const double x = gamma * (1.0 - al) / be;
-  const double lb = -expm1(-0.5 * (x * x));
+  return -expm1(-0.5 * (x * x));
+}
+
+// One (cell, t, tau) record except its lower bound, from the cell's 2T x 2T covariance C (row
+// stride `rows`) and mean mu (v8ideal/__init__.py:893-943), written straight to `out`.
+__device__ void minkowski_pair(const double *C, const double *mu, const double *ref, int rows,
+                               int t, int tau, double chi_r, double chi_p, double R, double tol,
+                               int maxiter, ccmpc_halfspace *out) {
+  const PairMoments pm = pair_moments(C, rows, t, tau);
+  int status = 0;
   // two MVOE calls (:915, :917-918)
   double b1 = NAN, b2 = NAN;
   M2 Q = {NAN, NAN, NAN, NAN}, QR = {NAN, NAN, NAN, NAN};
-  ok = ok && compute_mvoe(scale(cov_infer, chi_r), scale(cov_mu, chi_p), tol, maxiter, b1, Q);
+  bool ok = pm.ok;
+  ok = ok && compute_mvoe(scale(pm.cov_infer, chi_r), scale(pm.cov_mu, chi_p), tol, maxiter, b1,
+                          Q);
   ok = ok && compute_mvoe(Q, M2{R * R, 0.0, 0.0, R * R}, tol, maxiter, b2, QR);
-  if (!ok) h.status = CCMPC_REC_SINGULAR;
+  if (!ok) status = CCMPC_REC_SINGULAR;
   // slope-m tangent of the QR ellipse closest to the reference point (:920-924)
   const double m0 = mu[2 * t], m1 = mu[2 * t + 1];
   const double a0 = ref[2 * t], a1 = ref[2 * t + 1];
@@ -163,9 +194,9 @@ __device__ double minkowski_pair(const double *C, const double *mu, const double
   double d = NAN;
   int which = 0, side = 0;
   if (!isfinite(m)) {
-    if (h.status == 0) h.status = CCMPC_REC_NONFINITE;
+    if (status == 0) status = CCMPC_REC_NONFINITE;
   } else if (!(q > 0.0)) {
-    if (h.status == 0) h.status = CCMPC_REC_NO_TANGENT;
+    if (status == 0) status = CCMPC_REC_NO_TANGENT;
   } else {
     const double proj = n0 * m0 + n1 * m1;
     const double delta = 1.0 * sqrt(q);
@@ -177,42 +208,53 @@ __device__ double minkowski_pair(const double *C, const double *mu, const double
     d = which ? d2 : d1;
     side = (n0 * m0 + n1 * m1 <= d) ? 1 : -1;  // (:926) n.mean <= d  ->  n.x >= d
   }
-  if (h.status == 0 && !(isfinite(d) && isfinite(Q.a) && isfinite(QR.a) && isfinite(m0)))
-    h.status = CCMPC_REC_NONFINITE;
-  h.n0 = n0;
-  h.n1 = n1;
-  h.d = d;
-  h.q00 = Q.a;
-  h.q01 = Q.b;
-  h.q11 = Q.d;
-  h.r00 = QR.a;
-  h.r01 = QR.b;
-  h.r11 = QR.d;
-  h.beta1 = b1;
-  h.beta2 = b2;
-  h.lower_bound = lb;
-  h.mean0 = m0;
-  h.mean1 = m1;
-  h.which = which;
-  h.side = side;
-  return lb;
+  if (status == 0 && !(isfinite(d) && isfinite(Q.a) && isfinite(QR.a) && isfinite(m0)))
+    status = CCMPC_REC_NONFINITE;
+  out->n0 = n0;
+  out->n1 = n1;
+  out->d = d;
+  out->q00 = Q.a;
+  out->q01 = Q.b;
+  out->q11 = Q.d;
+  out->r00 = QR.a;
+  out->r01 = QR.b;
+  out->r11 = QR.d;
+  out->beta1 = b1;
+  out->beta2 = b2;
+  out->mean0 = m0;
+  out->mean1 = m1;
+  out->which = which;
+  out->side = side;
+  out->status = status;
+  out->t_tau = (t << 16) | tau;
 }
 
 // All pairs of one cell by the threads [0, nthreads) of the calling group, with the cell's
 // reference trajectory `ref` ([T][2]) and risk constants already at hand; lb_s has room for
-// T(T-1)/2 doubles.  Includes the barrier needed before the per-t minimum.
+// T(T-1)/2 doubles.  The record of a pair is a serial chain (two MVOE fixed points, then the
+// tangent) on one lane; its lower bound does not depend on that chain, so with >= 2 waves the
+// lower bounds run on the upper half of the group -- other waves, i.e. truly concurrently --
+// and write their record field themselves.  Includes the barrier needed before the per-t
+// minimum.
 __device__ void minkowski_cell(const double *C, const double *mu, int T, int cell,
                                const double *ref, double chi_r, double chi_p, double gamma,
                                const MinkParams &mp, double *lb_s, int tid, int nthreads) {
   const int rows = 2 * T;
   const int P = T * (T - 1) / 2;
-  for (int p = tid; p < P; p += nthreads) {
+  ccmpc_halfspace *rec = mp.out_rec + static_cast<int64_t>(cell) * P;
+  const int half = (nthreads >= 128) ? nthreads / 2 : 0;  // wave-aligned when blockDim % 128 == 0
+  const bool lb_side = half && tid >= half;
+  const int base = lb_side ? tid - half : tid, stride = half ? half : nthreads;
+  for (int p = base; p < P; p += stride) {
     int t, tau;
     pair_of(p, t, tau);
-    ccmpc_halfspace h;
-    lb_s[p] = minkowski_pair(C, mu, ref, rows, t, tau, chi_r, chi_p, gamma, mp.R, mp.tol,
-                             mp.maxiter, h);
-    mp.out_rec[static_cast<int64_t>(cell) * P + p] = h;
+    if (lb_side || !half) {
+      const double lb = pair_lower_bound(pair_moments(C, rows, t, tau), gamma);
+      lb_s[p] = lb;
+      rec[p].lower_bound = lb;
+    }
+    if (!lb_side)
+      minkowski_pair(C, mu, ref, rows, t, tau, chi_r, chi_p, mp.R, mp.tol, mp.maxiter, rec + p);
   }
   __syncthreads();
   for (int t = tid; t < T; t += nthreads) {
