@@ -77,57 +77,46 @@ struct ItemLoc {
   int cell;
   int32_t ref_sel;  // cell_ref[cell] (0 when no table is given)
   int32_t chunk_idx;
+  int32_t first;    // the cell's first item (= its first level-0 tree node)
   int64_t cnt, off;
-  int32_t level_first[kMaxLevels + 1];  // index of the cell's first node at each tree level
 };
 
-// Item id -> (cell, chunk index, cell count, cell offset, and the cell's first node at every
-// level of the combine tree): one wave-parallel scan over the cells in 32-bit item arithmetic
-// (items and nodes < 2^31: the grid is sized by them), so everything the item needs arrives
-// with a single memory round trip.  False for ids past the last item (the grid is sized by an
-// upper bound).
+// Item id -> (cell, chunk index, the cell's first item, count, offset, reference selector):
+// one wave-parallel prefix scan of the cells' item counts in 32-bit arithmetic (items < 2^31:
+// the grid is sized by them), so everything an item needs arrives with one memory round trip.
+// The combine tree needs nothing more: its node numbering is closed-form in `first` (see
+// tree_next_first).  False for ids past the last item (the grid is sized by an upper bound).
 __device__ __forceinline__ bool locate_item(int32_t item, const int64_t *__restrict__ cnt,
                                             const int64_t *__restrict__ off, int n_cells,
                                             int lg_chunk, ItemLoc &loc,
                                             const int32_t *__restrict__ cell_ref = nullptr) {
   const int lane = threadIdx.x & 63;
-  int32_t before[kMaxLevels + 1];
-#pragma unroll
-  for (int l = 0; l <= kMaxLevels; ++l) before[l] = 0;
+  int32_t before = 0;
   for (int base = 0; base < n_cells; base += 64) {
     const int c = base + lane;
     const int64_t n = (c < n_cells) ? cnt[c] : 0;
     const int64_t o = (c < n_cells) ? off[c] : 0;
     const int32_t rs = (cell_ref && c < n_cells) ? cell_ref[c] : 0;  // same round trip
-    int32_t my = (c < n_cells) ? items_of(n, lg_chunk) : 0;
-    int32_t incl[kMaxLevels + 1], mine[kMaxLevels + 1];
+    const int32_t mine = (c < n_cells) ? items_of(n, lg_chunk) : 0;
+    int32_t incl = mine;
 #pragma unroll
-    for (int l = 0; l <= kMaxLevels; ++l) {
-      mine[l] = my;
-      incl[l] = my;
-#pragma unroll
-      for (int s = 1; s < 64; s <<= 1) {
-        const int32_t y = __shfl_up(incl[l], s, 64);
-        if (lane >= s) incl[l] += y;
-      }
-      my = (my + kFanIn - 1) >> kLgFanIn;
+    for (int s = 1; s < 64; s <<= 1) {
+      const int32_t y = __shfl_up(incl, s, 64);
+      if (lane >= s) incl += y;
     }
-    const int32_t total = __shfl(incl[0], 63, 64);
-    if (item < before[0] + total) {
-      const unsigned long long m = __ballot(before[0] + incl[0] > item);
+    const int32_t total = __shfl(incl, 63, 64);
+    if (item < before + total) {
+      const unsigned long long m = __ballot(before + incl > item);
       const int l = __ffsll(static_cast<long long>(m)) - 1;
       loc.cell = base + l;
-#pragma unroll
-      for (int k = 0; k <= kMaxLevels; ++k)
-        loc.level_first[k] = before[k] + __shfl(incl[k] - mine[k], l, 64);
-      loc.chunk_idx = item - loc.level_first[0];
+      loc.first = before + __shfl(incl - mine, l, 64);
+      loc.chunk_idx = item - loc.first;
       loc.cnt = __shfl(n, l, 64);
       loc.off = __shfl(o, l, 64);
       loc.ref_sel = __shfl(rs, l, 64);
       return true;
     }
-#pragma unroll
-    for (int k = 0; k <= kMaxLevels; ++k) before[k] += __shfl(incl[k], 63, 64);
+    before += total;
   }
   return false;
 }
@@ -143,26 +132,32 @@ __device__ __forceinline__ int64_t wave_prefix(int cell, F f) {
   return s;
 }
 
+// One lane's 4 consecutive particles of a row, in the store's element type: two 16-byte loads
+// (f64) or one (f32).  Kept unconverted until the consumer, so a load group has no use before
+// its MFMA phase (a convert right after the load would force the wait there).
 template <typename P>
-__device__ __forceinline__ void load4(const P *__restrict__ p, double (&v)[4]);
-
+struct Quad;
 template <>
-__device__ __forceinline__ void load4<double>(const double *__restrict__ p, double (&v)[4]) {
-  const double2 a = *reinterpret_cast<const double2 *>(p);
-  const double2 b = *reinterpret_cast<const double2 *>(p + 2);
-  v[0] = a.x;
-  v[1] = a.y;
-  v[2] = b.x;
-  v[3] = b.y;
+struct Quad<double> {
+  double2 lo, hi;
+  __device__ __forceinline__ double operator[](int j) const {
+    return j == 0 ? lo.x : j == 1 ? lo.y : j == 2 ? hi.x : hi.y;
+  }
+};
+template <>
+struct Quad<float> {
+  float4 v;
+  __device__ __forceinline__ double operator[](int j) const {
+    return static_cast<double>(j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w);
+  }
+};
+
+__device__ __forceinline__ void load_quad(const double *__restrict__ p, Quad<double> &q) {
+  q.lo = *reinterpret_cast<const double2 *>(p);
+  q.hi = *reinterpret_cast<const double2 *>(p + 2);
 }
-
-template <>
-__device__ __forceinline__ void load4<float>(const float *__restrict__ p, double (&v)[4]) {
-  const float4 a = *reinterpret_cast<const float4 *>(p);
-  v[0] = a.x;
-  v[1] = a.y;
-  v[2] = a.z;
-  v[3] = a.w;
+__device__ __forceinline__ void load_quad(const float *__restrict__ p, Quad<float> &q) {
+  q.v = *reinterpret_cast<const float4 *>(p);
 }
 
 // 16-byte write-through (sc1) buffer accesses: one dwordx4 transaction per lane instead of two
@@ -294,12 +289,20 @@ struct TreeLayout {
   double *slabs[kMaxLevels];      // level l: node slabs (level 0 = work items)
 };
 
-// nodes of a cell with `nit` items at level l
-__device__ __forceinline__ int64_t nodes_at(int64_t nit, int l) {
-  int64_t n = nit;
-  for (int i = 0; i < l; ++i) n = ceil_div(n, kFanIn);
-  return n;
+// Combine-tree numbering.  A cell's level-l nodes are [F_l, F_l + n_l); its level-(l+1) nodes
+// start at F_{l+1} = floor(F_l / 16) + cell.  Collision-free by induction: the next cell
+// starts at floor((F_l + n_l) / 16) + cell + 1 >= floor(F_l / 16) + ceil(n_l / 16) + cell, and
+// level l+1 never holds more than ceil(n_l / 16) of this cell's nodes.  So every level's first
+// node follows from the level-0 prefix alone (no per-level scans), and level l+1 needs at most
+// (level-l nodes) / 16 + n_cells + 1 slots (level_capacity).
+__device__ __forceinline__ int32_t tree_next_first(int32_t first_l, int cell) {
+  return (first_l >> kLgFanIn) + cell;
 }
+
+// A level with at most kRootFanIn nodes is combined by ONE last arriver (the root); larger
+// levels are reduced in fixed groups of kFanIn first.  Cells up to 64 items thus need a single
+// arrival round trip.
+constexpr int kRootFanIn = 64;
 
 // Host: capacity of level l (nodes) for n_cells cells holding <= max_items items in total.
 inline int64_t level_capacity(int64_t max_items, int64_t n_cells, int l) {
@@ -361,29 +364,31 @@ __device__ __forceinline__ double2 sum_group2(const double *__restrict__ slab0, 
 // Climb the tree from a published leaf.  Returns true in the workgroup that must finalise the
 // cell; then *root points at the last level's first slab and *root_n is its node count (<= 16).
 // node_prefix(l) must return the index of the cell's first level-l node within level l.
-template <int E, typename Prefix>
-__device__ bool tree_climb(const TreeLayout &L, int64_t idx, int64_t nit, Prefix node_prefix,
-                           int *flag, const double **root, int64_t *root_n) {
-  int64_t n_l = nit;
+template <int E>
+__device__ bool tree_climb(const TreeLayout &L, int32_t idx, int32_t nit, int32_t first0,
+                           int cell, int *flag, const double **root, int32_t *root_n) {
+  int32_t n_l = nit, first_l = first0;
   for (int l = 0; l < kMaxLevels; ++l) {
-    const int64_t grp = idx / kFanIn;
-    const int64_t gsize = (n_l - grp * kFanIn) < kFanIn ? (n_l - grp * kFanIn) : kFanIn;
-    const int64_t pre_l = node_prefix(l), pre_up = node_prefix(l + 1);
-    if (!arrive_last(L.counters[l] + pre_up + grp, gsize, flag)) return false;
-    const double *children = L.slabs[l] + (pre_l + grp * kFanIn) * E;
-    if (n_l <= kFanIn || l + 1 == kMaxLevels) {
-      *root = children;
-      *root_n = gsize;
+    const int32_t first_up = tree_next_first(first_l, cell);
+    const bool is_root = n_l <= kRootFanIn || l + 1 == kMaxLevels;
+    const int32_t grp = is_root ? 0 : idx >> kLgFanIn;
+    const int32_t gsize = is_root ? n_l : min(n_l - grp * kFanIn, kFanIn);
+    if (!arrive_last(L.counters[l] + first_up + grp, gsize, flag)) return false;
+    const double *children = L.slabs[l] + static_cast<int64_t>(first_l + grp * kFanIn) * E;
+    if (is_root) {
+      *root = L.slabs[l] + static_cast<int64_t>(first_l) * E;
+      *root_n = n_l;
       return true;
     }
-    double *parent = L.slabs[l + 1] + (pre_up + grp) * E;
+    double *parent = L.slabs[l + 1] + static_cast<int64_t>(first_up + grp) * E;
     const __amdgpu_buffer_rsrc_t rp = slab_rsrc(parent);
     for (int e = 2 * threadIdx.x; e < E; e += 2 * blockDim.x) {
       const double2 s = sum_group2(children, gsize, E, e);
       st2_sc1(rp, 8 * e, s.x, s.y);
     }
     idx = grp;
-    n_l = ceil_div(n_l, kFanIn);
+    n_l = (n_l + kFanIn - 1) >> kLgFanIn;
+    first_l = first_up;
   }
   return false;
 }
@@ -393,10 +398,16 @@ __device__ bool tree_climb(const TreeLayout &L, int64_t idx, int64_t nit, Prefix
 // second dependent global round trip for the Gram tiles after the row sums).  Ends with a
 // barrier.
 template <int E>
-__device__ __forceinline__ void gather_root(const double *__restrict__ root, int64_t root_n,
+__device__ __forceinline__ void gather_root(const double *__restrict__ root, int32_t root_n,
                                             double *dst_lds) {
   for (int e = 2 * threadIdx.x; e < E; e += 2 * blockDim.x) {
-    const double2 s = sum_group2(root, root_n, E, e);
+    double2 s = sum_group2(root, min(root_n, kFanIn), E, e);
+    for (int k = kFanIn; k < root_n; k += kFanIn) {  // fixed order: deterministic
+      const double2 t = sum_group2(root + static_cast<int64_t>(k) * E, min(root_n - k, kFanIn),
+                                   E, e);
+      s.x += t.x;
+      s.y += t.y;
+    }
     dst_lds[e] = s.x;
     dst_lds[e + 1] = s.y;
   }

@@ -56,7 +56,7 @@ namespace ccmpc {
 // the loop into branches, and the waitcnt pass then drained vmcnt(0) before every MFMA group --
 // waiting on the NEXT group's loads too, which serialised the double buffer.
 template <typename P, int RB, int S>
-__device__ __forceinline__ void load_group(double (&v)[S][RB][4], const P *const (&rowp)[RB],
+__device__ __forceinline__ void load_group(Quad<P> (&v)[S][RB], const P *const (&rowp)[RB],
                                            int64_t gbase, int64_t p1, int g) {
   const int64_t qlast = (p1 - 1) & ~int64_t(3);
 #pragma unroll
@@ -65,28 +65,29 @@ __device__ __forceinline__ void load_group(double (&v)[S][RB][4], const P *const
     const int64_t qc = q < qlast ? q : qlast;
 #pragma unroll
     for (int b = 0; b < RB; ++b) {
-#if CCMPC_PROBE & 2  // diagnostic build only: no memory traffic
-      for (int j = 0; j < 4; ++j) v[s][b][j] = static_cast<double>(qc + j + b) * 1e-3;
+#if CCMPC_PROBE & 2  // diagnostic build only: every lane re-reads one cached quad
+      load_quad(rowp[b] + (qc & 3), v[s][b]);
 #else
-      load4<P>(rowp[b] + qc, v[s][b]);
+      load_quad(rowp[b] + qc, v[s][b]);
 #endif
     }
   }
 }
 
-template <int RB, int S, int NACC>
-__device__ __forceinline__ void mfma_group(double (&v)[S][RB][4], const double (&sh)[RB],
+template <typename P, int RB, int S, int NACC>
+__device__ __forceinline__ void mfma_group(const Quad<P> (&raw)[S][RB], const double (&sh)[RB],
                                            const bool (&live)[RB], int64_t gbase, int64_t p1,
                                            int g, d4 (&acc)[NACC][n_tiles(RB)],
                                            double (&s1)[RB]) {
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int64_t q = gbase + 16 * s + 4 * g;
+    double v[RB][4];
 #pragma unroll
     for (int b = 0; b < RB; ++b)
 #pragma unroll
       for (int j = 0; j < 4; ++j)  // shifted; out-of-range slots and dead rows become 0
-        v[s][b][j] = (live[b] && q + j < p1) ? v[s][b][j] - sh[b] : 0.0;
+        v[b][j] = (live[b] && q + j < p1) ? raw[s][b][j] - sh[b] : 0.0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int a = (NACC == 2) ? (j & 1) : 0;
@@ -96,21 +97,23 @@ __device__ __forceinline__ void mfma_group(double (&v)[S][RB][4], const double (
 #pragma unroll
         for (int bj = bi; bj < RB; ++bj) {
 #if CCMPC_PROBE & 1  // diagnostic build only: no matrix-core work
-          acc[a][t][0] += v[s][bi][j] * v[s][bj][j];
+          acc[a][t][0] += v[bi][j] * v[bj][j];
 #else
-          acc[a][t] =
-              __builtin_amdgcn_mfma_f64_16x16x4f64(v[s][bi][j], v[s][bj][j], acc[a][t], 0, 0, 0);
+          acc[a][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[bi][j], v[bj][j], acc[a][t], 0, 0, 0);
 #endif
           ++t;
         }
     }
 #pragma unroll
-    for (int b = 0; b < RB; ++b) s1[b] += (v[s][b][0] + v[s][b][1]) + (v[s][b][2] + v[s][b][3]);
+    for (int b = 0; b < RB; ++b) s1[b] += (v[b][0] + v[b][1]) + (v[b][2] + v[b][3]);
   }
 }
 
 template <typename P, int RB, bool MINK>
-__global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void moments_kernel(
+// The fused half-space tail needs a few more registers than the 128 of 4 waves/SIMD at RB = 1.
+__global__ __launch_bounds__(Geo<RB>::NW * 64,
+                             (MINK && RB == 1) ? 3 : Geo<RB>::MIN_WAVES_PER_SIMD)
+void moments_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
     int lg_wq, TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void
   // MFMAs.  The prefetch is unconditional (a group past the end is clamped + masked and
   // never multiplied) so there is no divergent join for the waitcnt pass to merge.
   const int64_t ngroups = p1 > p0 ? ceil_div(p1 - p0, 16 * S) : 0;
-  double va[S][RB][4], vb[S][RB][4];
+  Quad<P> va[S][RB], vb[S][RB];
   // sched_barrier(0) fences keep the four phases in program order, so each MFMA group waits
   // (vmcnt) only for its own buffer while the other buffer's loads stay in flight.
   if (ngroups > 0) {
@@ -195,14 +198,14 @@ __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void
       const int64_t ga = p0 + gi * 16 * S, gb = ga + 16 * S;
       load_group<P, RB, S>(vb, rowp, gb, p1, g);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_group<RB, S, NACC>(va, sh, live, ga, p1, g, acc, s1);
+      mfma_group<P, RB, S, NACC>(va, sh, live, ga, p1, g, acc, s1);
       __builtin_amdgcn_sched_barrier(0);
       load_group<P, RB, S>(va, rowp, gb + 16 * S, p1, g);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_group<RB, S, NACC>(vb, sh, live, gb, p1, g, acc, s1);
+      mfma_group<P, RB, S, NACC>(vb, sh, live, gb, p1, g, acc, s1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (gi < ngroups) mfma_group<RB, S, NACC>(va, sh, live, p0 + gi * 16 * S, p1, g, acc, s1);
+    if (gi < ngroups) mfma_group<P, RB, S, NACC>(va, sh, live, p0 + gi * 16 * S, p1, g, acc, s1);
   }
   PROBE_TS(2);
 
@@ -227,10 +230,10 @@ __global__ __launch_bounds__(Geo<RB>::NW * 64, Geo<RB>::MIN_WAVES_PER_SIMD) void
   } else {
     combine_waves<RB, NACC, G::NW>(acc, s1, xch, tree.slabs[0] + blockIdx.x * E, false);
     PROBE_TS(3);
-    auto prefix = [&](int l) -> int64_t { return loc.level_first[l]; };
     const double *root;
-    int64_t root_n;
-    const bool last = tree_climb<E>(tree, loc.chunk_idx, nit, prefix, &flag, &root, &root_n);
+    int32_t root_n;
+    const bool last = tree_climb<E>(tree, loc.chunk_idx, nit, loc.first, cell, &flag, &root,
+                                    &root_n);
     PROBE_TS(4);
     if (!last) return;
     gather_root<E>(root, root_n, slab_lds);

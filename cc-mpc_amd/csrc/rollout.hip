@@ -255,10 +255,11 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
   }
 
   combine_waves<RB, 1, NW>(acc, s1, xch, tree.slabs[0] + item * E, false);
-  auto prefix = [&](int l) -> int64_t { return cell * nodes_at(items_per_cell, l); };
   const double *root;
-  int64_t root_n;
-  if (!tree_climb<E>(tree, cidx, items_per_cell, prefix, &flag, &root, &root_n)) return;
+  int32_t root_n;
+  if (!tree_climb<E>(tree, static_cast<int32_t>(cidx), static_cast<int32_t>(items_per_cell),
+                     static_cast<int32_t>(cell * items_per_cell), cell, &flag, &root, &root_n))
+    return;
   double *mean = out_mean + static_cast<int64_t>(cell) * rows;
   double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
   static_assert(NW * D * kStageStride >= E, "root staging reuses the sample stage");
