@@ -393,6 +393,116 @@ __device__ bool tree_climb(const TreeLayout &L, int32_t idx, int32_t nit, int32_
   return false;
 }
 
+// ---- Gram schemes: how a slab's entries map to Gram positions -------------------------------
+// Scheme16<RB>: f64 16x16x4 MFMA tiles (any T <= 40); Scheme4<NB>: f64 4x4x4_4b MFMA blocks of
+// 4 rows (T <= 12), which compute 4-row block pairs instead of 16-row tiles -- far less
+// padding work when 2T is not a multiple of 16 (T = 12: 21 block pairs = 336 products per
+// 16 particles vs 3 tiles = 768), at the same flop rate per cycle.
+template <int RB>
+struct Scheme16 {
+  static constexpr int GRAM = n_tiles(RB) * 256;
+  static constexpr int D = 16 * RB;
+  static constexpr int E = GRAM + D;
+  __device__ static void decode(int e, int &i, int &j) { decode_entry(e, RB, i, j); }
+};
+
+__host__ __device__ constexpr int n_pairs(int nb) { return nb * (nb + 1) / 2; }
+
+template <int NB>
+struct Scheme4 {
+  static constexpr int NP = n_pairs(NB);
+  static constexpr int GRAM = NP * 16;  // entry p*16 + 4i + j: G[4I + i][4J + j], pair p = (I, J)
+  static constexpr int D = 4 * NB;
+  static constexpr int E = GRAM + D;
+  __device__ static void decode(int e, int &i, int &j) {
+    int p = e >> 4, I = 0;
+    while (p >= NB - I) {  // pairs in row-major upper-triangle order
+      p -= NB - I;
+      ++I;
+    }
+    i = 4 * I + ((e >> 2) & 3);
+    j = 4 * (I + p) + (e & 3);
+  }
+};
+
+// DPP rotate within 16-lane rows (row_ror:k, dpp_ctrl 0x120 + k) of an f64, as two 32-bit moves.
+template <int K>
+__device__ __forceinline__ double row_ror(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x120 + K, 0xf, 0xf, false);
+  const int hi =
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), 0x120 + K, 0xf, 0xf, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) |
+                              static_cast<unsigned int>(lo));
+}
+
+// Scheme4 cross-wave combine.  acc[p] holds, in lane c + 4b + 16i, block b's partial of
+// G[4I + i][4J + c] (v_mfma_f64_4x4x4_4b layout: D[b][i][j] -> lane j + 4b + 16i); s1[I]
+// holds row 4I + c summed over this lane's particles.  The 4 blocks of a 16-lane row fold
+// with two DPP row rotations (register moves, no LDS traffic); lanes b == 0 then write one
+// E4-vector per wave (Gram entries final, row sums still split over the 4 rows i), and the
+// whole workgroup adds the waves (and the row-sum rows) in fixed order into dst -- an LDS slab,
+// or a global slab with 16-byte write-through stores.  Ends with a barrier.
+template <int NB>
+struct Combine4Layout {
+  static constexpr int GRAM = n_pairs(NB) * 16;
+  static constexpr int XS = GRAM + 16 * NB;  // per-wave exchange vector
+};
+
+template <int NB, int NW>
+__device__ __forceinline__ void combine4(const double (&acc)[n_pairs(NB)], const double (&s1)[NB],
+                                         double *xch, double *dst, bool to_lds) {
+  using Sch = Scheme4<NB>;
+  constexpr int XS = Combine4Layout<NB>::XS;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool writer = (lane & 12) == 0;  // b == 0
+  const int slot = 4 * (lane >> 4) + (lane & 3);  // 4i + c
+  double *mine = xch + w * XS;
+#pragma unroll
+  for (int p = 0; p < Sch::NP; ++p) {
+    double v = acc[p];
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    if (writer) mine[p * 16 + slot] = v;
+  }
+#pragma unroll
+  for (int I = 0; I < NB; ++I) {
+    double v = s1[I];
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    if (writer) mine[Sch::GRAM + 16 * I + slot] = v;  // row 4I + c, particle row i
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(dst);
+  for (int e = 2 * threadIdx.x; e < Sch::E; e += 2 * blockDim.x) {
+    double a = 0.0, b = 0.0;
+    if (e < Sch::GRAM) {
+#pragma unroll
+      for (int o = 0; o < NW; ++o) {
+        a += xch[o * XS + e];
+        b += xch[o * XS + e + 1];
+      }
+    } else {  // row sums: rows r = e - GRAM (block I = r / 4, c = r % 4), summed over i and w
+      const int r = e - Sch::GRAM, I = r >> 2, c = r & 3;
+      const double *base = xch + Sch::GRAM + 16 * I;
+#pragma unroll
+      for (int o = 0; o < NW; ++o)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a += base[o * XS + 4 * i + c];
+          b += base[o * XS + 4 * i + c + 1];
+        }
+    }
+    if (to_lds) {
+      dst[e] = a;
+      dst[e + 1] = b;
+    } else {
+      st2_sc1(rs, 8 * e, a, b);
+    }
+  }
+  __syncthreads();
+}
+
 // The last arriver's root combine: every summed entry pair of the n <= 16 root slabs into LDS
 // in ONE round of 16-byte sc1 loads (the finaliser then reads LDS only, instead of paying a
 // second dependent global round trip for the Gram tiles after the row sums).  Ends with a
@@ -419,18 +529,18 @@ __device__ __forceinline__ void gather_root(const double *__restrict__ root, int
 // shift_lds.  Writes cov to global memory and, when cov_lds != nullptr, to LDS as well (row
 // stride 2T) for the fused half-space tail.  Called by every thread of the workgroup; ends
 // with a barrier.
-template <int RB, typename Reader>
+template <typename Sch, typename Reader>
 __device__ void finalize_cell(Reader rd, int64_t cnt, int T, const double *shift_lds,
                               double *S_lds, double o0, double o1, double *__restrict__ mean,
                               double *__restrict__ cov, double *mean_lds, double *cov_lds) {
-  constexpr int NT = n_tiles(RB);
-  constexpr int D = 16 * RB;
+  constexpr int GRAM = Sch::GRAM;
+  constexpr int D = Sch::D;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int rows = 2 * T;
   const double n = static_cast<double>(cnt);
   // rd(e) returns the summed entry pair (e, e+1), e even
   for (int r = 2 * tid; r < D; r += 2 * nth) {
-    const double2 s = r < rows ? rd(NT * 256 + r) : double2{0.0, 0.0};
+    const double2 s = r < rows ? rd(GRAM + r) : double2{0.0, 0.0};
     S_lds[r] = s.x;
     S_lds[r + 1] = s.y;
   }
@@ -440,10 +550,10 @@ __device__ void finalize_cell(Reader rd, int64_t cnt, int T, const double *shift
     mean[r] = m;
     if (mean_lds) mean_lds[r] = m;
   }
-  for (int e = 2 * tid; e < NT * 256; e += 2 * nth) {
+  for (int e = 2 * tid; e < GRAM; e += 2 * nth) {
     int i0, j0, i1, j1;
-    decode_entry(e, RB, i0, j0);
-    decode_entry(e + 1, RB, i1, j1);
+    Sch::decode(e, i0, j0);
+    Sch::decode(e + 1, i1, j1);
     const bool use0 = i0 < rows && j0 < rows && i0 <= j0;  // one value per symmetric pair
     const bool use1 = i1 < rows && j1 < rows && i1 <= j1;
     if (!use0 && !use1) continue;

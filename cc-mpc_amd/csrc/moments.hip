@@ -109,6 +109,52 @@ __device__ __forceinline__ void mfma_group(const Quad<P> (&raw)[S][RB], const do
   }
 }
 
+// Everything after a work item's stream loop, shared by both Gram schemes: publish the item's
+// partial Gram (publish(dst, to_lds) = the scheme's cross-wave combine), then either finalise
+// in LDS (the cell is this one item) or climb the combine tree, and as the cell's last arriver
+// gather the root, finalise and (MINK) build the cell's half-spaces.
+struct EpilogueLds {
+  double *slab, *shift, *S, *mean, *cov, *lb, *ref;
+  int *flag;
+};
+
+template <typename Sch, bool MINK, bool COV_IN_LDS, typename Publish>
+__device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &loc, int32_t nit,
+                                              int T, const TreeLayout &tree,
+                                              const double *__restrict__ origin,
+                                              double *__restrict__ out_mean,
+                                              double *__restrict__ out_cov, const MinkParams &mp,
+                                              const EpilogueLds &L) {
+  constexpr int E = Sch::E;
+  const int cell = loc.cell, rows = 2 * T;
+  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
+  double *mean = out_mean + static_cast<int64_t>(cell) * rows;
+  double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
+  if (nit == 1) {
+    // the whole cell lives in this workgroup: combine in LDS, no global round trip
+    publish(L.slab, true);
+    PROBE_TS(3);
+    PROBE_TS(4);
+  } else {
+    publish(tree.slabs[0] + static_cast<int64_t>(blockIdx.x) * E, false);
+    PROBE_TS(3);
+    const double *root;
+    int32_t root_n;
+    const bool last = tree_climb<E>(tree, loc.chunk_idx, nit, loc.first, cell, L.flag, &root,
+                                    &root_n);
+    PROBE_TS(4);
+    if (!last) return;
+    gather_root<E>(root, root_n, L.slab);
+  }
+  finalize_cell<Sch>([&](int e) { return double2{L.slab[e], L.slab[e + 1]}; }, loc.cnt, T,
+                     L.shift, L.S, o0, o1, mean, cov, L.mean, COV_IN_LDS ? L.cov : nullptr);
+  PROBE_TS(5);
+  if (MINK)
+    minkowski_cell(COV_IN_LDS ? L.cov : cov, L.mean, T, cell, L.ref, L.ref[rows],
+                   L.ref[rows + 1], L.ref[rows + 2], mp, L.lb, threadIdx.x, blockDim.x);
+  PROBE_TS(6);
+}
+
 template <typename P, int RB, bool MINK>
 // The fused half-space tail needs a few more registers than the 128 of 4 waves/SIMD at RB = 1.
 __global__ __launch_bounds__(Geo<RB>::NW * 64,
@@ -215,37 +261,166 @@ void moments_kernel(
   for (int b = 0; b < RB; ++b) {
     if (w == 0 && g == 0) shift_lds[16 * b + r] = sh[b];
   }
-  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
-  double *mean = out_mean + static_cast<int64_t>(cell) * rows;
-  double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
+  const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
+  cell_epilogue<Scheme16<RB>, MINK, COV_IN_LDS>(
+      [&](double *dst, bool to_lds) { combine_waves<RB, NACC, G::NW>(acc, s1, xch, dst, to_lds); },
+      loc, nit, T, tree, origin, out_mean, out_cov, mp, L);
+}
 
-  if (nit == 1) {
-    // the whole cell lives in this workgroup: combine in LDS, no global round trip
-    combine_waves<RB, NACC, G::NW>(acc, s1, xch, slab_lds, true);
-    PROBE_TS(3);
-    PROBE_TS(4);
-    finalize_cell<RB>([&](int e) { return double2{slab_lds[e], slab_lds[e + 1]}; }, cnt, T,
-                      shift_lds, S_lds, o0, o1, mean, cov, mean_lds,
-                      COV_IN_LDS ? cov_lds : nullptr);
-  } else {
-    combine_waves<RB, NACC, G::NW>(acc, s1, xch, tree.slabs[0] + blockIdx.x * E, false);
-    PROBE_TS(3);
-    const double *root;
-    int32_t root_n;
-    const bool last = tree_climb<E>(tree, loc.chunk_idx, nit, loc.first, cell, &flag, &root,
-                                    &root_n);
-    PROBE_TS(4);
-    if (!last) return;
-    gather_root<E>(root, root_n, slab_lds);
-    finalize_cell<RB>([&](int e) { return double2{slab_lds[e], slab_lds[e + 1]}; }, cnt, T,
-                      shift_lds, S_lds, o0, o1, mean, cov, mean_lds,
-                      COV_IN_LDS ? cov_lds : nullptr);
+// ---- Scheme4: f64 4x4x4_4b MFMA over 4-row blocks (T <= 12) -------------------------------
+// Lane l holds row 4I + (l & 3) of block I for the 2 consecutive particles base + 2m, +1
+// (m = l >> 2; one 16-byte load per block, so a row's 16 lanes read 256 contiguous bytes and
+// an instruction covers whole lines).  Sub-step j feeds particle base + 2m + j: m = b + 4k is
+// the instruction's A[b][i][k] lane i + 4b + 16k, so ONE register per block is both the A
+// and the B operand of every block pair (I, J), as for the 16x16 tiles.  A group is 32
+// particles per wave.
+template <typename P>
+struct Pair;
+template <>
+struct Pair<double> {
+  double2 v;
+  __device__ __forceinline__ double operator[](int j) const { return j ? v.y : v.x; }
+};
+template <>
+struct Pair<float> {
+  float2 v;
+  __device__ __forceinline__ double operator[](int j) const {
+    return static_cast<double>(j ? v.y : v.x);
   }
-  PROBE_TS(5);
-  if (MINK)
-    minkowski_cell(COV_IN_LDS ? cov_lds : cov, mean_lds, T, cell, ref_lds, ref_lds[rows],
-                   ref_lds[rows + 1], ref_lds[rows + 2], mp, lb_s, threadIdx.x, blockDim.x);
-  PROBE_TS(6);
+};
+__device__ __forceinline__ void load_pair(const double *__restrict__ p, Pair<double> &q) {
+  q.v = *reinterpret_cast<const double2 *>(p);
+}
+__device__ __forceinline__ void load_pair(const float *__restrict__ p, Pair<float> &q) {
+  q.v = *reinterpret_cast<const float2 *>(p);
+}
+
+template <typename P, int NB>
+__device__ __forceinline__ void load_group4(Pair<P> (&v)[NB], const P *const (&rowp)[NB],
+                                            int64_t gbase, int64_t p1, int m) {
+  const int64_t qlast = (p1 - 1) & ~int64_t(1);
+  const int64_t q = gbase + 2 * m;
+  const int64_t qc = q < qlast ? q : qlast;
+#pragma unroll
+  for (int I = 0; I < NB; ++I) load_pair(rowp[I] + qc, v[I]);
+}
+
+template <typename P, int NB>
+__device__ __forceinline__ void mfma_group4(const Pair<P> (&raw)[NB], const double (&sh)[NB],
+                                            const bool (&live)[NB], int64_t gbase, int64_t p1,
+                                            int m, double (&acc)[n_pairs(NB)],
+                                            double (&s1)[NB]) {
+  const int64_t q = gbase + 2 * m;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    double v[NB];  // sub-step j: shifted; out-of-range slots and dead rows become 0
+#pragma unroll
+    for (int I = 0; I < NB; ++I) {
+      v[I] = (live[I] && q + j < p1) ? raw[I][j] - sh[I] : 0.0;
+      s1[I] += v[I];
+    }
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NB; ++I)
+#pragma unroll
+      for (int J = I; J < NB; ++J) {
+        acc[p] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[I], v[J], acc[p], 0, 0, 0);
+        ++p;
+      }
+  }
+}
+
+constexpr int kNW4 = 4;  // waves per Scheme4 work item
+
+template <typename P, int NB, bool MINK>
+__global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
+    int lg_wq, TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
+    MinkParams mp) {
+  using Sch = Scheme4<NB>;
+  constexpr int NP = Sch::NP, D = Sch::D, E = Sch::E;
+  __shared__ double xch[kNW4 * Combine4Layout<NB>::XS];
+  __shared__ double slab_lds[E];
+  __shared__ double shift_lds[D];
+  __shared__ double S_lds[D];
+  __shared__ double mean_lds[D];
+  __shared__ double cov_lds[MINK ? D * D : 1];
+  __shared__ double lb_s[MINK ? 12 * 11 / 2 : 1];
+  __shared__ double ref_lds[MINK ? D + 3 : 1];  // reference trajectory [T][2], then risk[3]
+  __shared__ int flag;
+
+  ItemLoc loc;
+  const int lg_chunk = lg_wq + 2;
+  const int64_t wq = int64_t(1) << lg_wq, chunk = int64_t(1) << lg_chunk;
+  PROBE_TS(0);
+  if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc,
+                   MINK ? mp.cell_ref : nullptr))
+    return;  // uniform
+  PROBE_TS(1);
+  const int64_t cnt = loc.cnt;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+  const int c = lane & 3, m = lane >> 2;
+  const int rows = 2 * T;
+  const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
+  double pre = 0.0;  // the half-space tail's per-cell inputs, landing behind the stream loop
+  if (MINK) {
+    if (threadIdx.x < rows)
+      pre = mp.ref_traj[static_cast<int64_t>(loc.ref_sel) * rows + threadIdx.x];
+    else if (threadIdx.x < rows + 3)
+      pre = mp.cell_risk[3 * loc.cell + (threadIdx.x - rows)];
+  }
+  const int64_t i1 = (i0 + chunk < cnt) ? i0 + chunk : cnt;
+  const int64_t p0 = i0 + static_cast<int64_t>(w) * wq;
+  const int64_t p1 = (p0 + wq < i1) ? p0 + wq : i1;
+
+  double sh[NB];
+  const P *rowp[NB];
+  bool live[NB];
+#pragma unroll
+  for (int I = 0; I < NB; ++I) {
+    const int R = 4 * I + c;
+    live[I] = R < rows;
+    rowp[I] = pos + static_cast<int64_t>(live[I] ? R : 0) * ld + loc.off;
+    sh[I] = (live[I] && cnt > 0) ? static_cast<double>(rowp[I][0]) : 0.0;
+  }
+  double acc[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) acc[p] = 0.0;
+  double s1[NB];
+#pragma unroll
+  for (int I = 0; I < NB; ++I) s1[I] = 0.0;
+
+  const int64_t ngroups = p1 > p0 ? ceil_div(p1 - p0, 32) : 0;
+  Pair<P> va[NB], vb[NB];
+  if (ngroups > 0) {
+    load_group4<P, NB>(va, rowp, p0, p1, m);
+    int64_t gi = 0;
+    for (; gi + 2 <= ngroups; gi += 2) {
+      const int64_t ga = p0 + gi * 32, gb = ga + 32;
+      load_group4<P, NB>(vb, rowp, gb, p1, m);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_group4<P, NB>(va, sh, live, ga, p1, m, acc, s1);
+      __builtin_amdgcn_sched_barrier(0);
+      load_group4<P, NB>(va, rowp, gb + 32, p1, m);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_group4<P, NB>(vb, sh, live, gb, p1, m, acc, s1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (gi < ngroups) mfma_group4<P, NB>(va, sh, live, p0 + gi * 32, p1, m, acc, s1);
+  }
+  PROBE_TS(2);
+
+  const int32_t nit = items_of(cnt, lg_chunk);
+  if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
+#pragma unroll
+  for (int I = 0; I < NB; ++I)
+    if (w == 0 && m == 0) shift_lds[4 * I + c] = sh[I];
+  const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
+  cell_epilogue<Sch, MINK, MINK>(
+      [&](double *dst, bool to_lds) { combine4<NB, kNW4>(acc, s1, xch, dst, to_lds); }, loc,
+      nit, T, tree, origin, out_mean, out_cov, mp, L);
 }
 
 template <typename P, int RB, bool MINK>
@@ -260,10 +435,39 @@ static void launch(const P *pos, int64_t ld, int T, const double *origin, const 
                      tree, mean, cov, mp);
 }
 
+template <typename P, int NB, bool MINK>
+static void launch4(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
+                    const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
+                    double *cov, const MinkParams &mp, hipStream_t s) {
+  const int lg_wq = store_lg_wave_quota(1, n_bound);
+  const int64_t items = max_items(n_cells, n_bound, int64_t(1) << (lg_wq + 2));
+  const TreeLayout tree = tree_layout(ws, items, n_cells, Scheme4<NB>::E);
+  hipLaunchKernelGGL((moments4_kernel<P, NB, MINK>), dim3(static_cast<unsigned>(items)),
+                     dim3(kNW4 * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
+                     mean, cov, mp);
+}
+
+// Scheme4 (4-row blocks) where 16-row tiles would pad heavily: T = 9..12 (18-24 rows in two
+// 16-row blocks; C4 at T = 12: 30 -> 38 us moments-only with Scheme16).  At T <= 8 the 16 rows
+// fill one tile exactly and Scheme16's cheaper combine wins (C2: 11.7 vs 12.5 us); above
+// T = 12 the block-pair accumulators outgrow the register file.
+inline int scheme4_blocks(int64_t T) {
+  return (T > 8 && T <= 12) ? static_cast<int>((2 * T + 3) / 4) : 0;
+}
+
 template <typename P, bool MINK>
 static int dispatch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
                     const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
                     double *cov, const MinkParams &mp, hipStream_t s) {
+  switch (scheme4_blocks(T)) {
+    case 1: launch4<P, 1, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
+    case 2: launch4<P, 2, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
+    case 3: launch4<P, 3, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
+    case 4: launch4<P, 4, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
+    case 5: launch4<P, 5, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
+    case 6: launch4<P, 6, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
+    default: break;
+  }
   switch (row_blocks(T)) {
     case 1: launch<P, 1, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
     case 2: launch<P, 2, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
@@ -319,6 +523,12 @@ extern "C" int ccmpc_probe_timestamps(void *host, int reset) {
 extern "C" size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells,
                                                 int64_t n_particles_bound) {
   if (T < 1 || T > kMaxT || n_cells < 0 || n_particles_bound < 0) return 0;
+  const int nb = scheme4_blocks(T);
+  if (nb > 0) {
+    const int64_t items = max_items(
+        n_cells, n_particles_bound, int64_t(1) << (store_lg_wave_quota(1, n_particles_bound) + 2));
+    return tree_bytes(items, n_cells, n_pairs(nb) * 16 + 4 * nb);
+  }
   const int rb = row_blocks(T);
   const int64_t items =
       max_items(n_cells, n_particles_bound, int64_t(1) << store_lg_chunk(rb, n_particles_bound));

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
   double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
   static_assert(NW * D * kStageStride >= E, "root staging reuses the sample stage");
   gather_root<E>(root, root_n, stage_all);  // the sample stage is free after combine_waves
-  finalize_cell<RB>([&](int e) { return double2{stage_all[e], stage_all[e + 1]}; }, n, T,
+  finalize_cell<Scheme16<RB>>([&](int e) { return double2{stage_all[e], stage_all[e + 1]}; }, n, T,
                     shift_s, S_lds, 0.0, 0.0, mean, cov, mean_lds, nullptr);
   if (MINK) minkowski_cell(cov, mean_lds, T, cell, mp, lb_s, threadIdx.x, blockDim.x);
 }

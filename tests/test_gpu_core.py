@@ -39,6 +39,9 @@ def oracle_cell_moments(cell):
     (1, [2, 3, 17]),
     (3, [5, 15, 16, 17, 63, 64, 65]),
     (12, [256, 97, 1000]),
+    (9, [4, 2, 255, 256, 257]),          # 4-row-block (Scheme4) path from here to T = 12
+    (10, [20000, 31, 4096]),             # > 64 items: two combine-tree levels
+    (11, [700, 5, 1300]),
     (20, [33, 700]),
     (40, [129, 2051]),
 ])
@@ -56,12 +59,12 @@ def test_moments_f64_match_numpy(gpu, T, counts):
         np.testing.assert_array_equal(cov[j], cov[j].T)
 
 
-def test_moments_f32_relative_store(gpu):
+@pytest.mark.parametrize("T", [8, 11])
+def test_moments_f32_relative_store(gpu, T):
     """Trajectron++ hands float32 scene-relative positions; the reference adds minpos in
     float64 (v8ideal/__init__.py:486).  The F32 store keeps them relative + per-cell origin."""
     eng = ccmpc()
     rng = np.random.default_rng(5)
-    T = 8
     minpos = np.array([123.25, -211.5])
     rel = [np.cumsum(rng.normal(0, 0.7, size=(n, T, 2)), axis=1).astype(np.float32) + 60
            for n in (511, 64, 3)]

@@ -15,9 +15,10 @@ def eng():
     return e
 
 
-def test_fused_cycle_bitwise_equals_two_calls(gpu, golden):
+@pytest.mark.parametrize("name", ["cycle_o2_t8", "cycle_o1_t12"])  # 16-row tiles / 4-row blocks
+def test_fused_cycle_bitwise_equals_two_calls(gpu, golden, name):
     from ccmpc import cycle
-    g = golden("cycle_o2_t8")
+    g = golden(name)
     T = int(g["T"])
     store = eng().ParticleStore.from_cells(cells_from_fixture(g), device=gpu)
     cyc = cycle.MinkowskiCycle(store, [int(k) for k in g["K"]], g["ref_traj"])

@@ -19,6 +19,19 @@ __global__ __launch_bounds__(256) void mfma_loop(double *out, double a0) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+__global__ __launch_bounds__(256) void mfma4_loop(double *out, double a0) {
+  double acc[8];
+  for (int i = 0; i < 8; ++i) acc[i] = 0;
+  double a = a0 + threadIdx.x, b = a0 - threadIdx.x;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, acc[i], 0, 0, 0);
+  }
+  double s = 0;
+  for (int i = 0; i < 8; ++i) s += acc[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 __global__ __launch_bounds__(256) void fma_loop(double *out, double a0) {
   double acc[16];
   for (int i = 0; i < 16; ++i) acc[i] = i;
@@ -52,6 +65,17 @@ int main() {
     const double flops = n_mfma * 16 * 16 * 4 * 2;
     printf("mfma_f64_16x16x4 waves/SIMD=%d: %.3f ms  %.1f TFLOP/s  %.1f cycles/MFMA/SIMD @2.4GHz\n",
            wps, ms, flops / ms / 1e9, (ms * 1e-3 * 2.4e9) / (n_mfma / 1024));
+    mfma4_loop<<<blocks, 256>>>(out, 1.0);
+    hipEventRecord(e0);
+    mfma4_loop<<<blocks, 256>>>(out, 1.0);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&ms, e0, e1);
+    {
+      const double n4 = double(blocks) * 4 * ITERS * 8;
+      printf("mfma_f64_4x4x4_4b waves/SIMD=%d: %.3f ms  %.1f TFLOP/s  %.1f cycles/MFMA/SIMD @2.4GHz\n",
+             wps, ms, n4 * 4 * 4 * 4 * 4 * 2 / ms / 1e9, (ms * 1e-3 * 2.4e9) / (n4 / 1024));
+    }
     fma_loop<<<blocks, 256>>>(out, 1.0);
     hipEventRecord(e0);
     fma_loop<<<blocks, 256>>>(out, 1.0);
