@@ -51,34 +51,40 @@ def parse():
     return ap.parse_args()
 
 
+def time_config(dev, seed, name, O, N, T, scenes):
+    """Kernel time and algorithmic HBM rate of the one-launch cycle (and of the moment
+    reduction alone) for one synthetic configuration."""
+    from ccmpc import cycle, engine, synthetic
+    cells, K, refs = [], [], []
+    for sc in range(scenes):
+        ovs, ref, _ = synthetic.scene(seed + 1000 + sc, O=O, N=N, T=T)
+        cells += [c for o in ovs for c in o]
+        K += [len(o) for o in ovs]
+        refs.append(ref)
+    store = engine.ParticleStore.from_cells(cells, device=dev)
+    cyc = cycle.MinkowskiCycle(store, K, refs[0])
+    t = time_kernel_live(cyc.run, dev, per_graph=10, replays=5)
+    tm = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev,
+                          per_graph=10, replays=5)
+    b = int(sum(store.counts)) * 2 * T * 8
+    return {"config": name, "particles": int(sum(store.counts)), "T": T,
+            "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
+            "alg_GBps": round(b / t / 1e9, 1), "frac": round(b / t / HBM_PEAK, 4),
+            "moments_only_us": round(tm * 1e6, 2),
+            "moments_only_frac": round(b / tm / HBM_PEAK, 4)}
+
+
+C4_GPU = ("C4/GPU@8: 8 scenes x 4 OVs np=20000 T=12", 4, 20000, 12, 8)
+
+
 def sweep(dev, seed):
-    """Kernel time and algorithmic HBM rate of the one-launch cycle at the configs where the
-    path is bandwidth-bound.  Not part of `value`."""
-    from ccmpc import cycle, engine, risk, synthetic
-    rows = []
+    """The one-launch cycle at the configs where the path is bandwidth-bound.
+    Not part of `value`."""
+    from ccmpc import engine, risk, synthetic
     configs = [("C3 np=1000 O=1 T=8", 1, 1000, 8, 1), ("C3 np=5000 O=1 T=8", 1, 5000, 8, 1),
                ("C3 np=20000 O=1 T=8", 1, 20000, 8, 1), ("C3 np=100000 O=1 T=8", 1, 100000, 8, 1),
-               ("C4/GPU@8: 8 scenes x 4 OVs np=20000 T=12", 4, 20000, 12, 8),
-               ("C5 O=8 np=50000 T=40", 8, 50000, 40, 1)]
-    for name, O, N, T, scenes in configs:
-        cells, K, refs = [], [], []
-        for sc in range(scenes):
-            ovs, ref, _ = synthetic.scene(seed + 1000 + sc, O=O, N=N, T=T)
-            cells += [c for o in ovs for c in o]
-            K += [len(o) for o in ovs]
-            refs.append(ref)
-        store = engine.ParticleStore.from_cells(cells, device=dev)
-        cyc = cycle.MinkowskiCycle(store, K, refs[0])
-        t = time_kernel_live(cyc.run, dev, per_graph=10, replays=5)
-        tm = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev,
-                              per_graph=10, replays=5)
-        b = int(sum(store.counts)) * 2 * T * 8
-        rows.append({"config": name, "particles": int(sum(store.counts)), "T": T,
-                     "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
-                     "alg_GBps": round(b / t / 1e9, 1), "frac": round(b / t / HBM_PEAK, 4),
-                     "moments_only_us": round(tm * 1e6, 2),
-                     "moments_only_frac": round(b / tm / HBM_PEAK, 4)})
-        del store, cyc
+               C4_GPU, ("C5 O=8 np=50000 T=40", 8, 50000, 40, 1)]
+    rows = [time_config(dev, seed, *c) for c in configs]
     # shrinking-horizon step: 1e6-sample ideal rollout fused with moments + half-spaces
     ovs, ref, _ = synthetic.scene(seed + 7, O=1, N=100000, T=8, K=2)
     store = engine.ParticleStore.from_cells(ovs[0], device=dev)
@@ -316,6 +322,14 @@ def main():
                       "oracle restatement of v8ideal/__init__.py:881-947 (numpy/scipy)",
         }
         out["speedup_vs_cpu"] = round(value / (1.0 / med), 1)
+    if rank == 0:
+        # C2 is launch/latency-bound (2.56 MB per cycle); the HBM roofline of the
+        # same kernel is meaningful at the per-GPU C4 batch, reported beside it
+        c4 = time_config(dev, args.seed, *C4_GPU)
+        c4["traffic"], c4["traffic_source"] = pmc_traffic(
+            "void ccmpc::moments4_kernel<double, 6, true>")
+        c4["alg_bytes_per_launch"] = c4["particles"] * 2 * C4_GPU[3] * 8
+        out["roofline_c4_batch"] = c4
     if args.sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)
     if rank == 0:
