@@ -190,6 +190,58 @@ def cpu_baseline(ovs, ref, T, cycles):
     return best[0], best[1], best[2], total
 
 
+def episode_c1(dev, cpu_steps=2, with_cpu=True):
+    """BASELINE configs[0] (tests/Hz20/test_montecarlo.py v8ideal scene4_ov1_brake ph8
+    np5000): one obstacle, the full planning schedule of an episode through
+    MidlevelAgent -- 8 shrinking Minkowski steps (T = 8..1; T < 8 on 1e6-sample predict_ideal
+    rollouts) and 4 receding GMM-affine steps -- each step end to end (GPU sampler -> bucketing
+    -> one fused launch -> host HalfSpace objects), synchronised.  Beside it, the oracle on the
+    first `cpu_steps` planning steps with the same particles and the same Philox draws."""
+    from ccmpc import episode
+    rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=1_000_000, receding_steps=4,
+                                device=dev)
+    rep.run()                                   # warm-up (allocations, first launches)
+    rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=1_000_000, receding_steps=4,
+                                device=dev)
+    log = rep.run()
+    out = {"config": "C1 schedule: 1 OV, np=5000, ph=8, n_ideal=1e6, 8 shrinking + 4 receding "
+                     "planning steps (synthetic GMM predictions)",
+           "steps": [{k: (round(v, 3) if k == "ms" else v) for k, v in st.items()}
+                     for st in log],
+           "total_ms": round(sum(st["ms"] for st in log), 3)}
+    if not with_cpu:
+        return out
+    from oracle import ccmpc_oracle as orc
+    rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=1_000_000, receding_steps=0,
+                                device=dev)
+    cpu = []
+    mom = None
+    for frame, T, kind in rep.schedule()[:cpu_steps]:
+        ovs, _ = rep.step(frame, T, kind)
+        K = [ov.n_states for ov in ovs]
+        cells = [[np.asarray(p, float) for p in ov.pred_positions] for ov in ovs]
+        pasts = [np.asarray(ov.past, float).reshape(-1, 2) for ov in ovs]
+        t0 = time.perf_counter()
+        oovs = [orc.OVehicle(T, pasts[o], np.ones(K[o]) / K[o], cells[o],
+                             [orc._step_yaws(c, pasts[o][-1], rep.ph) for c in cells[o]],
+                             np.zeros((K[o], 2)), np.array([4.5, 2.5])) for o in range(len(K))]
+        if T == rep.ph:
+            orc.minkowski_generator(oovs, T, rep.ph, rep.ref_traj(frame), with_l4=False)
+            mom = orc.save_moments(cells, T)
+        else:
+            ideal = orc.predict_ideal(mom, K, T, 1_000_000, seed=frame)
+            orc.minkowski_generator(oovs, T, rep.ph, rep.ref_traj(frame), ideal_trajs=ideal,
+                                    with_l4=False)
+            mom = orc.save_moments([[ideal[o][k] for k in range(K[o])]
+                                    for o in range(len(K))], T)
+        cpu.append({"frame": frame, "T": T, "ms": round((time.perf_counter() - t0) * 1e3, 1)})
+    out["cpu_oracle_sample"] = {
+        "steps": cpu, "cores": 1, "kind": "port",
+        "note": "oracle restatement of v8ideal/__init__.py:781-964 + :2620-2711 on the first "
+                f"{cpu_steps} planning steps (generators only; no sampler, no bucketing)"}
+    return out
+
+
 def pmc_traffic(kernel_prefix):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
     (profiles/<round>/summary.json, written by profiles/collect.sh on this same default
@@ -322,6 +374,23 @@ def main():
                       "oracle restatement of v8ideal/__init__.py:881-947 (numpy/scipy)",
         }
         out["speedup_vs_cpu"] = round(value / (1.0 / med), 1)
+    if world > 1:
+        # the north star's one exchange: every rank's fixed-size half-space records gathered
+        # over RCCL (xGMI).  The QP of a scene stays on its owning rank, so this is reported
+        # beside `value`, not inside the timed step.
+        from ccmpc import dist as cdist
+        rec2 = cyc.rec.view(cyc.rec.shape[0], -1, 128)
+        for _ in range(5):
+            cdist.gather_records(rec2)
+        torch.cuda.synchronize(dev)
+        barrier(world)
+        tg = time.perf_counter()
+        for _ in range(50):
+            cdist.gather_records(rec2)
+        torch.cuda.synchronize(dev)
+        tg = max_over_ranks((time.perf_counter() - tg) / 50, world, dev)
+        out["record_allgather"] = {"us": round(tg * 1e6, 2),
+                                   "bytes_per_rank": int(rec2.numel()), "backend": "nccl(RCCL)"}
     if rank == 0:
         # C2 is launch/latency-bound (2.56 MB per cycle); the HBM roofline of the
         # same kernel is meaningful at the per-GPU C4 batch, reported beside it
@@ -330,6 +399,10 @@ def main():
             "void ccmpc::moments4_kernel<double, 6, true>")
         c4["alg_bytes_per_launch"] = c4["particles"] * 2 * C4_GPU[3] * 8
         out["roofline_c4_batch"] = c4
+    if rank == 0 and world == 1:
+        from threadpoolctl import threadpool_limits
+        with threadpool_limits(limits=1):
+            out["episode_c1"] = episode_c1(dev, with_cpu=not args.no_cpu)
     if args.sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)
     if rank == 0:

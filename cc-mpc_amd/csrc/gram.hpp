@@ -318,28 +318,52 @@ inline size_t tree_counter_bytes(int64_t max_items, int64_t n_cells) {
   return (ctr + kCounterAlign - 1) / kCounterAlign * kCounterAlign;
 }
 
-inline size_t tree_bytes(int64_t max_items, int64_t n_cells, int E) {
+inline size_t tree_slab_bytes(int64_t max_items, int64_t n_cells, int E) {
   size_t slab = 0;
   for (int l = 0; l < kMaxLevels; ++l)
     slab += static_cast<size_t>(level_capacity(max_items, n_cells, l)) * E * sizeof(double);
-  return tree_counter_bytes(max_items, n_cells) + slab;
+  return slab;
 }
 
-inline TreeLayout tree_layout(void *ws, int64_t max_items, int64_t n_cells, int E) {
-  TreeLayout L;
+// Workspace layout.  The arrival counters live in the first ctr_region(ws_bytes) =
+// round_up(ws_bytes / 32, 256) bytes -- a function of the WHOLE buffer only -- and the slabs
+// after it.  Calls of different shapes sharing one buffer (e.g. a moments call on a small
+// store, then a 1e6-sample rollout) therefore agree on where counters are: a per-call
+// counter size would let one call's slabs land on another call's counters, which must be
+// zero when a launch starts (every launch leaves them zero).  Counters are <= 1.7 % of the
+// slab bytes (E >= 176 doubles per node), so 1/32 of the buffer always holds them.
+inline size_t ctr_region(size_t ws_bytes) {
+  return (ws_bytes / 32 + kCounterAlign - 1) / kCounterAlign * kCounterAlign;
+}
+
+inline size_t tree_bytes(int64_t max_items, int64_t n_cells, int E) {
+  const size_t c = tree_counter_bytes(max_items, n_cells);
+  const size_t s = tree_slab_bytes(max_items, n_cells, E);
+  size_t ws = (c + s) + (c + s) / 31 + 2 * kCounterAlign;  // ws - ctr_region(ws) >= s
+  if (ctr_region(ws) < c) ws = 32 * c;                     // never binds at E >= 176
+  return (ws + kCounterAlign - 1) / kCounterAlign * kCounterAlign;
+}
+
+// False when the buffer cannot hold this call's counters or slabs.
+inline bool tree_layout(void *ws, size_t ws_bytes, int64_t max_items, int64_t n_cells, int E,
+                        TreeLayout &L) {
+  const size_t region = ctr_region(ws_bytes);
+  if (tree_counter_bytes(max_items, n_cells) > region ||
+      region + tree_slab_bytes(max_items, n_cells, E) > ws_bytes)
+    return false;
   int32_t *c = static_cast<int32_t *>(ws);
   for (int l = 0; l < kMaxLevels; ++l) {
     L.counters[l] = c;
     c += level_capacity(max_items, n_cells, l + 1);
   }
-  double *s = reinterpret_cast<double *>(static_cast<char *>(ws) +
-                                         tree_counter_bytes(max_items, n_cells));
+  double *s = reinterpret_cast<double *>(static_cast<char *>(ws) + region);
   for (int l = 0; l < kMaxLevels; ++l) {
     L.slabs[l] = s;
     s += level_capacity(max_items, n_cells, l) * E;
   }
-  return L;
+  return true;
 }
+
 
 // Sum the entry pair (e, e+1), e even, over n <= kFanIn consecutive slabs: all 16-byte sc1 loads
 // issued first (indices clamped, no per-load branch), then a fixed-order sum.
@@ -362,8 +386,8 @@ __device__ __forceinline__ double2 sum_group2(const double *__restrict__ slab0, 
 }
 
 // Climb the tree from a published leaf.  Returns true in the workgroup that must finalise the
-// cell; then *root points at the last level's first slab and *root_n is its node count (<= 16).
-// node_prefix(l) must return the index of the cell's first level-l node within level l.
+// cell; then *root points at the root level's first slab and *root_n is its node count
+// (<= kRootFanIn).  first0 is the cell's first item; deeper levels follow tree_next_first.
 template <int E>
 __device__ bool tree_climb(const TreeLayout &L, int32_t idx, int32_t nit, int32_t first0,
                            int cell, int *flag, const double **root, int32_t *root_n) {

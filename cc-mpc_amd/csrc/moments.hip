@@ -189,7 +189,6 @@ void moments_kernel(
                    MINK ? mp.cell_ref : nullptr))
     return;  // uniform
   PROBE_TS(1);
-  const int cell = loc.cell;
   const int64_t cnt = loc.cnt;
 
   const int lane = threadIdx.x & 63;
@@ -424,27 +423,31 @@ __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
 }
 
 template <typename P, int RB, bool MINK>
-static void launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
-                   const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
-                   double *cov, const MinkParams &mp, hipStream_t s) {
+static int launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
+                  const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
+                  double *mean, double *cov, const MinkParams &mp, hipStream_t s) {
   const int lg_wq = store_lg_wave_quota(RB, n_bound);
   const int64_t items = max_items(n_cells, n_bound, int64_t(1) << store_lg_chunk(RB, n_bound));
-  const TreeLayout tree = tree_layout(ws, items, n_cells, slab_doubles(RB));
+  TreeLayout tree;
+  if (!tree_layout(ws, ws_bytes, items, n_cells, slab_doubles(RB), tree)) return CCMPC_ERR_WORKSPACE;
   hipLaunchKernelGGL((moments_kernel<P, RB, MINK>), dim3(static_cast<unsigned>(items)),
                      dim3(Geo<RB>::NW * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq,
                      tree, mean, cov, mp);
+  return CCMPC_OK;
 }
 
 template <typename P, int NB, bool MINK>
-static void launch4(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
-                    const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
-                    double *cov, const MinkParams &mp, hipStream_t s) {
+static int launch4(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
+                   const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
+                   double *mean, double *cov, const MinkParams &mp, hipStream_t s) {
   const int lg_wq = store_lg_wave_quota(1, n_bound);
   const int64_t items = max_items(n_cells, n_bound, int64_t(1) << (lg_wq + 2));
-  const TreeLayout tree = tree_layout(ws, items, n_cells, Scheme4<NB>::E);
+  TreeLayout tree;
+  if (!tree_layout(ws, ws_bytes, items, n_cells, Scheme4<NB>::E, tree)) return CCMPC_ERR_WORKSPACE;
   hipLaunchKernelGGL((moments4_kernel<P, NB, MINK>), dim3(static_cast<unsigned>(items)),
                      dim3(kNW4 * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
                      mean, cov, mp);
+  return CCMPC_OK;
 }
 
 // Scheme4 (4-row blocks) where 16-row tiles would pad heavily: T = 9..12 (18-24 rows in two
@@ -457,44 +460,48 @@ inline int scheme4_blocks(int64_t T) {
 
 template <typename P, bool MINK>
 static int dispatch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
-                    const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, double *mean,
-                    double *cov, const MinkParams &mp, hipStream_t s) {
+                    const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
+                    double *mean, double *cov, const MinkParams &mp, hipStream_t s) {
+#define CCMPC_ARGS pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, ws_bytes, mean, cov, mp, s
   switch (scheme4_blocks(T)) {
-    case 1: launch4<P, 1, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
-    case 2: launch4<P, 2, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
-    case 3: launch4<P, 3, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
-    case 4: launch4<P, 4, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
-    case 5: launch4<P, 5, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
-    case 6: launch4<P, 6, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); return CCMPC_OK;
+    case 1: return launch4<P, 1, MINK>(CCMPC_ARGS);
+    case 2: return launch4<P, 2, MINK>(CCMPC_ARGS);
+    case 3: return launch4<P, 3, MINK>(CCMPC_ARGS);
+    case 4: return launch4<P, 4, MINK>(CCMPC_ARGS);
+    case 5: return launch4<P, 5, MINK>(CCMPC_ARGS);
+    case 6: return launch4<P, 6, MINK>(CCMPC_ARGS);
     default: break;
   }
   switch (row_blocks(T)) {
-    case 1: launch<P, 1, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
-    case 2: launch<P, 2, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
-    case 3: launch<P, 3, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
-    case 4: launch<P, 4, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
-    case 5: launch<P, 5, MINK>(pos, ld, T, origin, off, cnt, n_cells, n_bound, ws, mean, cov, mp, s); break;
+    case 1: return launch<P, 1, MINK>(CCMPC_ARGS);
+    case 2: return launch<P, 2, MINK>(CCMPC_ARGS);
+    case 3: return launch<P, 3, MINK>(CCMPC_ARGS);
+    case 4: return launch<P, 4, MINK>(CCMPC_ARGS);
+    case 5: return launch<P, 5, MINK>(CCMPC_ARGS);
     default: return CCMPC_ERR_UNSUPPORTED;
   }
-  return CCMPC_OK;
+#undef CCMPC_ARGS
 }
 
 template <bool MINK>
 static int run(const void *positions, int dtype, int64_t ld, int64_t T, const double *origin,
                const int64_t *cell_off, const int64_t *cell_cnt, int64_t n_cells,
-               int64_t n_bound, void *workspace, double *out_mean, double *out_cov,
-               const MinkParams &mp, ccmpc_stream_t stream, const char *who) {
+               int64_t n_bound, void *workspace, size_t ws_bytes, double *out_mean,
+               double *out_cov, const MinkParams &mp, ccmpc_stream_t stream, const char *who) {
   hipStream_t s = as_stream(stream);
   const int Ti = static_cast<int>(T), nc = static_cast<int>(n_cells);
   int rc;
   if (dtype == CCMPC_F64)
     rc = dispatch<double, MINK>(static_cast<const double *>(positions), ld, Ti, origin, cell_off,
-                                cell_cnt, nc, n_bound, workspace, out_mean, out_cov, mp, s);
+                                cell_cnt, nc, n_bound, workspace, ws_bytes, out_mean, out_cov, mp,
+                                s);
   else
     rc = dispatch<float, MINK>(static_cast<const float *>(positions), ld, Ti, origin, cell_off,
-                               cell_cnt, nc, n_bound, workspace, out_mean, out_cov, mp, s);
+                               cell_cnt, nc, n_bound, workspace, ws_bytes, out_mean, out_cov, mp,
+                               s);
   if (rc != CCMPC_OK) {
-    set_error(std::string(who) + ": unsupported T");
+    set_error(std::string(who) + (rc == CCMPC_ERR_WORKSPACE ? ": workspace too small"
+                                                            : ": unsupported T"));
     return rc;
   }
   hipError_t e = hipGetLastError();
@@ -557,7 +564,7 @@ extern "C" int ccmpc_moments(const void *positions, int dtype, int64_t ld, int64
   CHECK_STORE_ARGS();
   const MinkParams none{};
   return run<false>(positions, dtype, ld, T, origin, cell_off, cell_cnt, n_cells,
-                    n_particles_bound, workspace, out_mean, out_cov, none, stream,
+                    n_particles_bound, workspace, workspace_bytes, out_mean, out_cov, none, stream,
                     "ccmpc_moments");
 }
 
@@ -575,6 +582,6 @@ extern "C" int ccmpc_minkowski_cycle(const void *positions, int dtype, int64_t l
   CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
   const MinkParams mp{ref_traj, cell_ref, cell_risk, R, tol, maxiter, out_rec, out_prob_lower};
   return run<true>(positions, dtype, ld, T, origin, cell_off, cell_cnt, n_cells,
-                   n_particles_bound, workspace, out_mean, out_cov, mp, stream,
+                   n_particles_bound, workspace, workspace_bytes, out_mean, out_cov, mp, stream,
                    "ccmpc_minkowski_cycle");
 }

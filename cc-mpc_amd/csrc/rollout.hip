@@ -279,33 +279,46 @@ inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
 }
 
 template <int RB, bool MINK>
-static void launch_ideal_gram(const double *pm, const double *pc, int T_src, const int32_t *src,
-                              int n_cells, int T, int64_t n, const double *x0, uint64_t seed,
-                              const int32_t *rng, void *ws, double *out_mean, double *out_cov,
-                              int32_t *status, const MinkParams &mp, hipStream_t s) {
+static int launch_ideal_gram(const double *pm, const double *pc, int T_src, const int32_t *src,
+                             int n_cells, int T, int64_t n, const double *x0, uint64_t seed,
+                             const int32_t *rng, void *ws, size_t ws_bytes, double *out_mean,
+                             double *out_cov, int32_t *status, const MinkParams &mp,
+                             hipStream_t s) {
   const int64_t chunk = ideal_chunk(n_cells, n);
   const int64_t ipc = (n + chunk - 1) / chunk;
-  const TreeLayout tree = tree_layout(ws, ipc * n_cells, n_cells, slab_doubles(RB));
+  TreeLayout tree;
+  if (!tree_layout(ws, ws_bytes, ipc * n_cells, n_cells, slab_doubles(RB), tree))
+    return CCMPC_ERR_WORKSPACE;
   hipLaunchKernelGGL((ideal_gram_kernel<RB, MINK>), dim3(static_cast<unsigned>(ipc * n_cells)),
                      dim3(64 * ideal_waves(RB)), 0, s, pm, pc, T_src, src, T, n, chunk, ipc, x0,
                      seed, rng, tree, out_mean, out_cov, status, mp);
+  return CCMPC_OK;
 }
 
 template <bool MINK>
 static int run_ideal(const double *prev_mean, const double *prev_cov, int64_t T_src,
                      const int32_t *src_cell, int64_t n_cells, int64_t T, int64_t n_samples,
                      const double *x0, uint64_t seed, const int32_t *rng_cell, void *workspace,
-                     double *out_mean, double *out_cov, int32_t *out_status, const MinkParams &mp,
-                     ccmpc_stream_t stream) {
+                     size_t ws_bytes, double *out_mean, double *out_cov, int32_t *out_status,
+                     const MinkParams &mp, ccmpc_stream_t stream) {
   hipStream_t s = as_stream(stream);
   const int nc = static_cast<int>(n_cells), Ti = static_cast<int>(T), Ts = static_cast<int>(T_src);
+#define IDEAL_ARGS                                                                            \
+  prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, ws_bytes, \
+      out_mean, out_cov, out_status, mp, s
+  int rc;
   switch (row_blocks(T)) {
-    case 1: launch_ideal_gram<1, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
-    case 2: launch_ideal_gram<2, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
-    case 3: launch_ideal_gram<3, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
-    case 4: launch_ideal_gram<4, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
-    case 5: launch_ideal_gram<5, MINK>(prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, out_mean, out_cov, out_status, mp, s); break;
+    case 1: rc = launch_ideal_gram<1, MINK>(IDEAL_ARGS); break;
+    case 2: rc = launch_ideal_gram<2, MINK>(IDEAL_ARGS); break;
+    case 3: rc = launch_ideal_gram<3, MINK>(IDEAL_ARGS); break;
+    case 4: rc = launch_ideal_gram<4, MINK>(IDEAL_ARGS); break;
+    case 5: rc = launch_ideal_gram<5, MINK>(IDEAL_ARGS); break;
     default: set_error("ideal moments: unsupported T"); return CCMPC_ERR_UNSUPPORTED;
+  }
+#undef IDEAL_ARGS
+  if (rc != CCMPC_OK) {
+    set_error("ideal moments: workspace too small");
+    return rc;
   }
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
@@ -368,7 +381,8 @@ extern "C" int ccmpc_ideal_moments(const double *prev_mean, const double *prev_c
   CHECK_IDEAL_ARGS();
   const MinkParams none{};
   return run_ideal<false>(prev_mean, prev_cov, T_src, src_cell, n_cells, T, n_samples, x0, seed,
-                          rng_cell, workspace, out_mean, out_cov, out_status, none, stream);
+                          rng_cell, workspace, workspace_bytes, out_mean, out_cov, out_status, none,
+                          stream);
 }
 
 extern "C" int ccmpc_ideal_minkowski_cycle(
@@ -383,5 +397,6 @@ extern "C" int ccmpc_ideal_minkowski_cycle(
   CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
   const MinkParams mp{ref_traj, cell_ref, cell_risk, R, tol, maxiter, out_rec, out_prob_lower};
   return run_ideal<true>(prev_mean, prev_cov, T_src, src_cell, n_cells, T, n_samples, x0, seed,
-                         rng_cell, workspace, out_mean, out_cov, out_status, mp, stream);
+                         rng_cell, workspace, workspace_bytes, out_mean, out_cov, out_status, mp,
+                         stream);
 }

@@ -109,9 +109,14 @@ const char *ccmpc_status_string(int status);
  * fixed fan-in-16 tree of arrival counters (the last arriver of each group combines it), so
  * the result is deterministic and uses no float atomics.
  *
- * Workspace contract (every *_workspace_bytes-sized workspace): its head holds the tree's
- * arrival counters.  Zero-fill a fresh workspace ONCE (hipMemset after allocating); every call
- * leaves the counters zero again.  Do not share one workspace between concurrent streams.
+ * Workspace contract (every *_workspace_bytes-sized workspace): its first
+ * round_up(workspace_bytes / 32, 256) bytes hold the tree's arrival counters, the rest the
+ * partial-Gram slabs.  Zero-fill a fresh workspace ONCE (hipMemset after allocating); every
+ * call leaves the counters zero again.  One workspace may serve calls of ANY shape (moments,
+ * cycles, ideal rollouts, any T / cell count) as long as every call passes the same
+ * workspace_bytes (the whole buffer) and that is >= the call's *_workspace_bytes: the counter
+ * region depends on workspace_bytes only, so no call's slabs overwrite another call's
+ * counters.  Do not share one workspace between concurrent streams.
  * ------------------------------------------------------------------------------------- */
 size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_particles_bound);
 int ccmpc_moments(const void *positions, int dtype, int64_t ld, int64_t T,

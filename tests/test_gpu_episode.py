@@ -1,0 +1,63 @@
+"""One episode's planning schedule through the drop-in surface, against the
+oracle chained the same way: frame 0 on sampler particles, frames 10..70 on predict_ideal
+rollouts of the previous frame's moments (same Philox draws), then receding affine steps."""
+import numpy as np
+import pytest
+
+from oracle import ccmpc_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_ovs(ovs, T):
+    out = []
+    for ov in ovs:
+        cells = [np.asarray(p, float) for p in ov.pred_positions]
+        past = np.asarray(ov.past, float).reshape(-1, 2)
+        out.append(orc.OVehicle(T, past, np.asarray(ov.latent_pmf), cells,
+                                [orc._step_yaws(c, past[-1], T) for c in cells],
+                                np.zeros((len(cells), 2)), np.array([4.5, 2.5])))
+    return out
+
+
+def test_episode_schedule_matches_oracle_chain(gpu):
+    from ccmpc import episode
+    n_ideal, seed = 20_000, 3
+    rep = episode.EpisodeReplay(O=2, N=3000, ph=8, n_ideal=n_ideal, receding_steps=2,
+                                seed=seed, device=gpu)
+    mom = None
+    for frame, T, kind in rep.schedule():
+        ovs, out = rep.step(frame, T, kind)
+        K = [ov.n_states for ov in ovs]
+        cons = out[0]
+        if kind == "affine":
+            assert len(cons) == sum(K) * T
+            assert all(c.side in (-1, 1) for c in cons)
+            continue
+        oracle_ovs = _oracle_ovs(ovs, rep.ph)
+        ref = rep.ref_traj(frame)
+        if T == rep.ph:
+            want = orc.minkowski_generator(oracle_ovs, T, rep.ph, ref, with_l4=False)
+            mom = orc.save_moments([ov.pred_positions for ov in oracle_ovs], T)
+        else:
+            ideal = orc.predict_ideal(mom, K, T, n_ideal, seed=seed * 1_000_003 + frame)
+            want = orc.minkowski_generator(oracle_ovs, T, rep.ph, ref, ideal_trajs=ideal,
+                                           with_l4=False)
+            mom = orc.save_moments([[ideal[o][k] for k in range(K[o])]
+                                    for o in range(len(K))], T)
+        recs = want["records"]
+        assert len(cons) == len(recs) == sum(K) * T * (T - 1) // 2, (frame, T)
+        for c, r in zip(cons, recs):
+            assert (c.ov, c.k, c.t, c.tau) == (r["ov"], r["k"], r["t"], r["tau"])
+            assert c.which == r["which"] and c.side == r["side"], (frame, T, c)
+            assert c.d == pytest.approx(r["d"], rel=1e-8)
+
+
+def test_episode_timing_log(gpu):
+    from ccmpc import episode
+    rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=100_000, receding_steps=2,
+                                device=gpu)
+    log = rep.run()
+    assert [s["T"] for s in log] == [8, 7, 6, 5, 4, 3, 2, 1, 8, 8]
+    assert all(s["ms"] > 0 for s in log)
+    assert log[-1]["generator"] == "affine"

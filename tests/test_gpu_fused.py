@@ -78,6 +78,34 @@ def test_workspace_reused_across_shapes(gpu):
             np.testing.assert_allclose(c[j].cpu().numpy(), np.cov(X), rtol=1e-9, atol=1e-12)
 
 
+def test_workspace_shared_by_calls_of_different_shapes(gpu):
+    """Regression: a moments call on a small store and a 1e6-sample fused rollout (two tree
+    levels) alternating on ONE workspace, as the planner's shrinking steps do.  The counter
+    region depends on the buffer size only, so neither call's slabs land on the other's
+    counters; results equal fresh-workspace calls bit for bit."""
+    from ccmpc import risk
+    e = eng()
+    rng = np.random.default_rng(12)
+    cells = [190 + np.cumsum(rng.normal(0, 0.4, size=(n, 8, 2)), axis=1) for n in (900, 1500)]
+    store = e.ParticleStore.from_cells(cells, device=gpu)
+    src = torch.tensor([0, 1], dtype=torch.int32, device=gpu)
+    cr = torch.as_tensor(risk.cell_risk(risk.eps_ura([2]), [2], 8), device=gpu)
+    shared = e.Workspace(gpu)
+    m, c = e.moments(store, workspace=shared)
+    for Tn in (7, 6, 5):
+        ref = torch.as_tensor((np.array([170.0, 5.0]) + np.arange(1, Tn + 1)[:, None] * [4.0, 0.5])
+                              [None], device=gpu)
+        e.moments(store, workspace=shared)                        # small call in between
+        got = e.ideal_minkowski_cycle(m, c, src, Tn, 1_000_000, ref, cr, seed=Tn,
+                                      workspace=shared)
+        want = e.ideal_minkowski_cycle(m, c, src, Tn, 1_000_000, ref, cr, seed=Tn,
+                                       workspace=e.Workspace(gpu))
+        for a, b in zip(got, want):
+            assert torch.equal(a, b)
+        assert np.all(e.halfspaces(got[3])["status"] == 0)
+        m, c = got[0], got[1]
+
+
 def test_empty_and_singleton_cells_give_nan_like_numpy(gpu):
     e = eng()
     store = e.ParticleStore(4, [0, 1, 6], device=gpu)
