@@ -104,13 +104,21 @@ def sweep(dev, seed):
 
 
 def init_dist(args):
+    """One process per GPU (torchrun env).  Backend nccl (= RCCL over xGMI); the env override
+    CCMPC_BENCH_BACKEND=gloo exists only to rehearse the N > 1 code path with several ranks on
+    one card (RCCL will not form a communicator from two ranks on one device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("CCMPC_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -124,7 +132,8 @@ def max_over_ranks(x, world, dev):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    gloo = dist.get_backend() == "gloo"
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if gloo else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -153,6 +162,20 @@ def time_kernel_live(fn, dev, per_graph=50, replays=20):
     ev1.record()
     ev1.synchronize()
     return ev0.elapsed_time(ev1) * 1e-3 / (per_graph * replays)
+
+
+def host_cpu():
+    """CPU model and logical core count of this host (the box's CPU share is 16 of them)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "logical_cores": os.cpu_count()}
 
 
 def cpu_baseline(ovs, ref, T, cycles):
@@ -283,7 +306,7 @@ def pcie_inclusive(cyc, step, dev, iters=200):
 def main():
     args = parse()
     world, rank, local = init_dist(args)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", torch.cuda.current_device() if world > 1 else local)
     torch.cuda.set_device(dev)
 
     from ccmpc import cycle, engine, synthetic
@@ -369,6 +392,7 @@ def main():
         med, threads, n, total = cpu_baseline(ovs, ref, args.T, args.cpu_cycles)
         out["cpu_baseline"] = {
             "value": round(1.0 / med, 3), "unit": "cycles/s", "cores": threads, "kind": "port",
+            "host_cpu": host_cpu(),
             "sample": f"median of {n} full C2 cycles (same scene) at BLAS threads={threads}; "
                       f"{total:.1f} s of CPU work in total (1 and min(16, cores) threads); "
                       "oracle restatement of v8ideal/__init__.py:881-947 (numpy/scipy)",
@@ -378,8 +402,11 @@ def main():
         # the north star's one exchange: every rank's fixed-size half-space records gathered
         # over RCCL (xGMI).  The QP of a scene stays on its owning rank, so this is reported
         # beside `value`, not inside the timed step.
+        import torch.distributed as dist
         from ccmpc import dist as cdist
         rec2 = cyc.rec.view(cyc.rec.shape[0], -1, 128)
+        if dist.get_backend() == "gloo":
+            rec2 = rec2.cpu()
         for _ in range(5):
             cdist.gather_records(rec2)
         torch.cuda.synchronize(dev)
@@ -390,7 +417,9 @@ def main():
         torch.cuda.synchronize(dev)
         tg = max_over_ranks((time.perf_counter() - tg) / 50, world, dev)
         out["record_allgather"] = {"us": round(tg * 1e6, 2),
-                                   "bytes_per_rank": int(rec2.numel()), "backend": "nccl(RCCL)"}
+                                   "bytes_per_rank": int(rec2.numel()),
+                                   "backend": "RCCL" if dist.get_backend() == "nccl" else
+                                   dist.get_backend()}
     if rank == 0:
         # C2 is launch/latency-bound (2.56 MB per cycle); the HBM roofline of the
         # same kernel is meaningful at the per-GPU C4 batch, reported beside it

@@ -3,6 +3,8 @@
 These are per-cell scalars computed once per planning step with the same scipy calls the
 reference makes inside its inner loop; the kernels receive them as data.
 """
+import functools
+
 import numpy as np
 import scipy.stats
 
@@ -21,15 +23,27 @@ def eps_ura(K, eps=EPS_TOTAL):
     return out
 
 
+@functools.lru_cache(maxsize=4096)
+def _chi2_ppf2(p):
+    """scipy.stats.chi2.ppf(p, df=2), memoised: the reference's value, computed once per
+    distinct probability (a planning episode reuses a handful)."""
+    return float(scipy.stats.chi2.ppf(p, df=2))
+
+
+@functools.lru_cache(maxsize=4096)
+def _norm_ppf(p):
+    return float(scipy.stats.norm.ppf(p))
+
+
 def cell_risk(eps_ura_mat, K, ph, target_p=TARGET_P):
     """(n_cells, 3) = chi2.ppf(1-eps_ijt, 2), chi2.ppf(target_p, 2), norm.ppf(1-eps_ijt) with
     eps_ijt = eps_ura[ov, k] / ph, cells in (ov, k) order."""
-    chi_p = scipy.stats.chi2.ppf(target_p, df=2)
+    chi_p = _chi2_ppf2(float(target_p))
     rows = []
     for o, k_o in enumerate(K):
         for k in range(int(k_o)):
-            e = eps_ura_mat[o, k] / ph
-            rows.append((scipy.stats.chi2.ppf(1 - e, df=2), chi_p, scipy.stats.norm.ppf(1 - e)))
+            e = float(eps_ura_mat[o, k]) / ph
+            rows.append((_chi2_ppf2(1 - e), chi_p, _norm_ppf(1 - e)))
     return np.asarray(rows, dtype=np.float64).reshape(-1, 3)
 
 
