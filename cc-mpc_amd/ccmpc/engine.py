@@ -271,6 +271,31 @@ def affine(mean, cov, ref_traj, cell_gamma, cell_ref=None, R=3.4, out_rec=None):
     return out_rec
 
 
+TANGENT_CHOOSE = -2  # CCMPC_TANGENT_CHOOSE: the reference's const_idx = None
+
+
+def affine_scale(mean, cov, ref_traj, cell_risk, tangent=None, const_idx=None, cell_ref=None,
+                 R=3.4, out_rec=None):
+    """GMM-affine half-spaces with the recursive-feasibility covariance scale
+    (ccmpc_affine_scale; v8ideal/__init__.py:2074-2456).  tangent [C, T] float64 and
+    const_idx [C, T] int32 carry the previous frame's slopes / tangent indices (T < ph);
+    None -> slopes from ref_traj and the closest tangent (T == ph)."""
+    lib = _lib.load()
+    C, T = mean.shape[0], mean.shape[1]
+    dev = mean.device
+    if out_rec is None:
+        out_rec = torch.empty((C, T, 128), dtype=torch.uint8, device=dev)
+    tg = ci = None
+    if tangent is not None:
+        tg = torch.as_tensor(np.asarray(tangent, np.float64).reshape(C, T), device=dev)
+        ci = torch.as_tensor(np.asarray(const_idx, np.int32).reshape(C, T), device=dev)
+    _lib.check(lib.ccmpc_affine_scale(_p(mean), _p(cov), T, C, _p(ref_traj), _p(cell_ref),
+                                      _p(cell_risk), float(R), _p(tg), _p(ci), _p(out_rec),
+                                      _stream()), "ccmpc_affine_scale")
+    out_rec._keepalive = (tg, ci)
+    return out_rec
+
+
 def ideal_rollout(prev_mean, prev_cov, src_cell, T, n_samples, x0=None, Z=None, seed=0,
                   rng_cell=None):
     """Materialised predict_ideal trajectories as an F64 ParticleStore + per-cell status."""

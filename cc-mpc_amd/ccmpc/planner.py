@@ -107,6 +107,29 @@ class _VertTK:
         return v[8 * self.t:8 * self.t + 8, o:o + n].T.cpu().numpy().reshape(n, 4, 2)
 
 
+def _match_modes(mean_loaded, x_init, cur_means, n_states, M_big):
+    """Previous-frame mode per current mode: argmin of ||x_init - mean'_0|| + sum_t ||mean_t -
+    mean'_{t+1}||, modes >= n_states (and missing ones) scored M_big, first minimum on ties
+    (v8ideal/__init__.py:2190-2276)."""
+    num_mode = len(mean_loaded)
+    xi = np.asarray(x_init, np.float64).reshape(-1)[:2]
+    picks = []
+    for k in range(n_states):
+        md = np.zeros(num_mode)
+        for mode in range(num_mode):
+            entry = mean_loaded[mode]
+            if entry is None or entry[0] is None:
+                md[mode] = M_big
+                continue
+            v = np.linalg.norm(xi - np.asarray(entry[0], np.float64))
+            for t in range(len(cur_means[k])):
+                v += np.linalg.norm(np.asarray(cur_means[k][t]) - np.asarray(entry[t + 1]))
+            md[mode] = v
+        md[n_states:] = M_big
+        picks.append(int(np.argmin(md)))
+    return picks
+
+
 def _object_grid(*shape):
     return np.empty(shape, dtype=object).tolist()
 
@@ -131,6 +154,8 @@ class MidlevelAgent:
         self.road_boundary_constraints = road_boundary_constraints
         self.R = risk.R_COLLISION
         self._moments = {}                 # frame -> (mean [C,T,2], cov [C,2T,2T], K, T)
+        self._mean_tangent = {}            # frame -> affine_scale meanNtangent (save_data)
+        self.M_big = 10_000                # params.M_big (v8ideal/__init__.py:86)
         self._ws = engine.Workspace(self.device)
         self.prob_lower_save = None
         self.last_records = None
@@ -150,12 +175,12 @@ class MidlevelAgent:
     def _cell_risk(self, eps_ura, K):
         """Per-cell (chi_r, chi_p, gamma) from the caller's eps_ura (:910-913)."""
         ph = self.prediction_horizon
-        chi_p = scipy.stats.chi2.ppf(risk.TARGET_P, df=2)
+        chi_p = risk._chi2_ppf2(risk.TARGET_P)
         rows = []
         for o, k_o in enumerate(K):
             for k in range(k_o):
-                e = eps_ura[o, k] / ph
-                rows.append((scipy.stats.chi2.ppf(1 - e, df=2), chi_p, scipy.stats.norm.ppf(1 - e)))
+                e = float(eps_ura[o, k]) / ph
+                rows.append((risk._chi2_ppf2(1 - e), chi_p, risk._norm_ppf(1 - e)))
         return torch.as_tensor(np.asarray(rows, np.float64).reshape(-1, 3), device=self.device)
 
     def _ref(self, ref_traj, T):
@@ -311,6 +336,95 @@ class MidlevelAgent:
         vertices, A_union, b_union = self._l4_lists(scene)
         return (cons, vertices, A_union, b_union, False, _object_grid(scene.O), st_mean, st_cov,
                 0)
+
+    def compute_obstacle_constraints_GMM_affine_scale_ideal(
+            self, params, ovehicles, Delta2, Omicron, temp_x, eps_ura, segments, Tsh, ref_traj,
+            Relax=None):
+        """v8ideal/__init__.py:2074-2456: GMM-affine half-spaces with the recursive-feasibility
+        covariance scale; at Tsh < ph on a 1e6-sample predict_ideal rollout, with the slopes
+        and tangent indices of the previous frame's meanNtangent (save_data / load_data,
+        :3064-3104) matched per mode.  Returns the 9-tuple with meanNtangent =
+        (mean_p0p1, tangent, cov_p0p1, 0, const_idx)."""
+        if self.road_boundary_constraints:
+            raise NotImplementedError("road-boundary QP variables are outside the GPU path")
+        T, ph = int(Tsh), self.prediction_horizon
+        scene = self._scene(ovehicles)
+        K = scene.K
+        cr = self._cell_risk(np.asarray(eps_ura), K)
+        ref = self._ref(ref_traj, T)
+        m_scene, c_scene = engine.moments(scene.store, workspace=self._ws)
+        tangent = const_idx = None
+        if T < ph:
+            prev = self._moments.get(params.frame - self.record_interval)
+            if prev is None:
+                raise KeyError(f"no moments saved for frame {params.frame - self.record_interval}")
+            src = self._src_cells(prev[2], K)
+            seed = (self.seed * 1_000_003 + int(params.frame)) & (2**63 - 1)
+            mean, cov, status = engine.ideal_moments(prev[0], prev[1], src, T, self.n_ideal,
+                                                     seed=seed, workspace=self._ws)
+            if np.any(status.cpu().numpy() != 0):
+                raise np.linalg.LinAlgError("predict_ideal: conditional covariance not PD")
+            loaded = self._mean_tangent.get(params.frame - self.record_interval)
+            tangent, const_idx = self._loaded_tangents(loaded, mean.cpu().numpy(), K, T,
+                                                       getattr(params, "x_init", None),
+                                                       ref.cpu().numpy()[0])
+        else:
+            mean, cov = m_scene, c_scene
+        rec = engine.affine_scale(mean, cov, ref, cr, tangent, const_idx, R=self.R)
+        h = engine.affine_records(rec)
+        self.last_records = h
+        cons = []
+        O, maxK = scene.O, max(K)
+        mean_p0p1 = _object_grid(O, maxK, T)
+        tangent_s = _object_grid(O, maxK, T)
+        cov_p0p1 = _object_grid(O, maxK, T)
+        const_s = _object_grid(O, maxK, T)
+        for c, (o, k) in enumerate(scene.cell_of):
+            for t in range(T):
+                r = h[c, t]
+                if r["status"] != 0:
+                    raise FloatingPointError(f"affine-scale constraint (ov={o}, k={k}, t={t}) "
+                                             f"failed: {engine._lib.STATUS.get(int(r['status']))}")
+                cons.append(HalfSpace(o, k, t, -1, np.array([r["n0"], r["n1"]]), float(r["d"]),
+                                      float(r["rhs"]), int(r["side"]), int(r["which"]),
+                                      float(r["margin"])))
+                mean_p0p1[o][k][t] = np.array([r["mean0"], r["mean1"]])
+                tangent_s[o][k][t] = float(r["m"])
+                cov_p0p1[o][k][t] = np.array([[r["c00"], r["c01"]], [r["c01"], r["c11"]]])
+                const_s[o][k][t] = int(r["which"])
+        meanNtangent = (mean_p0p1, tangent_s, cov_p0p1, 0, const_s)
+        self._mean_tangent[params.frame] = meanNtangent
+        self._moments[params.frame] = (mean, cov, list(K), T)   # save_moments (:2438)
+        mean0 = m_scene[:, 0, :].cpu().numpy()
+        cov0 = c_scene[:, 0:2, 0:2].cpu().numpy()
+        st_mean, st_cov = self._state_stats(scene, mean0, cov0)
+        vertices, A_union, b_union = self._l4_lists(scene)
+        return (cons, vertices, A_union, b_union, self._ov_in_junction(scene, mean0),
+                _object_grid(scene.O), st_mean, st_cov, meanNtangent)
+
+    def _loaded_tangents(self, loaded, mean, K, T, x_init, ref):
+        """The previous frame's slopes / tangent indices for every (cell, t) of this frame
+        (v8ideal/__init__.py:2190-2276 mode matching, :2349-2370 lookup); an OV without
+        loaded data keeps slope-from-ref and const_idx = -1 (the reference's initial value)."""
+        C = sum(K)
+        tangent = np.zeros((C, T))
+        const_idx = np.full((C, T), -1, np.int32)
+        c0 = 0
+        for o, k_o in enumerate(K):
+            mean_l = loaded[0][o] if loaded is not None and o < len(loaded[0]) else None
+            if mean_l is not None and len(mean_l) > 0 and x_init is not None:
+                cur = [[mean[c0 + k, t] for t in range(T)] for k in range(k_o)]
+                picks = _match_modes(mean_l, x_init, cur, k_o, self.M_big)
+                for k, idx in enumerate(picks):
+                    for t in range(T):
+                        tangent[c0 + k, t] = loaded[1][o][idx][t + 1]
+                        const_idx[c0 + k, t] = loaded[4][o][idx][t + 1]
+            else:   # slope from ref (the same IEEE ops as the kernel's), const_idx stays -1
+                for k in range(k_o):
+                    tangent[c0 + k] = -(ref[:T, 0] - mean[c0 + k, :, 0]) / (
+                        ref[:T, 1] - mean[c0 + k, :, 1])
+            c0 += k_o
+        return tangent, const_idx
 
     # ------------------------------------------------------------------------------------
     def save_moments(self, ovehicles, O, K, T, Tpred, ego_vehicle_id, params):

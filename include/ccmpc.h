@@ -167,6 +167,26 @@ int ccmpc_affine(const double *mean, const double *cov, int64_t T, int64_t n_cel
                  double R, ccmpc_affine_rec *out_rec, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * GMM-affine half-spaces with the recursive-feasibility covariance scale, for every (cell, t):
+ * compute_obstacle_constraints_GMM_affine_scale_ideal (v8ideal/__init__.py:2320-2425).
+ *  scale(t) = max(1, max_{tau<t} compute_scale(predict_moments(t, tau), Gamma, chi_p))
+ *             (makeconstraint.py:259-280); cov = scale C_tt
+ *  cell_risk[c][3]     as ccmpc_minkowski_cycle (chi_p = chi2.ppf(0.9999, 2), Gamma = norm.ppf(1 - eps))
+ *  tangent_in[c][T]    slope m per (cell, t); NULL -> m from ref_traj (the T == ph case)
+ *  const_idx_in[c][T]  with tangent_in: CCMPC_TANGENT_CHOOSE (-2) = the reference's None (closest
+ *                      tangent to ref), or -1 / 0 / 1 = the index it passes (Python indexing; -1 is
+ *                      the last candidate and is also what the record reports in `which`)
+ * Constraint: n.x >= rhs (side +1) or <= rhs (side -1), rhs = d +/- Gamma sqrt(|cov|_F) |[m, -1]|.
+ * Record fields: c00/c01/c11 = the unscaled cov (what the generator saves), s00 = scale,
+ * s01 = sqrt(|cov|_F) of the scaled cov, s11 = 0.
+ * ------------------------------------------------------------------------------------- */
+#define CCMPC_TANGENT_CHOOSE -2
+int ccmpc_affine_scale(const double *mean, const double *cov, int64_t T, int64_t n_cells,
+                       const double *ref_traj, const int32_t *cell_ref, const double *cell_risk,
+                       double R, const double *tangent_in, const int32_t *const_idx_in,
+                       ccmpc_affine_rec *out_rec, ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * predict_ideal: affine conditional-Gaussian forward rollout (v8ideal/__init__.py:2620-2711)
  * from the PREVIOUS planning step's moments, which stay device-resident (no pickle round trip).
  *  prev_mean[s][T_src][2], prev_cov[s][2T_src][2T_src]  -- ccmpc_moments output of that step

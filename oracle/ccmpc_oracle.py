@@ -406,6 +406,120 @@ def affine_generator(ovehicles, T, ph, ref_traj, R=R_COLLISION, with_l4=True, mc
     return out
 
 
+M_BIG = 10_000             # params.M_big (v8ideal/__init__.py:86): the mode match's "no such mode"
+
+
+def match_loaded_modes(mean_loaded, x_init, cur_means, n_states, M_big=M_BIG):
+    """Mode matching of compute_obstacle_constraints_GMM_affine_scale_ideal for one OV
+    (v8ideal/__init__.py:2190-2276): for each current mode k, the previous frame's mode
+    minimising ||x_init - mean'_0|| + sum_t ||mean_t - mean'_{t+1}||, modes >= the current
+    n_states (and missing ones) scored M_big, first minimum on ties (np.argmin).
+    mean_loaded[mode][t] (2,) or None; cur_means[k][t] (2,).  Returns the chosen mode per k."""
+    num_mode = len(mean_loaded)
+    picks = []
+    for k in range(n_states):
+        md = [0.0] * num_mode
+        for mode in range(num_mode):
+            entry = mean_loaded[mode]
+            if entry is None or entry[0] is None:
+                md[mode] = M_big
+                continue
+            v = np.linalg.norm(np.asarray(x_init, float)[:2] - np.asarray(entry[0], float))
+            for t in range(len(cur_means[k])):
+                v += np.linalg.norm(np.asarray(cur_means[k][t]) - np.asarray(entry[t + 1], float))
+            md[mode] = v
+        for rest in range(n_states, num_mode):
+            md[rest] = M_big
+        picks.append(int(np.argmin(md)))
+    return picks
+
+
+def affine_scale_generator(ovehicles, T, ph, ref_traj, x_init=None, loaded=None,
+                           ideal_trajs=None, R=R_COLLISION, target_p=TARGET_P, mc=None):
+    """compute_obstacle_constraints_GMM_affine_scale_ideal restated without cvxpy
+    (v8ideal/__init__.py:2074-2456).  Per (ov, k, t): scale = max(1, max_{tau<t}
+    compute_scale(predict_moments(t, tau), Gamma)) (:2320-2340), cov = scale * np.cov(p_t),
+    a slope-m tangent of the radius-R circle (choose_closest_tangent with const_idx, :2376), and
+    n.x >= d + Gamma sqrt(|cov|_F) |[m, -1]| if n.mean <= d else n.x <= d - ... (:2379-2398).
+    At T < ph the clouds are ideal_trajs and m / const_idx come from the previous frame's
+    meanNtangent `loaded` = (mean_p0p1, tangent, const_idx) matched per mode; an OV without
+    loaded data keeps const_idx = -1 (the reference's initial value: Python's last candidate).
+    Returns records and meanNtangent = (mean_p0p1, tangent, cov_p0p1, 0, const_idx)."""
+    mc = mc if mc is not None else _SELF
+    K = [ov.n_states for ov in ovehicles]
+    O = len(ovehicles)
+    eps_ura = eps_ura_matrix(K)
+    use_ideal = T < ph
+    tangent_saved, const_saved = {}, {}
+    if use_ideal and loaded is not None:
+        mean_l, tangent_l, const_l = loaded
+        for o, ov in enumerate(ovehicles):
+            if o >= len(mean_l) or mean_l[o] is None or len(mean_l[o]) == 0:
+                continue
+            cur = []
+            for k in range(ov.n_states):
+                pd = np.vstack(ideal_trajs[o][k])
+                cur.append([np.array([np.mean(pd[t::T, 0]), np.mean(pd[t::T, 1])])
+                            for t in range(T)])
+            for k, idx in enumerate(match_loaded_modes(mean_l[o], x_init, cur, ov.n_states)):
+                tangent_saved[(o, k)] = tangent_l[o][idx]
+                const_saved[(o, k)] = const_l[o][idx]
+    mean_p0p1 = [[[None] * T for _ in range(max(K))] for _ in range(O)]
+    tangent = [[[None] * T for _ in range(max(K))] for _ in range(O)]
+    cov_p0p1 = [[[None] * T for _ in range(max(K))] for _ in range(O)]
+    const_save = [[[None] * T for _ in range(max(K))] for _ in range(O)]
+    records = []
+    eye = np.identity(2)
+    for o, ov in enumerate(ovehicles):
+        for k in range(ov.n_states):
+            if use_ideal:
+                poseData = np.vstack(ideal_trajs[o][k])
+                Tpred = T
+            else:
+                poseData = np.vstack(ov.pred_positions[k])
+                Tpred = ph
+            for t in range(T):
+                const_idx = -1
+                eps_ijt = eps_ura[o, k] / ph
+                gamma = scipy.stats.norm.ppf(1 - eps_ijt)
+                p0 = poseData[t::Tpred, 0]
+                p1 = poseData[t::Tpred, 1]
+                mean = np.array([np.mean(p0), np.mean(p1)])
+                scale = 1.0
+                for tau in range(t):
+                    p_t_tau = [p0, p1, poseData[tau::Tpred, 0], poseData[tau::Tpred, 1]]
+                    cov_infer, cov_mu, cov_t = mc.predict_moments(p_t_tau)
+                    scale_temp = mc.compute_scale(cov_infer, cov_mu, cov_t, gamma,
+                                                  target_p=target_p)
+                    scale = np.max((scale_temp, scale))
+                cov = scale * np.cov([p0, p1])
+                cov_fro_sqrt = np.sqrt(np.linalg.norm(cov, 'fro'))
+                if T == ph:
+                    m = -(ref_traj[t][0] - mean[0]) / (ref_traj[t][1] - mean[1])
+                    const_idx = None
+                elif (o, k) in tangent_saved:
+                    m = tangent_saved[(o, k)][t + 1]
+                    const_idx = const_saved[(o, k)][t + 1]
+                else:
+                    m = -(ref_traj[t][0] - mean[0]) / (ref_traj[t][1] - mean[1])
+                M = np.array([m, -1])
+                ref_pose = np.array((ref_traj[t][0], ref_traj[t][1]))
+                n, d, const_idx = mc.choose_closest_tangent(mean, eye, R, m, ref_pose,
+                                                            const_idx)[:3]
+                margin = gamma * cov_fro_sqrt * np.linalg.norm(M.T, 2)
+                side = 1 if n @ mean <= d else -1
+                rhs = d + margin if side == 1 else d - margin
+                records.append(dict(ov=o, k=k, t=t, n=np.array(n), d=float(d),
+                                    which=int(const_idx), side=side, margin=float(margin),
+                                    rhs=float(rhs), mean=mean, cov=cov / scale, m=float(m),
+                                    scale=float(scale), gamma=float(gamma)))
+                mean_p0p1[o][k][t] = mean
+                tangent[o][k][t] = m
+                cov_p0p1[o][k][t] = cov / scale
+                const_save[o][k][t] = const_idx
+    return dict(records=records, meanNtangent=(mean_p0p1, tangent, cov_p0p1, 0, const_save))
+
+
 def save_moments(positions, T):
     """mean / cov per (ov, k, t) and cross_cov[t][tau] = cov(p_t, p_tau)[0:2, 2:4]
     (v8ideal/__init__.py:2575-2618).  ``positions[o][k]`` is (N_k, T, 2)."""

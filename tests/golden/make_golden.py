@@ -206,6 +206,47 @@ def main():
              xcov=np.array([[[mom["cross_cov"][0][k][t][tau] if tau < t else np.zeros((2, 2))
                               for tau in range(T)] for t in range(T)] for k in range(2)]),
              x0=np.array(x0s[0]), Z=np.array(Zs[0]), traj=np.array([traj[0][k] for k in range(2)]))
+    # --- GMM-affine with covariance scale (v8ideal/__init__.py:2074-2456): a T == ph step,
+    #     then a T < ph step on injected ideal clouds that loads the first step's meanNtangent
+    T, Ks, Ns = 8, (2, 1), (300, 250, 350)
+    it = iter(Ns)
+    cells_per_ov = [[random_walk_cell(rng, next(it), T) for _ in range(k)] for k in Ks]
+    ovs = make_ovs(cells_per_ov, T)
+    ego = np.array(cells_per_ov[0][0][:, 0].mean(0)) + np.array([-12.0, 3.0])
+    ref1 = np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
+    ref2 = ref1 + np.array([2.0, 0.25])
+    x_init = np.array([ego[0] + 1.0, ego[1], 0.0, 5.0])
+    g1 = orc.affine_scale_generator(ovs, T, T, ref1, mc=ref)
+    mean1, tan1, _, _, ci1 = g1["meanNtangent"]
+    mom = orc.save_moments(cells_per_ov, T)
+    Tn, ns = T - 1, 200
+    x0s = [[mom["mean_p0p1"][o][k][0] + rng.normal(0, 0.3, 2) for k in range(Ks[o])]
+           for o in range(2)]
+    Zs = [[[rng.normal(size=(ns, 2)) for _ in range(Tn)] for _ in range(Ks[o])]
+          for o in range(2)]
+    ideal = orc.predict_ideal(mom, list(Ks), Tn, ns, x0s=x0s, Zs=Zs)
+    g2 = orc.affine_scale_generator(ovs, Tn, T, ref2, x_init=x_init,
+                                    loaded=(mean1, tan1, ci1), ideal_trajs=ideal, mc=ref)
+    counts, flat = pack_cells([c for cs in cells_per_ov for c in cs])
+
+    def recs(g, key, dtype=float):
+        return np.array([r[key] for r in g["records"]], dtype=dtype)
+
+    np.savez(os.path.join(HERE, "affine_scale.npz"),
+             T=T, K=np.array(Ks), counts=counts, positions=flat, ref1=ref1, ref2=ref2,
+             x_init=x_init, past=np.array([ov.past[-1] for ov in ovs]),
+             ideal=np.array([ideal[o][k] for o in range(2) for k in range(Ks[o])]),
+             load_mean=np.array([[mean1[o][k][t] for t in range(T)]
+                                 for o in range(2) for k in range(Ks[o])]),
+             load_tangent=np.array([[tan1[o][k][t] for t in range(T)]
+                                    for o in range(2) for k in range(Ks[o])]),
+             load_const=np.array([[ci1[o][k][t] for t in range(T)]
+                                  for o in range(2) for k in range(Ks[o])]),
+             **{f"s{i}_{key}": recs(g, key, int if key in ("which", "side") else float)
+                for i, g in ((1, g1), (2, g2))
+                for key in ("d", "which", "side", "margin", "rhs", "scale", "m")},
+             s1_n=np.array([r["n"] for r in g1["records"]]),
+             s2_n=np.array([r["n"] for r in g2["records"]]))
     print("golden fixtures written to", HERE)
 
 

@@ -153,3 +153,41 @@ def test_make_ovehicles_matches_reference_bucketing(gpu):
             np.testing.assert_array_equal(ovs[o].pred_positions[k], want[o].pred_positions[k])
             np.testing.assert_allclose(ovs[o].pred_yaws[k], want[o].pred_yaws[k], rtol=1e-12,
                                        atol=1e-13)
+
+
+def test_affine_scale_ideal_two_frames(gpu):
+    """compute_obstacle_constraints_GMM_affine_scale_ideal through the agent: frame 300 at
+    T == ph, frame 310 at T < ph on the Philox ideal rollout of frame 300's moments with
+    frame 300's meanNtangent loaded -- against the oracle chained the same way."""
+    from ccmpc import ovehicle, planner
+    T, n_ideal, seed = 8, 20_000, 6
+    ov_cells, ref, pasts = _scene(61, O=2, N=2500, T=T)
+    K = [len(c) for c in ov_cells]
+    ovs = ovehicle.scene_from_positions(ov_cells, pasts, device=gpu)
+    agent = planner.MidlevelAgent(prediction_horizon=T, n_ideal=n_ideal, seed=seed, device=gpu)
+    eps = orc.eps_ura_matrix(K)
+    x_init = np.array([ref[0][0] - 4.0, ref[0][1] - 0.5, 0.0, 5.0])
+    p1 = Params(len(K), K, 300)
+    p1.x_init = x_init
+    out1 = agent.compute_obstacle_constraints_GMM_affine_scale_ideal(
+        p1, ovs, None, None, None, eps, None, T, ref)
+    ref2 = ref + np.array([2.0, 0.25])
+    p2 = Params(len(K), K, 310)
+    p2.x_init = x_init
+    out2 = agent.compute_obstacle_constraints_GMM_affine_scale_ideal(
+        p2, ovs, None, None, None, eps, None, T - 1, ref2)
+    oracle_ovs = _oracle_ovs(ov_cells, pasts, T)
+    w1 = orc.affine_scale_generator(oracle_ovs, T, T, ref)
+    mom = orc.save_moments([ov.pred_positions for ov in oracle_ovs], T)
+    ideal = orc.predict_ideal(mom, K, T - 1, n_ideal, seed=seed * 1_000_003 + 310)
+    m1, t1, _, _, c1 = w1["meanNtangent"]
+    w2 = orc.affine_scale_generator(oracle_ovs, T - 1, T, ref2, x_init=x_init,
+                                    loaded=(m1, t1, c1), ideal_trajs=ideal)
+    for out, want in ((out1, w1), (out2, w2)):
+        assert len(out[0]) == len(want["records"])
+        for c, r in zip(out[0], want["records"]):
+            assert (c.ov, c.k, c.t) == (r["ov"], r["k"], r["t"])
+            assert c.which == r["which"] and c.side == r["side"]
+            assert c.rhs == pytest.approx(r["rhs"], rel=1e-9)
+    # meanNtangent (the 9th element) carries the saved slopes / indices for the next frame
+    assert out2[8][1][0][0][0] == pytest.approx(w2["meanNtangent"][1][0][0][0], rel=1e-9)

@@ -129,3 +129,37 @@ def test_philox_known_answer():
     w = philox.philox4x32(0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff,
                           0xffffffffffffffff)
     assert [int(x) for x in w] == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+
+
+def _ideal_from_fixture(g):
+    K = [int(k) for k in g["K"]]
+    ideal, j = {}, 0
+    for o, k_o in enumerate(K):
+        ideal[o] = {}
+        for k in range(k_o):
+            ideal[o][k] = g["ideal"][j]
+            j += 1
+    return ideal
+
+
+def test_affine_scale_generator_matches_reference(golden):
+    """compute_obstacle_constraints_GMM_affine_scale_ideal restated (v8ideal/__init__.py:
+    2074-2456) vs the golden made with the reference's compute_scale / predict_moments /
+    choose_closest_tangent: the T == ph step, then a T < ph step on injected ideal clouds that
+    loads the first step's meanNtangent (mode matching, const_idx override)."""
+    g = golden("affine_scale")
+    T = int(g["T"])
+    ovs = ovehicles_from_fixture(g)
+    g1 = orc.affine_scale_generator(ovs, T, T, g["ref1"])
+    mean1, tan1, _, _, ci1 = g1["meanNtangent"]
+    g2 = orc.affine_scale_generator(ovs, T - 1, T, g["ref2"], x_init=g["x_init"],
+                                    loaded=(mean1, tan1, ci1), ideal_trajs=_ideal_from_fixture(g))
+    for i, out in ((1, g1), (2, g2)):
+        recs = out["records"]
+        np.testing.assert_array_equal([r["which"] for r in recs], g[f"s{i}_which"])
+        np.testing.assert_array_equal([r["side"] for r in recs], g[f"s{i}_side"])
+        for key, rtol in (("d", 1e-13), ("margin", 1e-12), ("rhs", 1e-13), ("scale", 1e-12),
+                          ("m", 1e-13)):
+            np.testing.assert_allclose([r[key] for r in recs], g[f"s{i}_{key}"], rtol=rtol)
+    # the T < ph step really used loaded indices: they differ from a fresh closest choice
+    assert set(g["s2_which"]) <= {-1, 0, 1}
