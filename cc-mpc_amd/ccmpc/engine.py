@@ -275,11 +275,12 @@ TANGENT_CHOOSE = -2  # CCMPC_TANGENT_CHOOSE: the reference's const_idx = None
 
 
 def affine_scale(mean, cov, ref_traj, cell_risk, tangent=None, const_idx=None, cell_ref=None,
-                 R=3.4, out_rec=None):
+                 R=3.4, out_rec=None, scaled=True):
     """GMM-affine half-spaces with the recursive-feasibility covariance scale
     (ccmpc_affine_scale; v8ideal/__init__.py:2074-2456).  tangent [C, T] float64 and
     const_idx [C, T] int32 carry the previous frame's slopes / tangent indices (T < ph);
-    None -> slopes from ref_traj and the closest tangent (T == ph)."""
+    None -> slopes from ref_traj and the closest tangent (T == ph).  scaled=False is
+    compute_obstacle_constraints_GMM_affine_robust (:1541-1878): scale = 1."""
     lib = _lib.load()
     C, T = mean.shape[0], mean.shape[1]
     dev = mean.device
@@ -290,7 +291,8 @@ def affine_scale(mean, cov, ref_traj, cell_risk, tangent=None, const_idx=None, c
         tg = torch.as_tensor(np.asarray(tangent, np.float64).reshape(C, T), device=dev)
         ci = torch.as_tensor(np.asarray(const_idx, np.int32).reshape(C, T), device=dev)
     _lib.check(lib.ccmpc_affine_scale(_p(mean), _p(cov), T, C, _p(ref_traj), _p(cell_ref),
-                                      _p(cell_risk), float(R), _p(tg), _p(ci), _p(out_rec),
+                                      _p(cell_risk), float(R), int(bool(scaled)), _p(tg),
+                                      _p(ci), _p(out_rec),
                                       _stream()), "ccmpc_affine_scale")
     out_rec._keepalive = (tg, ci)
     return out_rec

@@ -345,6 +345,16 @@ class MidlevelAgent:
         and tangent indices of the previous frame's meanNtangent (save_data / load_data,
         :3064-3104) matched per mode.  Returns the 9-tuple with meanNtangent =
         (mean_p0p1, tangent, cov_p0p1, 0, const_idx)."""
+        return self._affine_tangent_generator(params, ovehicles, eps_ura, Tsh, ref_traj,
+                                              scaled=True)
+
+    def compute_obstacle_constraints_GMM_affine_robust(
+            self, params, ovehicles, Delta2, Omicron, temp_x, eps_ura, segments, Tsh, ref_traj):
+        """v8ideal/__init__.py:1541-1878: the same generator without the covariance scale."""
+        return self._affine_tangent_generator(params, ovehicles, eps_ura, Tsh, ref_traj,
+                                              scaled=False)
+
+    def _affine_tangent_generator(self, params, ovehicles, eps_ura, Tsh, ref_traj, scaled):
         if self.road_boundary_constraints:
             raise NotImplementedError("road-boundary QP variables are outside the GPU path")
         T, ph = int(Tsh), self.prediction_horizon
@@ -370,7 +380,8 @@ class MidlevelAgent:
                                                        ref.cpu().numpy()[0])
         else:
             mean, cov = m_scene, c_scene
-        rec = engine.affine_scale(mean, cov, ref, cr, tangent, const_idx, R=self.R)
+        rec = engine.affine_scale(mean, cov, ref, cr, tangent, const_idx, R=self.R,
+                                  scaled=scaled)
         h = engine.affine_records(rec)
         self.last_records = h
         cons = []

@@ -106,8 +106,9 @@ __global__ __launch_bounds__(64) void affine_kernel(
 __global__ __launch_bounds__(256) void affine_scale_kernel(
     const double *__restrict__ mean, const double *__restrict__ cov, int T,
     const double *__restrict__ ref_traj, const int32_t *__restrict__ cell_ref,
-    const double *__restrict__ cell_risk, double R, const double *__restrict__ tangent_in,
-    const int32_t *__restrict__ const_idx_in, ccmpc_affine_rec *__restrict__ out) {
+    const double *__restrict__ cell_risk, double R, int scaled,
+    const double *__restrict__ tangent_in, const int32_t *__restrict__ const_idx_in,
+    ccmpc_affine_rec *__restrict__ out) {
   __shared__ unsigned long long scale_bits[40];
   const int cell = blockIdx.x, rows = 2 * T;
   const double *C = cov + static_cast<int64_t>(cell) * rows * rows;
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(256) void affine_scale_kernel(
   for (int t = threadIdx.x; t < T; t += blockDim.x)
     scale_bits[t] = static_cast<unsigned long long>(__double_as_longlong(one));
   __syncthreads();
-  const int P = T * (T - 1) / 2;
+  const int P = scaled ? T * (T - 1) / 2 : 0;  // _affine_robust: scale = 1 (:1766)
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
     int t, tau;
     pair_of(p, t, tau);
@@ -235,15 +236,17 @@ extern "C" int ccmpc_affine(const double *mean, const double *cov, int64_t T, in
 extern "C" int ccmpc_affine_scale(const double *mean, const double *cov, int64_t T,
                                   int64_t n_cells, const double *ref_traj,
                                   const int32_t *cell_ref, const double *cell_risk, double R,
-                                  const double *tangent_in, const int32_t *const_idx_in,
-                                  ccmpc_affine_rec *out_rec, ccmpc_stream_t stream) {
+                                  int32_t scaled, const double *tangent_in,
+                                  const int32_t *const_idx_in, ccmpc_affine_rec *out_rec,
+                                  ccmpc_stream_t stream) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_cells >= 0 && n_cells < (1 << 30), "bad n_cells");
   if (n_cells == 0) return CCMPC_OK;
   CCMPC_REQUIRE(mean && cov && ref_traj && cell_risk && out_rec, "null pointer");
   hipLaunchKernelGGL(affine_scale_kernel, dim3(static_cast<unsigned>(n_cells)), dim3(256), 0,
                      as_stream(stream), mean, cov, static_cast<int>(T), ref_traj, cell_ref,
-                     cell_risk, R, tangent_in, const_idx_in, out_rec);
+                     cell_risk, R, static_cast<int>(scaled != 0), tangent_in, const_idx_in,
+                     out_rec);
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

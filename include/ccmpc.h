@@ -168,9 +168,10 @@ int ccmpc_affine(const double *mean, const double *cov, int64_t T, int64_t n_cel
 
 /* ---------------------------------------------------------------------------------------
  * GMM-affine half-spaces with the recursive-feasibility covariance scale, for every (cell, t):
- * compute_obstacle_constraints_GMM_affine_scale_ideal (v8ideal/__init__.py:2320-2425).
+ * compute_obstacle_constraints_GMM_affine_scale_ideal (v8ideal/__init__.py:2320-2425), and with
+ * scaled = 0 its unscaled twin compute_obstacle_constraints_GMM_affine_robust (:1541-1878).
  *  scale(t) = max(1, max_{tau<t} compute_scale(predict_moments(t, tau), Gamma, chi_p))
- *             (makeconstraint.py:259-280); cov = scale C_tt
+ *             (makeconstraint.py:259-280) if scaled, else 1; cov = scale C_tt
  *  cell_risk[c][3]     as ccmpc_minkowski_cycle (chi_p = chi2.ppf(0.9999, 2), Gamma = norm.ppf(1 - eps))
  *  tangent_in[c][T]    slope m per (cell, t); NULL -> m from ref_traj (the T == ph case)
  *  const_idx_in[c][T]  with tangent_in: CCMPC_TANGENT_CHOOSE (-2) = the reference's None (closest
@@ -183,8 +184,9 @@ int ccmpc_affine(const double *mean, const double *cov, int64_t T, int64_t n_cel
 #define CCMPC_TANGENT_CHOOSE -2
 int ccmpc_affine_scale(const double *mean, const double *cov, int64_t T, int64_t n_cells,
                        const double *ref_traj, const int32_t *cell_ref, const double *cell_risk,
-                       double R, const double *tangent_in, const int32_t *const_idx_in,
-                       ccmpc_affine_rec *out_rec, ccmpc_stream_t stream);
+                       double R, int32_t scaled, const double *tangent_in,
+                       const int32_t *const_idx_in, ccmpc_affine_rec *out_rec,
+                       ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * predict_ideal: affine conditional-Gaussian forward rollout (v8ideal/__init__.py:2620-2711)

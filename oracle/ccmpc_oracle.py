@@ -435,7 +435,8 @@ def match_loaded_modes(mean_loaded, x_init, cur_means, n_states, M_big=M_BIG):
 
 
 def affine_scale_generator(ovehicles, T, ph, ref_traj, x_init=None, loaded=None,
-                           ideal_trajs=None, R=R_COLLISION, target_p=TARGET_P, mc=None):
+                           ideal_trajs=None, R=R_COLLISION, target_p=TARGET_P, mc=None,
+                           scaled=True):
     """compute_obstacle_constraints_GMM_affine_scale_ideal restated without cvxpy
     (v8ideal/__init__.py:2074-2456).  Per (ov, k, t): scale = max(1, max_{tau<t}
     compute_scale(predict_moments(t, tau), Gamma)) (:2320-2340), cov = scale * np.cov(p_t),
@@ -444,6 +445,8 @@ def affine_scale_generator(ovehicles, T, ph, ref_traj, x_init=None, loaded=None,
     At T < ph the clouds are ideal_trajs and m / const_idx come from the previous frame's
     meanNtangent `loaded` = (mean_p0p1, tangent, const_idx) matched per mode; an OV without
     loaded data keeps const_idx = -1 (the reference's initial value: Python's last candidate).
+    scaled=False is compute_obstacle_constraints_GMM_affine_robust (:1541-1878): the same
+    generator without the scale loop (scale = 1).
     Returns records and meanNtangent = (mean_p0p1, tangent, cov_p0p1, 0, const_idx)."""
     mc = mc if mc is not None else _SELF
     K = [ov.n_states for ov in ovehicles]
@@ -486,7 +489,7 @@ def affine_scale_generator(ovehicles, T, ph, ref_traj, x_init=None, loaded=None,
                 p1 = poseData[t::Tpred, 1]
                 mean = np.array([np.mean(p0), np.mean(p1)])
                 scale = 1.0
-                for tau in range(t):
+                for tau in (range(t) if scaled else ()):
                     p_t_tau = [p0, p1, poseData[tau::Tpred, 0], poseData[tau::Tpred, 1]]
                     cov_infer, cov_mu, cov_t = mc.predict_moments(p_t_tau)
                     scale_temp = mc.compute_scale(cov_infer, cov_mu, cov_t, gamma,

@@ -227,6 +227,11 @@ def main():
     ideal = orc.predict_ideal(mom, list(Ks), Tn, ns, x0s=x0s, Zs=Zs)
     g2 = orc.affine_scale_generator(ovs, Tn, T, ref2, x_init=x_init,
                                     loaded=(mean1, tan1, ci1), ideal_trajs=ideal, mc=ref)
+    # compute_obstacle_constraints_GMM_affine_robust (:1541-1878): the unscaled twin
+    r1 = orc.affine_scale_generator(ovs, T, T, ref1, mc=ref, scaled=False)
+    rm1, rt1, _, _, rc1 = r1["meanNtangent"]
+    r2 = orc.affine_scale_generator(ovs, Tn, T, ref2, x_init=x_init, loaded=(rm1, rt1, rc1),
+                                    ideal_trajs=ideal, mc=ref, scaled=False)
     counts, flat = pack_cells([c for cs in cells_per_ov for c in cs])
 
     def recs(g, key, dtype=float):
@@ -243,7 +248,7 @@ def main():
              load_const=np.array([[ci1[o][k][t] for t in range(T)]
                                   for o in range(2) for k in range(Ks[o])]),
              **{f"s{i}_{key}": recs(g, key, int if key in ("which", "side") else float)
-                for i, g in ((1, g1), (2, g2))
+                for i, g in ((1, g1), (2, g2), ("r1", r1), ("r2", r2))
                 for key in ("d", "which", "side", "margin", "rhs", "scale", "m")},
              s1_n=np.array([r["n"] for r in g1["records"]]),
              s2_n=np.array([r["n"] for r in g2["records"]]))

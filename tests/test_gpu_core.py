@@ -276,7 +276,8 @@ def test_moments_deterministic(gpu):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
-def test_affine_scale_records_match_reference_golden(gpu, golden):
+@pytest.mark.parametrize("scaled,pre", [(True, "s"), (False, "sr")])   # scale / _affine_robust
+def test_affine_scale_records_match_reference_golden(gpu, golden, scaled, pre):
     """ccmpc_affine_scale (v8ideal/__init__.py:2074-2456) vs the reference-driven golden: the
     T == ph step from the particle cells, then the T < ph step from the ideal clouds with the
     slopes / tangent indices of the first step's meanNtangent matched per mode on the host."""
@@ -290,17 +291,17 @@ def test_affine_scale_records_match_reference_golden(gpu, golden):
     def check(h, i):
         h = h.reshape(-1)
         assert np.all(h["status"] == 0)
-        np.testing.assert_array_equal(h["which"], g[f"s{i}_which"])
-        np.testing.assert_array_equal(h["side"], g[f"s{i}_side"])
-        np.testing.assert_allclose(h["s00"], g[f"s{i}_scale"], rtol=1e-10)
-        np.testing.assert_allclose(h["margin"], g[f"s{i}_margin"], rtol=1e-10)
-        np.testing.assert_allclose(h["rhs"], g[f"s{i}_rhs"], rtol=1e-12)
-        np.testing.assert_allclose(h["d"], g[f"s{i}_d"], rtol=1e-12)
+        np.testing.assert_array_equal(h["which"], g[f"{pre}{i}_which"])
+        np.testing.assert_array_equal(h["side"], g[f"{pre}{i}_side"])
+        np.testing.assert_allclose(h["s00"], g[f"{pre}{i}_scale"], rtol=1e-10)
+        np.testing.assert_allclose(h["margin"], g[f"{pre}{i}_margin"], rtol=1e-10)
+        np.testing.assert_allclose(h["rhs"], g[f"{pre}{i}_rhs"], rtol=1e-12)
+        np.testing.assert_allclose(h["d"], g[f"{pre}{i}_d"], rtol=1e-12)
 
     store = eng.ParticleStore.from_cells(cells_from_fixture(g), device=gpu)
     mean, cov = eng.moments(store)
     ref1 = torch.as_tensor(g["ref1"][None], device=gpu)
-    check(eng.affine_records(eng.affine_scale(mean, cov, ref1, cr)), 1)
+    check(eng.affine_records(eng.affine_scale(mean, cov, ref1, cr, scaled=scaled)), 1)
 
     Tn = T - 1
     store2 = eng.ParticleStore.from_cells(list(g["ideal"]), device=gpu)
@@ -310,12 +311,15 @@ def test_affine_scale_records_match_reference_golden(gpu, golden):
     const = np.zeros((sum(K), Tn), np.int32)
     c0 = 0
     for o, k_o in enumerate(K):
+        # the first step's saved means are the particle means either way (scale only changes
+        # the spread); slopes and indices are the variant's own
         mean_l = [[g["load_mean"][c0 + j][t] for t in range(T)] for j in range(k_o)]
         picks = planner._match_modes(mean_l, g["x_init"], [m2[c0 + k] for k in range(k_o)],
                                      k_o, 10_000)
         for k, idx in enumerate(picks):
-            tangent[c0 + k] = g["load_tangent"][c0 + idx][1:]
-            const[c0 + k] = g["load_const"][c0 + idx][1:]
+            tangent[c0 + k] = g[f"{pre}1_m"][(c0 + idx) * T:(c0 + idx + 1) * T][1:]
+            const[c0 + k] = g[f"{pre}1_which"][(c0 + idx) * T:(c0 + idx + 1) * T][1:]
         c0 += k_o
     ref2 = torch.as_tensor(g["ref2"][None, :Tn], device=gpu)
-    check(eng.affine_records(eng.affine_scale(mean2, cov2, ref2, cr, tangent, const)), 2)
+    check(eng.affine_records(eng.affine_scale(mean2, cov2, ref2, cr, tangent, const,
+                                              scaled=scaled)), 2)

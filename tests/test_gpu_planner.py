@@ -155,7 +155,10 @@ def test_make_ovehicles_matches_reference_bucketing(gpu):
                                        atol=1e-13)
 
 
-def test_affine_scale_ideal_two_frames(gpu):
+@pytest.mark.parametrize("method,scaled", [
+    ("compute_obstacle_constraints_GMM_affine_scale_ideal", True),
+    ("compute_obstacle_constraints_GMM_affine_robust", False)])
+def test_affine_scale_ideal_two_frames(gpu, method, scaled):
     """compute_obstacle_constraints_GMM_affine_scale_ideal through the agent: frame 300 at
     T == ph, frame 310 at T < ph on the Philox ideal rollout of frame 300's moments with
     frame 300's meanNtangent loaded -- against the oracle chained the same way."""
@@ -169,20 +172,20 @@ def test_affine_scale_ideal_two_frames(gpu):
     x_init = np.array([ref[0][0] - 4.0, ref[0][1] - 0.5, 0.0, 5.0])
     p1 = Params(len(K), K, 300)
     p1.x_init = x_init
-    out1 = agent.compute_obstacle_constraints_GMM_affine_scale_ideal(
+    out1 = getattr(agent, method)(
         p1, ovs, None, None, None, eps, None, T, ref)
     ref2 = ref + np.array([2.0, 0.25])
     p2 = Params(len(K), K, 310)
     p2.x_init = x_init
-    out2 = agent.compute_obstacle_constraints_GMM_affine_scale_ideal(
+    out2 = getattr(agent, method)(
         p2, ovs, None, None, None, eps, None, T - 1, ref2)
     oracle_ovs = _oracle_ovs(ov_cells, pasts, T)
-    w1 = orc.affine_scale_generator(oracle_ovs, T, T, ref)
+    w1 = orc.affine_scale_generator(oracle_ovs, T, T, ref, scaled=scaled)
     mom = orc.save_moments([ov.pred_positions for ov in oracle_ovs], T)
     ideal = orc.predict_ideal(mom, K, T - 1, n_ideal, seed=seed * 1_000_003 + 310)
     m1, t1, _, _, c1 = w1["meanNtangent"]
     w2 = orc.affine_scale_generator(oracle_ovs, T - 1, T, ref2, x_init=x_init,
-                                    loaded=(m1, t1, c1), ideal_trajs=ideal)
+                                    loaded=(m1, t1, c1), ideal_trajs=ideal, scaled=scaled)
     for out, want in ((out1, w1), (out2, w2)):
         assert len(out[0]) == len(want["records"])
         for c, r in zip(out[0], want["records"]):

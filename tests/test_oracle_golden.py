@@ -142,7 +142,8 @@ def _ideal_from_fixture(g):
     return ideal
 
 
-def test_affine_scale_generator_matches_reference(golden):
+@pytest.mark.parametrize("scaled,pre", [(True, "s"), (False, "sr")])   # scale / _affine_robust
+def test_affine_scale_generator_matches_reference(golden, scaled, pre):
     """compute_obstacle_constraints_GMM_affine_scale_ideal restated (v8ideal/__init__.py:
     2074-2456) vs the golden made with the reference's compute_scale / predict_moments /
     choose_closest_tangent: the T == ph step, then a T < ph step on injected ideal clouds that
@@ -150,16 +151,18 @@ def test_affine_scale_generator_matches_reference(golden):
     g = golden("affine_scale")
     T = int(g["T"])
     ovs = ovehicles_from_fixture(g)
-    g1 = orc.affine_scale_generator(ovs, T, T, g["ref1"])
+    g1 = orc.affine_scale_generator(ovs, T, T, g["ref1"], scaled=scaled)
     mean1, tan1, _, _, ci1 = g1["meanNtangent"]
     g2 = orc.affine_scale_generator(ovs, T - 1, T, g["ref2"], x_init=g["x_init"],
-                                    loaded=(mean1, tan1, ci1), ideal_trajs=_ideal_from_fixture(g))
+                                    loaded=(mean1, tan1, ci1), ideal_trajs=_ideal_from_fixture(g),
+                                    scaled=scaled)
     for i, out in ((1, g1), (2, g2)):
         recs = out["records"]
-        np.testing.assert_array_equal([r["which"] for r in recs], g[f"s{i}_which"])
-        np.testing.assert_array_equal([r["side"] for r in recs], g[f"s{i}_side"])
+        np.testing.assert_array_equal([r["which"] for r in recs], g[f"{pre}{i}_which"])
+        np.testing.assert_array_equal([r["side"] for r in recs], g[f"{pre}{i}_side"])
         for key, rtol in (("d", 1e-13), ("margin", 1e-12), ("rhs", 1e-13), ("scale", 1e-12),
                           ("m", 1e-13)):
-            np.testing.assert_allclose([r[key] for r in recs], g[f"s{i}_{key}"], rtol=rtol)
-    # the T < ph step really used loaded indices: they differ from a fresh closest choice
-    assert set(g["s2_which"]) <= {-1, 0, 1}
+            np.testing.assert_allclose([r[key] for r in recs], g[f"{pre}{i}_{key}"], rtol=rtol)
+    assert set(g[f"{pre}2_which"]) <= {-1, 0, 1}
+    if not scaled:
+        assert np.all(g["sr1_scale"] == 1.0) and np.all(g["sr2_scale"] == 1.0)
