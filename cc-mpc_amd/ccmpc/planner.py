@@ -23,6 +23,8 @@ Differences from the reference, all at the boundary:
   * the unseeded RNG of predict_ideal (:2664, :2699) is a Philox stream keyed by
     (seed, frame, cell), so runs are reproducible.
 """
+import os
+
 import numpy as np
 import scipy.stats
 import torch
@@ -134,6 +136,65 @@ def _object_grid(*shape):
     return np.empty(shape, dtype=object).tolist()
 
 
+def _grid_cells(grid, K, shape):
+    """[o][k][...] object grid -> (sum K, *shape) array in (ov, k) cell order."""
+    out = np.zeros((sum(K),) + shape)
+    c = 0
+    for o, k_o in enumerate(K):
+        for k in range(k_o):
+            out[c] = np.asarray(grid[o][k], dtype=float).reshape(shape)
+            c += 1
+    return out
+
+
+def _cells_grid(arr, K, T):
+    """Inverse of _grid_cells for [o][k][t] leaves."""
+    grid = _object_grid(len(K), max(K), T)
+    c = 0
+    for o, k_o in enumerate(K):
+        for k in range(k_o):
+            for t in range(T):
+                grid[o][k][t] = arr[c, t]
+            c += 1
+    return grid
+
+
+def _data_arrays(d, K):
+    """Flatten the generator keys of a data_save dict into npz-safe arrays, cells in (ov, k)
+    order: ovState*_tau_1 (C, 3) = (x, y, yaw); mnt_* = meanNtangent's (C, T, ...) fields."""
+    out = {"K": np.asarray(K, np.int64), "MeanCov": np.bool_(d.get("MeanCov", False)),
+           "shrinking": np.bool_(d.get("shrinking", False)),
+           "OVconstraint": np.bool_(bool(d.get("OVconstraint", False)))}
+    if "ovStateMean_tau_1" in d:
+        out["ovStateMean_tau_1"] = np.stack([_grid_cells(g, K, ()) for g in d["ovStateMean_tau_1"]], 1)
+        out["ovStateCov_tau_1"] = np.stack([_grid_cells(g, K, ()) for g in d["ovStateCov_tau_1"]], 1)
+    if "meanNtangent" in d:
+        mean_p, tangent, cov_p, _, const_idx = d["meanNtangent"]
+        T = len(mean_p[0][0])
+        out["mnt_mean"] = _grid_cells(mean_p, K, (T, 2))
+        out["mnt_tangent"] = _grid_cells(tangent, K, (T,))
+        out["mnt_cov"] = _grid_cells(cov_p, K, (T, 2, 2))
+        out["mnt_const_idx"] = _grid_cells(const_idx, K, (T,)).astype(np.int32)
+    if "x_init" in d:
+        out["x_init"] = np.asarray(d["x_init"], float)
+    for key in ("solve_time", "process_time", "cost", "timeout", "infeasible"):
+        if d.get(key) is not None:
+            out[key] = np.asarray(d[key])
+    return out
+
+
+def _mean_tangent_from_arrays(d):
+    K = [int(k) for k in d["K"]]
+    T = d["mnt_mean"].shape[1]
+    const_idx = _cells_grid(d["mnt_const_idx"], K, T)
+    for row in const_idx:
+        for cell in row:
+            if cell[0] is not None:
+                cell[:] = [int(v) for v in cell]
+    return (_cells_grid(d["mnt_mean"], K, T), _cells_grid(d["mnt_tangent"], K, T),
+            _cells_grid(d["mnt_cov"], K, T), 0, const_idx)
+
+
 class MidlevelAgent:
     """Constraint-generation surface of v8ideal.MidlevelAgent (v8ideal/__init__.py:202-235).
 
@@ -142,7 +203,7 @@ class MidlevelAgent:
 
     def __init__(self, prediction_horizon=8, control_horizon=None, n_predictions=100,
                  ego_vehicle_id=0, n_ideal=1_000_000, record_interval=10, seed=0,
-                 road_boundary_constraints=False, device="cuda", **kwargs):
+                 road_boundary_constraints=False, device="cuda", data_dir=None, **kwargs):
         self.device = engine.require_device(device)
         self.prediction_horizon = int(prediction_horizon)
         self.control_horizon = int(control_horizon or prediction_horizon)
@@ -155,6 +216,8 @@ class MidlevelAgent:
         self.R = risk.R_COLLISION
         self._moments = {}                 # frame -> (mean [C,T,2], cov [C,2T,2T], K, T)
         self._mean_tangent = {}            # frame -> affine_scale meanNtangent (save_data)
+        self._data = {}                    # frame -> data_save dict (save_data / load_data)
+        self.data_dir = data_dir           # load_data from .npz files here (None: in memory)
         self.M_big = 10_000                # params.M_big (v8ideal/__init__.py:86)
         self._ws = engine.Workspace(self.device)
         self.prob_lower_save = None
@@ -374,7 +437,7 @@ class MidlevelAgent:
                                                      seed=seed, workspace=self._ws)
             if np.any(status.cpu().numpy() != 0):
                 raise np.linalg.LinAlgError("predict_ideal: conditional covariance not PD")
-            loaded = self._mean_tangent.get(params.frame - self.record_interval)
+            loaded = self.load_data(params, self.ego_vehicle_id, self.data_dir)
             tangent, const_idx = self._loaded_tangents(loaded, mean.cpu().numpy(), K, T,
                                                        getattr(params, "x_init", None),
                                                        ref.cpu().numpy()[0])
@@ -436,6 +499,58 @@ class MidlevelAgent:
                         ref[:T, 1] - mean[c0 + k, :, 1])
             c0 += k_o
         return tangent, const_idx
+
+    # ------------------------------------------------------------------------------------
+    # Cross-step state: the `agent{id}_frame{f}_cov` data_save dict
+    # (v8ideal/__init__.py:2979-3001, save_data :2559-2567, load_data :2547-2557).  It is kept
+    # in memory by frame; with `directory` it is also written as an .npz with the generator
+    # keys (no pickle).  The QP-side keys (cost, U_star, X_star, ...) belong to the solver,
+    # which is outside this path; scalar ones are carried into the .npz when present.
+
+    def data_save(self, out, params, shrinking=True, apply_robust=True):
+        """The generator part of do_highlevel_control's data_save (:2979-2993) for a 9-tuple
+        `out` returned by one of the compute_obstacle_constraints_* methods."""
+        d = {"direct": out[5], "MeanCov": True, "OVconstraint": out[4],
+             "ovStateMean_tau_1": out[6], "ovStateCov_tau_1": out[7], "shrinking": shrinking}
+        if shrinking and apply_robust and not isinstance(out[8], int):
+            d["meanNtangent"] = out[8]
+        d["params"] = params
+        if getattr(params, "x_init", None) is not None:
+            d["x_init"] = np.asarray(params.x_init)
+        return d
+
+    def save_data(self, data_save, params, ego_vehicle_id, directory=None):
+        """v8ideal/__init__.py:2559-2567 (the pickle is an .npz when `directory` is given)."""
+        frame = int(params.frame)
+        self._data[frame] = data_save
+        if "meanNtangent" in data_save:
+            self._mean_tangent[frame] = data_save["meanNtangent"]
+        if directory is not None:
+            np.savez(self._data_path(directory, ego_vehicle_id, frame),
+                     **_data_arrays(data_save, [int(k) for k in np.asarray(params.K)]))
+
+    def load_data(self, params, ego_vehicle_id, directory=None):
+        """v8ideal/__init__.py:2547-2557: meanNtangent of frame - record_interval.  The
+        reference's load fails (UnboundLocalError) when that frame saved none; so does this
+        (KeyError)."""
+        frame = int(params.frame) - self.record_interval
+        if directory is not None:
+            path = self._data_path(directory, ego_vehicle_id, frame)
+            try:
+                d = np.load(path, allow_pickle=False)
+            except OSError as e:
+                raise KeyError(f"no saved data for frame {frame}: {e}") from None
+            if "mnt_mean" not in d:
+                raise KeyError(f"frame {frame} saved no meanNtangent ({path})")
+            return _mean_tangent_from_arrays(d)
+        if frame not in self._mean_tangent:
+            raise KeyError(f"no meanNtangent saved for frame {frame} (the reference fails to "
+                           "load its _cov pickle here)")
+        return self._mean_tangent[frame]
+
+    @staticmethod
+    def _data_path(directory, ego_vehicle_id, frame):
+        return os.path.join(directory, f"agent{ego_vehicle_id}_frame{frame}_cov.npz")
 
     # ------------------------------------------------------------------------------------
     def save_moments(self, ovehicles, O, K, T, Tpred, ego_vehicle_id, params):

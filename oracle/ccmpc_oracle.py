@@ -255,6 +255,29 @@ def vertices_and_l4(ovehicles, ph):
     return vertices, A_union, b_union
 
 
+def milp_obstacle_rows(ovehicles, T, ph, diag, M_big=10_000):
+    """v8/__init__.py:692-724 (road boundaries off, S_big = 0): per (ov, k, t) the L4 faces
+    as big-M rows.  Returns a list of (c, t, A (4,2), rhs (4,)) with rhs = b + diag and
+    c = sum(K[:ov]) + k, plus a checker  holds(xy, delta) -> bool per row, in the reference's
+    constraint order (4 face rows then the sum row)."""
+    _, A_union, b_union = vertices_and_l4(ovehicles, ph)
+    rows, c = [], 0
+    for o, ov in enumerate(ovehicles):
+        for k in range(ov.n_states):
+            for t in range(T):
+                rows.append((c, t, A_union[t][k][o], b_union[t][k][o] + diag))
+            c += 1
+
+    def holds(xy, delta):
+        out = []
+        for c, t, A, rhs in rows:
+            lhs = A @ xy[t, :2] + M_big * (1 - delta[c, t])
+            out.extend(bool(v) for v in lhs >= rhs)
+            out.append(bool(np.sum(delta[c, t]) >= 1))
+        return out
+    return rows, holds
+
+
 # ----------------------------------------------------------------------------------------
 # Generators
 # ----------------------------------------------------------------------------------------

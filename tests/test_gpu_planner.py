@@ -194,3 +194,72 @@ def test_affine_scale_ideal_two_frames(gpu, method, scaled):
             assert c.rhs == pytest.approx(r["rhs"], rel=1e-9)
     # meanNtangent (the 9th element) carries the saved slopes / indices for the next frame
     assert out2[8][1][0][0][0] == pytest.approx(w2["meanNtangent"][1][0][0][0], rel=1e-9)
+
+
+def test_data_save_npz_carries_mean_tangent_across_agents(gpu, tmp_path):
+    """save_data / load_data (v8ideal/__init__.py:2547-2567, :2979-2993) through .npz files:
+    a fresh agent that loads frame 300's moments and meanNtangent from disk generates frame
+    310 exactly as the agent that produced them; without the file the T < ph step fails as
+    the reference's does."""
+    from ccmpc import ovehicle, planner
+    T, n_ideal, seed = 8, 20_000, 4
+    ov_cells, ref, pasts = _scene(62, O=2, N=2500, T=T)
+    K = [len(c) for c in ov_cells]
+    ovs = ovehicle.scene_from_positions(ov_cells, pasts, device=gpu)
+    eps = orc.eps_ura_matrix(K)
+    x_init = np.array([ref[0][0] - 4.0, ref[0][1] - 0.5, 0.0, 5.0])
+    p1, p2 = Params(len(K), K, 300), Params(len(K), K, 310)
+    p1.x_init = p2.x_init = x_init
+    ref2 = ref + np.array([2.0, 0.25])
+    a = planner.MidlevelAgent(prediction_horizon=T, n_ideal=n_ideal, seed=seed, device=gpu)
+    out1 = a.compute_obstacle_constraints_GMM_affine_scale_ideal(p1, ovs, None, None, None, eps,
+                                                                 None, T, ref)
+    a.save_data(a.data_save(out1, p1), p1, a.ego_vehicle_id, directory=str(tmp_path))
+    a.save_moments_npz(300, str(tmp_path / "m300.npz"))
+    want = a.compute_obstacle_constraints_GMM_affine_scale_ideal(p2, ovs, None, None, None, eps,
+                                                                 None, T - 1, ref2)
+    b = planner.MidlevelAgent(prediction_horizon=T, n_ideal=n_ideal, seed=seed, device=gpu,
+                              data_dir=str(tmp_path))
+    with pytest.raises(KeyError):       # no moments / meanNtangent yet
+        b.compute_obstacle_constraints_GMM_affine_scale_ideal(p2, ovs, None, None, None, eps,
+                                                              None, T - 1, ref2)
+    b.load_moments_npz(300, str(tmp_path / "m300.npz"))
+    got = b.compute_obstacle_constraints_GMM_affine_scale_ideal(p2, ovs, None, None, None, eps,
+                                                                None, T - 1, ref2)
+    assert len(got[0]) == len(want[0])
+    for c, r in zip(got[0], want[0]):
+        assert (c.ov, c.k, c.t, c.which, c.side) == (r.ov, r.k, r.t, r.which, r.side)
+        assert c.rhs == r.rhs and c.d == r.d
+    d = np.load(tmp_path / f"agent{a.ego_vehicle_id}_frame300_cov.npz", allow_pickle=False)
+    assert d["mnt_mean"].shape == (sum(K), T, 2) and d["mnt_const_idx"].dtype == np.int32
+    assert bool(d["MeanCov"]) and bool(d["shrinking"])
+    np.testing.assert_array_equal(d["x_init"], x_init)
+
+
+@pytest.mark.parametrize("T_ctrl", [8, 6])
+def test_v8_milp_rows_match_oracle(gpu, T_ctrl):
+    """v8.MidlevelAgent.compute_obstacle_constraints (v8/__init__.py:692-724): the big-M rows
+    over the device L4 polytopes against the oracle restatement, numerically (BigMRows) and
+    as the reference's expression list evaluated at sample (X, Delta)."""
+    from ccmpc import milp, ovehicle
+    T = 8
+    ov_cells, ref, pasts = _scene(63, O=3, N=2000, T=T)
+    K = [len(c) for c in ov_cells]
+    ovs = ovehicle.scene_from_positions(ov_cells, pasts, device=gpu)
+    diag = milp.ego_diag(4.7, 1.9)
+    agent = milp.MidlevelAgentV8(prediction_horizon=T, control_horizon=T_ctrl, diag=diag,
+                                 device=gpu)
+    p = Params(len(K), K, 0)
+    rows, vertices, A_union, b_union = agent.compute_obstacle_constraints(
+        p, ovs, None, None, None, None)
+    want, holds = orc.milp_obstacle_rows(_oracle_ovs(ov_cells, pasts, T), T_ctrl, T, diag)
+    assert len(rows) == 5 * len(want)
+    for c, t, A, rhs in want:
+        np.testing.assert_allclose(rows.A[c, t], A, rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(rows.rhs[c, t], rhs, rtol=1e-12)
+    rng = np.random.default_rng(0)
+    X = rng.normal(ref[0], 6.0, size=(T_ctrl, 2))
+    Delta = rng.integers(0, 2, size=(sum(K), T_ctrl, 4)).astype(float)
+    cons, *_ = agent.compute_obstacle_constraints(p, ovs, X, Delta, None, None)
+    assert [bool(v) for v in cons] == holds(X, Delta)
+    assert len(A_union) == T and np.allclose(A_union[0][0][0], rows.A[0, 0])
