@@ -77,11 +77,13 @@ class ParticleStore:
         return F64 if self.dtype == torch.float64 else F32
 
     @classmethod
-    def from_cells(cls, cells, device="cuda", dtype=torch.float64, origin=None):
+    def from_cells(cls, cells, device="cuda", dtype=torch.float64, origin=None, capacity=None):
         """cells: list of (N_j, T, 2) arrays (the reference's pred_positions[k] layout).
-        For a float32 store, ``origin`` (n_cells, 2) is subtracted in float64 before the cast."""
+        For a float32 store, ``origin`` (n_cells, 2) is subtracted in float64 before the cast.
+        ``capacity`` raises the particle bound the kernels are sized for (n_particles_bound)."""
         T = cells[0].shape[1]
-        store = cls(T, [c.shape[0] for c in cells], dtype=dtype, device=device, origin=origin)
+        store = cls(T, [c.shape[0] for c in cells], dtype=dtype, device=device, origin=origin,
+                    capacity=capacity)
         host = np.zeros((2 * T, store.ld), dtype=np.float64 if dtype == torch.float64
                         else np.float32)
         for j, c in enumerate(cells):

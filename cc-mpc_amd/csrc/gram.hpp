@@ -47,6 +47,10 @@ struct Geo {
 // and a shallower tree.  (64 at RB >= 3 balances the f64 matrix pipes better per wave but
 // pays the per-workgroup combine ~3x more often: C5 went from 94 to 134 us.)
 inline int store_lg_wave_quota(int /*rb*/, int64_t n_bound) {
+#if CCMPC_PROBE & 8  // diagnostic build only: CCMPC_LG_WQ overrides the large-input quota
+  static const int ov = [] { const char *e = getenv("CCMPC_LG_WQ"); return e ? atoi(e) : 0; }();
+  if (ov && n_bound > (int64_t(1) << 18)) return ov;
+#endif
   return n_bound <= (int64_t(1) << 18) ? 6 : 8;
 }
 
@@ -119,6 +123,146 @@ __device__ __forceinline__ bool locate_item(int32_t item, const int64_t *__restr
     before += total;
   }
   return false;
+}
+
+// ---- balanced mode (bandwidth-bound inputs) -------------------------------------------------
+// Power-of-two items leave the chip unevenly loaded once the input is large: C4 (640k
+// particles in 67 cells) made 693 items of 1024 particles for 768 resident slots, so 181 CUs
+// ran 3 items and 75 ran 2, and the launch lasted as long as the 3-item CUs (measured,
+// tools/probe_balance.py); smaller power-of-two items pay the per-item combine more often
+// (C4 29.6 -> 34.1 -> 45.7 us at 256 -> 128 -> 64 particles per wave).  Slices of equal length
+// across cell boundaries balance the stream exactly, but a workgroup holding two cells' segments
+// runs two pipelines back to back and its second cell finalises ~5 us late.  Balanced mode keeps
+// one item per workgroup: the grid is the device's resident capacity G and the chunk is
+// total / (G - n_cells) rounded up to kChunkAlign, computed on the device from the counts.  It
+// always fits (sum_c ceil(n_c / chunk) <= total / chunk + n_cells <= G), and no CU streams
+// more than its slots x chunk.  (A binary search for the smallest fitting chunk cost ~3 us of
+// wave reductions per launch on C4, more than the ~5% shorter stream it bought.)
+inline bool balanced_mode(int64_t n_bound) { return n_bound > (int64_t(1) << 18); }
+constexpr int kChunkAlign = 16;  // item boundaries: whole 128-byte f64 lines, aligned quads
+
+// ceil(n / d) for n >= 0, d > 0: 32-bit when both fit (every realistic cell), else 64-bit.
+__device__ __forceinline__ int64_t ceil_div_fast(int64_t n, int64_t d) {
+  if (n < (int64_t(1) << 31) && d < (int64_t(1) << 31))
+    return static_cast<int64_t>((static_cast<uint32_t>(n) + static_cast<uint32_t>(d) - 1u) /
+                                static_cast<uint32_t>(d));
+  return (n + d - 1) / d;
+}
+
+// Wave sum of a double (two 32-bit DPP moves per step; exact for integer-valued inputs).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo =
+      __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(u), CTRL, 0xf, 0xf, false);
+  const uint32_t hi =
+      __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+__device__ __forceinline__ double wave_sum_dpp_f64(double v) {
+  v += dpp_f64<0x111>(v);
+  v += dpp_f64<0x112>(v);
+  v += dpp_f64<0x114>(v);
+  v += dpp_f64<0x118>(v);
+  auto lane_val = [&](int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), l);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), l);
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  return (lane_val(15) + lane_val(31)) + (lane_val(47) + lane_val(63));
+}
+
+// Item id -> (cell, chunk index, ...) as locate_item, with the balanced chunk (returned in
+// *chunk_out).
+__device__ __forceinline__ bool locate_balanced(int32_t item, int G,
+                                                const int64_t *__restrict__ cnt,
+                                                const int64_t *__restrict__ off, int n_cells,
+                                                ItemLoc &loc, int64_t *chunk_out,
+                                                const int32_t *__restrict__ cell_ref = nullptr) {
+  const int lane = threadIdx.x & 63;
+  // cells 0..127 (every realistic batch) arrive in ONE round trip and stay in registers;
+  // blocks beyond are re-read where needed
+  const bool in0 = lane < n_cells, in1 = lane + 64 < n_cells;
+  const int64_t n0 = in0 ? cnt[lane] : 0, n1 = in1 ? cnt[lane + 64] : 0;
+  const int64_t o0 = in0 ? off[lane] : 0, o1 = in1 ? off[lane + 64] : 0;
+  const int32_t rs0 = (cell_ref && in0) ? cell_ref[lane] : 0;
+  const int32_t rs1 = (cell_ref && in1) ? cell_ref[lane + 64] : 0;
+  auto count_at = [&](int base) -> int64_t {
+    return base == 0 ? n0 : base == 64 ? n1 : (base + lane < n_cells ? cnt[base + lane] : 0);
+  };
+  double part = 0.0;  // exact: counts and their sum < 2^53
+  for (int base = 0; base < n_cells; base += 64) part += static_cast<double>(count_at(base));
+  const double td = wave_sum_dpp_f64(part);
+  const int64_t A = kChunkAlign;
+  // in units of A, +1 against the rounding of the division (the host keeps 2 n_cells <= G)
+  const int64_t chunk =
+      (static_cast<int64_t>(td / (static_cast<double>(G - n_cells) * A)) + 1) * A;
+  *chunk_out = chunk;
+  int32_t before = 0;
+  for (int base = 0; base < n_cells; base += 64) {
+    const int c = base + lane;
+    const bool in = c < n_cells;
+    const int64_t n = count_at(base);
+    const int64_t o = base == 0 ? o0 : base == 64 ? o1 : (in ? off[c] : 0);
+    const int32_t rs = base == 0 ? rs0 : base == 64 ? rs1 : ((cell_ref && in) ? cell_ref[c] : 0);
+    const int32_t mine = in ? static_cast<int32_t>(n > 0 ? ceil_div_fast(n, chunk) : 1) : 0;
+    int32_t incl = mine;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const int32_t y = __shfl_up(incl, s, 64);
+      if (lane >= s) incl += y;
+    }
+    const int32_t tot = __shfl(incl, 63, 64);
+    if (item < before + tot) {
+      const unsigned long long m = __ballot(before + incl > item);
+      const int l = __ffsll(static_cast<long long>(m)) - 1;
+      loc.cell = base + l;
+      loc.first = before + __shfl(incl - mine, l, 64);
+      loc.chunk_idx = item - loc.first;
+      loc.cnt = __shfl(n, l, 64);
+      loc.off = __shfl(o, l, 64);
+      loc.ref_sel = __shfl(rs, l, 64);
+      return true;
+    }
+    before += tot;
+  }
+  return false;
+}
+
+// Host: the device's CU count (cached per device).
+inline int device_cus() {
+  static int cache[64];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
+  if (cache[d] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0)
+      n = 256;
+    cache[d] = n;
+  }
+  return cache[d];
+}
+
+// Host: balanced-mode grid = resident workgroups of `kernel` at `threads` per workgroup.
+template <auto Kernel>
+inline int resident_grid(int threads) {
+  static int cache[64];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) d = 0;
+  if (cache[d] == 0) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, Kernel, threads, 0) !=
+            hipSuccess || per_cu <= 0)
+      per_cu = 1;
+    cache[d] = per_cu * device_cus();
+  }
+  return cache[d];
+}
+
+// Host: bound on the balanced-mode items of any kernel (<= 2048 threads per CU resident).
+inline int64_t balanced_max_items(int threads) {
+  return static_cast<int64_t>(device_cus()) * (2048 / threads);
 }
 
 // Sum over cells c < cell of f(c), wave-parallel (every wave computes it redundantly).

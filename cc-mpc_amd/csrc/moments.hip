@@ -25,6 +25,8 @@
 //    (cycle variant) builds its T(T-1)/2 half-spaces from the covariance it just produced in
 //    LDS -- no kernel boundary between moments and constraints.
 #include "constraints.hpp"
+#include <algorithm>
+
 #include "gram.hpp"
 
 #ifndef CCMPC_PROBE
@@ -40,6 +42,10 @@ __device__ unsigned long long g_probe_ts[kProbeMaxWG * kProbeSlots];
   do {                                                                                         \
     if (threadIdx.x == 0 && blockIdx.x < kProbeMaxWG)                                          \
       g_probe_ts[blockIdx.x * kProbeSlots + (k)] = __builtin_amdgcn_s_memrealtime();           \
+    if ((k) == 0 && threadIdx.x == 0 && blockIdx.x < kProbeMaxWG)                              \
+      g_probe_ts[blockIdx.x * kProbeSlots + 7] =                                               \
+          (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg(0xF814)) << 32) |         \
+          __builtin_amdgcn_s_getreg(0xF804); /* XCC_ID : HW_ID, slot 7 */                       \
   } while (0)
 #else
 #define PROBE_TS(k) \
@@ -136,7 +142,7 @@ __device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &lo
     PROBE_TS(3);
     PROBE_TS(4);
   } else {
-    publish(tree.slabs[0] + static_cast<int64_t>(blockIdx.x) * E, false);
+    publish(tree.slabs[0] + static_cast<int64_t>(loc.first + loc.chunk_idx) * E, false);
     PROBE_TS(3);
     const double *root;
     int32_t root_n;
@@ -155,7 +161,40 @@ __device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &lo
   PROBE_TS(6);
 }
 
-template <typename P, int RB, bool MINK>
+// Per-wave share of an item's particles [a, b): contiguous quota ranges (power-of-two items,
+// quota wq) or, in balanced mode, load groups of GS particles dealt round-robin to the NW
+// waves (every wave within one group of the others, whatever the chunk).
+struct WaveRange {
+  int64_t p0, stride, p1, ngroups;
+};
+template <bool BAL>
+__device__ __forceinline__ WaveRange wave_range(int64_t a, int64_t b, int w, int nw, int64_t wq,
+                                                int64_t gs) {
+  WaveRange r;
+  if (BAL) {
+    r.p0 = a + static_cast<int64_t>(w) * gs;
+    r.stride = nw * gs;
+    r.p1 = b;
+    r.ngroups = r.p0 < b ? ceil_div(b - r.p0, r.stride) : 0;
+  } else {
+    r.p0 = a + static_cast<int64_t>(w) * wq;
+    r.stride = gs;
+    r.p1 = (r.p0 + wq < b) ? r.p0 + wq : b;
+    r.ngroups = r.p1 > r.p0 ? ceil_div(r.p1 - r.p0, gs) : 0;
+  }
+  return r;
+}
+
+// The per-cell inputs of the half-space tail: issued at an item's start, landing behind its
+// stream loop (thread i < 2T: ref_traj row, then the 3 risk constants).
+__device__ __forceinline__ double prefetch_tail(const MinkParams &mp, const ItemLoc &loc,
+                                                int rows) {
+  if (threadIdx.x < rows) return mp.ref_traj[static_cast<int64_t>(loc.ref_sel) * rows + threadIdx.x];
+  if (threadIdx.x < rows + 3) return mp.cell_risk[3 * loc.cell + (threadIdx.x - rows)];
+  return 0.0;
+}
+
+template <typename P, int RB, bool MINK, bool BAL>
 // The fused half-space tail needs a few more registers than the 128 of 4 waves/SIMD at RB = 1.
 __global__ __launch_bounds__(Geo<RB>::NW * 64,
                              (MINK && RB == 1) ? 3 : Geo<RB>::MIN_WAVES_PER_SIMD)
@@ -181,89 +220,99 @@ void moments_kernel(
   __shared__ double ref_lds[MINK ? D + 3 : 1];  // reference trajectory [T][2], then risk[3]
   __shared__ int flag;
 
-  ItemLoc loc;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+  const int rows = 2 * T;
   const int lg_chunk = lg_wq + (G::NW == 4 ? 2 : 3);
-  const int64_t wq = int64_t(1) << lg_wq, chunk = int64_t(1) << lg_chunk;
+
+  // one work item: the cell's particles [a, b) -> partial Gram -> combine tree / finalise
+  auto item = [=](const ItemLoc &loc, int32_t nit, int64_t a, int64_t b) {
+    const int r = lane & 15;
+    const int g = lane >> 4;
+    const int64_t cnt = loc.cnt;
+    const double pre = MINK ? prefetch_tail(mp, loc, rows) : 0.0;
+    const WaveRange wr = wave_range<BAL>(a, b, w, G::NW, int64_t(1) << lg_wq, 16 * S);
+    const int64_t p1 = wr.p1;
+
+    double sh[RB];
+    const P *rowp[RB];
+    bool live[RB];
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) {
+      const int R = 16 * bb + r;
+      live[bb] = R < rows;
+      rowp[bb] = pos + static_cast<int64_t>(live[bb] ? R : 0) * ld + loc.off;
+      sh[bb] = (live[bb] && cnt > 0) ? static_cast<double>(rowp[bb][0]) : 0.0;
+    }
+
+    d4 acc[NACC][NT];
+#pragma unroll
+    for (int x = 0; x < NACC; ++x)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[x][t] = d4{0.0, 0.0, 0.0, 0.0};
+    double s1[RB];
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) s1[bb] = 0.0;
+
+    // double-buffered load groups: the next group's loads are in flight during this group's
+    // MFMAs.  The prefetch is unconditional (a group past the end is clamped + masked and
+    // never multiplied) so there is no divergent join for the waitcnt pass to merge.
+    // sched_barrier(0) fences keep the four phases in program order, so each MFMA group waits
+    // (vmcnt) only for its own buffer while the other buffer's loads stay in flight.
+    const int64_t ngroups = wr.ngroups, st = wr.stride;
+    Quad<P> va[S][RB], vb[S][RB];
+    if (ngroups > 0) {
+      load_group<P, RB, S>(va, rowp, wr.p0, p1, g);
+      int64_t gi = 0;
+      for (; gi + 2 <= ngroups; gi += 2) {
+        const int64_t ga = wr.p0 + gi * st, gb = ga + st;
+        load_group<P, RB, S>(vb, rowp, gb, p1, g);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group<P, RB, S, NACC>(va, sh, live, ga, p1, g, acc, s1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_group<P, RB, S>(va, rowp, gb + st, p1, g);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group<P, RB, S, NACC>(vb, sh, live, gb, p1, g, acc, s1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (gi < ngroups) mfma_group<P, RB, S, NACC>(va, sh, live, wr.p0 + gi * st, p1, g, acc, s1);
+    }
+    PROBE_TS(2);
+
+    if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
+#pragma unroll
+    for (int bb = 0; bb < RB; ++bb) {
+      if (w == 0 && g == 0) shift_lds[16 * bb + r] = sh[bb];
+    }
+    const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
+    cell_epilogue<Scheme16<RB>, MINK, COV_IN_LDS>(
+        [&](double *dst, bool to_lds) {
+          combine_waves<RB, NACC, G::NW>(acc, s1, xch, dst, to_lds);
+        },
+        loc, nit, T, tree, origin, out_mean, out_cov, mp, L);
+  };
+
   PROBE_TS(0);
+  if (BAL) {
+    ItemLoc loc;
+    int64_t chunk;
+    if (!locate_balanced(blockIdx.x, gridDim.x, cell_cnt, cell_off, n_cells, loc, &chunk,
+                         MINK ? mp.cell_ref : nullptr))
+      return;  // uniform
+    PROBE_TS(1);
+    const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) * chunk;
+    item(loc, static_cast<int32_t>(loc.cnt > 0 ? ceil_div_fast(loc.cnt, chunk) : 1), i0,
+         min(i0 + chunk, loc.cnt));
+    return;
+  }
+  ItemLoc loc;
   if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc,
                    MINK ? mp.cell_ref : nullptr))
     return;  // uniform
   PROBE_TS(1);
-  const int64_t cnt = loc.cnt;
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  const int r = lane & 15;
-  const int g = lane >> 4;
-  const int rows = 2 * T;
   const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
-  // the half-space tail's per-cell inputs: loads issued now, landing behind the stream loop
-  double pre = 0.0;
-  if (MINK) {
-    if (threadIdx.x < rows)
-      pre = mp.ref_traj[static_cast<int64_t>(loc.ref_sel) * rows + threadIdx.x];
-    else if (threadIdx.x < rows + 3)
-      pre = mp.cell_risk[3 * loc.cell + (threadIdx.x - rows)];
-  }
-  const int64_t i1 = (i0 + chunk < cnt) ? i0 + chunk : cnt;
-  const int64_t p0 = i0 + static_cast<int64_t>(w) * wq;
-  const int64_t p1 = (p0 + wq < i1) ? p0 + wq : i1;
-
-  double sh[RB];
-  const P *rowp[RB];
-  bool live[RB];
-#pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    const int R = 16 * b + r;
-    live[b] = R < rows;
-    rowp[b] = pos + static_cast<int64_t>(live[b] ? R : 0) * ld + loc.off;
-    sh[b] = (live[b] && cnt > 0) ? static_cast<double>(rowp[b][0]) : 0.0;
-  }
-
-  d4 acc[NACC][NT];
-#pragma unroll
-  for (int a = 0; a < NACC; ++a)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[a][t] = d4{0.0, 0.0, 0.0, 0.0};
-  double s1[RB];
-#pragma unroll
-  for (int b = 0; b < RB; ++b) s1[b] = 0.0;
-
-  // double-buffered load groups: the next group's loads are in flight during this group's
-  // MFMAs.  The prefetch is unconditional (a group past the end is clamped + masked and
-  // never multiplied) so there is no divergent join for the waitcnt pass to merge.
-  const int64_t ngroups = p1 > p0 ? ceil_div(p1 - p0, 16 * S) : 0;
-  Quad<P> va[S][RB], vb[S][RB];
-  // sched_barrier(0) fences keep the four phases in program order, so each MFMA group waits
-  // (vmcnt) only for its own buffer while the other buffer's loads stay in flight.
-  if (ngroups > 0) {
-    load_group<P, RB, S>(va, rowp, p0, p1, g);
-    int64_t gi = 0;
-    for (; gi + 2 <= ngroups; gi += 2) {
-      const int64_t ga = p0 + gi * 16 * S, gb = ga + 16 * S;
-      load_group<P, RB, S>(vb, rowp, gb, p1, g);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_group<P, RB, S, NACC>(va, sh, live, ga, p1, g, acc, s1);
-      __builtin_amdgcn_sched_barrier(0);
-      load_group<P, RB, S>(va, rowp, gb + 16 * S, p1, g);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_group<P, RB, S, NACC>(vb, sh, live, gb, p1, g, acc, s1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (gi < ngroups) mfma_group<P, RB, S, NACC>(va, sh, live, p0 + gi * 16 * S, p1, g, acc, s1);
-  }
-  PROBE_TS(2);
-
-  const int32_t nit = items_of(cnt, lg_chunk);
-  if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
-#pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    if (w == 0 && g == 0) shift_lds[16 * b + r] = sh[b];
-  }
-  const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
-  cell_epilogue<Scheme16<RB>, MINK, COV_IN_LDS>(
-      [&](double *dst, bool to_lds) { combine_waves<RB, NACC, G::NW>(acc, s1, xch, dst, to_lds); },
-      loc, nit, T, tree, origin, out_mean, out_cov, mp, L);
+  const int64_t i1 = min(i0 + (int64_t(1) << lg_chunk), loc.cnt);
+  item(loc, items_of(loc.cnt, lg_chunk), i0, i1);
 }
 
 // ---- Scheme4: f64 4x4x4_4b MFMA over 4-row blocks (T <= 12) -------------------------------
@@ -331,7 +380,7 @@ __device__ __forceinline__ void mfma_group4(const Pair<P> (&raw)[NB], const doub
 
 constexpr int kNW4 = 4;  // waves per Scheme4 work item
 
-template <typename P, int NB, bool MINK>
+template <typename P, int NB, bool MINK, bool BAL>
 __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
@@ -349,90 +398,111 @@ __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
   __shared__ double ref_lds[MINK ? D + 3 : 1];  // reference trajectory [T][2], then risk[3]
   __shared__ int flag;
 
-  ItemLoc loc;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+  const int rows = 2 * T;
   const int lg_chunk = lg_wq + 2;
-  const int64_t wq = int64_t(1) << lg_wq, chunk = int64_t(1) << lg_chunk;
+
+  auto item = [=](const ItemLoc &loc, int32_t nit, int64_t a, int64_t b) {
+    const int c = lane & 3, m = lane >> 2;
+    const int64_t cnt = loc.cnt;
+    const double pre = MINK ? prefetch_tail(mp, loc, rows) : 0.0;
+    const WaveRange wr = wave_range<BAL>(a, b, w, kNW4, int64_t(1) << lg_wq, 32);
+    const int64_t p1 = wr.p1;
+
+    double sh[NB];
+    const P *rowp[NB];
+    bool live[NB];
+#pragma unroll
+    for (int I = 0; I < NB; ++I) {
+      const int R = 4 * I + c;
+      live[I] = R < rows;
+      rowp[I] = pos + static_cast<int64_t>(live[I] ? R : 0) * ld + loc.off;
+      sh[I] = (live[I] && cnt > 0) ? static_cast<double>(rowp[I][0]) : 0.0;
+    }
+    double acc[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) acc[p] = 0.0;
+    double s1[NB];
+#pragma unroll
+    for (int I = 0; I < NB; ++I) s1[I] = 0.0;
+
+    const int64_t ngroups = wr.ngroups, st = wr.stride;
+    Pair<P> va[NB], vb[NB];
+    if (ngroups > 0) {
+      load_group4<P, NB>(va, rowp, wr.p0, p1, m);
+      int64_t gi = 0;
+      for (; gi + 2 <= ngroups; gi += 2) {
+        const int64_t ga = wr.p0 + gi * st, gb = ga + st;
+        load_group4<P, NB>(vb, rowp, gb, p1, m);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group4<P, NB>(va, sh, live, ga, p1, m, acc, s1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_group4<P, NB>(va, rowp, gb + st, p1, m);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_group4<P, NB>(vb, sh, live, gb, p1, m, acc, s1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (gi < ngroups) mfma_group4<P, NB>(va, sh, live, wr.p0 + gi * st, p1, m, acc, s1);
+    }
+    PROBE_TS(2);
+
+    if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
+#pragma unroll
+    for (int I = 0; I < NB; ++I)
+      if (w == 0 && m == 0) shift_lds[4 * I + c] = sh[I];
+    const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
+    cell_epilogue<Sch, MINK, MINK>(
+        [&](double *dst, bool to_lds) { combine4<NB, kNW4>(acc, s1, xch, dst, to_lds); }, loc,
+        nit, T, tree, origin, out_mean, out_cov, mp, L);
+  };
+
   PROBE_TS(0);
+  if (BAL) {
+    ItemLoc loc;
+    int64_t chunk;
+    if (!locate_balanced(blockIdx.x, gridDim.x, cell_cnt, cell_off, n_cells, loc, &chunk,
+                         MINK ? mp.cell_ref : nullptr))
+      return;  // uniform
+    PROBE_TS(1);
+    const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) * chunk;
+    item(loc, static_cast<int32_t>(loc.cnt > 0 ? ceil_div_fast(loc.cnt, chunk) : 1), i0,
+         min(i0 + chunk, loc.cnt));
+    return;
+  }
+  ItemLoc loc;
   if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc,
                    MINK ? mp.cell_ref : nullptr))
     return;  // uniform
   PROBE_TS(1);
-  const int64_t cnt = loc.cnt;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  const int c = lane & 3, m = lane >> 2;
-  const int rows = 2 * T;
   const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
-  double pre = 0.0;  // the half-space tail's per-cell inputs, landing behind the stream loop
-  if (MINK) {
-    if (threadIdx.x < rows)
-      pre = mp.ref_traj[static_cast<int64_t>(loc.ref_sel) * rows + threadIdx.x];
-    else if (threadIdx.x < rows + 3)
-      pre = mp.cell_risk[3 * loc.cell + (threadIdx.x - rows)];
-  }
-  const int64_t i1 = (i0 + chunk < cnt) ? i0 + chunk : cnt;
-  const int64_t p0 = i0 + static_cast<int64_t>(w) * wq;
-  const int64_t p1 = (p0 + wq < i1) ? p0 + wq : i1;
-
-  double sh[NB];
-  const P *rowp[NB];
-  bool live[NB];
-#pragma unroll
-  for (int I = 0; I < NB; ++I) {
-    const int R = 4 * I + c;
-    live[I] = R < rows;
-    rowp[I] = pos + static_cast<int64_t>(live[I] ? R : 0) * ld + loc.off;
-    sh[I] = (live[I] && cnt > 0) ? static_cast<double>(rowp[I][0]) : 0.0;
-  }
-  double acc[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) acc[p] = 0.0;
-  double s1[NB];
-#pragma unroll
-  for (int I = 0; I < NB; ++I) s1[I] = 0.0;
-
-  const int64_t ngroups = p1 > p0 ? ceil_div(p1 - p0, 32) : 0;
-  Pair<P> va[NB], vb[NB];
-  if (ngroups > 0) {
-    load_group4<P, NB>(va, rowp, p0, p1, m);
-    int64_t gi = 0;
-    for (; gi + 2 <= ngroups; gi += 2) {
-      const int64_t ga = p0 + gi * 32, gb = ga + 32;
-      load_group4<P, NB>(vb, rowp, gb, p1, m);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_group4<P, NB>(va, sh, live, ga, p1, m, acc, s1);
-      __builtin_amdgcn_sched_barrier(0);
-      load_group4<P, NB>(va, rowp, gb + 32, p1, m);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_group4<P, NB>(vb, sh, live, gb, p1, m, acc, s1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (gi < ngroups) mfma_group4<P, NB>(va, sh, live, p0 + gi * 32, p1, m, acc, s1);
-  }
-  PROBE_TS(2);
-
-  const int32_t nit = items_of(cnt, lg_chunk);
-  if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
-#pragma unroll
-  for (int I = 0; I < NB; ++I)
-    if (w == 0 && m == 0) shift_lds[4 * I + c] = sh[I];
-  const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
-  cell_epilogue<Sch, MINK, MINK>(
-      [&](double *dst, bool to_lds) { combine4<NB, kNW4>(acc, s1, xch, dst, to_lds); }, loc,
-      nit, T, tree, origin, out_mean, out_cov, mp, L);
+  const int64_t i1 = min(i0 + (int64_t(1) << lg_chunk), loc.cnt);
+  item(loc, items_of(loc.cnt, lg_chunk), i0, i1);
 }
 
 template <typename P, int RB, bool MINK>
 static int launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
                   const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
                   double *mean, double *cov, const MinkParams &mp, hipStream_t s) {
+  constexpr int threads = Geo<RB>::NW * 64;
   const int lg_wq = store_lg_wave_quota(RB, n_bound);
-  const int64_t items = max_items(n_cells, n_bound, int64_t(1) << store_lg_chunk(RB, n_bound));
   TreeLayout tree;
+  const int grid =
+      balanced_mode(n_bound) ? resident_grid<moments_kernel<P, RB, MINK, true>>(threads) : 0;
+  if (grid > 0 && 2 * n_cells <= grid) {
+    if (!tree_layout(ws, ws_bytes, balanced_max_items(threads), n_cells, slab_doubles(RB),
+                     tree))
+      return CCMPC_ERR_WORKSPACE;
+    hipLaunchKernelGGL((moments_kernel<P, RB, MINK, true>), dim3(static_cast<unsigned>(grid)),
+                       dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
+                       mean, cov, mp);
+    return CCMPC_OK;
+  }
+  const int64_t items = max_items(n_cells, n_bound, int64_t(1) << store_lg_chunk(RB, n_bound));
   if (!tree_layout(ws, ws_bytes, items, n_cells, slab_doubles(RB), tree)) return CCMPC_ERR_WORKSPACE;
-  hipLaunchKernelGGL((moments_kernel<P, RB, MINK>), dim3(static_cast<unsigned>(items)),
-                     dim3(Geo<RB>::NW * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq,
-                     tree, mean, cov, mp);
+  hipLaunchKernelGGL((moments_kernel<P, RB, MINK, false>), dim3(static_cast<unsigned>(items)),
+                     dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
+                     mean, cov, mp);
   return CCMPC_OK;
 }
 
@@ -440,12 +510,24 @@ template <typename P, int NB, bool MINK>
 static int launch4(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
                    const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
                    double *mean, double *cov, const MinkParams &mp, hipStream_t s) {
+  constexpr int threads = kNW4 * 64;
   const int lg_wq = store_lg_wave_quota(1, n_bound);
-  const int64_t items = max_items(n_cells, n_bound, int64_t(1) << (lg_wq + 2));
   TreeLayout tree;
+  const int grid =
+      balanced_mode(n_bound) ? resident_grid<moments4_kernel<P, NB, MINK, true>>(threads) : 0;
+  if (grid > 0 && 2 * n_cells <= grid) {
+    if (!tree_layout(ws, ws_bytes, balanced_max_items(threads), n_cells, Scheme4<NB>::E,
+                     tree))
+      return CCMPC_ERR_WORKSPACE;
+    hipLaunchKernelGGL((moments4_kernel<P, NB, MINK, true>), dim3(static_cast<unsigned>(grid)),
+                       dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
+                       mean, cov, mp);
+    return CCMPC_OK;
+  }
+  const int64_t items = max_items(n_cells, n_bound, int64_t(1) << (lg_wq + 2));
   if (!tree_layout(ws, ws_bytes, items, n_cells, Scheme4<NB>::E, tree)) return CCMPC_ERR_WORKSPACE;
-  hipLaunchKernelGGL((moments4_kernel<P, NB, MINK>), dim3(static_cast<unsigned>(items)),
-                     dim3(kNW4 * 64), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
+  hipLaunchKernelGGL((moments4_kernel<P, NB, MINK, false>), dim3(static_cast<unsigned>(items)),
+                     dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
                      mean, cov, mp);
   return CCMPC_OK;
 }
@@ -530,15 +612,19 @@ extern "C" int ccmpc_probe_timestamps(void *host, int reset) {
 extern "C" size_t ccmpc_moments_workspace_bytes(int64_t T, int64_t n_cells,
                                                 int64_t n_particles_bound) {
   if (T < 1 || T > kMaxT || n_cells < 0 || n_particles_bound < 0) return 0;
+  // balanced mode (<= the resident grid) when the launch picks it, else power-of-two items
+  const bool bal = balanced_mode(n_particles_bound);
   const int nb = scheme4_blocks(T);
   if (nb > 0) {
-    const int64_t items = max_items(
-        n_cells, n_particles_bound, int64_t(1) << (store_lg_wave_quota(1, n_particles_bound) + 2));
+    int64_t items = max_items(n_cells, n_particles_bound,
+                              int64_t(1) << (store_lg_wave_quota(1, n_particles_bound) + 2));
+    if (bal) items = std::max(items, balanced_max_items(kNW4 * 64));
     return tree_bytes(items, n_cells, n_pairs(nb) * 16 + 4 * nb);
   }
   const int rb = row_blocks(T);
-  const int64_t items =
+  int64_t items =
       max_items(n_cells, n_particles_bound, int64_t(1) << store_lg_chunk(rb, n_particles_bound));
+  if (bal) items = std::max(items, balanced_max_items((1 << lg_waves_per_item(rb)) * 64));
   return tree_bytes(items, n_cells, slab_doubles(rb));
 }
 

@@ -6,6 +6,6 @@ LIB=$ROOT/cc-mpc_amd/ccmpc/libccmpc.so
 OUT=$ROOT/gpurun_out/variants
 mkdir -p "$OUT"
 cp "$LIB" /tmp/libccmpc.real.so
-cp "$ROOT/cc-mpc_amd/csrc/build_p4/libccmpc.so" "$LIB"
+cp "$ROOT/cc-mpc_amd/csrc/${PROBE_LIB:-build_p4}/libccmpc.so" "$LIB"
 timeout -k 10 300 python3 "$ROOT/tools/probe_phases.py" > "$OUT/timeline.txt" 2>&1
 cp /tmp/libccmpc.real.so "$LIB"
