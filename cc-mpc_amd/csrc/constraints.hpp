@@ -94,14 +94,21 @@ __device__ bool compute_mvoe(const M2 &S1, const M2 &S2, double tol, int maxiter
   // complex pair (disc < 0): .real keeps the real part of both
   const double sd = disc >= 0.0 ? sqrt_gs(disc) : 0.0;
   const double l1 = half_tr + sd, l2 = half_tr - sd;
-  // beta' = sqrt(sum 1/w / sum l/w), w = 1 + beta l  ==  sqrt((w1 + w2) / (l1 w2 + l2 w1)):
-  // the same fixed point with one division per iteration instead of five (the iteration is a
-  // serial chain per record, so the division latency is the tail's critical path).  Rounding
-  // differs from the reference's order by ~1 ulp per step; the contraction damps it.
+  // beta' = sqrt(sum 1/w / sum l/w), w = 1 + beta l  ==  sqrt(N / D) with N = w1 + w2 =
+  // 2 + s beta and D = l1 w2 + l2 w1 = s + 2 p beta (s = l1 + l2, p = l1 l2)  ==  N rsqrt(N D):
+  // the same fixed point, each step one product, one hardware rsqrt and one Goldschmidt step
+  // (7 dependent f64 operations, against 17 for an IEEE division + square root; the iteration
+  // is a serial chain per record, so its latency is the tail's critical path).  Rounding
+  // differs from the reference's order by a few ulp per step; the contraction damps it.
+  const double s = l1 + l2, p2 = 2.0 * (l1 * l2);
   double b = 1.0;
   for (int it = 0; it < maxiter; ++it) {
-    const double w1 = 1.0 + b * l1, w2 = 1.0 + b * l2;
-    const double bn = sqrt_gs(div_nr(w1 + w2, l1 * w2 + l2 * w1));
+    const double N = fma(s, b, 2.0), D = fma(p2, b, s);
+    const double x = N * D;
+    const double y = __builtin_amdgcn_rsq(x);
+    const double g = x * y, h = 0.5 * y;
+    const double r = fma(-g, h, 0.5);
+    const double bn = (2.0 * N) * fma(h, r, h);
     const bool done = fabs(bn - b) < tol;
     b = bn;
     if (done) break;
@@ -128,6 +135,16 @@ __device__ __forceinline__ void pair_of(int p, int &t, int &tau) {
   tau = p - tt * (tt - 1) / 2;
 }
 
+
+// 16-byte store of two adjacent record fields (records are 128-byte aligned).
+static_assert(sizeof(ccmpc_halfspace) == 128, "record size");
+static_assert(offsetof(ccmpc_halfspace, d) == 16 && offsetof(ccmpc_halfspace, q01) == 32 &&
+                  offsetof(ccmpc_halfspace, r00) == 48 && offsetof(ccmpc_halfspace, r11) == 64 &&
+                  offsetof(ccmpc_halfspace, mean0) == 96 && offsetof(ccmpc_halfspace, which) == 112,
+              "16-byte field pairs of ccmpc_halfspace");
+__device__ __forceinline__ void store_pair(double *p, double a, double b) {
+  *reinterpret_cast<double2 *>(p) = make_double2(a, b);
+}
 
 struct MinkParams {
   const double *ref_traj;    // [n_ref][T][2]
@@ -174,6 +191,20 @@ __device__ __forceinline__ double pair_lower_bound(const PairMoments &pm, double
 __device__ void minkowski_pair(const double *C, const double *mu, const double *ref, int rows,
                                int t, int tau, double chi_r, double chi_p, double R, double tol,
                                int maxiter, ccmpc_halfspace *out) {
+  // the tangent's slope and everything that depends only on the mean and the reference
+  // point: computed ahead of the MVOE fixed points (straight-line code the scheduler overlaps
+  // with the pair-moment chain; after the data-dependent loops it would be pure latency)
+  const double m0 = mu[2 * t], m1 = mu[2 * t + 1];
+  const double a0 = ref[2 * t], a1 = ref[2 * t + 1];
+  const double m = -(a0 - m0) / (a1 - m1);
+  const double n0 = -m, n1 = 1.0;
+  const double proj = n0 * m0 + n1 * m1;
+  const double nrm = sqrt(n0 * n0 + n1 * n1);
+  const double na = n0 * a0 + n1 * a1;
+  // the record goes out in 16-byte pairs (the lower bound at byte 88 belongs to another
+  // thread), the fields known early ahead of the chain, so few stores follow its end
+  store_pair(&out->n0, n0, n1);
+  store_pair(&out->mean0, m0, m1);
   const PairMoments pm = pair_moments(C, rows, t, tau);
   int status = 0;
   // two MVOE calls (:915, :917-918)
@@ -182,13 +213,13 @@ __device__ void minkowski_pair(const double *C, const double *mu, const double *
   bool ok = pm.ok;
   ok = ok && compute_mvoe(scale(pm.cov_infer, chi_r), scale(pm.cov_mu, chi_p), tol, maxiter, b1,
                           Q);
+  store_pair(&out->q01, Q.b, Q.d);
   ok = ok && compute_mvoe(Q, M2{R * R, 0.0, 0.0, R * R}, tol, maxiter, b2, QR);
   if (!ok) status = CCMPC_REC_SINGULAR;
+  store_pair(&out->r00, QR.a, QR.b);
+  store_pair(&out->r11, QR.d, b1);
+  out->beta2 = b2;
   // slope-m tangent of the QR ellipse closest to the reference point (:920-924)
-  const double m0 = mu[2 * t], m1 = mu[2 * t + 1];
-  const double a0 = ref[2 * t], a1 = ref[2 * t + 1];
-  const double m = -(a0 - m0) / (a1 - m1);
-  const double n0 = -m, n1 = 1.0;
   const double sn0 = QR.a * n0 + QR.b * n1, sn1 = QR.c * n0 + QR.d * n1;
   const double q = n0 * sn0 + n1 * sn1;
   double d = NAN;
@@ -198,11 +229,8 @@ __device__ void minkowski_pair(const double *C, const double *mu, const double *
   } else if (!(q > 0.0)) {
     if (status == 0) status = CCMPC_REC_NO_TANGENT;
   } else {
-    const double proj = n0 * m0 + n1 * m1;
     const double delta = 1.0 * sqrt(q);
     const double d1 = proj + delta, d2 = proj - delta;
-    const double nrm = sqrt(n0 * n0 + n1 * n1);
-    const double na = n0 * a0 + n1 * a1;
     const double dist0 = fabs(na - d1) / nrm, dist1 = fabs(na - d2) / nrm;
     which = (dist1 < dist0) ? 1 : 0;
     d = which ? d2 : d1;
@@ -210,23 +238,8 @@ __device__ void minkowski_pair(const double *C, const double *mu, const double *
   }
   if (status == 0 && !(isfinite(d) && isfinite(Q.a) && isfinite(QR.a) && isfinite(m0)))
     status = CCMPC_REC_NONFINITE;
-  out->n0 = n0;
-  out->n1 = n1;
-  out->d = d;
-  out->q00 = Q.a;
-  out->q01 = Q.b;
-  out->q11 = Q.d;
-  out->r00 = QR.a;
-  out->r01 = QR.b;
-  out->r11 = QR.d;
-  out->beta1 = b1;
-  out->beta2 = b2;
-  out->mean0 = m0;
-  out->mean1 = m1;
-  out->which = which;
-  out->side = side;
-  out->status = status;
-  out->t_tau = (t << 16) | tau;
+  store_pair(&out->d, d, Q.a);
+  *reinterpret_cast<int4 *>(&out->which) = make_int4(which, side, status, (t << 16) | tau);
 }
 
 // All pairs of one cell by the threads [0, nthreads) of the calling group, with the cell's
