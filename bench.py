@@ -267,6 +267,7 @@ def episode_c1(dev, cpu_steps=2, with_cpu=True):
 
 def pmc_traffic(kernel_prefix):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (kernel_prefix stops before the balanced-mode template flag, so both names match)
     (profiles/<round>/summary.json, written by profiles/collect.sh on this same default
     workload: FETCH_SIZE x2 (gfx950) + WRITE_SIZE).  None when no summary is committed."""
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")))
@@ -349,7 +350,7 @@ def main():
     t_mom = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev)
 
     pcie = pcie_inclusive(cyc, step, dev)
-    traffic, traffic_src = pmc_traffic("void ccmpc::moments_kernel<double, 1, true>")
+    traffic, traffic_src = pmc_traffic("void ccmpc::moments_kernel<double, 1, true")
     value = world * args.steps / elapsed
     out = {
         "metric": METRIC,
@@ -425,7 +426,7 @@ def main():
         # same kernel is meaningful at the per-GPU C4 batch, reported beside it
         c4 = time_config(dev, args.seed, *C4_GPU)
         c4["traffic"], c4["traffic_source"] = pmc_traffic(
-            "void ccmpc::moments4_kernel<double, 6, true>")
+            "void ccmpc::moments4_kernel<double, 6, true")
         c4["alg_bytes_per_launch"] = c4["particles"] * 2 * C4_GPU[3] * 8
         out["roofline_c4_batch"] = c4
     if rank == 0 and world == 1:

@@ -199,10 +199,10 @@ template <typename P, int RB, bool MINK, bool BAL>
 __global__ __launch_bounds__(Geo<RB>::NW * 64,
                              (MINK && RB == 1) ? 3 : Geo<RB>::MIN_WAVES_PER_SIMD)
 void moments_kernel(
-    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
-    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
-    int lg_wq, TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
-    MinkParams mp) {
+    const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off,
+    const int32_t *__restrict__ cell_ref, int n_cells, const P *__restrict__ pos, int64_t ld,
+    int T, const double *__restrict__ origin, int lg_wq, TreeLayout tree,
+    double *__restrict__ out_mean, double *__restrict__ out_cov, MinkParams mp) {
   using G = Geo<RB>;
   constexpr int NT = n_tiles(RB);
   constexpr int NACC = G::NACC;
@@ -297,7 +297,7 @@ void moments_kernel(
     ItemLoc loc;
     int64_t chunk;
     if (!locate_balanced(blockIdx.x, gridDim.x, cell_cnt, cell_off, n_cells, loc, &chunk,
-                         MINK ? mp.cell_ref : nullptr))
+                         cell_ref))
       return;  // uniform
     PROBE_TS(1);
     const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) * chunk;
@@ -307,7 +307,7 @@ void moments_kernel(
   }
   ItemLoc loc;
   if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc,
-                   MINK ? mp.cell_ref : nullptr))
+                   cell_ref))
     return;  // uniform
   PROBE_TS(1);
   const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
@@ -382,10 +382,10 @@ constexpr int kNW4 = 4;  // waves per Scheme4 work item
 
 template <typename P, int NB, bool MINK, bool BAL>
 __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
-    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
-    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt, int n_cells,
-    int lg_wq, TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
-    MinkParams mp) {
+    const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off,
+    const int32_t *__restrict__ cell_ref, int n_cells, const P *__restrict__ pos, int64_t ld,
+    int T, const double *__restrict__ origin, int lg_wq, TreeLayout tree,
+    double *__restrict__ out_mean, double *__restrict__ out_cov, MinkParams mp) {
   using Sch = Scheme4<NB>;
   constexpr int NP = Sch::NP, D = Sch::D, E = Sch::E;
   __shared__ double xch[kNW4 * Combine4Layout<NB>::XS];
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
     ItemLoc loc;
     int64_t chunk;
     if (!locate_balanced(blockIdx.x, gridDim.x, cell_cnt, cell_off, n_cells, loc, &chunk,
-                         MINK ? mp.cell_ref : nullptr))
+                         cell_ref))
       return;  // uniform
     PROBE_TS(1);
     const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) * chunk;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
   }
   ItemLoc loc;
   if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc,
-                   MINK ? mp.cell_ref : nullptr))
+                   cell_ref))
     return;  // uniform
   PROBE_TS(1);
   const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
@@ -494,15 +494,15 @@ static int launch(const P *pos, int64_t ld, int T, const double *origin, const i
                      tree))
       return CCMPC_ERR_WORKSPACE;
     hipLaunchKernelGGL((moments_kernel<P, RB, MINK, true>), dim3(static_cast<unsigned>(grid)),
-                       dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
-                       mean, cov, mp);
+                       dim3(threads), 0, s, cnt, off, MINK ? mp.cell_ref : nullptr, n_cells, pos, ld,
+                       T, origin, lg_wq, tree, mean, cov, mp);
     return CCMPC_OK;
   }
   const int64_t items = max_items(n_cells, n_bound, int64_t(1) << store_lg_chunk(RB, n_bound));
   if (!tree_layout(ws, ws_bytes, items, n_cells, slab_doubles(RB), tree)) return CCMPC_ERR_WORKSPACE;
   hipLaunchKernelGGL((moments_kernel<P, RB, MINK, false>), dim3(static_cast<unsigned>(items)),
-                     dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
-                     mean, cov, mp);
+                     dim3(threads), 0, s, cnt, off, MINK ? mp.cell_ref : nullptr, n_cells, pos, ld, T,
+                     origin, lg_wq, tree, mean, cov, mp);
   return CCMPC_OK;
 }
 
@@ -520,15 +520,15 @@ static int launch4(const P *pos, int64_t ld, int T, const double *origin, const 
                      tree))
       return CCMPC_ERR_WORKSPACE;
     hipLaunchKernelGGL((moments4_kernel<P, NB, MINK, true>), dim3(static_cast<unsigned>(grid)),
-                       dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
-                       mean, cov, mp);
+                       dim3(threads), 0, s, cnt, off, MINK ? mp.cell_ref : nullptr, n_cells, pos, ld,
+                       T, origin, lg_wq, tree, mean, cov, mp);
     return CCMPC_OK;
   }
   const int64_t items = max_items(n_cells, n_bound, int64_t(1) << (lg_wq + 2));
   if (!tree_layout(ws, ws_bytes, items, n_cells, Scheme4<NB>::E, tree)) return CCMPC_ERR_WORKSPACE;
   hipLaunchKernelGGL((moments4_kernel<P, NB, MINK, false>), dim3(static_cast<unsigned>(items)),
-                     dim3(threads), 0, s, pos, ld, T, origin, off, cnt, n_cells, lg_wq, tree,
-                     mean, cov, mp);
+                     dim3(threads), 0, s, cnt, off, MINK ? mp.cell_ref : nullptr, n_cells, pos, ld, T,
+                     origin, lg_wq, tree, mean, cov, mp);
   return CCMPC_OK;
 }
 
