@@ -103,6 +103,63 @@ def sweep(dev, seed):
     return rows
 
 
+def planning_qp(dev, seed, scenes=64, O=4, N=5000, T=8, with_cpu=True):
+    """The caller side of the path: do_highlevel_control's QP
+    (v8ideal/__init__.py:2850-2930) for `scenes` planning steps whose obstacles cross the ego's
+    path (ccmpc.synthetic.crossing_scene: O OVs x 2 modes, N particles per OV, T steps), solved
+    in one ccmpc_mpc_qp launch on the half-spaces one ccmpc_minkowski_cycle made for all of
+    them.  Beside it, the oracle's dense SciPy solve of the first feasible scene (CPLEX itself
+    is absent).  Not part of `value`."""
+    from ccmpc import cycle, engine, mpc, synthetic
+    cells, K, cps, x0s, goals, refs = [], [], [], [], [], []
+    for sc in range(scenes):
+        c, k, ref, goal, x0, _ = synthetic.crossing_scene(seed + 5000 + sc, O=O, N=N, T=T)
+        cells += c
+        K += k
+        cps.append(len(c))
+        refs.append(ref)
+        goals.append(goal)
+        x0s.append(x0)
+    store = engine.ParticleStore.from_cells(cells, device=dev)
+    cyc = cycle.MinkowskiCycle(store, K, refs[0])
+    cyc.run()
+    xbar, gamma = mpc.ltv(np.array(x0s), T, lon=3.7)
+    goal_t = torch.as_tensor(np.array(goals), device=dev)
+    ref_t = torch.as_tensor(np.array(refs), device=dev)
+    qp = mpc.PlanningQP(cps, T)
+    fn = lambda: qp.solve(gamma, xbar, goal_t, ref_t, cyc.rec)
+    t = time_kernel_live(fn, dev, per_graph=5, replays=5)
+    fn()
+    status, iters = qp.status.cpu().numpy(), qp.iters.cpu().numpy()
+    ok = status == mpc.QP_OK
+    out = {"config": f"{scenes} crossing scenes x {O} OVs x 2 modes, np={N}/OV, T={T}: one "
+                     f"ccmpc_mpc_qp launch over {cyc.n_constraints} half-spaces",
+           "scenes": scenes, "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
+           "qps_per_s": round(scenes / t, 1), "solved": int(ok.sum()),
+           "infeasible": int((status == mpc.QP_MAXITER).sum()),
+           "iters_solved_max": int(iters[ok].max()) if ok.any() else None}
+    if with_cpu and ok.any():
+        from oracle import mpc_oracle as mo
+        i = int(np.argmax(ok))
+        recs = cyc.records().reshape(-1)
+        xb, _, G, _, _ = mo.VehicleModel(T, 0.5, 1.85, 3.7).get_optimization_ltv(
+            np.array(x0s[i]), np.zeros(2))
+        P = T * (T - 1) // 2
+        c0 = int(sum(cps[:i]))
+        mine = recs[c0 * P:(c0 + cps[i]) * P]
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            r = mo.solve_step(G, xb, T, T, goals[i], refs[i], mine, "halfspace",
+                              mo.DEFAULT_PARAMS)
+            ts.append(time.perf_counter() - t0)
+        out["cpu_oracle_qp_ms"] = round(statistics.median(ts) * 1e3, 2)
+        out["max_abs_du_vs_oracle"] = float(np.max(np.abs(qp.u[i].cpu().numpy() - r["u"])))
+        out["cpu_note"] = ("oracle/mpc_oracle.py dense assembly + SLSQP + active-set polish of "
+                           "one scene, median of 5, 1 process (stand-in for cvxpy+CPLEX, absent)")
+    return out
+
+
 def init_dist(args):
     """One process per GPU (torchrun env).  Backend nccl (= RCCL over xGMI); the env override
     CCMPC_BENCH_BACKEND=gloo exists only to rehearse the N > 1 code path with several ranks on
@@ -433,6 +490,7 @@ def main():
         from threadpoolctl import threadpool_limits
         with threadpool_limits(limits=1):
             out["episode_c1"] = episode_c1(dev, with_cpu=not args.no_cpu)
+            out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
     if args.sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)
     if rank == 0:

@@ -81,6 +81,11 @@ SIGNATURES = {
                                 _P, _P, _P, _P, _P]),
     "ccmpc_ideal_moments": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _U64, _P,
                                            _P, _SZ, _P, _P, _P, _P]),
+    "ccmpc_mpc_ltv": (ctypes.c_int, [_P, _I64, _I64, _D, _D, _D, _P, _P, _P]),
+    "ccmpc_mpc_qp_workspace_bytes": (_SZ, [_I64, _I64, _I64, ctypes.c_int]),
+    "ccmpc_mpc_qp": (ctypes.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _I64, _P,
+                                    ctypes.c_int, _P, _I64, _P, ctypes.c_int, _I32, _D, _P, _SZ,
+                                    _P, _P, _P, _P, _P, _P]),
 }
 
 

@@ -57,3 +57,34 @@ def scene(seed, O=4, N=5000, T=8, K=None):
     ego = np.array([165.0, -60.0])
     ref = np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
     return ovs, ref, np.array(pasts)
+
+
+def crossing_scene(seed, O=2, N=400, T=8, K=2, lateral=8.0):
+    """A planning step whose obstacles cross the ego's path, so half-spaces bind in the QP:
+    the ego drives the reference trajectory of `scene` at ~8 m/s; each OV starts `lateral` m
+    beside the reference point of a random step and heads across it, K modes per OV.
+    Returns (cells: list of (N/K, T, 2) clouds in (OV, mode) order, K per OV, ref (T, 2),
+    goal (2,), x_init [x, y, psi, v], pasts (O, 2))."""
+    rng = np.random.default_rng(np.random.Philox(seed))
+    ego = np.array([165.0, -60.0])
+    ref = np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
+    goal = ref[-1] + np.array([4.0, 0.5])
+    x_init = np.array([ego[0], ego[1], np.arctan2(0.5, 4.0), 8.0 + rng.uniform(-1, 1)])
+    cells, Ks, pasts = [], [], []
+    for _ in range(O):
+        t0 = int(rng.integers(T // 3, T))
+        side = 1.0 if rng.uniform() < 0.5 else -1.0
+        p0 = ref[t0] + side * lateral * np.array([-0.124, 0.992]) + rng.normal(0, 1.0, 2)
+        heading = np.arctan2(-side * 0.992, side * 0.124) + rng.normal(0, 0.4)
+        for _k in range(K):
+            n = int(N // K)
+            h = heading + rng.normal(0, 0.3) + rng.normal(0, 0.1, size=(n, 1))
+            v = np.maximum(1.0 + rng.uniform(0, 1.5) + rng.normal(0, 0.3, size=(n, 1)), 0.0)
+            tt = np.arange(1, T + 1)[None, :] * DT
+            hh = h + 0.05 * tt
+            x = p0[0] + np.cumsum(v * np.cos(hh) * DT, axis=1) + rng.normal(0, 0.05, (n, T))
+            y = p0[1] + np.cumsum(v * np.sin(hh) * DT, axis=1) + rng.normal(0, 0.05, (n, T))
+            cells.append(np.stack((x, y), axis=-1))
+        pasts.append(p0 - np.array([1.0, 0.2]))
+        Ks.append(K)
+    return cells, Ks, ref, goal, x_init, np.array(pasts)

@@ -1,0 +1,1099 @@
+// The planning step's quadratic program, batched over scenes: the caller side of the path
+// (SURVEY.md 8f row 3).  Replaces do_highlevel_control's cvxpy + CPLEX problem
+// (v8ideal/__init__.py:2850-2930, objective :2478-2507, speed limits :610-626) with the
+// road-boundary MILP off (the reference default, :217), which leaves a convex QP in the 2T
+// controls u.  The LTV model it needs comes from ccmpc_mpc_ltv (dynamics/bicycle_v2.py
+// :240-308, linearised about u_init = 0 as make_local_params does, v8ideal :537-557).
+//
+// Design (gfx950): one workgroup of 4 waves per scene runs a primal-dual interior point method
+// (Mehrotra predictor-corrector) entirely in LDS.  Every constraint acts on a handful of
+// "output" rows of the state -- x_t, y_t (obstacle half-spaces, 2 nonzeros in output space)
+// and v_t (speed limits) -- or on u itself (control bounds), so the normal matrix is
+//   M = H_ctrl + diag(w_box) + Gs^T B Gs,
+// Gs = the 3T selected rows of Gamma_f (x, y, v of each step), B = per-step 3x3 blocks holding
+// the objective's position weights plus sum_r w_r a_r a_r^T of that step's half-spaces.  The
+// records are read in place (the generators' [cell][pair] layout puts step t's half-spaces of
+// a cell in one contiguous run), so an iteration costs O(records) + O(T n^2), not O(m n^2),
+// and needs no sort.  Per-step sums are wave reductions in a fixed order: the solve is
+// bitwise reproducible.  Cholesky and both triangular solves run on wave 0 (lane = row),
+// wave-synchronous, with no workgroup barrier per column.
+#include "ccmpc_common.hpp"
+
+namespace ccmpc {
+
+constexpr int kQpThreads = 256;
+constexpr int kQpWaves = kQpThreads / 64;
+constexpr int kQpMaxT = 40;
+constexpr size_t kQpLdsBytes = 160 * 1024;
+
+// ---- the LTV model ---------------------------------------------------------------------------
+// About u = 0 the bicycle model's nominal trajectory is straight at constant speed
+// (bicycle_kinematics: psi' = v/L cos(beta) tan(u_2) = 0, v' = u_1 = 0, beta from the 'delta'
+// parameter, 0), so X_bar[i] = x0 + i Ts v (cos psi, sin psi), and every step shares
+// A = d f / d x with A^2 = 0.  Zero-order hold of [[A, B], [0, 0]] is then exact in closed form:
+// Ad = I + Ts A, Bd = Ts B + Ts^2/2 A B (cont2discrete 'zoh' = expm of that block matrix).
+// Gamma = A_bar^{-1} B_bar (:296-306) is block lower triangular with block (t, k) =
+// Ad^{t-k} Bd = (I + (t-k) Ts A) Bd.
+__global__ void mpc_ltv_kernel(const double *__restrict__ x_init, int64_t S, int T, double Ts,
+                               double l_r, double L, double *__restrict__ out_xbar,
+                               double *__restrict__ out_gamma) {
+  const int64_t s = blockIdx.x;
+  if (s >= S) return;
+  const double x0 = x_init[4 * s], y0 = x_init[4 * s + 1], psi = x_init[4 * s + 2],
+               v = x_init[4 * s + 3];
+  const double cp = cos(psi), sp = sin(psi);
+  // get_dbeta_ddelta at delta = 0 (:19-24): 1 when l_r == L, else 1 / (L / l_r)
+  const double dbeta = (l_r == L) ? 1.0 : 1.0 / (L / l_r);
+  // A (get_state_matrix :103-115 at delta = 0): nonzeros A[0][2], A[0][3], A[1][2], A[1][3]
+  const double a02 = -v * sp, a03 = cp, a12 = v * cp, a13 = sp;
+  // B (get_input_matrix :117-130 at delta = 0)
+  const double b01 = -v * sp * dbeta, b11 = v * cp * dbeta, b21 = (v / L) * 1.0, b30 = 1.0;
+  // Bd = Ts B + Ts^2/2 A B;  (A B)[r][c] = sum_k A[r][k] B[k][c]
+  const double h = 0.5 * Ts * Ts;
+  double Bd[4][2];
+  Bd[0][0] = h * (a03 * b30);
+  Bd[0][1] = Ts * b01 + h * (a02 * b21);
+  Bd[1][0] = h * (a13 * b30);
+  Bd[1][1] = Ts * b11 + h * (a12 * b21);
+  Bd[2][0] = 0.0;
+  Bd[2][1] = Ts * b21;
+  Bd[3][0] = Ts * b30;
+  Bd[3][1] = 0.0;
+  const int nx = 4, nu = 2, rows = nx * T, cols = nu * T;
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+    const int r = e / cols, c = e % cols;
+    const int t = r / nx, i = r % nx, k = c / nu, j = c % nu;
+    double g = 0.0;
+    if (k <= t) {
+      // (I + m Ts A) Bd, m = t - k
+      const double mt = static_cast<double>(t - k) * Ts;
+      g = Bd[i][j];
+      if (i == 0) g += mt * (a02 * Bd[2][j] + a03 * Bd[3][j]);
+      if (i == 1) g += mt * (a12 * Bd[2][j] + a13 * Bd[3][j]);
+    }
+    out_gamma[s * rows * cols + e] = g;
+  }
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    const int t = r / nx + 1, i = r % nx;  // X_bar[1:]
+    const double tt = static_cast<double>(t) * Ts;
+    out_xbar[s * rows + r] = i == 0 ? x0 + v * cp * tt : i == 1 ? y0 + v * sp * tt
+                           : i == 2 ? psi : v;
+  }
+}
+
+// ---- the QP ---------------------------------------------------------------------------------
+struct QpArgs {
+  int64_t S;
+  int T, Tf, n_ref, u_order, rec_kind, max_iter, rows_in_lds, polish;
+  int64_t max_cells;
+  double tol;
+  const double *gamma, *xbar, *ubar, *u_prev, *goal, *ref;
+  const unsigned char *rec;
+  const int64_t *scene_cell;
+  ccmpc_mpc_params p;
+  double *ws;  // per-scene row store when it does not fit LDS
+  double *out_u, *out_x, *out_cost;
+  int32_t *out_status, *out_iter;
+};
+
+// Sizes (doubles) of the LDS image; shared by host (launch sizing) and device (carving).
+struct QpLayout {
+  int n, T3, ldm;
+  int gs, m, c3, y, yd, qf, q, bw, f, z, dz, rd, rh, e2, lb, ub, dinv, red;
+  int pw, ps, pact, pdinv;  // the polish step's W = L^{-1} G_A^T, S = W^T W, active rows
+  int rows, total;
+  __host__ __device__ QpLayout(int T, int64_t R, bool rows_lds, bool polish) {
+    n = 2 * T;
+    T3 = 3 * T;
+    ldm = n + 1;  // odd row stride: column reads of the Cholesky spread over the banks
+    int o = 0;
+    gs = o; o += T3 * n;
+    m = o; o += n * ldm;
+    c3 = o; o += T3;
+    y = o; o += T3;
+    yd = o; o += T3;
+    qf = o; o += T3;
+    q = o; o += T3;
+    bw = o; o += 4 * T;
+    f = o; o += n;
+    z = o; o += n;
+    dz = o; o += n;
+    rd = o; o += n;
+    rh = o; o += n;
+    e2 = o; o += n;
+    lb = o; o += n;
+    ub = o; o += n;
+    dinv = o; o += n;
+    red = o; o += 8 * kQpWaves;
+    pw = ps = pact = pdinv = o;
+    if (polish) {
+      pw = o; o += n * n;
+      ps = o; o += n * ldm;
+      pact = o; o += n;
+      pdinv = o; o += n;
+    }
+    rows = o;
+    const int64_t mrows = 2 * n + 2 * T + R;
+    if (rows_lds) o += static_cast<int>(4 * mrows + 3 * R);
+    total = o;
+  }
+};
+
+__host__ __device__ inline int64_t qp_rows_per_cell(int T, int kind) {
+  return kind == CCMPC_REC_KIND_HALFSPACE ? int64_t(T) * (T - 1) / 2 : T;
+}
+
+// row store: s, l, ds, dl over all m rows (box 2n, speed 2T, obstacle R), then the obstacle
+// rows' a0, a1, b' (b' = b - a . c_xy, the constant part of the state moved to the right)
+struct Rows {
+  double *s, *l, *ds, *dl, *a0, *a1, *b;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block reductions of up to 2 values (every thread gets the result); two barriers.
+__device__ __forceinline__ void block_max2(double &a, double &b, double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a = wave_max(a);
+  b = wave_max(b);
+  if (lane == 0) {
+    red[2 * w] = a;
+    red[2 * w + 1] = b;
+  }
+  __syncthreads();
+  a = red[0];
+  b = red[1];
+  for (int k = 1; k < kQpWaves; ++k) {
+    a = fmax(a, red[2 * k]);
+    b = fmax(b, red[2 * k + 1]);
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ double block_sum(double a, double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a = wave_sum(a);
+  if (lane == 0) red[w] = a;
+  __syncthreads();
+  a = red[0];
+  for (int k = 1; k < kQpWaves; ++k) a += red[k];
+  __syncthreads();
+  return a;
+}
+__device__ __forceinline__ double block_min(double a, double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a = wave_min(a);
+  if (lane == 0) red[w] = a;
+  __syncthreads();
+  a = red[0];
+  for (int k = 1; k < kQpWaves; ++k) a = fmin(a, red[k]);
+  __syncthreads();
+  return a;
+}
+
+__device__ __forceinline__ double lane_bcast(double v, int src) {  // src wave-uniform
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), src);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), src);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// wave-level ordering of LDS traffic between the lanes of wave 0 (one wave executes its LDS
+// instructions in order; this keeps the compiler from moving them across the step)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-level dense Cholesky and triangular solves (called by one whole wave; lane = row, two
+// rows per lane, so N <= 128).  A holds the lower triangle, row stride ld; it is overwritten by
+// L, and dinv[j] = 1 / L[j][j].  With pivot_skip a pivot that cancellation drove to <= 0 is
+// replaced by a huge one (see the IPM below); otherwise it fails.  Returns true on failure.
+__device__ bool wave_cholesky(double *A, int N, int ld, double *dinv, bool pivot_skip) {
+  const int lane = threadIdx.x & 63;
+  bool fail = false;
+  for (int j = 0; j < N; ++j) {
+    double sv[2];
+    const double ajj = A[j * ld + j];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = j + lane + 64 * h;
+      double v = 0.0;
+      if (i < N) {
+        v = A[i * ld + j];
+        for (int k = 0; k < j; ++k) v -= A[i * ld + k] * A[j * ld + k];
+      }
+      sv[h] = v;
+    }
+    double dj = lane_bcast(sv[0], 0);
+    fail = fail || !isfinite(dj) || !isfinite(ajj);
+    if (!(dj > 1e-30 * ajj)) {
+      fail = fail || !pivot_skip;
+      dj = 1e128;
+    }
+    const double ljj = sqrt(dj), inv = 1.0 / ljj;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = j + lane + 64 * h;
+      if (i < N) A[i * ld + j] = (i == j) ? ljj : sv[h] * inv;
+    }
+    if (lane == 0) dinv[j] = inv;
+    wave_sync();
+  }
+  return fail;
+}
+
+// b <- L^{-1} b (b[h] is row lane + 64 h)
+__device__ __forceinline__ void wave_forward(const double *L, int N, int ld, const double *dinv,
+                                             double b[2]) {
+  const int lane = threadIdx.x & 63;
+  for (int j = 0; j < N; ++j) {
+    const double yj = lane_bcast((j >> 6) ? b[1] : b[0], j & 63) * dinv[j];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = lane + 64 * h;
+      if (i == j) b[h] = yj;
+      else if (i > j && i < N) b[h] -= L[i * ld + j] * yj;
+    }
+  }
+}
+
+// b <- L^{-T} b
+__device__ __forceinline__ void wave_backward(const double *L, int N, int ld, const double *dinv,
+                                              double b[2]) {
+  const int lane = threadIdx.x & 63;
+  for (int j = N - 1; j >= 0; --j) {
+    const double xj = lane_bcast((j >> 6) ? b[1] : b[0], j & 63) * dinv[j];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = lane + 64 * h;
+      if (i == j) b[h] = xj;
+      else if (i < j) b[h] -= L[j * ld + i] * xj;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_load2(const double *x, int N, double b[2]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) b[h] = (lane + 64 * h < N) ? x[lane + 64 * h] : 0.0;
+}
+__device__ __forceinline__ void wave_store2(double *x, int N, const double b[2]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (lane + 64 * h < N) x[lane + 64 * h] = b[h];
+}
+
+// control index of U_t component c: cp.reshape(u, (T, 2)) is column-major by default
+__device__ __forceinline__ int u_index(int t, int c, int T, int order) {
+  return order == CCMPC_U_ORDER_C ? 2 * t + c : t + c * T;
+}
+__device__ __forceinline__ void u_decode(int i, int T, int order, int &t, int &c) {
+  if (order == CCMPC_U_ORDER_C) {
+    t = i >> 1;
+    c = i & 1;
+  } else {
+    c = i >= T;
+    t = i - c * T;
+  }
+}
+
+// H_ctrl[i][j] = 2 (R1 + [t >= 1] R2 + [t <= T-2] R2)[a][b] on the diagonal step block,
+// -2 R2[a][b] on the two neighbouring step blocks (:2504-2506), 0 elsewhere
+__device__ __forceinline__ double hctrl(int i, int j, int T, int order, const ccmpc_mpc_params &p) {
+  int ti, ci, tj, cj;
+  u_decode(i, T, order, ti, ci);
+  u_decode(j, T, order, tj, cj);
+  const double r1 = ci == cj ? (ci == 0 ? p.w_accel : p.w_turning) : p.w_joint;
+  const double r2 = ci == cj ? (ci == 0 ? p.w_ch_accel : p.w_ch_turning) : p.w_ch_joint;
+  if (ti == tj) {
+    double k = r1;
+    if (ti >= 1) k += r2;
+    if (ti <= T - 2) k += r2;
+    return 2.0 * k;
+  }
+  if (ti - tj == 1 || tj - ti == 1) return -2.0 * r2;
+  return 0.0;
+}
+
+__device__ __forceinline__ double hctrl_mul(const double *z, int i, int T, int order,
+                                            const ccmpc_mpc_params &p) {
+  int ti, ci;
+  u_decode(i, T, order, ti, ci);
+  double acc = 0.0;
+  for (int tj = ti - 1; tj <= ti + 1; ++tj) {
+    if (tj < 0 || tj >= T) continue;
+    for (int cj = 0; cj < 2; ++cj) {
+      const int j = u_index(tj, cj, T, order);
+      acc += hctrl(i, j, T, order, p) * z[j];
+    }
+  }
+  return acc;
+}
+
+template <bool ROWS_LDS>
+__global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
+  extern __shared__ double lds[];
+  const int64_t sc = blockIdx.x;
+  if (sc >= A.S) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int T = A.T, Tf = A.Tf, Tp = Tf - T;
+  const int64_t c0 = A.scene_cell[sc], ncell = A.scene_cell[sc + 1] - c0;
+  const int P = static_cast<int>(qp_rows_per_cell(T, A.rec_kind));
+  const int64_t R = ncell * P;
+  const QpLayout lay(T, ROWS_LDS ? R : 0, ROWS_LDS, A.polish != 0);
+  const int n = lay.n, T3 = lay.T3, ldm = lay.ldm;
+  const int nbox = 2 * n, nv = 2 * T;
+  const int64_t mrows = nbox + nv + R;
+  double *Gs = lds + lay.gs, *M = lds + lay.m, *c3 = lds + lay.c3, *y = lds + lay.y,
+         *yd = lds + lay.yd, *qf = lds + lay.qf, *q = lds + lay.q, *bw = lds + lay.bw,
+         *z = lds + lay.z, *dz = lds + lay.dz, *rd = lds + lay.rd, *rh = lds + lay.rh,
+         *e2 = lds + lay.e2, *lb = lds + lay.lb,
+         *ub = lds + lay.ub, *dinv = lds + lay.dinv, *red = lds + lay.red;
+  double *rbase;
+  if (ROWS_LDS) {
+    rbase = lds + lay.rows;
+  } else {
+    const int64_t mcap = 2 * n + 2 * T + A.max_cells * P;
+    rbase = A.ws + sc * (4 * mcap + 3 * A.max_cells * P);
+  }
+  const Rows rw{rbase, rbase + mrows, rbase + 2 * mrows, rbase + 3 * mrows, rbase + 4 * mrows,
+                rbase + 4 * mrows + R, rbase + 4 * mrows + 2 * R};
+  const ccmpc_mpc_params &p = A.p;
+  const int order = A.u_order;
+  const int ncol = 2 * Tf;
+  const double *Gam = A.gamma + sc * (4 * Tf) * ncol;
+  const double *xb = A.xbar + sc * 4 * Tf;
+  const double *ubar = A.ubar ? A.ubar + sc * ncol : nullptr;
+  const double *uprev = (A.u_prev && Tp > 0) ? A.u_prev + sc * 2 * Tp : nullptr;
+  const double g0 = A.goal[2 * sc], g1 = A.goal[2 * sc + 1];
+  const double *ref = A.ref + sc * 2 * A.n_ref;
+  // output row k = 3t + a of the selected state rows: x, y, v of step t (state index 0, 1, 3)
+  auto grow = [&](int k) { return 4 * (Tp + k / 3) + (k % 3 == 2 ? 3 : k % 3); };
+
+  // ---- setup -------------------------------------------------------------------------------
+  for (int e = tid; e < T3 * n; e += kQpThreads) {
+    const int k = e / n, j = e % n;
+    Gs[e] = Gam[static_cast<int64_t>(grow(k)) * ncol + 2 * Tp + j];
+  }
+  for (int k = tid; k < T3; k += kQpThreads) {
+    // constant part of the state: x_bar + Gamma_p u_prev - Gamma_f u_bar (:2877-2891)
+    const int r = grow(k);
+    const double *gr = Gam + static_cast<int64_t>(r) * ncol;
+    double c = xb[r];
+    if (uprev)
+      for (int j = 0; j < 2 * Tp; ++j) c += gr[j] * uprev[j];
+    if (ubar)
+      for (int j = 0; j < n; ++j) c -= gr[2 * Tp + j] * ubar[2 * Tp + j];
+    c3[k] = c;
+    y[k] = 0.0;
+  }
+  for (int j = tid; j < n; j += kQpThreads) {
+    int t, c;
+    u_decode(j, T, order, t, c);
+    ub[j] = c == 0 ? p.max_a : p.max_delta;
+    lb[j] = c == 0 ? p.min_a : -p.max_delta;
+    z[j] = 0.0;
+  }
+  __syncthreads();
+  for (int k = tid; k < T3; k += kQpThreads) {
+    // objective's linear term in output space: 2 (w_ref (c - ref_t) + [t = T-1] w_final (c - g))
+    const int t = k / 3, a = k % 3;
+    double v = 0.0;
+    if (a < 2) {
+      const int tr = t < A.n_ref ? t : A.n_ref - 1;
+      v = 2.0 * p.w_ref * (c3[k] - ref[2 * tr + a]);
+      if (t == T - 1) v += 2.0 * p.w_final * (c3[k] - (a == 0 ? g0 : g1));
+    }
+    qf[k] = v;
+  }
+  // obstacle rows: a . (y_xy + c_xy) <= b  ->  a . y_xy <= b' = b - a . c_xy
+  int skipped = 0;
+  double hmax = 0.0;
+  for (int64_t r = tid; r < R; r += kQpThreads) {
+    const int64_t cell = r / P;
+    const int pp = static_cast<int>(r - cell * P);
+    const unsigned char *rec = A.rec + (c0 * P + r) * 128;
+    const double n0 = *reinterpret_cast<const double *>(rec);
+    const double n1 = *reinterpret_cast<const double *>(rec + 8);
+    const double d = *reinterpret_cast<const double *>(
+        rec + (A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? 16 : 32));
+    const int side = *reinterpret_cast<const int32_t *>(rec + 116);
+    const int status = *reinterpret_cast<const int32_t *>(rec + 120);
+    int t;
+    if (A.rec_kind == CCMPC_REC_KIND_HALFSPACE) {
+      t = *reinterpret_cast<const int32_t *>(rec + 124) >> 16;
+    } else {
+      t = *reinterpret_cast<const int32_t *>(rec + 124);
+    }
+    (void)pp;
+    const bool ok = status == 0 && isfinite(n0) && isfinite(n1) && isfinite(d) && t >= 0 &&
+                    t < T && (side == 1 || side == -1);
+    double a0 = 0.0, a1 = 0.0, b = 1.0;
+    if (ok) {
+      // side +1: n . x >= d  ->  -n . x <= -d ;  side -1: n . x <= d  (:926-939, :1503-1515)
+      a0 = side == 1 ? -n0 : n0;
+      a1 = side == 1 ? -n1 : n1;
+      b = (side == 1 ? -d : d) - (a0 * c3[3 * t] + a1 * c3[3 * t + 1]);
+    } else {
+      skipped = 1;
+    }
+    rw.a0[r] = a0;
+    rw.a1[r] = a1;
+    rw.b[r] = b;
+    hmax = fmax(hmax, fabs(b));
+  }
+  __syncthreads();
+  // f = Gs^T qf (for the scaling of the dual residual)
+  double fmax_ = 0.0;
+  for (int j = tid; j < n; j += kQpThreads) {
+    double v = 0.0;
+    for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * qf[k];
+    fmax_ = fmax(fmax_, fabs(v));
+  }
+  // initial point: z = 0 (inside the control box), s = max(-g(0), 1), lambda = 1
+  // step t of obstacle row o (records of a cell in (t, tau) order, or one per t for affine)
+  auto obst_step = [&](int64_t o) -> int {
+    const int64_t cell = o / P;
+    const int pp = static_cast<int>(o - cell * P);
+    if (A.rec_kind != CCMPC_REC_KIND_HALFSPACE) return pp;
+    int t = static_cast<int>((1.0f + sqrtf(1.0f + 8.0f * static_cast<float>(pp))) * 0.5f);
+    while (t * (t - 1) / 2 > pp) --t;
+    while ((t + 1) * t / 2 <= pp) ++t;
+    return t;
+  };
+  // g(z) = row_lin(r, Gs z, z) + row_const(r): the linear part in the state's output rows
+  // yy = Gs z (or in z itself for the control bounds), constants folded into b' and the bounds
+  auto row_lin = [&](int64_t r, const double *yy, const double *zz) -> double {
+    if (r < nbox) {
+      const int j = static_cast<int>(r >> 1);
+      return (r & 1) ? -zz[j] : zz[j];
+    }
+    if (r < nbox + nv) {
+      const int t = static_cast<int>((r - nbox) >> 1);
+      return ((r - nbox) & 1) ? -yy[3 * t + 2] : yy[3 * t + 2];
+    }
+    const int64_t o = r - nbox - nv;
+    const int t = obst_step(o);
+    return rw.a0[o] * yy[3 * t] + rw.a1[o] * yy[3 * t + 1];
+  };
+  auto row_const = [&](int64_t r) -> double {
+    if (r < nbox) {
+      const int j = static_cast<int>(r >> 1);
+      return (r & 1) ? lb[j] : -ub[j];
+    }
+    if (r < nbox + nv) {
+      const int t = static_cast<int>((r - nbox) >> 1);
+      return ((r - nbox) & 1) ? -c3[3 * t + 2] : c3[3 * t + 2] - p.max_v;
+    }
+    return -rw.b[r - nbox - nv];
+  };
+  auto row_g = [&](int64_t r, const double *yy, const double *zz) -> double {
+    return row_lin(r, yy, zz) + row_const(r);
+  };
+  // Directional derivative of g along dz, given yd = Gs dz.  It must be the linear part
+  // itself, never g(dz) - const: near the solution lambda ds / s amplifies any rounding in ds
+  // by lambda / s, and an error here that the normal equations did not see leaves a dual
+  // residual the iteration can no longer remove.
+  auto row_gd = [&](int64_t r, const double *ydd, const double *dzz) -> double {
+    return row_lin(r, ydd, dzz);
+  };
+  for (int64_t r = tid; r < mrows; r += kQpThreads) {
+    const double g = row_g(r, y, z);
+    rw.s[r] = fmax(-g, 1.0);
+    rw.l[r] = 1.0;
+    if (r < nbox + nv) hmax = fmax(hmax, fabs(g));  // bounds' right-hand sides (z = y = 0)
+  }
+  block_max2(hmax, fmax_, red);
+  const double tol_p = A.tol * (1.0 + hmax), tol_d = A.tol * (1.0 + fmax_);
+
+  // Per-step sums over a step's obstacle rows, in a fixed order (wave per step, lane-strided,
+  // butterfly reduction).  Step t's rows of cell c are the run [start_t, start_t + cnt_t) of
+  // the cell's records.  `val(r, t)` returns 2 (or 3) contributions of row r.
+  auto step_rows = [&](int t, int64_t idx) -> int64_t {
+    if (A.rec_kind == CCMPC_REC_KIND_HALFSPACE) {
+      const int cnt = t;
+      const int64_t cell = idx / cnt;
+      return cell * P + t * (t - 1) / 2 + (idx - cell * cnt);
+    }
+    return idx * P + t;
+  };
+  auto step_count = [&](int t) -> int64_t {
+    return A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? ncell * t : ncell;
+  };
+
+  int status = 0, it = 0;
+  double mu = 0.0;
+  for (; it <= A.max_iter; ++it) {
+    // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
+    double rpmax = 0.0, sl = 0.0;
+    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+      const double rp = row_g(r, y, z) + rw.s[r];
+      rpmax = fmax(rpmax, fabs(rp));
+      sl += rw.s[r] * rw.l[r];
+    }
+    for (int t = w; t < T; t += kQpWaves) {
+      double la0 = 0.0, la1 = 0.0, w00 = 0.0, w01 = 0.0, w11 = 0.0;
+      const int64_t cnt = step_count(t);
+      for (int64_t i = lane; i < cnt; i += 64) {
+        const int64_t o = step_rows(t, i);
+        const int64_t r = nbox + nv + o;
+        const double a0 = rw.a0[o], a1 = rw.a1[o], lam = rw.l[r], wr = lam / rw.s[r];
+        la0 += lam * a0;
+        la1 += lam * a1;
+        w00 += wr * a0 * a0;
+        w01 += wr * a0 * a1;
+        w11 += wr * a1 * a1;
+      }
+      la0 = wave_sum(la0);
+      la1 = wave_sum(la1);
+      w00 = wave_sum(w00);
+      w01 = wave_sum(w01);
+      w11 = wave_sum(w11);
+      if (lane == 0) {
+        const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+        const int64_t rv = nbox + 2 * t;
+        q[3 * t] = wp * y[3 * t] + qf[3 * t] + la0;  // H_pos z + f + G^T lambda, output space
+        q[3 * t + 1] = wp * y[3 * t + 1] + qf[3 * t + 1] + la1;
+        q[3 * t + 2] = rw.l[rv] - rw.l[rv + 1];
+        bw[4 * t] = wp + w00;
+        bw[4 * t + 1] = w01;
+        bw[4 * t + 2] = wp + w11;
+        bw[4 * t + 3] = rw.l[rv] / rw.s[rv] + rw.l[rv + 1] / rw.s[rv + 1];
+      }
+    }
+    __syncthreads();
+    // ---- I2: dual residual, normal matrix ---------------------------------------------------
+    double rdmax = 0.0;
+    for (int j = tid; j < n; j += kQpThreads) {
+      double v = hctrl_mul(z, j, T, order, p) + rw.l[2 * j] - rw.l[2 * j + 1];
+      for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * q[k];
+      rd[j] = v;
+      rdmax = fmax(rdmax, fabs(v));
+    }
+    for (int e = tid; e < n * n; e += kQpThreads) {
+      const int i = e / n, j = e % n;
+      if (j > i) continue;
+      double v = hctrl(i, j, T, order, p);
+      if (i == j) v += rw.l[2 * i] / rw.s[2 * i] + rw.l[2 * i + 1] / rw.s[2 * i + 1];
+      for (int t = 0; t < T; ++t) {
+        const double xi = Gs[(3 * t) * n + i], yi = Gs[(3 * t + 1) * n + i],
+                     vi = Gs[(3 * t + 2) * n + i];
+        const double xj = Gs[(3 * t) * n + j], yj = Gs[(3 * t + 1) * n + j],
+                     vj = Gs[(3 * t + 2) * n + j];
+        v += xi * (bw[4 * t] * xj + bw[4 * t + 1] * yj) + yi * (bw[4 * t + 1] * xj +
+             bw[4 * t + 2] * yj) + bw[4 * t + 3] * vi * vj;
+      }
+      M[i * ldm + j] = v;
+    }
+    block_max2(rpmax, rdmax, red);
+    mu = block_sum(sl, red) / static_cast<double>(mrows);
+#ifdef CCMPC_QP_TRACE
+    if (tid == 0 && sc == 0)
+      printf("qp it %d rp %.3e/%.3e rd %.3e/%.3e mu %.3e\n", it, rpmax, tol_p, rdmax, tol_d, mu);
+#endif
+    if (rpmax <= tol_p && rdmax <= tol_d && mu <= A.tol) break;
+    // mu far below the tolerance without the residuals following: the normal equations have
+    // run out of accuracy (weights ~ 1/mu); stop and leave it to the polish step
+    if (it == A.max_iter || !isfinite(mu) || !isfinite(rpmax) || !isfinite(rdmax) ||
+        mu <= 1e-6 * A.tol * A.tol) {
+      status = CCMPC_QP_MAXITER;
+      break;
+    }
+    // ---- I3: Cholesky on wave 0 (left-looking, lane = row) ---------------------------------
+    // Near the solution the active rows' weights lambda/s grow without bound, and a pivot of
+    // the (mathematically positive definite) M can come out <= 0 after cancellation against
+    // them.  Such a pivot is replaced by a huge one (the pivot-skip modified Cholesky of
+    // interior point codes): that direction's component of dz becomes 0, which is what the
+    // huge weight enforces anyway.
+    if (w == 0) {
+      const bool fail = wave_cholesky(M, n, ldm, dinv, true);
+      if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (red[8 * kQpWaves - 1] != 0.0) {  // weights overflowed: the iteration broke down;
+      status = CCMPC_QP_MAXITER;           // only a verified polish can still answer
+      break;
+    }
+    // triangular solves on wave 0: L L^T x = rhs (rhs in registers, lane = row)
+    auto chol_solve = [&](double *x) {
+      if (w != 0) return;
+      double b[2];
+      wave_load2(x, n, b);
+      wave_forward(M, n, ldm, dinv, b);
+      wave_backward(M, n, ldm, dinv, b);
+      wave_store2(x, n, b);
+    };
+    auto gs_times_dz = [&]() {
+      for (int k = tid; k < T3; k += kQpThreads) {
+        double v = 0.0;
+        for (int j = 0; j < n; ++j) v += Gs[k * n + j] * dz[j];
+        yd[k] = v;
+      }
+      __syncthreads();
+    };
+    // One step of iterative refinement with the product M dz taken from its structure.  The
+    // assembled M carries the weights lambda/s of the active rows, which grow like 1/mu, and
+    // the backward error of its Cholesky grows with them; the structured residual only sees
+    // w_r (a_r . yd_t), which stays small for those rows, so the step recovers the accuracy
+    // the dual residual needs once mu is small.
+    auto refine = [&]() {
+      for (int t = w; t < T; t += kQpWaves) {
+        double p0 = 0.0, p1 = 0.0;
+        const int64_t cnt = step_count(t);
+        const double yx = yd[3 * t], yy = yd[3 * t + 1];
+        for (int64_t i = lane; i < cnt; i += 64) {
+          const int64_t o = step_rows(t, i);
+          const int64_t r = nbox + nv + o;
+          const double a0 = rw.a0[o], a1 = rw.a1[o];
+          const double wa = rw.l[r] / rw.s[r] * (a0 * yx + a1 * yy);
+          p0 += wa * a0;
+          p1 += wa * a1;
+        }
+        p0 = wave_sum(p0);
+        p1 = wave_sum(p1);
+        if (lane == 0) {
+          const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+          q[3 * t] = wp * yx + p0;
+          q[3 * t + 1] = wp * yy + p1;
+          q[3 * t + 2] = bw[4 * t + 3] * yd[3 * t + 2];
+        }
+      }
+      __syncthreads();
+      for (int j = tid; j < n; j += kQpThreads) {
+        double v = rh[j] - hctrl_mul(dz, j, T, order, p) -
+                   (rw.l[2 * j] / rw.s[2 * j] + rw.l[2 * j + 1] / rw.s[2 * j + 1]) * dz[j];
+        for (int k = 0; k < T3; ++k) v -= Gs[k * n + j] * q[k];
+        e2[j] = v;
+      }
+      __syncthreads();
+      chol_solve(e2);
+      __syncthreads();
+      for (int j = tid; j < n; j += kQpThreads) dz[j] += e2[j];
+      __syncthreads();
+      gs_times_dz();
+    };
+    // rhs = -r_d - G^T u with u_r given per row; q (output space) and dz (rhs) staged in LDS
+    auto build_rhs = [&](auto urow) {
+      for (int t = w; t < T; t += kQpWaves) {
+        double u0 = 0.0, u1 = 0.0;
+        const int64_t cnt = step_count(t);
+        for (int64_t i = lane; i < cnt; i += 64) {
+          const int64_t o = step_rows(t, i);
+          const double u = urow(nbox + nv + o);
+          u0 += u * rw.a0[o];
+          u1 += u * rw.a1[o];
+        }
+        u0 = wave_sum(u0);
+        u1 = wave_sum(u1);
+        if (lane == 0) {
+          const int64_t rv = nbox + 2 * t;
+          q[3 * t] = u0;
+          q[3 * t + 1] = u1;
+          q[3 * t + 2] = urow(rv) - urow(rv + 1);
+        }
+      }
+      __syncthreads();
+      for (int j = tid; j < n; j += kQpThreads) {
+        double v = -rd[j] - (urow(2 * j) - urow(2 * j + 1));
+        for (int k = 0; k < T3; ++k) v -= Gs[k * n + j] * q[k];
+        dz[j] = v;
+        rh[j] = v;
+      }
+      __syncthreads();
+      chol_solve(dz);
+      __syncthreads();
+      gs_times_dz();
+      refine();
+    };
+    // ---- predictor (affine scaling): r_c = s l  ->  u = w r_p - l ---------------------------
+    build_rhs([&](int64_t r) {
+      const double rp = row_g(r, y, z) + rw.s[r];
+      return rw.l[r] / rw.s[r] * rp - rw.l[r];
+    });
+    double amax = 1.0;
+    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+      const double s = rw.s[r], l = rw.l[r];
+      const double rp = row_g(r, y, z) + s, gd = row_gd(r, yd, dz);
+      const double ds = -rp - gd, dl = l / s * (gd + rp) - l;
+      rw.ds[r] = ds;
+      rw.dl[r] = dl;
+      if (ds < 0.0) amax = fmin(amax, -s / ds);
+      if (dl < 0.0) amax = fmin(amax, -l / dl);
+    }
+    const double aaff = block_min(amax, red);
+    double slaff = 0.0;
+    for (int64_t r = tid; r < mrows; r += kQpThreads)
+      slaff += (rw.s[r] + aaff * rw.ds[r]) * (rw.l[r] + aaff * rw.dl[r]);
+    const double muaff = block_sum(slaff, red) / static_cast<double>(mrows);
+    const double sr = muaff / mu, sigma = sr * sr * sr;
+    // ---- corrector: r_c = s l + ds_aff dl_aff - sigma mu;  u = w r_p - r_c / s ----------
+    auto rc_of = [&](int64_t r) {
+      return rw.s[r] * rw.l[r] + rw.ds[r] * rw.dl[r] - sigma * mu;
+    };
+    build_rhs([&](int64_t r) {
+      const double rp = row_g(r, y, z) + rw.s[r];
+      return rw.l[r] / rw.s[r] * rp - rc_of(r) / rw.s[r];
+    });
+    amax = 1e300;
+    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+      const double s = rw.s[r], l = rw.l[r];
+      const double rp = row_g(r, y, z) + s, gd = row_gd(r, yd, dz);
+      const double rc = rc_of(r);
+      const double ds = -rp - gd, dl = (-rc - l * ds) / s;
+      rw.ds[r] = ds;  // every read of this row's ds_aff / dl_aff happened above in this thread
+      rw.dl[r] = dl;
+      if (ds < 0.0) amax = fmin(amax, -s / ds);
+      if (dl < 0.0) amax = fmin(amax, -l / dl);
+    }
+    const double alpha = fmin(1.0, 0.995 * block_min(amax, red));
+#ifdef CCMPC_QP_TRACE
+    if (tid == 0 && sc == 0) printf("   aaff %.3e sigma %.3e alpha %.3e\n", aaff, sigma, alpha);
+#endif
+    for (int j = tid; j < n; j += kQpThreads) z[j] += alpha * dz[j];
+    for (int k = tid; k < T3; k += kQpThreads) y[k] += alpha * yd[k];
+    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+      rw.s[r] += alpha * rw.ds[r];
+      rw.l[r] += alpha * rw.dl[r];
+    }
+    __syncthreads();
+  }
+
+  // ---- polish: the equality-constrained QP on the IPM's active set ---------------------------
+  // (as OSQP polishes an ADMM iterate).  Rows with s < lambda are taken as active; the KKT
+  // system of  min 1/2 z^T H z + f^T z  s.t.  G_A z = h_A  is solved through H = L L^T and
+  // S = W^T W, W = L^{-1} G_A^T:  lambda = S^{-1}(W^T y0 - h_A), y0 = -L^{-1} f,
+  // z = L^{-T}(y0 - W lambda).  H carries no barrier weights, so this is as accurate as the
+  // problem itself.  The result is kept only if it is a verified KKT point: every row within
+  // tol_p and lambda >= -tol_d (stationarity holds by construction), which also makes a
+  // stalled IPM's answer exact and leaves infeasible problems reported as such.
+  if (A.polish) {
+    double *Wm = lds + lay.pw, *Sm = lds + lay.ps, *act = lds + lay.pact,
+           *sdinv = lds + lay.pdinv;
+    double *fu = lds + lay.f, *y0 = rh, *rs = e2, *lam = q, *zp = dz, *yp = yd;
+    // H (no barrier terms) into M; f in control space
+    for (int e = tid; e < n * n; e += kQpThreads) {
+      const int i = e / n, j = e % n;
+      if (j > i) continue;
+      double v = hctrl(i, j, T, order, p);
+      for (int t = 0; t < T; ++t) {
+        const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+        v += wp * (Gs[(3 * t) * n + i] * Gs[(3 * t) * n + j] +
+                   Gs[(3 * t + 1) * n + i] * Gs[(3 * t + 1) * n + j]);
+      }
+      M[i * ldm + j] = v;
+    }
+    for (int j = tid; j < n; j += kQpThreads) {
+      double v = 0.0;
+      for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * qf[k];
+      fu[j] = v;
+    }
+    // active rows, compacted in row order (ballot + prefix: deterministic)
+    int na = 0;
+    for (int64_t base = 0; base < mrows; base += kQpThreads) {
+      const int64_t r = base + tid;
+      const bool on = r < mrows && rw.s[r] < rw.l[r];
+      const uint64_t mask = __ballot(on);
+      if (lane == 0) red[w] = static_cast<double>(__popcll(mask));
+      __syncthreads();
+      int off = na;
+      for (int k = 0; k < w; ++k) off += static_cast<int>(red[k]);
+      int tot = na;
+      for (int k = 0; k < kQpWaves; ++k) tot += static_cast<int>(red[k]);
+      const int pos = off + __popcll(mask & ((uint64_t(1) << lane) - 1));
+      if (on && pos < n) act[pos] = static_cast<double>(r);
+      na = tot;
+      __syncthreads();
+    }
+    if (na <= n) {  // more active rows than controls: degenerate, keep the IPM's answer
+      if (w == 0) {
+        const bool fail = wave_cholesky(M, n, ldm, dinv, false);
+        double b[2];
+        wave_load2(fu, n, b);
+        b[0] = -b[0];
+        b[1] = -b[1];
+        wave_forward(M, n, ldm, dinv, b);
+        wave_store2(y0, n, b);
+        if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      bool ok = red[8 * kQpWaves - 1] == 0.0;
+      if (!ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
+      if (ok) {
+        // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
+        for (int a = w; a < na; a += kQpWaves) {
+          const int64_t r = static_cast<int64_t>(act[a]);
+          double b[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = lane + 64 * h;
+            double g = 0.0;
+            if (j < n) {
+              if (r < nbox) {
+                g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
+              } else if (r < nbox + nv) {
+                const int t = static_cast<int>((r - nbox) >> 1);
+                g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
+              } else {
+                // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
+                const int64_t o = r - nbox - nv;
+                const int t = obst_step(o);
+                g = rw.a0[o] * Gs[(3 * t) * n + j] + rw.a1[o] * Gs[(3 * t + 1) * n + j];
+              }
+            }
+            b[h] = g;
+          }
+          wave_forward(M, n, ldm, dinv, b);
+          wave_store2(Wm + a * n, n, b);
+          double d = 0.0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (lane + 64 * h < n) d += b[h] * y0[lane + 64 * h];
+          d = wave_sum(d);
+          if (lane == 0) rs[a] = d + row_const(r);
+        }
+        __syncthreads();
+        for (int e = tid; e < na * na; e += kQpThreads) {
+          const int i = e / na, j = e % na;
+          if (j > i) continue;
+          double v = 0.0;
+          for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
+          Sm[i * ldm + j] = v;
+        }
+        __syncthreads();
+        if (w == 0) {
+          const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
+          double b[2];
+          if (!fail) {
+            wave_load2(rs, na, b);
+            wave_forward(Sm, na, ldm, sdinv, b);
+            wave_backward(Sm, na, ldm, sdinv, b);
+            wave_store2(lam, na, b);
+          }
+          if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        ok = red[8 * kQpWaves - 1] == 0.0;
+      }
+      if (ok) {
+        // z = L^{-T}(y0 - W^T lambda)
+        for (int j = tid; j < n; j += kQpThreads) {
+          double v = y0[j];
+          for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
+          zp[j] = v;
+        }
+        __syncthreads();
+        if (w == 0) {
+          double b[2];
+          wave_load2(zp, n, b);
+          wave_backward(M, n, ldm, dinv, b);
+          wave_store2(zp, n, b);
+        }
+        __syncthreads();
+        for (int k = tid; k < T3; k += kQpThreads) {
+          double v = 0.0;
+          for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
+          yp[k] = v;
+        }
+        __syncthreads();
+        double viol = 0.0, lneg = 0.0;
+        for (int64_t r = tid; r < mrows; r += kQpThreads) viol = fmax(viol, row_g(r, yp, zp));
+        for (int a = tid; a < na; a += kQpThreads) lneg = fmax(lneg, -lam[a]);
+        block_max2(viol, lneg, red);
+        if (viol <= tol_p && lneg <= tol_d && isfinite(viol) && isfinite(lneg)) {
+          for (int j = tid; j < n; j += kQpThreads) z[j] = zp[j];
+          status = 0;
+        }
+        __syncthreads();
+      }
+    }
+  }
+
+  // ---- outputs: u, X = Gamma_f u + const (all four state rows), the objective value ----------
+  for (int j = tid; j < n; j += kQpThreads) A.out_u[sc * n + j] = z[j];
+  double part = 0.0;
+  for (int r = tid; r < 4 * T; r += kQpThreads) {
+    const int gr = 4 * Tp + r;
+    const double *g = Gam + static_cast<int64_t>(gr) * ncol;
+    double x = xb[gr];
+    if (uprev)
+      for (int j = 0; j < 2 * Tp; ++j) x += g[j] * uprev[j];
+    for (int j = 0; j < n; ++j) x += g[2 * Tp + j] * (z[j] - (ubar ? ubar[2 * Tp + j] : 0.0));
+    A.out_x[sc * 4 * T + r] = x;
+    const int t = r / 4, a = r % 4;
+    if (a < 2) {  // compute_objective_referenceTraj (:2478-2507) at the solution
+      const int tr = t < A.n_ref ? t : A.n_ref - 1;
+      const double e = x - ref[2 * tr + a];
+      part += p.w_ref * e * e;
+      if (t == T - 1) {
+        const double ef = x - (a == 0 ? g0 : g1);
+        part += p.w_final * ef * ef;
+      }
+    }
+  }
+  for (int t = tid; t < T; t += kQpThreads) {
+    const double a0 = z[u_index(t, 0, T, order)], a1 = z[u_index(t, 1, T, order)];
+    part += a0 * (p.w_accel * a0 + p.w_joint * a1) + a1 * (p.w_joint * a0 + p.w_turning * a1);
+    if (t >= 1) {
+      const double d0 = a0 - z[u_index(t - 1, 0, T, order)];
+      const double d1 = a1 - z[u_index(t - 1, 1, T, order)];
+      part += d0 * (p.w_ch_accel * d0 + p.w_ch_joint * d1) +
+              d1 * (p.w_ch_joint * d0 + p.w_ch_turning * d1);
+    }
+  }
+  const double cost = block_sum(part, red);
+  double sk = skipped;
+  double dummy = 0.0;
+  block_max2(sk, dummy, red);
+  if (tid == 0) {
+    A.out_cost[sc] = cost;
+    A.out_status[sc] = status | (sk > 0.0 ? CCMPC_QP_SKIPPED_ROWS : 0);
+    A.out_iter[sc] = it;
+  }
+}
+
+// Where the per-scene state lives: the polish step's matrices come first (they make the
+// answer exact), then the row store if it still fits; otherwise the rows go to the workspace.
+struct QpPlan {
+  bool rows_lds, polish;
+};
+inline bool qp_fits(int T, int64_t R, bool rows_lds, bool polish) {
+  return static_cast<size_t>(QpLayout(T, rows_lds ? R : 0, rows_lds, polish).total) *
+             sizeof(double) <= kQpLdsBytes;
+}
+inline QpPlan qp_plan(int T, int64_t R) {
+  if (qp_fits(T, R, true, true)) return {true, true};
+  if (qp_fits(T, R, false, true)) return {false, true};
+  if (qp_fits(T, R, true, false)) return {true, false};
+  return {false, false};
+}
+
+}  // namespace ccmpc
+
+using namespace ccmpc;
+
+extern "C" int ccmpc_mpc_ltv(const double *x_init, int64_t n_scenes, int64_t T, double Ts,
+                             double l_r, double L, double *out_xbar, double *out_gamma,
+                             ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(T >= 1 && T <= kQpMaxT, "T must be in [1, 40]");
+  CCMPC_REQUIRE(n_scenes >= 0, "bad n_scenes");
+  if (n_scenes == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(x_init && out_xbar && out_gamma, "null pointer");
+  CCMPC_REQUIRE(Ts > 0.0 && L > 0.0 && l_r > 0.0, "Ts, L, l_r must be positive");
+  hipLaunchKernelGGL(mpc_ltv_kernel, dim3(static_cast<unsigned>(n_scenes)), dim3(256), 0,
+                     as_stream(stream), x_init, n_scenes, static_cast<int>(T), Ts, l_r, L,
+                     out_xbar, out_gamma);
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}
+
+extern "C" size_t ccmpc_mpc_qp_workspace_bytes(int64_t n_scenes, int64_t T,
+                                               int64_t max_cells_per_scene, int rec_kind) {
+  if (T < 1 || T > kQpMaxT || n_scenes < 0 || max_cells_per_scene < 0) return 0;
+  const int64_t R = max_cells_per_scene * qp_rows_per_cell(static_cast<int>(T), rec_kind);
+  if (qp_plan(static_cast<int>(T), R).rows_lds) return 16;  // rows live in LDS
+  const int64_t m = 4 * T + 2 * T + R;
+  return static_cast<size_t>(n_scenes * (4 * m + 3 * R)) * sizeof(double) + 16;
+}
+
+extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamma,
+                            const double *xbar, const double *ubar, const double *u_prev,
+                            const double *goal, const double *ref, int64_t n_ref,
+                            const void *rec, int rec_kind, const int64_t *scene_cell,
+                            int64_t max_cells_per_scene, const ccmpc_mpc_params *params,
+                            int u_order, int32_t max_iter, double tol, void *workspace,
+                            size_t workspace_bytes, double *out_u, double *out_x,
+                            double *out_cost, int32_t *out_status, int32_t *out_iter,
+                            ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(T >= 1 && T <= kQpMaxT, "T must be in [1, 40]");
+  CCMPC_REQUIRE(T_full >= T && T_full <= kQpMaxT, "T_full must be in [T, 40]");
+  CCMPC_REQUIRE(n_scenes >= 0 && n_scenes < (int64_t(1) << 31), "bad n_scenes");
+  if (n_scenes == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(gamma && xbar && goal && ref && scene_cell && params, "null pointer");
+  CCMPC_REQUIRE(out_u && out_x && out_cost && out_status && out_iter, "null pointer");
+  CCMPC_REQUIRE(T_full == T || u_prev, "u_prev is required when T < T_full");
+  CCMPC_REQUIRE(n_ref >= 1, "n_ref must be >= 1");
+  CCMPC_REQUIRE(rec_kind == CCMPC_REC_KIND_HALFSPACE || rec_kind == CCMPC_REC_KIND_AFFINE,
+                "bad rec_kind");
+  CCMPC_REQUIRE(u_order == CCMPC_U_ORDER_F || u_order == CCMPC_U_ORDER_C, "bad u_order");
+  CCMPC_REQUIRE(max_cells_per_scene >= 0, "bad max_cells_per_scene");
+  CCMPC_REQUIRE(max_cells_per_scene == 0 || rec, "null records");
+  CCMPC_REQUIRE(max_iter >= 1 && tol > 0.0, "max_iter >= 1 and tol > 0 required");
+  if (workspace_bytes < ccmpc_mpc_qp_workspace_bytes(n_scenes, T, max_cells_per_scene,
+                                                     rec_kind)) {
+    set_error("ccmpc_mpc_qp: workspace too small");
+    return CCMPC_ERR_WORKSPACE;
+  }
+  const int Ti = static_cast<int>(T);
+  const int64_t R = max_cells_per_scene * qp_rows_per_cell(Ti, rec_kind);
+  const QpPlan plan = qp_plan(Ti, R);
+  const bool in_lds = plan.rows_lds;
+  CCMPC_REQUIRE(in_lds || workspace, "null workspace");
+  QpArgs a{};
+  a.S = n_scenes;
+  a.T = Ti;
+  a.Tf = static_cast<int>(T_full);
+  a.n_ref = static_cast<int>(n_ref);
+  a.u_order = u_order;
+  a.rec_kind = rec_kind;
+  a.max_iter = max_iter;
+  a.rows_in_lds = in_lds;
+  a.polish = plan.polish;
+  a.max_cells = max_cells_per_scene;
+  a.tol = tol;
+  a.gamma = gamma;
+  a.xbar = xbar;
+  a.ubar = ubar;
+  a.u_prev = u_prev;
+  a.goal = goal;
+  a.ref = ref;
+  a.rec = static_cast<const unsigned char *>(rec);
+  a.scene_cell = scene_cell;
+  a.p = *params;
+  a.ws = static_cast<double *>(workspace);
+  a.out_u = out_u;
+  a.out_x = out_x;
+  a.out_cost = out_cost;
+  a.out_status = out_status;
+  a.out_iter = out_iter;
+  const size_t lds = static_cast<size_t>(QpLayout(Ti, in_lds ? R : 0, in_lds, plan.polish).total) *
+                     sizeof(double);
+  hipStream_t s = as_stream(stream);
+  if (in_lds) {
+    static bool attr = [] {
+      return hipFuncSetAttribute(reinterpret_cast<const void *>(mpc_qp_kernel<true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 static_cast<int>(kQpLdsBytes)) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(mpc_qp_kernel<true>, dim3(static_cast<unsigned>(n_scenes)),
+                       dim3(kQpThreads), lds, s, a);
+  } else {
+    CCMPC_REQUIRE(lds <= kQpLdsBytes, "T too large for the LDS image");
+    static bool attr = [] {
+      return hipFuncSetAttribute(reinterpret_cast<const void *>(mpc_qp_kernel<false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 static_cast<int>(kQpLdsBytes)) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(mpc_qp_kernel<false>, dim3(static_cast<unsigned>(n_scenes)),
+                       dim3(kQpThreads), lds, s, a);
+  }
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}

@@ -294,6 +294,72 @@ int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T, const doub
              double *out_yaw_mean, double *out_yaw0_var, double *out_yaw, double *out_vertices,
              ccmpc_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * The caller of the path: the planning step's quadratic program,
+ * batched over scenes.  Replaces the cvxpy + CPLEX problem of do_highlevel_control
+ * (v8ideal/__init__.py:2850-2930, :2999-3012, :3040-3110) with the road-boundary MILP off (the reference
+ * default, :217), so the problem is a convex QP in the controls u (2T values):
+ *   state      x = Gamma_f (u - u_bar) + x_bar + Gamma_p u_prev            (:2877-2891)
+ *   bounds     [min_a, -max_delta] <= U_t <= [max_a, max_delta]            (:2873-2876)
+ *              0 <= v_t <= max_v                                           (:610-626)
+ *   obstacles  every record with status 0:  n . x_t >= d (side +1) or <= d (side -1)
+ *              (Minkowski :926-939; affine: rhs, :1503-1515 with S_big = 0)
+ *   objective  w_final |X_{T-1} - goal|^2 + sum_t w_ref |X_t - ref_t|^2
+ *              + sum_t U_t^T R1 U_t + sum_{t>=1} dU_t^T R2 dU_t                (:2478-2507)
+ * U = cp.reshape(u, (T, 2)) uses cvxpy's default column-major order (U_t = (u[t], u[T+t]),
+ * CCMPC_U_ORDER_F) in the reference; CCMPC_U_ORDER_C pairs (u[2t], u[2t+1]).
+ * Solved by a primal-dual interior point method (Mehrotra predictor-corrector), one workgroup
+ * per scene, the whole iteration in LDS, then polished: the equality-constrained QP on the
+ * IPM's active set, kept only when it is a verified KKT point (T <= 32; beyond, the IPM's
+ * answer at tol).
+ * ------------------------------------------------------------------------------------- */
+#define CCMPC_U_ORDER_F 0
+#define CCMPC_U_ORDER_C 1
+#define CCMPC_REC_KIND_HALFSPACE 0 /* ccmpc_halfspace records [cells][T(T-1)/2] */
+#define CCMPC_REC_KIND_AFFINE 1    /* ccmpc_affine_rec records [cells][T] */
+
+/* QP status per scene */
+#define CCMPC_QP_OK 0
+#define CCMPC_QP_MAXITER 1      /* no verified solution within max_iter: infeasible (the
+                                   reference returns InSimulationException, :3099-3110)   */
+#define CCMPC_QP_NUMERIC 2      /* the objective's Hessian is not positive definite       */
+#define CCMPC_QP_SKIPPED_ROWS 4 /* flag: records with status != 0 were left out */
+
+typedef struct ccmpc_mpc_params {
+  double w_final, w_ref;                     /* objective weights (:93-102)          */
+  double w_accel, w_joint, w_turning;        /* R1                                   */
+  double w_ch_accel, w_ch_joint, w_ch_turning; /* R2                                 */
+  double min_a, max_a, max_delta, max_v;     /* control / speed limits (:88-109)     */
+} ccmpc_mpc_params;
+
+/* LTV model of the ego vehicle about u_init = 0, the only linearisation input the planner
+ * uses (make_local_params, v8ideal/__init__.py:537-557 -> dynamics/bicycle_v2.py
+ * VehicleModel.get_optimization_ltv :261-308).  Per scene:
+ *  x_init[s][4] = [x, y, psi, v];  out_xbar[s][4T] = X_bar[1:];  out_gamma[s][4T][2T]. */
+int ccmpc_mpc_ltv(const double *x_init, int64_t n_scenes, int64_t T, double Ts, double l_r,
+                  double L, double *out_xbar, double *out_gamma, ccmpc_stream_t stream);
+
+/* Workspace for scenes holding at most max_cells_per_scene cells of records. */
+size_t ccmpc_mpc_qp_workspace_bytes(int64_t n_scenes, int64_t T, int64_t max_cells_per_scene,
+                                    int rec_kind);
+
+/* One QP per scene s, horizon T <= T_full, T_prev = T_full - T steps already executed:
+ *  gamma[s][4 T_full][2 T_full], xbar[s][4 T_full]  (the full-horizon model of the first step)
+ *  ubar[s][2 T_full] or NULL (= 0, u_init = 0);  u_prev[s][2 T_prev] or NULL when T_prev = 0
+ *  goal[s][2];  ref[s][n_ref][2] (step t uses ref[min(t, n_ref - 1)], :2492-2501)
+ *  rec: records of every scene's cells, scene s owning cells [scene_cell[s], scene_cell[s+1])
+ *  params: HOST pointer.
+ *  out_u[s][2T] (the cvxpy variable u), out_x[s][T][4], out_cost[s], out_status[s],
+ *  out_iter[s] (IPM iterations). */
+int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamma,
+                 const double *xbar, const double *ubar, const double *u_prev,
+                 const double *goal, const double *ref, int64_t n_ref, const void *rec,
+                 int rec_kind, const int64_t *scene_cell, int64_t max_cells_per_scene,
+                 const ccmpc_mpc_params *params, int u_order, int32_t max_iter, double tol,
+                 void *workspace, size_t workspace_bytes, double *out_u, double *out_x,
+                 double *out_cost, int32_t *out_status, int32_t *out_iter,
+                 ccmpc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
