@@ -59,10 +59,10 @@ def time_config(dev, seed, name, O, N, T, scenes):
     for sc in range(scenes):
         ovs, ref, _ = synthetic.scene(seed + 1000 + sc, O=O, N=N, T=T)
         cells += [c for o in ovs for c in o]
-        K += [len(o) for o in ovs]
+        K.append([len(o) for o in ovs])
         refs.append(ref)
     store = engine.ParticleStore.from_cells(cells, device=dev)
-    cyc = cycle.MinkowskiCycle(store, K, refs[0])
+    cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], refs[0], scene_K=K)
     t = time_kernel_live(cyc.run, dev, per_graph=10, replays=5)
     tm = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev,
                           per_graph=10, replays=5)
@@ -103,7 +103,7 @@ def sweep(dev, seed):
     return rows
 
 
-def planning_qp(dev, seed, scenes=64, O=4, N=5000, T=8, with_cpu=True):
+def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True):
     """The caller side of the path: do_highlevel_control's QP
     (v8ideal/__init__.py:2850-2930) for `scenes` planning steps whose obstacles cross the ego's
     path (ccmpc.synthetic.crossing_scene: O OVs x 2 modes, N particles per OV, T steps), solved
@@ -115,13 +115,13 @@ def planning_qp(dev, seed, scenes=64, O=4, N=5000, T=8, with_cpu=True):
     for sc in range(scenes):
         c, k, ref, goal, x0, _ = synthetic.crossing_scene(seed + 5000 + sc, O=O, N=N, T=T)
         cells += c
-        K += k
+        K.append(k)
         cps.append(len(c))
         refs.append(ref)
         goals.append(goal)
         x0s.append(x0)
     store = engine.ParticleStore.from_cells(cells, device=dev)
-    cyc = cycle.MinkowskiCycle(store, K, refs[0])
+    cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], refs[0], scene_K=K)
     cyc.run()
     xbar, gamma = mpc.ltv(np.array(x0s), T, lon=3.7)
     goal_t = torch.as_tensor(np.array(goals), device=dev)

@@ -19,7 +19,10 @@ from . import engine, risk
 
 
 class MinkowskiCycle:
-    def __init__(self, store, K, ref_traj, ph=None, R=risk.R_COLLISION, tol=1e-8, maxiter=1000):
+    def __init__(self, store, K, ref_traj, ph=None, R=risk.R_COLLISION, tol=1e-8, maxiter=1000,
+                 scene_K=None):
+        """scene_K: the per-scene split of K when several scenes' cells share one cycle (each
+        scene then allocates its own risk, risk.scenes_cell_risk); None = one scene."""
         self.store = store
         self.device = store.device
         self.T = store.T
@@ -29,8 +32,12 @@ class MinkowskiCycle:
         C, T = store.n_cells, self.T
         self.ref = torch.as_tensor(np.asarray(ref_traj, np.float64).reshape(-1, T, 2),
                                    device=self.device)
-        self.risk = torch.as_tensor(risk.cell_risk(risk.eps_ura(self.K), self.K, ph),
-                                    device=self.device)
+        if scene_K is None:
+            cr = risk.cell_risk(risk.eps_ura(self.K), self.K, ph)
+        else:
+            assert [int(k) for K_s in scene_K for k in K_s] == self.K
+            cr = risk.scenes_cell_risk(scene_K, ph)
+        self.risk = torch.as_tensor(cr, device=self.device)
         self.R, self.tol, self.maxiter = R, tol, maxiter
         self.mean = torch.empty((C, T, 2), dtype=torch.float64, device=self.device)
         self.cov = torch.empty((C, 2 * T, 2 * T), dtype=torch.float64, device=self.device)

@@ -47,6 +47,13 @@ def cell_risk(eps_ura_mat, K, ph, target_p=TARGET_P):
     return np.asarray(rows, dtype=np.float64).reshape(-1, 3)
 
 
+def scenes_cell_risk(scene_K, ph, target_p=TARGET_P):
+    """cell_risk of several independent planning steps batched into one cycle: each scene
+    allocates its own risk, eps_ura = 0.05 / O_scene (v8ideal/__init__.py:2920-2926)."""
+    parts = [cell_risk(eps_ura(K), K, ph, target_p) for K in scene_K]
+    return np.concatenate(parts, 0) if parts else np.zeros((0, 3))
+
+
 def cell_gamma(eps_ura_mat, K, ph):
     """(n_cells,) = norm.ppf(1 - eps_ura[ov, k] / ph) for the GMM-affine generator."""
     return cell_risk(eps_ura_mat, K, ph)[:, 2].copy()

@@ -166,3 +166,19 @@ def test_affine_scale_generator_matches_reference(golden, scaled, pre):
     assert set(g[f"{pre}2_which"]) <= {-1, 0, 1}
     if not scaled:
         assert np.all(g["sr1_scale"] == 1.0) and np.all(g["sr2_scale"] == 1.0)
+
+
+def test_batched_scenes_allocate_risk_per_scene():
+    """Several planning steps in one cycle keep eps_ura = 0.05 / O of their own scene
+    (v8ideal/__init__.py:2920-2926): the batched risk table is the per-scene tables stacked."""
+    import scipy.stats
+    from ccmpc import risk
+    scene_K = [[2, 1, 3], [1], [2, 2]]
+    got = risk.scenes_cell_risk(scene_K, 8)
+    want = []
+    for K in scene_K:
+        eps = orc.EPS_TOTAL / len(K) / 8
+        for k in K:
+            want += [[scipy.stats.chi2.ppf(1 - eps, 2), scipy.stats.chi2.ppf(orc.TARGET_P, 2),
+                      scipy.stats.norm.ppf(1 - eps)]] * k
+    np.testing.assert_allclose(got, np.array(want), rtol=1e-14)
