@@ -21,6 +21,12 @@
 
 namespace ccmpc {
 
+#ifdef CCMPC_QP_TRACE
+#define QP_MARK(i) (tmark[i] = wall_clock64())
+#else
+#define QP_MARK(i) ((void)0)
+#endif
+
 constexpr int kQpThreads = 256;
 constexpr int kQpWaves = kQpThreads / 64;
 constexpr int kQpMaxT = 40;
@@ -204,6 +210,33 @@ __device__ __forceinline__ double block_min(double a, double *red) {
   return a;
 }
 
+// Block argmax (largest value, smallest index on ties); every thread gets the result.
+__device__ __forceinline__ void block_argmax(double &v, double &idx, double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o, 64), oi = __shfl_xor(idx, o, 64);
+    if (ov > v || (ov == v && oi < idx)) {
+      v = ov;
+      idx = oi;
+    }
+  }
+  if (lane == 0) {
+    red[2 * w] = v;
+    red[2 * w + 1] = idx;
+  }
+  __syncthreads();
+  v = red[0];
+  idx = red[1];
+  for (int k = 1; k < kQpWaves; ++k) {
+    if (red[2 * k] > v || (red[2 * k] == v && red[2 * k + 1] < idx)) {
+      v = red[2 * k];
+      idx = red[2 * k + 1];
+    }
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ double lane_bcast(double v, int src) {  // src wave-uniform
   const uint64_t u = __builtin_bit_cast(uint64_t, v);
   const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), src);
@@ -299,6 +332,64 @@ __device__ __forceinline__ void wave_store2(double *x, int N, const double b[2])
     if (lane + 64 * h < N) x[lane + 64 * h] = b[h];
 }
 
+// Register-resident variants for n <= NM (one row per lane of the calling wave): the
+// IPM factors and solves twice per iteration, and with L in registers a column step is a
+// readlane and an FMA instead of a dependent LDS round trip.  a[k] = L[lane][k] (row form),
+// dl = 1 / L[lane][lane]; the L^T solve reads L's rows from LDS (independent of the chain, so
+// the unrolled loads issue ahead of it).
+template <int NM>
+__device__ __forceinline__ bool reg_cholesky(double (&a)[NM], int n, double &dl) {
+  const int lane = threadIdx.x & 63;
+  bool fail = false;
+  double diag0 = 0.0;  // the lane's original diagonal (for the pivot-skip threshold)
+#pragma unroll
+  for (int k = 0; k < NM; ++k)
+    if (k == lane) diag0 = a[k];
+#pragma unroll
+  for (int j = 0; j < NM; ++j) {
+    if (j < n) {
+      double d = lane_bcast(a[j], j);
+      const double ajj = lane_bcast(diag0, j);
+      fail = fail || !isfinite(d) || !isfinite(ajj);
+      if (!(d > 1e-30 * ajj)) d = 1e128;
+      const double ljj = sqrt(d), inv = 1.0 / ljj;
+      const double lij = lane > j ? a[j] * inv : (lane == j ? ljj : 0.0);
+      a[j] = lij;
+      if (lane == j) dl = inv;
+      // trailing update without an exec-mask branch: rows above k pick up values in their
+      // (never read) upper triangle; lij = 0 for rows < j keeps their finished rows intact
+#pragma unroll
+      for (int k = j + 1; k < NM; ++k) {
+        if (k < n) a[k] = fma(-lij, lane_bcast(lij, k), a[k]);
+      }
+    }
+  }
+  return fail;
+}
+
+template <int NM>
+__device__ __forceinline__ double reg_solve(const double (&a)[NM], const double *L, int ld,
+                                            double dl, int n, double b) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < NM; ++j) {  // L y = b
+    if (j < n) {
+      const double yj = lane_bcast(b, j) * lane_bcast(dl, j);
+      const double upd = fma(-a[j], yj, b);
+      b = lane == j ? yj : (lane > j ? upd : b);
+    }
+  }
+#pragma unroll
+  for (int j = NM - 1; j >= 0; --j) {  // L^T x = y
+    if (j < n) {
+      const double xj = lane_bcast(b, j) * lane_bcast(dl, j);
+      const double upd = fma(-L[j * ld + (lane < j ? lane : 0)], xj, b);
+      b = lane == j ? xj : (lane < j ? upd : b);
+    }
+  }
+  return b;
+}
+
 // control index of U_t component c: cp.reshape(u, (T, 2)) is column-major by default
 __device__ __forceinline__ int u_index(int t, int c, int T, int order) {
   return order == CCMPC_U_ORDER_C ? 2 * t + c : t + c * T;
@@ -346,7 +437,7 @@ __device__ __forceinline__ double hctrl_mul(const double *z, int i, int T, int o
   return acc;
 }
 
-template <bool ROWS_LDS>
+template <bool ROWS_LDS, int NM>
 __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
   extern __shared__ double lds[];
   const int64_t sc = blockIdx.x;
@@ -538,8 +629,15 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
   };
 
   int status = 0, it = 0;
-  double mu = 0.0;
+  double mu = 0.0, mu0 = 0.0;
+  bool infeasible = false;
+#ifdef CCMPC_QP_TRACE
+  uint64_t tmark[8] = {};
+#endif
+  constexpr int NR = NM > 0 ? NM : 1;
+  double La[NR], Ldl = 0.0;  // wave 0: L of the current M (register path, NM > 0)
   for (; it <= A.max_iter; ++it) {
+    QP_MARK(0);
     // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
     double rpmax = 0.0, sl = 0.0;
     for (int64_t r = tid; r < mrows; r += kQpThreads) {
@@ -578,6 +676,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       }
     }
     __syncthreads();
+    QP_MARK(1);
     // ---- I2: dual residual, normal matrix ---------------------------------------------------
     double rdmax = 0.0;
     for (int j = tid; j < n; j += kQpThreads) {
@@ -604,17 +703,31 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     block_max2(rpmax, rdmax, red);
     mu = block_sum(sl, red) / static_cast<double>(mrows);
 #ifdef CCMPC_QP_TRACE
-    if (tid == 0 && sc == 0)
-      printf("qp it %d rp %.3e/%.3e rd %.3e/%.3e mu %.3e\n", it, rpmax, tol_p, rdmax, tol_d, mu);
+    const double tr_rp = rpmax, tr_rd = rdmax;
+    if (it == 0 && tid == 0 && sc == 0)
+      printf("qp it %d rp %.3e/%.3e rd %.3e/%.3e mu %.3e\n", it, tr_rp, tol_p, tr_rd, tol_d, mu);
 #endif
+    if (it == 0) mu0 = mu;
     if (rpmax <= tol_p && rdmax <= tol_d && mu <= A.tol) break;
-    // mu far below the tolerance without the residuals following: the normal equations have
-    // run out of accuracy (weights ~ 1/mu); stop and leave it to the polish step
-    if (it == A.max_iter || !isfinite(mu) || !isfinite(rpmax) || !isfinite(rdmax) ||
-        mu <= 1e-6 * A.tol * A.tol) {
+    // mu far below the tolerance: the active set is settled, and from here the normal
+    // equations lose accuracy (weights ~ 1/mu), so stop and leave the last digits to the polish
+    // step; the iterate counts as solved if it is primal feasible with a near-zero dual
+    // residual, else only a verified polish can answer
+    if (mu <= 1e-3 * A.tol) {
+      status = (rpmax <= tol_p && rdmax <= 1e3 * tol_d) ? 0 : CCMPC_QP_MAXITER;
+      break;
+    }
+    // complementarity growing without bound: no interior solution (infeasible), no polish
+    if (mu > 1e6 * fmax(mu0, 1.0)) {
+      status = CCMPC_QP_MAXITER;
+      infeasible = true;
+      break;
+    }
+    if (it == A.max_iter || !isfinite(mu) || !isfinite(rpmax) || !isfinite(rdmax)) {
       status = CCMPC_QP_MAXITER;
       break;
     }
+    QP_MARK(2);
     // ---- I3: Cholesky on wave 0 (left-looking, lane = row) ---------------------------------
     // Near the solution the active rows' weights lambda/s grow without bound, and a pivot of
     // the (mathematically positive definite) M can come out <= 0 after cancellation against
@@ -622,7 +735,20 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     // interior point codes): that direction's component of dz becomes 0, which is what the
     // huge weight enforces anyway.
     if (w == 0) {
-      const bool fail = wave_cholesky(M, n, ldm, dinv, true);
+      bool fail;
+      if constexpr (NM > 0) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+          La[k] = (k < n && lane < n && k <= lane) ? M[lane * ldm + k] : 0.0;
+        fail = reg_cholesky(La, n, Ldl);
+        // L overwrites M's lower triangle (read by the L^T solves)
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+          if (k < n && lane < n && k <= lane) M[lane * ldm + k] = La[k];
+        wave_sync();
+      } else {
+        fail = wave_cholesky(M, n, ldm, dinv, true);
+      }
       if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
     }
     __syncthreads();
@@ -633,11 +759,16 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     // triangular solves on wave 0: L L^T x = rhs (rhs in registers, lane = row)
     auto chol_solve = [&](double *x) {
       if (w != 0) return;
-      double b[2];
-      wave_load2(x, n, b);
-      wave_forward(M, n, ldm, dinv, b);
-      wave_backward(M, n, ldm, dinv, b);
-      wave_store2(x, n, b);
+      if constexpr (NM > 0) {
+        const double b = reg_solve(La, M, ldm, Ldl, n, lane < n ? x[lane] : 0.0);
+        if (lane < n) x[lane] = b;
+      } else {
+        double b[2];
+        wave_load2(x, n, b);
+        wave_forward(M, n, ldm, dinv, b);
+        wave_backward(M, n, ldm, dinv, b);
+        wave_store2(x, n, b);
+      }
     };
     auto gs_times_dz = [&]() {
       for (int k = tid; k < T3; k += kQpThreads) {
@@ -646,47 +777,6 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
         yd[k] = v;
       }
       __syncthreads();
-    };
-    // One step of iterative refinement with the product M dz taken from its structure.  The
-    // assembled M carries the weights lambda/s of the active rows, which grow like 1/mu, and
-    // the backward error of its Cholesky grows with them; the structured residual only sees
-    // w_r (a_r . yd_t), which stays small for those rows, so the step recovers the accuracy
-    // the dual residual needs once mu is small.
-    auto refine = [&]() {
-      for (int t = w; t < T; t += kQpWaves) {
-        double p0 = 0.0, p1 = 0.0;
-        const int64_t cnt = step_count(t);
-        const double yx = yd[3 * t], yy = yd[3 * t + 1];
-        for (int64_t i = lane; i < cnt; i += 64) {
-          const int64_t o = step_rows(t, i);
-          const int64_t r = nbox + nv + o;
-          const double a0 = rw.a0[o], a1 = rw.a1[o];
-          const double wa = rw.l[r] / rw.s[r] * (a0 * yx + a1 * yy);
-          p0 += wa * a0;
-          p1 += wa * a1;
-        }
-        p0 = wave_sum(p0);
-        p1 = wave_sum(p1);
-        if (lane == 0) {
-          const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
-          q[3 * t] = wp * yx + p0;
-          q[3 * t + 1] = wp * yy + p1;
-          q[3 * t + 2] = bw[4 * t + 3] * yd[3 * t + 2];
-        }
-      }
-      __syncthreads();
-      for (int j = tid; j < n; j += kQpThreads) {
-        double v = rh[j] - hctrl_mul(dz, j, T, order, p) -
-                   (rw.l[2 * j] / rw.s[2 * j] + rw.l[2 * j + 1] / rw.s[2 * j + 1]) * dz[j];
-        for (int k = 0; k < T3; ++k) v -= Gs[k * n + j] * q[k];
-        e2[j] = v;
-      }
-      __syncthreads();
-      chol_solve(e2);
-      __syncthreads();
-      for (int j = tid; j < n; j += kQpThreads) dz[j] += e2[j];
-      __syncthreads();
-      gs_times_dz();
     };
     // rhs = -r_d - G^T u with u_r given per row; q (output space) and dz (rhs) staged in LDS
     auto build_rhs = [&](auto urow) {
@@ -713,19 +803,19 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
         double v = -rd[j] - (urow(2 * j) - urow(2 * j + 1));
         for (int k = 0; k < T3; ++k) v -= Gs[k * n + j] * q[k];
         dz[j] = v;
-        rh[j] = v;
       }
       __syncthreads();
       chol_solve(dz);
       __syncthreads();
       gs_times_dz();
-      refine();
     };
+    QP_MARK(3);
     // ---- predictor (affine scaling): r_c = s l  ->  u = w r_p - l ---------------------------
     build_rhs([&](int64_t r) {
       const double rp = row_g(r, y, z) + rw.s[r];
       return rw.l[r] / rw.s[r] * rp - rw.l[r];
     });
+    QP_MARK(4);
     double amax = 1.0;
     for (int64_t r = tid; r < mrows; r += kQpThreads) {
       const double s = rw.s[r], l = rw.l[r];
@@ -742,6 +832,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       slaff += (rw.s[r] + aaff * rw.ds[r]) * (rw.l[r] + aaff * rw.dl[r]);
     const double muaff = block_sum(slaff, red) / static_cast<double>(mrows);
     const double sr = muaff / mu, sigma = sr * sr * sr;
+    QP_MARK(5);
     // ---- corrector: r_c = s l + ds_aff dl_aff - sigma mu;  u = w r_p - r_c / s ----------
     auto rc_of = [&](int64_t r) {
       return rw.s[r] * rw.l[r] + rw.ds[r] * rw.dl[r] - sigma * mu;
@@ -750,6 +841,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       const double rp = row_g(r, y, z) + rw.s[r];
       return rw.l[r] / rw.s[r] * rp - rc_of(r) / rw.s[r];
     });
+    QP_MARK(6);
     amax = 1e300;
     for (int64_t r = tid; r < mrows; r += kQpThreads) {
       const double s = rw.s[r], l = rw.l[r];
@@ -762,9 +854,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       if (dl < 0.0) amax = fmin(amax, -l / dl);
     }
     const double alpha = fmin(1.0, 0.995 * block_min(amax, red));
-#ifdef CCMPC_QP_TRACE
-    if (tid == 0 && sc == 0) printf("   aaff %.3e sigma %.3e alpha %.3e\n", aaff, sigma, alpha);
-#endif
+
     for (int j = tid; j < n; j += kQpThreads) z[j] += alpha * dz[j];
     for (int k = tid; k < T3; k += kQpThreads) y[k] += alpha * yd[k];
     for (int64_t r = tid; r < mrows; r += kQpThreads) {
@@ -772,6 +862,15 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       rw.l[r] += alpha * rw.dl[r];
     }
     __syncthreads();
+#ifdef CCMPC_QP_TRACE
+    QP_MARK(7);
+    if (tid == 0 && sc == 0)
+      printf("qp it %d rp %.3e rd %.3e mu %.3e alpha %.3e\n   t(10ns) I1 %d I2 %d chol %d "
+             "pred_rhs %d pred_step %d corr_rhs %d corr_step %d\n", it, tr_rp, tr_rd, mu, alpha,
+             int(tmark[1] - tmark[0]), int(tmark[2] - tmark[1]), int(tmark[3] - tmark[2]),
+             int(tmark[4] - tmark[3]), int(tmark[5] - tmark[4]), int(tmark[6] - tmark[5]),
+             int(tmark[7] - tmark[6]));
+#endif
   }
 
   // ---- polish: the equality-constrained QP on the IPM's active set ---------------------------
@@ -782,7 +881,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
   // problem itself.  The result is kept only if it is a verified KKT point: every row within
   // tol_p and lambda >= -tol_d (stationarity holds by construction), which also makes a
   // stalled IPM's answer exact and leaves infeasible problems reported as such.
-  if (A.polish) {
+  if (A.polish && !infeasible) {
     double *Wm = lds + lay.pw, *Sm = lds + lay.ps, *act = lds + lay.pact,
            *sdinv = lds + lay.pdinv;
     double *fu = lds + lay.f, *y0 = rh, *rs = e2, *lam = q, *zp = dz, *yp = yd;
@@ -820,107 +919,135 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       na = tot;
       __syncthreads();
     }
-    if (na <= n) {  // more active rows than controls: degenerate, keep the IPM's answer
-      if (w == 0) {
-        const bool fail = wave_cholesky(M, n, ldm, dinv, false);
+    // factor H once; y0 = -L^{-1} f
+    if (w == 0) {
+      const bool fail = wave_cholesky(M, n, ldm, dinv, false);
+      double b[2];
+      wave_load2(fu, n, b);
+      b[0] = -b[0];
+      b[1] = -b[1];
+      wave_forward(M, n, ldm, dinv, b);
+      wave_store2(y0, n, b);
+      if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    const bool h_ok = red[8 * kQpWaves - 1] == 0.0;
+    if (!h_ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
+    // up to 4 rounds of active-set correction, as the oracle's polish does: drop rows whose
+    // multiplier comes out negative, else add the most violated row
+    for (int round = 0; h_ok && round < 4 && na <= n; ++round) {
+      // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
+      for (int a = w; a < na; a += kQpWaves) {
+        const int64_t r = static_cast<int64_t>(act[a]);
         double b[2];
-        wave_load2(fu, n, b);
-        b[0] = -b[0];
-        b[1] = -b[1];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = lane + 64 * h;
+          double g = 0.0;
+          if (j < n) {
+            if (r < nbox) {
+              g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
+            } else if (r < nbox + nv) {
+              const int t = static_cast<int>((r - nbox) >> 1);
+              g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
+            } else {
+              // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
+              const int64_t o = r - nbox - nv;
+              const int t = obst_step(o);
+              g = rw.a0[o] * Gs[(3 * t) * n + j] + rw.a1[o] * Gs[(3 * t + 1) * n + j];
+            }
+          }
+          b[h] = g;
+        }
         wave_forward(M, n, ldm, dinv, b);
-        wave_store2(y0, n, b);
+        wave_store2(Wm + a * n, n, b);
+        double d = 0.0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (lane + 64 * h < n) d += b[h] * y0[lane + 64 * h];
+        d = wave_sum(d);
+        if (lane == 0) rs[a] = d + row_const(r);
+      }
+      __syncthreads();
+      for (int e = tid; e < na * na; e += kQpThreads) {
+        const int i = e / na, j = e % na;
+        if (j > i) continue;
+        double v = 0.0;
+        for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
+        Sm[i * ldm + j] = v;
+      }
+      __syncthreads();
+      if (w == 0) {
+        const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
+        double b[2];
+        if (!fail) {
+          wave_load2(rs, na, b);
+          wave_forward(Sm, na, ldm, sdinv, b);
+          wave_backward(Sm, na, ldm, sdinv, b);
+          wave_store2(lam, na, b);
+        }
         if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
       }
       __syncthreads();
-      bool ok = red[8 * kQpWaves - 1] == 0.0;
-      if (!ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
-      if (ok) {
-        // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
-        for (int a = w; a < na; a += kQpWaves) {
-          const int64_t r = static_cast<int64_t>(act[a]);
-          double b[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int j = lane + 64 * h;
-            double g = 0.0;
-            if (j < n) {
-              if (r < nbox) {
-                g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
-              } else if (r < nbox + nv) {
-                const int t = static_cast<int>((r - nbox) >> 1);
-                g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
-              } else {
-                // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
-                const int64_t o = r - nbox - nv;
-                const int t = obst_step(o);
-                g = rw.a0[o] * Gs[(3 * t) * n + j] + rw.a1[o] * Gs[(3 * t + 1) * n + j];
-              }
-            }
-            b[h] = g;
-          }
-          wave_forward(M, n, ldm, dinv, b);
-          wave_store2(Wm + a * n, n, b);
-          double d = 0.0;
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            if (lane + 64 * h < n) d += b[h] * y0[lane + 64 * h];
-          d = wave_sum(d);
-          if (lane == 0) rs[a] = d + row_const(r);
-        }
-        __syncthreads();
-        for (int e = tid; e < na * na; e += kQpThreads) {
-          const int i = e / na, j = e % na;
-          if (j > i) continue;
-          double v = 0.0;
-          for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
-          Sm[i * ldm + j] = v;
-        }
-        __syncthreads();
-        if (w == 0) {
-          const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
-          double b[2];
-          if (!fail) {
-            wave_load2(rs, na, b);
-            wave_forward(Sm, na, ldm, sdinv, b);
-            wave_backward(Sm, na, ldm, sdinv, b);
-            wave_store2(lam, na, b);
-          }
-          if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
-        }
-        __syncthreads();
-        ok = red[8 * kQpWaves - 1] == 0.0;
+      if (red[8 * kQpWaves - 1] != 0.0) break;  // dependent active rows
+      // z = L^{-T}(y0 - W^T lambda)
+      for (int j = tid; j < n; j += kQpThreads) {
+        double v = y0[j];
+        for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
+        zp[j] = v;
       }
-      if (ok) {
-        // z = L^{-T}(y0 - W^T lambda)
-        for (int j = tid; j < n; j += kQpThreads) {
-          double v = y0[j];
-          for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
-          zp[j] = v;
-        }
-        __syncthreads();
-        if (w == 0) {
-          double b[2];
-          wave_load2(zp, n, b);
-          wave_backward(M, n, ldm, dinv, b);
-          wave_store2(zp, n, b);
-        }
-        __syncthreads();
-        for (int k = tid; k < T3; k += kQpThreads) {
-          double v = 0.0;
-          for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
-          yp[k] = v;
-        }
-        __syncthreads();
-        double viol = 0.0, lneg = 0.0;
-        for (int64_t r = tid; r < mrows; r += kQpThreads) viol = fmax(viol, row_g(r, yp, zp));
-        for (int a = tid; a < na; a += kQpThreads) lneg = fmax(lneg, -lam[a]);
-        block_max2(viol, lneg, red);
-        if (viol <= tol_p && lneg <= tol_d && isfinite(viol) && isfinite(lneg)) {
-          for (int j = tid; j < n; j += kQpThreads) z[j] = zp[j];
-          status = 0;
-        }
-        __syncthreads();
+      __syncthreads();
+      if (w == 0) {
+        double b[2];
+        wave_load2(zp, n, b);
+        wave_backward(M, n, ldm, dinv, b);
+        wave_store2(zp, n, b);
       }
+      __syncthreads();
+      for (int k = tid; k < T3; k += kQpThreads) {
+        double v = 0.0;
+        for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
+        yp[k] = v;
+      }
+      __syncthreads();
+      double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
+      for (int64_t r = tid; r < mrows; r += kQpThreads) {
+        const double g = row_g(r, yp, zp);
+        if (!isfinite(g)) bad = 1.0;
+        if (g > viol) {
+          viol = g;
+          vrow = static_cast<double>(r);
+        }
+      }
+      for (int a = tid; a < na; a += kQpThreads) {
+        if (!isfinite(lam[a])) bad = 1.0;
+        lneg = fmax(lneg, -lam[a]);
+      }
+      block_argmax(viol, vrow, red);
+      block_max2(lneg, bad, red);
+      if (bad != 0.0) break;
+      if (viol <= tol_p && lneg <= tol_d) {
+        for (int j = tid; j < n; j += kQpThreads) z[j] = zp[j];
+        status = 0;
+        __syncthreads();
+        break;
+      }
+      // next active set (thread 0; na <= n entries)
+      if (tid == 0) {
+        int m2 = 0;
+        if (lneg > tol_d) {
+          for (int a = 0; a < na; ++a)
+            if (lam[a] >= -tol_d) act[m2++] = act[a];
+        } else {
+          m2 = na;
+          if (na < n) act[m2++] = vrow;
+          else m2 = n + 1;  // nowhere to add: give up
+        }
+        red[8 * kQpWaves - 2] = static_cast<double>(m2);
+      }
+      __syncthreads();
+      na = static_cast<int>(red[8 * kQpWaves - 2]);
+      __syncthreads();
     }
   }
 
@@ -981,6 +1108,15 @@ inline QpPlan qp_plan(int T, int64_t R) {
   if (qp_fits(T, R, false, true)) return {false, true};
   if (qp_fits(T, R, true, false)) return {true, false};
   return {false, false};
+}
+
+template <bool ROWS_LDS, int NM>
+void launch_qp(dim3 grid, dim3 block, size_t lds, hipStream_t s, const QpArgs &a) {
+  static const bool attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kQpLdsBytes)) == hipSuccess;
+  (void)attr;
+  hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM>), grid, block, lds, s, a);
 }
 
 }  // namespace ccmpc
@@ -1073,26 +1209,18 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   a.out_iter = out_iter;
   const size_t lds = static_cast<size_t>(QpLayout(Ti, in_lds ? R : 0, in_lds, plan.polish).total) *
                      sizeof(double);
+  CCMPC_REQUIRE(lds <= kQpLdsBytes, "T too large for the LDS image");
+  const int n = 2 * Ti;
+  // register-resident factor up to n = 16 (T <= 8, the reference's ph); larger n spills
+  const int nm = n <= 16 ? 16 : 0;
+  const dim3 grid(static_cast<unsigned>(n_scenes)), block(kQpThreads);
   hipStream_t s = as_stream(stream);
   if (in_lds) {
-    static bool attr = [] {
-      return hipFuncSetAttribute(reinterpret_cast<const void *>(mpc_qp_kernel<true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 static_cast<int>(kQpLdsBytes)) == hipSuccess;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL(mpc_qp_kernel<true>, dim3(static_cast<unsigned>(n_scenes)),
-                       dim3(kQpThreads), lds, s, a);
+    if (nm == 16) launch_qp<true, 16>(grid, block, lds, s, a);
+    else launch_qp<true, 0>(grid, block, lds, s, a);
   } else {
-    CCMPC_REQUIRE(lds <= kQpLdsBytes, "T too large for the LDS image");
-    static bool attr = [] {
-      return hipFuncSetAttribute(reinterpret_cast<const void *>(mpc_qp_kernel<false>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 static_cast<int>(kQpLdsBytes)) == hipSuccess;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL(mpc_qp_kernel<false>, dim3(static_cast<unsigned>(n_scenes)),
-                       dim3(kQpThreads), lds, s, a);
+    if (nm == 16) launch_qp<false, 16>(grid, block, lds, s, a);
+    else launch_qp<false, 0>(grid, block, lds, s, a);
   }
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;

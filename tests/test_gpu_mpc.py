@@ -209,3 +209,27 @@ def test_qp_leaves_out_failed_records_and_flags_them(gpu):
     want = _oracle_solve(x0s[0], T, goals[0], refs[0], want_rows, "halfspace", prm)
     _check(u[0].cpu().numpy(), X[0].cpu().numpy(), float(cost[0]), want, T)
     assert h["status"][first_obstacle] == 0  # (the host copy taken before the edit)
+
+
+def test_qp_feasibility_and_solution_agree_with_oracle_on_many_scenes(gpu):
+    """32 more crossing scenes in one launch: the GPU solves exactly the scenes the oracle finds
+    feasible (HiGHS phase 1), to the oracle's KKT-certified minimiser, and reports the rest."""
+    T = 8
+    seeds = list(range(100, 132))
+    rec, cps, o_recs, refs, goals, x0s = _scene_inputs(seeds, T, gpu)
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    qp = mpc.PlanningQP(cps, T)
+    u, X, cost, status, _ = qp.solve(gamma, xbar, torch.as_tensor(goals, device=gpu),
+                                     torch.as_tensor(refs, device=gpu), rec)
+    u, X, cost, status = u.cpu().numpy(), X.cpu().numpy(), cost.cpu().numpy(), status.cpu().numpy()
+    prm = _params_dict(mpc.MPCParams.reference_defaults())
+    n_feas = 0
+    for i, s in enumerate(seeds):
+        want = _oracle_solve(x0s[i], T, goals[i], refs[i], o_recs[i], "halfspace", prm)
+        if not want["feasible"]:
+            assert status[i] == mpc.QP_MAXITER, (s, status[i])
+            continue
+        n_feas += 1
+        assert status[i] == mpc.QP_OK, (s, status[i])
+        _check(u[i], X[i], cost[i], want, T)
+    assert 4 <= n_feas <= 28   # both outcomes are exercised
