@@ -286,14 +286,15 @@ def episode_c1(dev, cpu_steps=2, with_cpu=True):
     log = rep.run()
     out = {"config": "C1 schedule: 1 OV, np=5000, ph=8, n_ideal=1e6, 8 shrinking + 4 receding "
                      "planning steps (synthetic GMM predictions)",
-           "steps": [{k: (round(v, 3) if k == "ms" else v) for k, v in st.items()}
+           "steps": [{k: (round(v, 3) if k in ("ms", "qp_ms") else v) for k, v in st.items()}
                      for st in log],
-           "total_ms": round(sum(st["ms"] for st in log), 3)}
+           "total_ms": round(sum(st["ms"] for st in log), 3),
+           "total_qp_ms": round(sum(st.get("qp_ms", 0.0) for st in log), 3)}
     if not with_cpu:
         return out
     from oracle import ccmpc_oracle as orc
     rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=1_000_000, receding_steps=0,
-                                device=dev)
+                                device=dev, with_qp=False)
     cpu = []
     mom = None
     for frame, T, kind in rep.schedule()[:cpu_steps]:

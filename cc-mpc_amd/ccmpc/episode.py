@@ -9,10 +9,14 @@ chance constraints:
                    predict_ideal (1e6 samples)
   receding phase   every later planning frame: the GMM-affine generator at Tsh = ph
 
-The CARLA world, the learned Trajectron++ encoder/decoder and the CPLEX QP are outside this
-path; the replay feeds the GPU sampler synthetic per-OV GMM action parameters (SURVEY.md 8d
-generator) and stops at the constraint records, timing each planning step end to end
-(sampler -> bucketing -> one fused launch -> host HalfSpace objects).
+The CARLA world and the learned Trajectron++ encoder/decoder are outside this path; the replay
+feeds the GPU sampler synthetic per-OV GMM action parameters (SURVEY.md 8d generator) and times
+each planning step end to end (sampler -> bucketing -> one fused launch -> host HalfSpace
+objects -> the QP on the device records, do_highlevel_control :2850-3110).  The ego is not
+simulated: each step plans from a synthetic state on the reference trajectory, and the
+shrinking steps pass the first control of every earlier step as the executed controls
+(U_prev, :3186).  An infeasible QP is logged (the reference raises InSimulationException and
+the episode ends; the replay continues with a zero control for that step).
 """
 import time
 
@@ -50,8 +54,10 @@ def synthetic_gmm(O, L=25, T=8, seed=20251015):
 
 class EpisodeReplay:
     def __init__(self, O=1, N=5000, ph=8, n_ideal=1_000_000, receding_steps=4, seed=0,
-                 device="cuda"):
+                 device="cuda", with_qp=True):
         self.O, self.N, self.ph = O, N, ph
+        self.with_qp = with_qp
+        self.u_prev = []
         self.device = engine.require_device(device)
         self.receding_steps = receding_steps
         self.seed = seed
@@ -73,6 +79,28 @@ class EpisodeReplay:
                                           seed=self.seed * 7919 + frame, device=self.device)
         return ovehicle.make_ovehicles(store, z, self.pmf, self.minpos, self.pasts,
                                        device=self.device)
+
+    def x_init(self, frame):
+        """Synthetic ego state [x, y, psi, v] at the start of the reference trajectory."""
+        ego = self.ref_traj(frame)[0] - np.array([4.0, 0.5])
+        return np.array([ego[0], ego[1], np.arctan2(0.5, 4.0), 8.0])
+
+    def plan(self, frame, T):
+        """The planning step's QP on the generator's device records."""
+        ref = self.ref_traj(frame)
+        if T == self.ph:
+            self.u_prev = []
+        up = np.concatenate(self.u_prev) if self.u_prev else None
+        try:
+            res = self.agent.solve_planning_qp(self.x_init(frame), ref[-1] + [4.0, 0.5], ref,
+                                               T, u_prev=up)
+        except planner.InSimulationException:
+            # the reference's episode ends here; the replay goes on timing the schedule with a
+            # zero control standing in for the step that was not planned
+            self.u_prev.append(np.zeros(2))
+            return None
+        self.u_prev.append(res["u"][:2])      # U_star.T.ravel()[:nu] (:3186)
+        return res
 
     def schedule(self):
         """(frame, Tsh, generator) of every planning step of the episode."""
@@ -101,7 +129,13 @@ class EpisodeReplay:
             ovs, out = self.step(frame, T, kind)
             if sync:
                 torch.cuda.synchronize(self.device)
-            log.append({"frame": frame, "T": T, "generator": kind,
-                        "K": [ov.n_states for ov in ovs], "constraints": len(out[0]),
-                        "ms": (time.perf_counter() - t0) * 1e3})
+            t1 = time.perf_counter()
+            entry = {"frame": frame, "T": T, "generator": kind,
+                     "K": [ov.n_states for ov in ovs], "constraints": len(out[0]),
+                     "ms": (t1 - t0) * 1e3}
+            if self.with_qp:
+                res = self.plan(frame, T)
+                entry["qp_ms"] = (time.perf_counter() - t1) * 1e3
+                entry["qp"] = "infeasible" if res is None else "solved"
+            log.append(entry)
         return log

@@ -29,8 +29,12 @@ import numpy as np
 import scipy.stats
 import torch
 
-from . import engine, risk
+from . import engine, mpc, risk
 from .ovehicle import OVehicle, ScenePredictions
+
+
+class InSimulationException(Exception):
+    """collect/exception.py:11: the planner's failure (an infeasible QP, :3099-3110)."""
 
 
 class HalfSpace:
@@ -222,6 +226,10 @@ class MidlevelAgent:
         self._ws = engine.Workspace(self.device)
         self.prob_lower_save = None
         self.last_records = None
+        self._last_rec = None              # (device records, kind, T) of the last generator
+        self.mpc_params = mpc.MPCParams.reference_defaults()
+        self._ltv = None                   # (x_init, T_full) -> (xbar, Gamma), first step's
+        self._qp = {}
 
     # ------------------------------------------------------------------------------------
     def _scene(self, ovehicles):
@@ -355,6 +363,7 @@ class MidlevelAgent:
         self._moments[params.frame] = (mean, cov, list(K), T)
         h = engine.halfspaces(rec)
         self.last_records = h
+        self._last_rec = (rec, mpc.REC_HALFSPACE, T)
         constraints = self._records_to_halfspaces(h, scene, T)
         pl_h = pl.cpu().numpy()
         if T == ph:
@@ -381,8 +390,10 @@ class MidlevelAgent:
         mean, cov = engine.moments(scene.store, workspace=self._ws)
         if T != scene.T:
             raise ValueError("the affine generator runs on the prediction horizon's particles")
-        h = engine.affine_records(engine.affine(mean, cov, ref, gamma, R=self.R))
+        rec = engine.affine(mean, cov, ref, gamma, R=self.R)
+        h = engine.affine_records(rec)
         self.last_records = h
+        self._last_rec = (rec, mpc.REC_AFFINE, T)
         cons = []
         for c, (o, k) in enumerate(scene.cell_of):
             for t in range(T):
@@ -447,6 +458,7 @@ class MidlevelAgent:
                                   scaled=scaled)
         h = engine.affine_records(rec)
         self.last_records = h
+        self._last_rec = (rec, mpc.REC_AFFINE, T)
         cons = []
         O, maxK = scene.O, max(K)
         mean_p0p1 = _object_grid(O, maxK, T)
@@ -475,6 +487,45 @@ class MidlevelAgent:
         vertices, A_union, b_union = self._l4_lists(scene)
         return (cons, vertices, A_union, b_union, self._ov_in_junction(scene, mean0),
                 _object_grid(scene.O), st_mean, st_cov, meanNtangent)
+
+    def solve_planning_qp(self, x_init, goal, ref_traj, Tsh, u_prev=None, lon=3.7,
+                          u_order=mpc.U_ORDER_F):
+        """do_highlevel_control's QP (:2850-3043) on the device, on the records of the last
+        generator call (read in place, never copied to the host).  The LTV model is the one of
+        the first shrinking step (the reference keeps its Gamma/x_bar across T < ph steps,
+        :2858-2891): it is recomputed when Tsh == ph and reused, sliced, below it, with u_prev
+        the executed controls (the reference's U_prev, :3186).  Returns the reference's
+        ctrl_result fields {cost, U_star (T, 2), X_star (T, 4), goal, u}; raises
+        InSimulationException where CPLEX fails (:3099-3110)."""
+        if self._last_rec is None:
+            raise RuntimeError("no constraint records: call a generator first")
+        rec, kind, T = self._last_rec
+        if int(Tsh) != T:
+            raise ValueError(f"records are for T = {T}, not Tsh = {Tsh}")
+        ph = self.prediction_horizon
+        if T == ph or self._ltv is None:
+            self._ltv = mpc.ltv(np.asarray(x_init, np.float64)[None], ph, Ts=0.5, lon=lon)
+        xbar, gamma = self._ltv
+        key = (rec.shape[0], T, kind, u_order)
+        qp = self._qp.get(key)
+        if qp is None:
+            qp = mpc.PlanningQP([rec.shape[0]], T, T_full=ph, kind=kind,
+                                params=self.mpc_params, u_order=u_order, device=self.device)
+            self._qp[key] = qp
+        dev = self.device
+        ref = torch.as_tensor(np.asarray(ref_traj, np.float64)[None, :T], device=dev)
+        goal_t = torch.as_tensor(np.asarray(goal, np.float64).reshape(1, 2), device=dev)
+        up = None
+        if T < ph:
+            up = torch.as_tensor(np.asarray(u_prev, np.float64).reshape(1, 2 * (ph - T)),
+                                 device=dev)
+        u, X, cost, status, _ = qp.solve(gamma, xbar, goal_t, ref, rec, u_prev=up)
+        st = int(status[0])
+        if st & (mpc.QP_MAXITER | mpc.QP_NUMERIC):
+            raise InSimulationException("Optimizer failed to find a solution")
+        return {"cost": float(cost[0]), "U_star": qp.U(u)[0].cpu().numpy(),
+                "X_star": X[0].cpu().numpy(), "goal": np.asarray(goal, np.float64),
+                "u": u[0].cpu().numpy(), "skipped_rows": bool(st & mpc.QP_SKIPPED_ROWS)}
 
     def _loaded_tangents(self, loaded, mean, K, T, x_init, ref):
         """The previous frame's slopes / tangent indices for every (cell, t) of this frame

@@ -61,3 +61,52 @@ def test_episode_timing_log(gpu):
     assert [s["T"] for s in log] == [8, 7, 6, 5, 4, 3, 2, 1, 8, 8]
     assert all(s["ms"] > 0 for s in log)
     assert log[-1]["generator"] == "affine"
+
+
+def test_episode_planning_qp_matches_oracle_chain(gpu):
+    """The caller's QP at every planning step of the schedule (do_highlevel_control
+    :2850-3110): the first step's LTV model, sliced with the executed controls U_prev at
+    Tsh < ph (:2858-2891, :3186), on the generator's device records; against the oracle's QP on
+    the oracle's records (same particles, same Philox draws)."""
+    from ccmpc import episode, mpc
+    from oracle import mpc_oracle as mo
+    n_ideal, seed = 20_000, 3
+    rep = episode.EpisodeReplay(O=2, N=3000, ph=8, n_ideal=n_ideal, receding_steps=2,
+                                seed=seed, device=gpu)
+    prm = mpc.MPCParams.reference_defaults().as_dict()
+    mom, model, n_solved = None, None, 0
+    for frame, T, kind in rep.schedule():
+        ovs, out = rep.step(frame, T, kind)
+        K = [ov.n_states for ov in ovs]
+        oracle_ovs = _oracle_ovs(ovs, rep.ph)
+        ref = rep.ref_traj(frame)
+        if kind == "affine":
+            want_rec = orc.affine_generator(oracle_ovs, T, rep.ph, ref, with_l4=False)["records"]
+        elif T == rep.ph:
+            want_rec = orc.minkowski_generator(oracle_ovs, T, rep.ph, ref, with_l4=False)["records"]
+            mom = orc.save_moments([ov.pred_positions for ov in oracle_ovs], T)
+        else:
+            ideal = orc.predict_ideal(mom, K, T, n_ideal, seed=seed * 1_000_003 + frame)
+            want_rec = orc.minkowski_generator(oracle_ovs, T, rep.ph, ref, ideal_trajs=ideal,
+                                               with_l4=False)["records"]
+            mom = orc.save_moments([[ideal[o][k] for k in range(K[o])]
+                                    for o in range(len(K))], T)
+        if T == rep.ph:
+            xb, _, G, _, _ = mo.VehicleModel(rep.ph, 0.5, 1.85, 3.7).get_optimization_ltv(
+                rep.x_init(frame), np.zeros(2))
+            model = (xb, G)
+        u_prev = np.concatenate(rep.u_prev) if (T < rep.ph and rep.u_prev) else None
+        got = rep.plan(frame, T)
+        want = mo.solve_step(model[1], model[0], T, rep.ph, ref[-1] + [4.0, 0.5], ref[:T],
+                             want_rec, "affine" if kind == "affine" else "halfspace", prm,
+                             u_prev=u_prev)
+        if not want["feasible"]:
+            assert got is None, (frame, T)
+            break                       # the reference's episode ends here
+        assert got is not None, (frame, T)
+        tol = 1e-6 * (1 + np.abs(want["u"]).max())
+        assert np.abs(got["u"] - want["u"]).max() <= tol, (frame, T)
+        np.testing.assert_allclose(got["X_star"], want["X"], rtol=0,
+                                   atol=1e-6 * (1 + np.abs(want["X"]).max()))
+        n_solved += 1
+    assert n_solved >= 3
