@@ -140,7 +140,7 @@ struct QpLayout {
     }
     rows = o;
     const int64_t mrows = 2 * n + 2 * T + R;
-    if (rows_lds) o += static_cast<int>(4 * mrows + 3 * R);
+    if (rows_lds) o += static_cast<int>(4 * mrows + 4 * R);
     total = o;
   }
 };
@@ -150,9 +150,10 @@ __host__ __device__ inline int64_t qp_rows_per_cell(int T, int kind) {
 }
 
 // row store: s, l, ds, dl over all m rows (box 2n, speed 2T, obstacle R), then the obstacle
-// rows' a0, a1, b' (b' = b - a . c_xy, the constant part of the state moved to the right)
+// rows' a0, a1, b' (b' = b - a . c_xy, the constant part of the state moved to the right) and
+// step t (as a double; a lookup instead of re-deriving it from the row index)
 struct Rows {
-  double *s, *l, *ds, *dl, *a0, *a1, *b;
+  double *s, *l, *ds, *dl, *a0, *a1, *b, *t;
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -352,7 +353,14 @@ __device__ __forceinline__ bool reg_cholesky(double (&a)[NM], int n, double &dl)
       const double ajj = lane_bcast(diag0, j);
       fail = fail || !isfinite(d) || !isfinite(ajj);
       if (!(d > 1e-30 * ajj)) d = 1e128;
-      const double ljj = sqrt(d), inv = 1.0 / ljj;
+      // sqrt and 1/sqrt from the hardware rsqrt + one Goldschmidt step (~1 ulp; the IPM's
+      // factor needs no IEEE rounding, the polish recomputes the answer from H exactly)
+      const double y = __builtin_amdgcn_rsq(d);
+      double g = d * y, h = 0.5 * y;
+      const double rr = fma(-g, h, 0.5);
+      g = fma(g, rr, g);
+      h = fma(h, rr, h);
+      const double ljj = g, inv = 2.0 * h;
       const double lij = lane > j ? a[j] * inv : (lane == j ? ljj : 0.0);
       a[j] = lij;
       if (lane == j) dl = inv;
@@ -461,10 +469,20 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     rbase = lds + lay.rows;
   } else {
     const int64_t mcap = 2 * n + 2 * T + A.max_cells * P;
-    rbase = A.ws + sc * (4 * mcap + 3 * A.max_cells * P);
+    rbase = A.ws + sc * (4 * mcap + 4 * A.max_cells * P);
   }
   const Rows rw{rbase, rbase + mrows, rbase + 2 * mrows, rbase + 3 * mrows, rbase + 4 * mrows,
-                rbase + 4 * mrows + R, rbase + 4 * mrows + 2 * R};
+                rbase + 4 * mrows + R, rbase + 4 * mrows + 2 * R, rbase + 4 * mrows + 3 * R};
+  // step t of obstacle row o (records of a cell in (t, tau) order, or one per t for affine)
+  auto obst_step = [&](int64_t o) -> int {
+    const int64_t cell = o / P;
+    const int pp = static_cast<int>(o - cell * P);
+    if (A.rec_kind != CCMPC_REC_KIND_HALFSPACE) return pp;
+    int t = static_cast<int>((1.0f + sqrtf(1.0f + 8.0f * static_cast<float>(pp))) * 0.5f);
+    while (t * (t - 1) / 2 > pp) --t;
+    while ((t + 1) * t / 2 <= pp) ++t;
+    return t;
+  };
   const ccmpc_mpc_params &p = A.p;
   const int order = A.u_order;
   const int ncol = 2 * Tf;
@@ -547,6 +565,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     rw.a0[r] = a0;
     rw.a1[r] = a1;
     rw.b[r] = b;
+    rw.t[r] = static_cast<double>(obst_step(r));
     hmax = fmax(hmax, fabs(b));
   }
   __syncthreads();
@@ -558,16 +577,6 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     fmax_ = fmax(fmax_, fabs(v));
   }
   // initial point: z = 0 (inside the control box), s = max(-g(0), 1), lambda = 1
-  // step t of obstacle row o (records of a cell in (t, tau) order, or one per t for affine)
-  auto obst_step = [&](int64_t o) -> int {
-    const int64_t cell = o / P;
-    const int pp = static_cast<int>(o - cell * P);
-    if (A.rec_kind != CCMPC_REC_KIND_HALFSPACE) return pp;
-    int t = static_cast<int>((1.0f + sqrtf(1.0f + 8.0f * static_cast<float>(pp))) * 0.5f);
-    while (t * (t - 1) / 2 > pp) --t;
-    while ((t + 1) * t / 2 <= pp) ++t;
-    return t;
-  };
   // g(z) = row_lin(r, Gs z, z) + row_const(r): the linear part in the state's output rows
   // yy = Gs z (or in z itself for the control bounds), constants folded into b' and the bounds
   auto row_lin = [&](int64_t r, const double *yy, const double *zz) -> double {
@@ -580,7 +589,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       return ((r - nbox) & 1) ? -yy[3 * t + 2] : yy[3 * t + 2];
     }
     const int64_t o = r - nbox - nv;
-    const int t = obst_step(o);
+    const int t = static_cast<int>(rw.t[o]);
     return rw.a0[o] * yy[3 * t] + rw.a1[o] * yy[3 * t + 1];
   };
   auto row_const = [&](int64_t r) -> double {
@@ -953,7 +962,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
             } else {
               // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
               const int64_t o = r - nbox - nv;
-              const int t = obst_step(o);
+              const int t = static_cast<int>(rw.t[o]);
               g = rw.a0[o] * Gs[(3 * t) * n + j] + rw.a1[o] * Gs[(3 * t + 1) * n + j];
             }
           }
@@ -1144,7 +1153,7 @@ extern "C" size_t ccmpc_mpc_qp_workspace_bytes(int64_t n_scenes, int64_t T,
   const int64_t R = max_cells_per_scene * qp_rows_per_cell(static_cast<int>(T), rec_kind);
   if (qp_plan(static_cast<int>(T), R).rows_lds) return 16;  // rows live in LDS
   const int64_t m = 4 * T + 2 * T + R;
-  return static_cast<size_t>(n_scenes * (4 * m + 3 * R)) * sizeof(double) + 16;
+  return static_cast<size_t>(n_scenes * (4 * m + 4 * R)) * sizeof(double) + 16;
 }
 
 extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamma,
