@@ -9,7 +9,7 @@ import pytest
 
 from oracle import ccmpc_oracle as orc
 from oracle import mpc_oracle as mo
-from _qp_inputs import crossing_scene
+from _qp_inputs import crossing_scene, pick_seeds
 
 P = mo.DEFAULT_PARAMS
 
@@ -83,9 +83,10 @@ def test_order_f_pairs_u_t_with_u_t_plus_T():
     assert f_cost == pytest.approx(p["w_turning"]) and c_cost == pytest.approx(p["w_accel"])
 
 
-@pytest.mark.parametrize("seed", [1, 5, 9, 15])
-def test_oracle_solution_satisfies_kkt(seed):
+@pytest.mark.parametrize("i", range(4))
+def test_oracle_solution_satisfies_kkt(i):
     T = 8
+    seed = pick_seeds("binding", 4)[i]
     ovs, cells, K, ref, goal, x0 = crossing_scene(seed, T=T)
     out = orc.minkowski_generator(ovs, T, T, ref, with_l4=False)
     xbar, _, G, _, _ = mo.VehicleModel(T, 0.5, 1.85, 3.7).get_optimization_ltv(x0, np.zeros(2))
@@ -102,9 +103,10 @@ def test_oracle_solution_satisfies_kkt(seed):
             assert mo.objective_value(v, r["Gf"], r["c"], T, goal, ref, P) >= r["cost"] - 1e-9
 
 
-@pytest.mark.parametrize("seed", [0, 3])
-def test_infeasible_scenes_are_reported(seed):
+@pytest.mark.parametrize("i", range(2))
+def test_infeasible_scenes_are_reported(i):
     T = 8
+    seed = pick_seeds("infeasible", 2)[i]
     ovs, cells, K, ref, goal, x0 = crossing_scene(seed, T=T)
     out = orc.minkowski_generator(ovs, T, T, ref, with_l4=False)
     xbar, _, G, _, _ = mo.VehicleModel(T, 0.5, 1.85, 3.7).get_optimization_ltv(x0, np.zeros(2))
