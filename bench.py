@@ -362,6 +362,36 @@ def pcie_inclusive(cyc, step, dev, iters=200):
             "d2h_bytes": host_rec.numel()}
 
 
+def ellipsoid_parity(ovs, ref, T, h):
+    """The metric's second half (BASELINE.json: "ellipsoid ΔF-norm vs ref"): the timed cycle's
+    records against the oracle's restatement of v8ideal/__init__.py:881-947 on the same
+    particles (golden-pinned to makeconstraint.py) -- the largest relative Frobenius error of
+    the ellipsoid shapes Q and QR and of the centre, and whether record order, `which` and
+    `side` agree bit for bit.  Bar: 1e-5 relative (BASELINE.json)."""
+    import scipy.stats
+    from oracle import ccmpc_oracle as orc
+    chi_p = scipy.stats.chi2.ppf(orc.TARGET_P, df=2)
+    eps = (orc.EPS_TOTAL / len(ovs)) / T
+    chi_r = scipy.stats.chi2.ppf(1 - eps, df=2)
+    want = []
+    for cells in ovs:
+        for traj in cells:
+            want += orc.minkowski_cell(np.vstack(traj), T, T, ref, eps, chi_r, chi_p)[0]
+    dq = dqr = dc = 0.0
+    exact = len(want) == len(h)
+    for r, g in zip(want, h):
+        Q = np.array([[g["q00"], g["q01"]], [g["q01"], g["q11"]]])
+        QR = np.array([[g["r00"], g["r01"]], [g["r01"], g["r11"]]])
+        c = np.array([g["mean0"], g["mean1"]])
+        dq = max(dq, float(np.linalg.norm(Q - r["Q"]) / np.linalg.norm(r["Q"])))
+        dqr = max(dqr, float(np.linalg.norm(QR - r["QR"]) / np.linalg.norm(r["QR"])))
+        dc = max(dc, float(np.linalg.norm(c - r["mean"]) / np.linalg.norm(r["mean"])))
+        exact = exact and (int(g["which"]), int(g["side"]), int(g["t_tau"]) >> 16,
+                           int(g["t_tau"]) & 0xFFFF) == (r["which"], r["side"], r["t"], r["tau"])
+    return {"Q_rel_fro_max": dq, "QR_rel_fro_max": dqr, "centre_rel_max": dc,
+            "order_which_side_exact": bool(exact), "records": len(want), "bar": 1e-5}
+
+
 def main():
     args = parse()
     world, rank, local = init_dist(args)
@@ -447,6 +477,8 @@ def main():
             "moments_only_avg_launch_us": round(t_mom * 1e6, 3),
         },
     }
+    if rank == 0:
+        out["ellipsoid_parity"] = ellipsoid_parity(ovs, ref, args.T, h)
     if rank == 0 and world == 1 and not args.no_cpu:
         med, threads, n, total = cpu_baseline(ovs, ref, args.T, args.cpu_cycles)
         out["cpu_baseline"] = {
