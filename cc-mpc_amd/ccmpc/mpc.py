@@ -79,6 +79,7 @@ class PlanningQP:
         self.S = len(cells)
         self.max_cells = max(cells) if cells else 0
         off = np.concatenate(([0], np.cumsum(cells))).astype(np.int64)
+        self.n_cells = int(off[-1])
         self.scene_cell = torch.as_tensor(off, device=self.device)
         lib = _lib.load()
         need = lib.ccmpc_mpc_qp_workspace_bytes(self.S, self.T, self.max_cells, self.kind)
@@ -90,13 +91,40 @@ class PlanningQP:
         self.status = torch.empty(S, dtype=torch.int32, device=dev)
         self.iters = torch.empty(S, dtype=torch.int32, device=dev)
 
+    def _need(self, t, name, shape, dtype=torch.float64):
+        """The kernel reads raw pointers: refuse anything that is not the contiguous device
+        array it assumes (a wrong shape would read out of bounds on the GPU)."""
+        dev = self.device
+        on_dev = isinstance(t, torch.Tensor) and t.device.type == dev.type and (
+            dev.index is None or t.device.index == dev.index)
+        if not on_dev or t.dtype != dtype or not t.is_contiguous():
+            raise ValueError(f"{name}: contiguous {dtype} tensor on {self.device} required")
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+
     def solve(self, gamma, xbar, goal, ref, rec, u_prev=None, ubar=None):
         """Enqueue the S solves.  gamma [S, 4T_full, 2T_full], xbar [S, 4T_full],
-        goal [S, 2], ref [S, n_ref, 2], rec the records (uint8 [..., 128] tensor)."""
+        goal [S, 2], ref [S, n_ref, 2], rec the records (uint8 [cells, P, 128] tensor)."""
         lib = _lib.load()
-        ref = ref.reshape(self.S, -1, 2)
-        if self.T_full > self.T and u_prev is None:
+        S, T, Tf = self.S, self.T, self.T_full
+        ref = ref.reshape(S, -1, 2)
+        if Tf > T and u_prev is None:
             raise ValueError("u_prev (the executed controls) is required when T < T_full")
+        self._need(gamma, "gamma", (S, 4 * Tf, 2 * Tf))
+        self._need(xbar, "xbar", (S, 4 * Tf))
+        self._need(goal, "goal", (S, 2))
+        self._need(ref, "ref", None)
+        if ref.shape[1] < 1:
+            raise ValueError("ref: at least one reference point per scene")
+        P = T * (T - 1) // 2 if self.kind == REC_HALFSPACE else T
+        if P > 0 and self.n_cells > 0:
+            self._need(rec, "rec", None, torch.uint8)
+            if rec.numel() < self.n_cells * P * 128 or (rec.dim() == 3 and rec.shape[1] != P):
+                raise ValueError(f"rec: [cells >= {self.n_cells}, {P}, 128] records expected")
+        if u_prev is not None and Tf > T:
+            self._need(u_prev, "u_prev", (S, 2 * (Tf - T)))
+        if ubar is not None:
+            self._need(ubar, "ubar", (S, 2 * Tf))
         p = engine._p
         _lib.check(lib.ccmpc_mpc_qp(
             self.S, self.T, self.T_full, p(gamma), p(xbar), p(ubar), p(u_prev), p(goal), p(ref),

@@ -273,3 +273,23 @@ def test_qp_longer_horizons_lds_factor(gpu, T):
         assert status[i] == mpc.QP_OK, (s, status[i])
         _check(u[i], X[i], cost[i], want, T)
     assert n_feas >= 1
+
+
+def test_qp_refuses_malformed_inputs(gpu):
+    """Raw pointers go to the kernel: wrong dtype, shape or record block must raise on the
+    host, never launch."""
+    T = 8
+    rec, cps, o_recs, refs, goals, x0s = _scene_inputs(_feasible(2), T, gpu)
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    g_t, r_t = torch.as_tensor(goals, device=gpu), torch.as_tensor(refs, device=gpu)
+    qp = mpc.PlanningQP(cps, T)
+    with pytest.raises(ValueError):
+        qp.solve(gamma.float(), xbar, g_t, r_t, rec)
+    with pytest.raises(ValueError):
+        qp.solve(gamma[:, :-4], xbar, g_t, r_t, rec)
+    with pytest.raises(ValueError):
+        qp.solve(gamma, xbar, g_t, r_t, rec[:1])
+    with pytest.raises(ValueError):
+        mpc.PlanningQP(cps, 5, T_full=8).solve(gamma, xbar, g_t, r_t[:, :5], rec)
+    qp.solve(gamma, xbar, g_t, r_t, rec)          # the well-formed call still runs
+    assert np.all(qp.status.cpu().numpy() >= 0)
