@@ -513,8 +513,9 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     y[k] = 0.0;
   }
   for (int j = tid; j < n; j += kQpThreads) {
-    int t, c;
-    u_decode(j, T, order, t, c);
+    // min_u / max_u = vstack((full(T, a), full(T, delta))).T.ravel() (:2874-2875): the bounds
+    // interleave (accel, steer) per step like Gamma's columns, whatever U's reshape order
+    const int c = j & 1;
     ub[j] = c == 0 ? p.max_a : p.max_delta;
     lb[j] = c == 0 ? p.min_a : -p.max_delta;
     z[j] = 0.0;

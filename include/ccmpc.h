@@ -300,14 +300,15 @@ int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T, const doub
  * (v8ideal/__init__.py:2850-2930, :2999-3012, :3040-3110) with the road-boundary MILP off (the reference
  * default, :217), so the problem is a convex QP in the controls u (2T values):
  *   state      x = Gamma_f (u - u_bar) + x_bar + Gamma_p u_prev            (:2877-2891)
- *   bounds     [min_a, -max_delta] <= U_t <= [max_a, max_delta]            (:2873-2876)
+ *   bounds     [min_a, -max_delta] <= (u[2t], u[2t+1]) <= [max_a, max_delta]  (:2874-2878)
  *              0 <= v_t <= max_v                                           (:610-626)
  *   obstacles  every record with status 0:  n . x_t >= d (side +1) or <= d (side -1)
  *              (Minkowski :926-939; affine: rhs, :1503-1515 with S_big = 0)
  *   objective  w_final |X_{T-1} - goal|^2 + sum_t w_ref |X_t - ref_t|^2
  *              + sum_t U_t^T R1 U_t + sum_{t>=1} dU_t^T R2 dU_t                (:2478-2507)
- * U = cp.reshape(u, (T, 2)) uses cvxpy's default column-major order (U_t = (u[t], u[T+t]),
- * CCMPC_U_ORDER_F) in the reference; CCMPC_U_ORDER_C pairs (u[2t], u[2t+1]).
+ * U = cp.reshape(u, (T, 2)) in the objective uses cvxpy's default column-major order
+ * (U_t = (u[t], u[T+t]), CCMPC_U_ORDER_F) in the reference, while the bounds and Gamma's columns
+ * interleave (accel, steer) per step; CCMPC_U_ORDER_C pairs the objective the same way.
  * Solved by a primal-dual interior point method (Mehrotra predictor-corrector), one workgroup
  * per scene, the whole iteration in LDS, then polished: the equality-constrained QP on the
  * IPM's active set, kept only when it is a verified KKT point (T <= 32; beyond, the IPM's

@@ -239,8 +239,8 @@ def assemble_qp(Gf, c, T, goal, ref_traj, rows, p, order="F"):
         D = E[t] - E[t - 1]
         H += 2.0 * D.T @ R2 @ D
     G, h = [], []
-    for j in range(n):  # control bounds (:2873-2876)
-        t_, cc = (j % T, j // T) if order == "F" else (j // 2, j % 2)
+    for j in range(n):  # control bounds (:2874-2878): interleaved (accel, steer) per step,
+        cc = j % 2      # min_u = vstack((full(T, min_a), full(T, -max_delta))).T.ravel()
         hi = p["max_a"] if cc == 0 else p["max_delta"]
         lo = p["min_a"] if cc == 0 else -p["max_delta"]
         e = np.zeros(n)
