@@ -62,7 +62,8 @@ def time_config(dev, seed, name, O, N, T, scenes):
         K.append([len(o) for o in ovs])
         refs.append(ref)
     store = engine.ParticleStore.from_cells(cells, device=dev)
-    cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], refs[0], scene_K=K)
+    cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], np.array(refs),
+                               scene_K=K)
     t = time_kernel_live(cyc.run, dev, per_graph=10, replays=5)
     tm = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev,
                           per_graph=10, replays=5)
@@ -121,7 +122,8 @@ def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True):
         goals.append(goal)
         x0s.append(x0)
     store = engine.ParticleStore.from_cells(cells, device=dev)
-    cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], refs[0], scene_K=K)
+    cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], np.array(refs),
+                               scene_K=K)
     cyc.run()
     xbar, gamma = mpc.ltv(np.array(x0s), T, lon=3.7)
     goal_t = torch.as_tensor(np.array(goals), device=dev)

@@ -18,11 +18,39 @@ import torch
 from . import engine, risk
 
 
+def _cell_ref(ref, n_cells, scene_K, cell_ref, device):
+    """The per-cell reference-trajectory selector of a batched cycle (int32 [n_cells] on the
+    device), or None when every cell uses ref[0].
+
+    Each scene of a batch is its own planning step with its own ref_traj (the reference plans
+    one scene per agent, v8ideal/__init__.py:2934-2976), so a batch of several scenes must say
+    which row of `ref` [n_ref, T, 2] each cell reads: explicitly (cell_ref), or by scene when
+    `ref` holds one row per scene of scene_K.  Indices are checked here, on the host: the kernel
+    reads ref[cell_ref[c]] unchecked."""
+    n_ref = int(ref.shape[0])
+    if cell_ref is None and scene_K is not None and n_ref > 1:
+        if n_ref != len(scene_K):
+            raise ValueError(f"{n_ref} reference trajectories for {len(scene_K)} scenes")
+        cell_ref = np.repeat(np.arange(n_ref), [sum(int(k) for k in K_s) for K_s in scene_K])
+    if cell_ref is None:
+        if n_ref != 1:
+            raise ValueError(f"{n_ref} reference trajectories need cell_ref (or scene_K)")
+        return None
+    cell_ref = np.asarray(cell_ref, np.int64).reshape(-1)
+    if cell_ref.shape[0] != n_cells:
+        raise ValueError(f"cell_ref has {cell_ref.shape[0]} entries for {n_cells} cells")
+    if n_cells and (cell_ref.min() < 0 or cell_ref.max() >= n_ref):
+        raise ValueError(f"cell_ref indices must lie in [0, {n_ref})")
+    return torch.as_tensor(cell_ref.astype(np.int32), device=device)
+
+
 class MinkowskiCycle:
     def __init__(self, store, K, ref_traj, ph=None, R=risk.R_COLLISION, tol=1e-8, maxiter=1000,
-                 scene_K=None):
+                 scene_K=None, cell_ref=None):
         """scene_K: the per-scene split of K when several scenes' cells share one cycle (each
-        scene then allocates its own risk, risk.scenes_cell_risk); None = one scene."""
+        scene then allocates its own risk, risk.scenes_cell_risk); None = one scene.
+        ref_traj: (T, 2) for one scene, or (n_ref, T, 2) with cell_ref [n_cells] selecting each
+        cell's row -- by default one row per scene of scene_K."""
         self.store = store
         self.device = store.device
         self.T = store.T
@@ -32,6 +60,7 @@ class MinkowskiCycle:
         C, T = store.n_cells, self.T
         self.ref = torch.as_tensor(np.asarray(ref_traj, np.float64).reshape(-1, T, 2),
                                    device=self.device)
+        self.cell_ref = _cell_ref(self.ref, C, scene_K, cell_ref, self.device)
         if scene_K is None:
             cr = risk.cell_risk(risk.eps_ura(self.K), self.K, ph)
         else:
@@ -50,7 +79,8 @@ class MinkowskiCycle:
 
     def run(self):
         """One launch: moments + every (cell, t, tau) half-space (ccmpc_minkowski_cycle)."""
-        engine.minkowski_cycle(self.store, self.ref, self.risk, R=self.R, tol=self.tol,
+        engine.minkowski_cycle(self.store, self.ref, self.risk, cell_ref=self.cell_ref,
+                               R=self.R, tol=self.tol,
                                maxiter=self.maxiter, workspace=self.ws, out_mean=self.mean,
                                out_cov=self.cov, out_rec=self.rec,
                                out_prob_lower=self.prob_lower)
@@ -66,8 +96,8 @@ class MinkowskiCycle:
         self._fn = lib.ccmpc_minkowski_cycle
         self._args = (p(st.pos), st.ccmpc_dtype, st.ld, self.T, p(st.origin), p(st.cell_off),
                       p(st.cell_cnt), st.n_cells, st.n_bound, p(ws), ws.numel(), p(self.ref),
-                      p(None), p(self.risk), float(self.R), float(self.tol), int(self.maxiter),
-                      p(self.mean), p(self.cov), p(self.rec), p(self.prob_lower),
+                      p(self.cell_ref), p(self.risk), float(self.R), float(self.tol),
+                      int(self.maxiter), p(self.mean), p(self.cov), p(self.rec), p(self.prob_lower),
                       engine._stream())
         return self
 
@@ -80,7 +110,8 @@ class MinkowskiCycle:
     def run_unfused(self):
         """Same cycle as two C-ABI calls (ccmpc_moments, ccmpc_minkowski)."""
         engine.moments(self.store, self.mean, self.cov, self.ws)
-        engine.minkowski(self.mean, self.cov, self.ref, self.risk, R=self.R, tol=self.tol,
+        engine.minkowski(self.mean, self.cov, self.ref, self.risk, cell_ref=self.cell_ref,
+                         R=self.R, tol=self.tol,
                          maxiter=self.maxiter, out_rec=self.rec, out_prob_lower=self.prob_lower)
 
     def capture(self, warmup=2):
@@ -110,17 +141,25 @@ class MinkowskiCycle:
 
 
 class AffineCycle:
-    def __init__(self, store, K, ref_traj, ph=None, R=risk.R_COLLISION):
+    def __init__(self, store, K, ref_traj, ph=None, R=risk.R_COLLISION, scene_K=None,
+                 cell_ref=None):
+        """scene_K / cell_ref as MinkowskiCycle."""
         self.store = store
         self.device = store.device
         self.T = store.T
         self.K = [int(k) for k in K]
+        assert sum(self.K) == store.n_cells
         ph = self.T if ph is None else ph
         C, T = store.n_cells, self.T
         self.ref = torch.as_tensor(np.asarray(ref_traj, np.float64).reshape(-1, T, 2),
                                    device=self.device)
-        self.gamma = torch.as_tensor(risk.cell_gamma(risk.eps_ura(self.K), self.K, ph),
-                                     device=self.device)
+        self.cell_ref = _cell_ref(self.ref, C, scene_K, cell_ref, self.device)
+        if scene_K is None:
+            g = risk.cell_gamma(risk.eps_ura(self.K), self.K, ph)
+        else:
+            assert [int(k) for K_s in scene_K for k in K_s] == self.K
+            g = risk.scenes_cell_risk(scene_K, ph)[:, 2].copy()
+        self.gamma = torch.as_tensor(g, device=self.device)
         self.R = R
         self.mean = torch.empty((C, T, 2), dtype=torch.float64, device=self.device)
         self.cov = torch.empty((C, 2 * T, 2 * T), dtype=torch.float64, device=self.device)
@@ -130,7 +169,8 @@ class AffineCycle:
 
     def run(self):
         engine.moments(self.store, self.mean, self.cov, self.ws)
-        engine.affine(self.mean, self.cov, self.ref, self.gamma, R=self.R, out_rec=self.rec)
+        engine.affine(self.mean, self.cov, self.ref, self.gamma, cell_ref=self.cell_ref,
+                      R=self.R, out_rec=self.rec)
 
     def records(self):
         return engine.affine_records(self.rec)

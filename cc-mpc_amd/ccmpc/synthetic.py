@@ -6,7 +6,8 @@ No datasets, weights or CARLA are available, so every benchmark input is synthet
   unicycle rollouts), around the Town03 scene-4 T-intersection (x ~ 180..200, y ~ -90..-70,
   v8ideal/__init__.py:836);
 * mode split: a peaked latent pmf, modes with pmf > 0.1 kept (ovehicle.py:58);
-* reference trajectory: ego ahead of the OVs, ref[t] = p_ego + (4 (t+1), 0.5 (t+1)).
+* reference trajectory: ego ahead of the OVs, ref[t] = p_ego + (4 (t+1), 0.5 (t+1)), with the
+  ego placed per seed (ego_offset), so every scene of a batch has its own ref_traj.
 """
 import numpy as np
 
@@ -43,6 +44,23 @@ def mode_cloud(rng, n, T, p0=None):
     return np.stack((x, y), axis=-1)
 
 
+EGO = np.array([165.0, -60.0])
+
+
+def ego_offset(seed):
+    """Seed-dependent placement of a scene's ego (a separate Philox stream, so the OV clouds of a
+    seed do not change with it): every scene of a batch has its own reference trajectory, and a
+    batched cycle that read another scene's ref_traj would show in its records."""
+    rng = np.random.default_rng(np.random.Philox(key=int(seed) ^ 0x5EED0E90))
+    return rng.uniform(-4.0, 4.0, size=2)
+
+
+def ego_ref(seed, T):
+    """ref_traj[t] = p_ego + (4 (t+1), 0.5 (t+1)) for the seed's ego."""
+    ego = EGO + ego_offset(seed)
+    return np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
+
+
 def scene(seed, O=4, N=5000, T=8, K=None):
     """One planning step: list over OVs of list over kept modes of (N_k, T, 2) clouds,
     plus ref_traj (T, 2) and each OV's past[-1]."""
@@ -54,8 +72,7 @@ def scene(seed, O=4, N=5000, T=8, K=None):
         counts = split_counts(rng, N, k)
         ovs.append([mode_cloud(rng, int(c), T, p0) for c in counts])
         pasts.append(p0 - np.array([2.0, 0.5]))
-    ego = np.array([165.0, -60.0])
-    ref = np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
+    ref = ego_ref(seed, T)
     return ovs, ref, np.array(pasts)
 
 
@@ -66,7 +83,7 @@ def crossing_scene(seed, O=2, N=400, T=8, K=2, lateral=8.0):
     Returns (cells: list of (N/K, T, 2) clouds in (OV, mode) order, K per OV, ref (T, 2),
     goal (2,), x_init [x, y, psi, v], pasts (O, 2))."""
     rng = np.random.default_rng(np.random.Philox(seed))
-    ego = np.array([165.0, -60.0])
+    ego = EGO + ego_offset(seed)               # the whole scene moves with its ego
     ref = np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
     goal = ref[-1] + np.array([4.0, 0.5])
     x_init = np.array([ego[0], ego[1], np.arctan2(0.5, 4.0), 8.0 + rng.uniform(-1, 1)])

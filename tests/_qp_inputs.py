@@ -3,6 +3,7 @@ clouds that cross the ego's path, so half-spaces bind), wrapped as the oracle's 
 import functools
 
 import numpy as np
+import scipy.optimize
 
 from ccmpc import synthetic
 from oracle import ccmpc_oracle as orc
@@ -42,12 +43,37 @@ def classify(seed, T=8, order="F"):
     return "binding" if any(a >= 6 * T for a in r["active"]) else "free"
 
 
-def pick_seeds(kind, count, start=0, T=8, limit=400):
-    """The first `count` seeds from `start` whose scene classifies as `kind`."""
-    out = []
-    for s in range(start, start + limit):
-        if classify(s, T) == kind:
-            out.append(s)
-            if len(out) == count:
-                return out
-    raise RuntimeError(f"fewer than {count} {kind!r} scenes in seeds {start}..{start + limit}")
+# Pinned verdicts of crossing_scene(seed, T) (recorded once with classify(); the tests check
+# them, so a regression in the oracle's feasibility or active-set logic fails a test instead of
+# silently moving which seeds get picked).
+SEEDS = {
+    8: {"binding": [1, 2, 4, 5, 7, 8, 9, 11, 13, 14, 17, 20],
+        "infeasible": [0, 3, 6, 10, 12, 15]},
+    12: {"binding": [3, 5, 6, 9], "infeasible": [0, 1, 2, 4]},
+}
+
+
+def pick_seeds(kind, count, T=8):
+    """The first `count` pinned seeds of verdict `kind` at horizon T."""
+    seeds = SEEDS[T][kind]
+    if count > len(seeds):
+        raise ValueError(f"only {len(seeds)} pinned {kind!r} seeds at T = {T}")
+    return seeds[:count]
+
+
+def farkas_certificate(G, h):
+    """An infeasibility certificate of {u : G u <= h} independent of the QP oracle: y >= 0 with
+    G^T y = 0 and h . y < 0 (Farkas' lemma), from the LP min h.y s.t. G^T y = 0, 0 <= y <= 1.
+    Returns y, or None when the LP finds none."""
+    m = G.shape[0]
+    lp = scipy.optimize.linprog(h, A_eq=G.T, b_eq=np.zeros(G.shape[1]), bounds=[(0, 1)] * m,
+                                method="highs")
+    if lp.status != 0 or lp.fun >= 0:
+        return None
+    return lp.x
+
+
+def check_farkas(G, h, y):
+    """y proves infeasibility: non-negative, G^T y ~ 0 at the rows' scale, h . y clearly < 0."""
+    scale = np.abs(G).max() * max(np.abs(y).sum(), 1.0)
+    return bool(np.all(y >= 0) and np.abs(G.T @ y).max() <= 1e-9 * scale and h @ y < -1e-6)

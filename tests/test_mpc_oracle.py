@@ -9,7 +9,8 @@ import pytest
 
 from oracle import ccmpc_oracle as orc
 from oracle import mpc_oracle as mo
-from _qp_inputs import crossing_scene, pick_seeds
+from _qp_inputs import (SEEDS, check_farkas, classify, crossing_scene, farkas_certificate,
+                        pick_seeds)
 
 P = mo.DEFAULT_PARAMS
 
@@ -103,15 +104,38 @@ def test_oracle_solution_satisfies_kkt(i):
             assert mo.objective_value(v, r["Gf"], r["c"], T, goal, ref, P) >= r["cost"] - 1e-9
 
 
-@pytest.mark.parametrize("i", range(2))
-def test_infeasible_scenes_are_reported(i):
+@pytest.mark.parametrize("T", [8, 12])
+def test_pinned_verdicts(T):
+    """The oracle still classifies every pinned seed as recorded in _qp_inputs.SEEDS."""
+    for kind, seeds in SEEDS[T].items():
+        for s in seeds:
+            assert classify(s, T) == kind, (T, s, kind)
+
+
+@pytest.mark.parametrize("seed", SEEDS[8]["infeasible"][:3])
+def test_infeasible_scenes_have_a_farkas_certificate(seed):
+    """Infeasibility proven independently of the oracle's phase-1 LP: a Farkas vector y >= 0,
+    G^T y = 0, h . y < 0 for the QP's inequality rows (the reference's CPLEX failure path,
+    v8ideal/__init__.py:3099-3110)."""
     T = 8
-    seed = pick_seeds("infeasible", 2)[i]
     ovs, cells, K, ref, goal, x0 = crossing_scene(seed, T=T)
     out = orc.minkowski_generator(ovs, T, T, ref, with_l4=False)
     xbar, _, G, _, _ = mo.VehicleModel(T, 0.5, 1.85, 3.7).get_optimization_ltv(x0, np.zeros(2))
     r = mo.solve_step(G, xbar, T, T, goal, ref, out["records"], "halfspace", P)
     assert not r["feasible"]
+    y = farkas_certificate(r["G"], r["h"])
+    assert y is not None and check_farkas(r["G"], r["h"], y)
+
+
+@pytest.mark.parametrize("seed", SEEDS[8]["binding"][:3])
+def test_feasible_scenes_have_no_farkas_certificate(seed):
+    T = 8
+    ovs, cells, K, ref, goal, x0 = crossing_scene(seed, T=T)
+    out = orc.minkowski_generator(ovs, T, T, ref, with_l4=False)
+    xbar, _, G, _, _ = mo.VehicleModel(T, 0.5, 1.85, 3.7).get_optimization_ltv(x0, np.zeros(2))
+    r = mo.solve_step(G, xbar, T, T, goal, ref, out["records"], "halfspace", P)
+    assert r["feasible"] and np.all(r["G"] @ r["u"] <= r["h"] + 1e-9)
+    assert farkas_certificate(r["G"], r["h"]) is None
 
 
 def test_shrinking_step_state_map_keeps_the_first_step_model():
