@@ -86,7 +86,10 @@ SIGNATURES = {
     "ccmpc_mpc_qp": (ctypes.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _I64, _P,
                                     ctypes.c_int, _P, _I64, _P, ctypes.c_int, _I32, _D, _P, _SZ,
                                     _P, _P, _P, _P, _P, _P]),
+    "ccmpc_selftest": (ctypes.c_int, [ctypes.c_int, _I64, _P, _P, _D, _I32, _P]),
 }
+
+SELFTEST_MVOE, SELFTEST_TANGENT, SELFTEST_BOUND, SELFTEST_PAIR = 0, 1, 2, 3
 
 
 class CcmpcError(RuntimeError):
@@ -114,6 +117,29 @@ def load():
         raise CcmpcError(f"libccmpc ABI {lib.ccmpc_abi_version()} != expected {ABI_VERSION}")
     _lib = lib
     return lib
+
+
+class NonFiniteRecordError(ValueError, TypeError):
+    """A record whose inputs or outputs are inf/NaN.  The reference fails at different places
+    for these, with different exception types: N_k < 2 gives a NaN np.cov that
+    scipy.linalg.solve rejects (ValueError, makeconstraint.py:21); ref_y == mean_y gives an
+    infinite slope whose candidate distances are NaN, so choose_closest_tangent indexes its
+    candidates with None (TypeError, makeconstraint.py:194-205).  Both types are caught."""
+
+
+def record_error(status, where):
+    """The exception the reference raises where a record carries `status` (CCMPC_REC_*):
+    SINGULAR / NOT_PD -> np.linalg.LinAlgError (np.linalg.inv, scipy.linalg.solve,
+    np.linalg.cholesky); NO_TANGENT -> ValueError (v8ideal/__init__.py:925 unpacks
+    choose_closest_tangent's 4-tuple of None into 3 names); NONFINITE / NOT_PSD ->
+    NonFiniteRecordError."""
+    msg = f"{where}: {STATUS.get(int(status), status)}"
+    status = int(status)
+    if status in (REC_SINGULAR, REC_NOT_PD):
+        return np.linalg.LinAlgError(msg)
+    if status == REC_NO_TANGENT:
+        return ValueError(msg + " (too many values to unpack: the reference's None tuple)")
+    return NonFiniteRecordError(msg)
 
 
 def check(rc, what):

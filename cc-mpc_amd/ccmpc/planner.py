@@ -318,9 +318,9 @@ class MidlevelAgent:
             for p in range(P):
                 r = h[c, p]
                 if r["status"] != 0:
-                    raise FloatingPointError(
-                        f"constraint (ov={o}, k={k}, t={r['t_tau'] >> 16}, tau="
-                        f"{r['t_tau'] & 0xFFFF}) failed: {engine._lib.STATUS.get(int(r['status']))}")
+                    raise engine._lib.record_error(
+                        r["status"], f"constraint (ov={o}, k={k}, t={r['t_tau'] >> 16}, tau="
+                                     f"{r['t_tau'] & 0xFFFF})")
                 n = np.array([r["n0"], r["n1"]])
                 cons.append(HalfSpace(o, k, int(r["t_tau"] >> 16), int(r["t_tau"] & 0xFFFF), n,
                                       float(r["d"]), float(r["d"]), int(r["side"]),
@@ -399,8 +399,8 @@ class MidlevelAgent:
             for t in range(T):
                 r = h[c, t]
                 if r["status"] != 0:
-                    raise FloatingPointError(f"affine constraint (ov={o}, k={k}, t={t}) failed:"
-                                             f" {engine._lib.STATUS.get(int(r['status']))}")
+                    raise engine._lib.record_error(r["status"],
+                                                   f"affine constraint (ov={o}, k={k}, t={t})")
                 cons.append(HalfSpace(o, k, t, -1, np.array([r["n0"], r["n1"]]), float(r["d"]),
                                       float(r["rhs"]), int(r["side"]), int(r["which"]),
                                       float(r["margin"])))
@@ -469,8 +469,8 @@ class MidlevelAgent:
             for t in range(T):
                 r = h[c, t]
                 if r["status"] != 0:
-                    raise FloatingPointError(f"affine-scale constraint (ov={o}, k={k}, t={t}) "
-                                             f"failed: {engine._lib.STATUS.get(int(r['status']))}")
+                    raise engine._lib.record_error(
+                        r["status"], f"affine-scale constraint (ov={o}, k={k}, t={t})")
                 cons.append(HalfSpace(o, k, t, -1, np.array([r["n0"], r["n1"]]), float(r["d"]),
                                       float(r["rhs"]), int(r["side"]), int(r["which"]),
                                       float(r["margin"])))

@@ -122,11 +122,7 @@ __global__ __launch_bounds__(256) void affine_scale_kernel(
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
     int t, tau;
     pair_of(p, t, tau);
-    const PairMoments pm = pair_moments(C, rows, t, tau);
-    const double root_t = sqrt(fro(pm.c_t));
-    const double alpha = sqrt(fro(pm.cov_infer)) / root_t;
-    const double beta = sqrt(fro(pm.cov_mu)) / root_t;
-    const double sc = (sqrt(chi_p) * beta / gamma + alpha) * (sqrt(chi_p) * beta / gamma + alpha);
+    const double sc = pair_scale(pair_moments(C, rows, t, tau), chi_p, gamma);
     // positive doubles order like their bit patterns; NaN (all-ones exponent) also wins, as
     // np.max propagates it
     atomicMax(&scale_bits[t], static_cast<unsigned long long>(__double_as_longlong(sc)));

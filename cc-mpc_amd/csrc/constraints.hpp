@@ -186,6 +186,40 @@ __device__ __forceinline__ double pair_lower_bound(const PairMoments &pm, double
   return -expm1(-0.5 * (x * x));
 }
 
+// compute_scale (makeconstraint.py:259-280): (sqrt(chi_p) beta / Gamma + alpha)^2.
+__device__ __forceinline__ double pair_scale(const PairMoments &pm, double chi_p, double gamma) {
+  const double root_t = sqrt(fro(pm.c_t));
+  const double alpha = sqrt(fro(pm.cov_infer)) / root_t;
+  const double beta = sqrt(fro(pm.cov_mu)) / root_t;
+  const double x = sqrt(chi_p) * beta / gamma + alpha;
+  return x * x;
+}
+
+// tangent_lines_of_slope_m + choose_closest_tangent (makeconstraint.py:134-207) for the normal
+// n = [n0, n1] = [-m, 1] of a finite slope m, with the quantities that depend only on the mean
+// and the point a precomputed by the caller: proj = n.mu, nrm = |n|, na = n.a.  Picks the
+// candidate d = proj +- c sqrt(n^T S n) nearer to a under the reference's strict '<' (ties and
+// NaN distances keep index 0).  Returns 0, or CCMPC_REC_NO_TANGENT where the reference returns
+// its None tuple (n^T S n <= 0; a NaN n^T S n gives NaN candidates, decided by the caller's
+// finiteness check).
+__device__ __forceinline__ int closest_tangent(const M2 &S, double c, double n0, double n1,
+                                               double proj, double nrm, double na, double &d,
+                                               int &which) {
+  const double sn0 = S.a * n0 + S.b * n1, sn1 = S.c * n0 + S.d * n1;
+  const double q = n0 * sn0 + n1 * sn1;
+  if (q <= 0.0) {
+    d = NAN;
+    which = 0;
+    return CCMPC_REC_NO_TANGENT;
+  }
+  const double delta = c * sqrt(q);
+  const double d1 = proj + delta, d2 = proj - delta;
+  const double dist0 = fabs(na - d1) / nrm, dist1 = fabs(na - d2) / nrm;
+  which = (dist1 < dist0) ? 1 : 0;
+  d = which ? d2 : d1;
+  return 0;
+}
+
 // One (cell, t, tau) record except its lower bound, from the cell's 2T x 2T covariance C (row
 // stride `rows`) and mean mu (v8ideal/__init__.py:893-943), written straight to `out`.
 __device__ void minkowski_pair(const double *C, const double *mu, const double *ref, int rows,
@@ -220,21 +254,17 @@ __device__ void minkowski_pair(const double *C, const double *mu, const double *
   store_pair(&out->r11, QR.d, b1);
   out->beta2 = b2;
   // slope-m tangent of the QR ellipse closest to the reference point (:920-924)
-  const double sn0 = QR.a * n0 + QR.b * n1, sn1 = QR.c * n0 + QR.d * n1;
-  const double q = n0 * sn0 + n1 * sn1;
   double d = NAN;
   int which = 0, side = 0;
   if (!isfinite(m)) {
     if (status == 0) status = CCMPC_REC_NONFINITE;
-  } else if (!(q > 0.0)) {
-    if (status == 0) status = CCMPC_REC_NO_TANGENT;
   } else {
-    const double delta = 1.0 * sqrt(q);
-    const double d1 = proj + delta, d2 = proj - delta;
-    const double dist0 = fabs(na - d1) / nrm, dist1 = fabs(na - d2) / nrm;
-    which = (dist1 < dist0) ? 1 : 0;
-    d = which ? d2 : d1;
-    side = (n0 * m0 + n1 * m1 <= d) ? 1 : -1;  // (:926) n.mean <= d  ->  n.x >= d
+    const int ts = closest_tangent(QR, 1.0, n0, n1, proj, nrm, na, d, which);
+    if (ts != 0) {
+      if (status == 0) status = ts;
+    } else if (isfinite(d)) {
+      side = (n0 * m0 + n1 * m1 <= d) ? 1 : -1;  // (:926) n.mean <= d  ->  n.x >= d
+    }
   }
   if (status == 0 && !(isfinite(d) && isfinite(Q.a) && isfinite(QR.a) && isfinite(m0)))
     status = CCMPC_REC_NONFINITE;

@@ -1,0 +1,93 @@
+// Test-only entry point: the half-space tail's __device__ functions (constraints.hpp) on batched
+// host-chosen inputs, so the reference's component golden vectors (tests/golden: mvoe.npz,
+// tangent.npz, lower_bound.npz, predict_moments.npz) and the failure modes reach the exact code
+// the fused cycle kernels run, not only the CPU oracle.  Not on any product path.
+#include "constraints.hpp"
+
+namespace ccmpc {
+
+__device__ __forceinline__ M2 ld_m2(const double *p) { return {p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ void st_m2(double *p, const M2 &m) {
+  p[0] = m.a;
+  p[1] = m.b;
+  p[2] = m.c;
+  p[3] = m.d;
+}
+
+__global__ __launch_bounds__(64) void selftest_kernel(int kind, int64_t n,
+                                                      const double *__restrict__ in,
+                                                      double *__restrict__ out, double tol,
+                                                      int maxiter) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  switch (kind) {
+    case CCMPC_SELFTEST_MVOE: {  // compute_mvoe (makeconstraint.py:7-38)
+      const double *x = in + i * 8;
+      double *y = out + i * 6;
+      double beta = NAN;
+      M2 Q = {NAN, NAN, NAN, NAN};
+      const bool ok = compute_mvoe(ld_m2(x), ld_m2(x + 4), tol, maxiter, beta, Q);
+      y[0] = beta;
+      st_m2(y + 1, Q);
+      y[5] = ok ? 1.0 : 0.0;
+      break;
+    }
+    case CCMPC_SELFTEST_TANGENT: {  // choose_closest_tangent (makeconstraint.py:134-207)
+      const double *x = in + i * 10;
+      double *y = out + i * 5;
+      const double mu0 = x[0], mu1 = x[1], c = x[6], m = x[7], a0 = x[8], a1 = x[9];
+      const double n0 = -m, n1 = 1.0;
+      double d = NAN;
+      int which = 0;
+      const int st = closest_tangent(ld_m2(x + 2), c, n0, n1, n0 * mu0 + n1 * mu1,
+                                     sqrt(n0 * n0 + n1 * n1), n0 * a0 + n1 * a1, d, which);
+      y[0] = n0;
+      y[1] = n1;
+      y[2] = d;
+      y[3] = which;
+      y[4] = st;
+      break;
+    }
+    case CCMPC_SELFTEST_BOUND: {  // compute_lower_bound / compute_scale (:259-303)
+      const double *x = in + i * 14;
+      PairMoments pm;
+      pm.cov_infer = ld_m2(x);
+      pm.cov_mu = ld_m2(x + 4);
+      pm.c_t = ld_m2(x + 8);
+      pm.ok = true;
+      out[i * 2] = pair_lower_bound(pm, x[12]);
+      out[i * 2 + 1] = pair_scale(pm, x[13], x[12]);
+      break;
+    }
+    case CCMPC_SELFTEST_PAIR: {  // predict_moments (makeconstraint.py:41-70) from a 4x4 cov
+      const double *x = in + i * 18;  // rows (x_tau, y_tau, x_t, y_t): pair (t, tau) = (1, 0)
+      double *y = out + i * 14;
+      const PairMoments pm = pair_moments(x, 4, 1, 0);
+      st_m2(y, pm.cov_infer);
+      st_m2(y + 4, pm.cov_mu);
+      st_m2(y + 8, pm.c_t);
+      y[12] = pair_lower_bound(pm, x[16]);
+      y[13] = pair_scale(pm, x[17], x[16]);
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+}  // namespace ccmpc
+
+using namespace ccmpc;
+
+extern "C" int ccmpc_selftest(int kind, int64_t n, const double *in, double *out, double tol,
+                              int32_t maxiter, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(kind >= CCMPC_SELFTEST_MVOE && kind <= CCMPC_SELFTEST_PAIR, "unknown kind");
+  CCMPC_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "bad n");
+  if (n == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(in && out, "null pointer");
+  CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
+  hipLaunchKernelGGL(selftest_kernel, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(64), 0,
+                     as_stream(stream), kind, n, in, out, tol, static_cast<int>(maxiter));
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}

@@ -361,6 +361,28 @@ int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamm
                  double *out_cost, int32_t *out_status, int32_t *out_iter,
                  ccmpc_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * TEST ONLY (not a reference interface): the half-space tail's device functions -- the ones
+ * ccmpc_minkowski_cycle / ccmpc_minkowski / ccmpc_affine_scale run per record -- on n batched
+ * inputs, so the reference's component golden vectors reach the device arithmetic.  Device
+ * pointers, float64, row-major 2x2 matrices (a, b, c, d):
+ *  MVOE     in[n][8]  = S1, S2                 out[n][6]  = beta, Q, ok (1/0)
+ *           (compute_mvoe, makeconstraint.py:7-38; tol / maxiter as the cycle's)
+ *  TANGENT  in[n][10] = mu[2], Sigma, c, m, a[2]  out[n][5] = n[2], d, which, status (0 or
+ *           CCMPC_REC_NO_TANGENT)  (choose_closest_tangent, makeconstraint.py:134-207)
+ *  BOUND    in[n][14] = cov_infer, cov_mu, cov_t, Gamma, chi_p   out[n][2] = lower bound,
+ *           scale  (compute_lower_bound / compute_scale, makeconstraint.py:259-303)
+ *  PAIR     in[n][18] = 4x4 cov of (x_tau, y_tau, x_t, y_t), Gamma, chi_p
+ *           out[n][14] = cov_infer, cov_mu, cov_t, lower bound, scale
+ *           (predict_moments, makeconstraint.py:41-70, then BOUND)
+ * ------------------------------------------------------------------------------------- */
+#define CCMPC_SELFTEST_MVOE 0
+#define CCMPC_SELFTEST_TANGENT 1
+#define CCMPC_SELFTEST_BOUND 2
+#define CCMPC_SELFTEST_PAIR 3
+int ccmpc_selftest(int kind, int64_t n, const double *in, double *out, double tol,
+                   int32_t maxiter, ccmpc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
