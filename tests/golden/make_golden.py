@@ -31,11 +31,31 @@ from oracle import ccmpc_oracle as orc  # noqa: E402
 REF_MC = "/root/reference/collect/in_simulation/midlevel/v8ideal/makeconstraint.py"
 
 
+REF_MID = "/root/reference/collect/in_simulation/midlevel"
+
+
 def load_reference():
     spec = importlib.util.spec_from_file_location("ref_makeconstraint", REF_MC)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
+
+
+def reference_function(path, name, cls=None, namespace=None):
+    """One function of a reference module whose module-level imports (carla, cvxpy, docplex,
+    Trajectron++) are absent here, although its own body needs only numpy/scipy: the function's
+    source is taken from the file's syntax tree unchanged (decorators dropped, so a classmethod
+    takes its class as a plain first argument) and executed in `namespace`."""
+    import ast
+    tree = ast.parse(open(path).read(), filename=path)
+    body = tree.body
+    if cls is not None:
+        body = next(n for n in body if isinstance(n, ast.ClassDef) and n.name == cls).body
+    fn = next(n for n in body if isinstance(n, ast.FunctionDef) and n.name == name)
+    fn.decorator_list = []
+    ns = dict(namespace or {})
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), path, "exec"), ns)
+    return ns[name]
 
 
 def rand_spd(rng, scale=1.0, cond=10.0):
@@ -255,5 +275,194 @@ def main():
     print("golden fixtures written to", HERE)
 
 
+# ---- reference-code pins for the restated glue (rows a2, a4, a12) ---------------------------
+class _Recorder:
+    """Stands in for the OVehicle class that from_trajectron instantiates: keeps the
+    constructor arguments (ovehicle.py:116-117 -> __init__ :119)."""
+
+    def __init__(self, node, T, past, ground_truth, latent_pmf, pred_positions, pred_yaws,
+                 init_center, bbox):
+        self.T, self.past, self.latent_pmf = T, past, latent_pmf
+        self.pred_positions, self.pred_yaws = pred_positions, pred_yaws
+        self.init_center, self.bbox = init_center, bbox
+        self.n_states = len(pred_positions)
+
+
+def _latent_predictions(rng, L, N, T, pmf):
+    """Sampler-shaped input of make_ovehicles: float32 scene-relative positions (N, T, 2)
+    whose latent z picks a heading/speed mode, and z itself."""
+    z = rng.choice(L, size=N, p=pmf)
+    heading = rng.uniform(-np.pi, np.pi, size=L)
+    speed = rng.uniform(2.0, 9.0, size=L)
+    p0 = rng.uniform(30.0, 60.0, size=2)
+    h = heading[z][:, None] + rng.normal(0, 0.08, size=(N, 1)) * np.arange(1, T + 1)
+    v = speed[z][:, None] + rng.normal(0, 0.5, size=(N, 1))
+    x = p0[0] + np.cumsum(v * np.cos(h) * 0.5, axis=1) + rng.normal(0, 0.05, size=(N, T))
+    y = p0[1] + np.cumsum(v * np.sin(h) * 0.5, axis=1) + rng.normal(0, 0.05, size=(N, T))
+    return np.stack((x, y), axis=-1).astype(np.float32), z.astype(np.int32)
+
+
+def pin_ovehicles_and_l4(rng):
+    """make_ovehicles (v8ideal/__init__.py:469-505) bucketing the sampler's output by z, then
+    the reference's own OVehicle.from_trajectron (ovehicle.py:24-117) and, per kept mode and
+    step, its own compute_L4_outerapproximation (midlevel/util.py:171-200) over bounding-box
+    corners from midlevel/util.py:104-124 (get_vertices_from_centers).  v8ideal itself calls
+    utility.npu.vertices_of_bboxes from the un-vendored python-utility submodule for those
+    corners; util.py's function gives the same four corners, and b is a max over all of them.
+    -> tests/golden/ovehicle_l4.npz"""
+    import scipy.spatial  # noqa: F401  (from_trajectron uses scipy.spatial.distance_matrix)
+    from_trajectron = reference_function(os.path.join(REF_MID, "ovehicle.py"), "from_trajectron",
+                                         cls="OVehicle",
+                                         namespace={"np": np, "scipy": scipy_mod(),
+                                                    "DEFAULT_BBOX": np.array([4.5, 2.5])})
+    util_ns = {"np": np}
+    vertices_fn = reference_function(os.path.join(REF_MID, "util.py"), "get_vertices_from_centers",
+                                     namespace=util_ns)
+    l4_fn = reference_function(os.path.join(REF_MID, "util.py"), "compute_L4_outerapproximation",
+                               namespace=util_ns)
+    O, L, N, T = 2, 25, 2000, 8
+    minpos = np.array([150.0, -120.0])
+    bbox = np.array([4.5, 2.5])
+    preds, zs, pmfs, pasts = [], [], [], []
+    out = {"K": [], "counts": [], "positions": [], "yaws": [], "A": [], "b": [], "yaw_mean": []}
+    pmf_out = np.zeros((O, L))
+    centre = np.zeros((O, L, 2))
+    for o in range(O):
+        pmf = np.exp(rng.normal(0, 1.2, L))
+        pmf[rng.choice(L, 3, replace=False)] += 3.0 * pmf.sum() / L   # a few kept modes
+        pmf /= pmf.sum()
+        pred, z = _latent_predictions(rng, L, N, T, pmf)
+        past = (pred[0, 0].astype(np.float64) + minpos - np.array([3.0, 1.0]))[None]
+        # make_ovehicles: world = float32 prediction + float64 minpos, appended per particle
+        veh_predict = pred + minpos
+        buckets = [[] for _ in range(L)]
+        for j, p in enumerate(veh_predict):
+            buckets[z[j]].append(p)
+        buckets = [np.array(b) for b in buckets]
+        ov = from_trajectron(_Recorder, None, T, None, past, pmf, buckets, filter_pmf=0.1,
+                             bbox=bbox)
+        preds.append(pred)
+        zs.append(z)
+        pmfs.append(pmf)
+        pasts.append(past)
+        out["K"].append(ov.n_states)
+        pmf_out[o, :ov.n_states] = ov.latent_pmf
+        centre[o, :ov.n_states] = ov.init_center
+        for k in range(ov.n_states):
+            ps, yw = ov.pred_positions[k], ov.pred_yaws[k]
+            out["counts"].append(ps.shape[0])
+            out["positions"].append(ps)
+            out["yaws"].append(yw)
+            A_k, b_k, m_k = [], [], []
+            for t in range(T):
+                theta = np.mean(yw[:, t])
+                vert = vertices_fn(ps[:, t], yw[:, t], bbox).reshape(-1, 4, 2)
+                A, b = l4_fn(theta, vert)
+                A_k.append(A)
+                b_k.append(b)
+                m_k.append(theta)
+            out["A"].append(A_k)
+            out["b"].append(b_k)
+            out["yaw_mean"].append(m_k)
+    np.savez(os.path.join(HERE, "ovehicle_l4.npz"), T=T, minpos=minpos, bbox=bbox,
+             pred=np.array(preds), z=np.array(zs), latent_pmf=np.array(pmfs),
+             past=np.array(pasts), K=np.array(out["K"]), counts=np.array(out["counts"]),
+             positions=np.concatenate(out["positions"]), yaws=np.concatenate(out["yaws"]),
+             pmf_out=pmf_out, init_center=centre, A=np.array(out["A"]), b=np.array(out["b"]),
+             yaw_mean=np.array(out["yaw_mean"]))
+
+
+def scipy_mod():
+    import scipy
+    import scipy.spatial  # noqa: F401
+    return scipy
+
+
+IDEAL_N = 1_000_000              # predict_ideal's own n_samples (v8ideal/__init__.py:2640)
+IDEAL_ROWS = 512
+
+
+def ideal_rows(n=IDEAL_N, rows=IDEAL_ROWS, seed=99):
+    """The sample indices the fixture keeps: the first half of `rows`, then a seeded spread."""
+    rest = np.random.default_rng(seed).choice(np.arange(rows // 2, n), rows - rows // 2,
+                                              replace=False)
+    return np.concatenate((np.arange(rows // 2), np.sort(rest)))
+
+
+def ideal_noise(zseed, cells, T, n=IDEAL_N):
+    """The injected standard normals, in predict_ideal's draw order ((ov, k) cells, then t):
+    [cell][t] -> (n, 2)."""
+    g = np.random.default_rng(zseed)
+    return [[g.standard_normal((n, 2)) for _ in range(T)] for _ in range(cells)]
+
+
+def pin_predict_ideal(rng):
+    """The reference's own MidlevelAgent.predict_ideal (v8ideal/__init__.py:2620-2711) run with
+    n_samples = 1e6 as written, its moments pickle, x0 draw and unseeded RandomState
+    (:2664, :2699) replaced by injected values: x0 per cell, and standard normals from a seeded
+    generator in the function's own draw order.  The fixture keeps the inputs, IDEAL_ROWS
+    sample rows of every cell's (1e6, T, 2) output and the output's per-cell mean / covariance.
+    -> tests/golden/ideal_ref.npz"""
+    import logging
+    import types
+    T_src, T, K = 8, 7, 2
+    cells = [random_walk_cell(rng, 600, T_src), random_walk_cell(rng, 450, T_src)]
+    mom = orc.save_moments([cells], T_src)                       # the inputs only
+    x0s = [mom["mean_p0p1"][0][k][0] + rng.normal(0, 0.3, 2) for k in range(K)]
+    zseed = 1234
+    noise = ideal_noise(zseed, K, T)
+
+    class _FakeFile:
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    x0_iter, z_iter = iter(x0s), iter([z for cell in noise for z in cell])
+
+    class _RandomState:
+        def __init__(self, seed=None):
+            pass
+
+        def standard_normal(self, shape):
+            z = next(z_iter)
+            assert z.shape == tuple(shape)
+            return z
+
+    fake_random = types.SimpleNamespace(
+        multivariate_normal=lambda mean, cov, size=1: np.asarray(next(x0_iter)).reshape(1, 2),
+        RandomState=_RandomState)
+    np_proxy = types.ModuleType("numpy_injected")
+    np_proxy.__dict__.update({k: getattr(np, k) for k in dir(np) if not k.startswith("__")})
+    np_proxy.random = fake_random
+    ns = {"np": np_proxy, "os": os, "logging": logging, "open": lambda *a, **k: _FakeFile(),
+          "pickle": types.SimpleNamespace(load=lambda f: mom)}
+    predict_ideal = reference_function(os.path.join(REF_MID, "v8ideal", "__init__.py"),
+                                       "predict_ideal", cls="MidlevelAgent", namespace=ns)
+    ovs = [types.SimpleNamespace(past=np.zeros((1, 2)), n_states=K)]
+    traj = predict_ideal(None, ovs, T, 0, types.SimpleNamespace(frame=20))
+    rows = ideal_rows()
+    sel = np.array([traj[0][k][rows] for k in range(K)])
+    mean = np.array([traj[0][k].mean(axis=0) for k in range(K)])
+    cov = np.array([np.cov(traj[0][k].reshape(IDEAL_N, 2 * T).T) for k in range(K)])
+    np.savez(os.path.join(HERE, "ideal_ref.npz"), T=T, n=IDEAL_N, zseed=zseed,
+             mean_in=np.array([mom["mean_p0p1"][0][k] for k in range(K)]),
+             cov_in=np.array([mom["cov_p0p1"][0][k] for k in range(K)]),
+             xcov_in=np.array([[[mom["cross_cov"][0][k][t][tau] if tau < t else np.zeros((2, 2))
+                                 for tau in range(T_src)] for t in range(T_src)]
+                               for k in range(K)]),
+             x0=np.array(x0s), rows=rows, traj_rows=sel, traj_mean=mean, traj_cov=cov)
+
+
+def main_reference_glue():
+    rng = np.random.default_rng(20261016)
+    pin_ovehicles_and_l4(rng)
+    pin_predict_ideal(rng)
+    print("reference-glue fixtures written to", HERE)
+
+
 if __name__ == "__main__":
-    main()
+    if "--glue-only" not in sys.argv:
+        main()
+    main_reference_glue()

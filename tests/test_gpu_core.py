@@ -323,3 +323,48 @@ def test_affine_scale_records_match_reference_golden(gpu, golden, scaled, pre):
     ref2 = torch.as_tensor(g["ref2"][None, :Tn], device=gpu)
     check(eng.affine_records(eng.affine_scale(mean2, cov2, ref2, cr, tangent, const,
                                               scaled=scaled)), 2)
+
+
+def test_ideal_rollout_matches_reference_predict_ideal(gpu, golden):
+    """Pinned to the reference's own MidlevelAgent.predict_ideal (v8ideal/__init__.py:
+    2620-2711) run at its 1e6 samples with injected x0 and normals (tests/golden/ideal_ref.npz):
+    the device rollout fed the same draws reproduces the kept sample rows, and the moment
+    kernel over the device's 1e6-sample store reproduces the reference output's mean and
+    covariance."""
+    import importlib.util
+    import os
+    eng = ccmpc()
+    g = golden("ideal_ref")
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "make_golden.py")
+    spec = importlib.util.spec_from_file_location("make_golden", here)
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    K, T, n = g["mean_in"].shape[0], int(g["T"]), int(g["n"])
+    T_src = g["mean_in"].shape[1]
+    cov = np.zeros((K, 2 * T_src, 2 * T_src))
+    for k in range(K):
+        for t in range(T_src):
+            cov[k, 2 * t:2 * t + 2, 2 * t:2 * t + 2] = g["cov_in"][k][t]
+            for tau in range(t):
+                cov[k, 2 * t:2 * t + 2, 2 * tau:2 * tau + 2] = g["xcov_in"][k][t][tau]
+                cov[k, 2 * tau:2 * tau + 2, 2 * t:2 * t + 2] = g["xcov_in"][k][t][tau].T
+    noise = mg.ideal_noise(int(g["zseed"]), K, T, n)
+    Z = torch.empty((K, T, 2, n), dtype=torch.float64, device=gpu)
+    for k in range(K):
+        for t in range(T):
+            Z[k, t] = torch.as_tensor(noise[k][t].T.copy(), device=gpu)
+    del noise
+    dev = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=gpu)
+    store, status = eng.ideal_rollout(dev(g["mean_in"]), dev(cov), dev(list(range(K)), torch.int32),
+                                      T, n, x0=dev(g["x0"]), Z=Z)
+    assert status.cpu().numpy().tolist() == [0] * K
+    mean, cv = eng.moments(store)
+    rows = torch.as_tensor(g["rows"], device=gpu)
+    for k in range(K):
+        o = store.offsets[k]
+        got = store.pos[:, o:o + n].index_select(1, rows).cpu().numpy()
+        got = got.reshape(T, 2, -1).transpose(2, 0, 1)
+        np.testing.assert_allclose(got, g["traj_rows"][k], rtol=1e-12)
+        np.testing.assert_allclose(mean[k].cpu().numpy(), g["traj_mean"][k], rtol=1e-12)
+        np.testing.assert_allclose(cv[k].cpu().numpy(), g["traj_cov"][k], rtol=1e-9,
+                                   atol=1e-12 * np.abs(g["traj_cov"][k]).max())

@@ -263,3 +263,34 @@ def test_v8_milp_rows_match_oracle(gpu, T_ctrl):
     cons, *_ = agent.compute_obstacle_constraints(p, ovs, X, Delta, None, None)
     assert [bool(v) for v in cons] == holds(X, Delta)
     assert len(A_union) == T and np.allclose(A_union[0][0][0], rows.A[0, 0])
+
+
+def test_make_ovehicles_and_l4_match_reference_functions(gpu, golden):
+    """Pinned to the reference's own code (tests/golden/ovehicle_l4.npz, made by running
+    OVehicle.from_trajectron, ovehicle.py:24-117, and midlevel/util.py:104-124 / :171-200 on
+    the same input): device bucketing (membership, order, pmf, init_center), the device
+    headings, and the device L4 polytopes A/b per kept mode and step."""
+    from ccmpc import ovehicle
+    g = golden("ovehicle_l4")
+    T, O = int(g["T"]), g["pred"].shape[0]
+    ovs = ovehicle.make_ovehicles(g["pred"], g["z"], g["latent_pmf"], g["minpos"],
+                                  list(g["past"]), bboxes=np.tile(g["bbox"], (O, 1)),
+                                  device=gpu)
+    assert [ov.n_states for ov in ovs] == g["K"].tolist()
+    c0 = 0
+    for o, ov in enumerate(ovs):
+        np.testing.assert_allclose(ov.latent_pmf, g["pmf_out"][o, :ov.n_states], rtol=1e-15)
+        np.testing.assert_allclose(ov.init_center, g["init_center"][o, :ov.n_states],
+                                   rtol=1e-12)
+        for k in range(ov.n_states):
+            n = g["counts"][c0 + k]
+            off = int(np.sum(g["counts"][:c0 + k]))
+            np.testing.assert_array_equal(ov.pred_positions[k], g["positions"][off:off + n])
+            np.testing.assert_allclose(ov.pred_yaws[k], g["yaws"][off:off + n], rtol=1e-12,
+                                       atol=1e-13)
+        c0 += ov.n_states
+    l4 = ovs[0].scene.l4()
+    np.testing.assert_allclose(l4["A"].cpu().numpy(), g["A"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(l4["b"].cpu().numpy(), g["b"], rtol=1e-12)
+    np.testing.assert_allclose(l4["yaw_mean"].cpu().numpy(), g["yaw_mean"], rtol=1e-12,
+                               atol=1e-14)

@@ -182,3 +182,71 @@ def test_batched_scenes_allocate_risk_per_scene():
             want += [[scipy.stats.chi2.ppf(1 - eps, 2), scipy.stats.chi2.ppf(orc.TARGET_P, 2),
                       scipy.stats.norm.ppf(1 - eps)]] * k
     np.testing.assert_allclose(got, np.array(want), rtol=1e-14)
+
+
+# ---- reference-code pins of the restated glue (make_golden.py main_reference_glue) ----------
+def test_make_ovehicles_matches_reference_from_trajectron(golden):
+    """The oracle's make_ovehicles / from_trajectron restatement against the reference's own
+    OVehicle.from_trajectron (ovehicle.py:24-117) run on the same sampler-shaped input: same
+    kept modes, the same particles in the same order, pmf, init_center and yaws."""
+    g = golden("ovehicle_l4")
+    T = int(g["T"])
+    O = g["pred"].shape[0]
+    ovs = orc.make_ovehicles(g["pred"], g["z"], g["latent_pmf"], g["minpos"],
+                             list(g["past"]), [g["bbox"]] * O, T)
+    np.testing.assert_array_equal([ov.n_states for ov in ovs], g["K"])
+    c0 = 0
+    for o, ov in enumerate(ovs):
+        np.testing.assert_array_equal(ov.latent_pmf, g["pmf_out"][o, :ov.n_states])
+        np.testing.assert_array_equal(ov.init_center, g["init_center"][o, :ov.n_states])
+        for k in range(ov.n_states):
+            n = g["counts"][c0 + k]
+            off = int(np.sum(g["counts"][:c0 + k]))
+            np.testing.assert_array_equal(ov.pred_positions[k], g["positions"][off:off + n])
+            np.testing.assert_array_equal(ov.pred_yaws[k], g["yaws"][off:off + n])
+        c0 += ov.n_states
+
+
+def test_l4_matches_reference_util(golden):
+    """vertices_of_bboxes + compute_L4_outerapproximation restated vs midlevel/util.py's own
+    get_vertices_from_centers / compute_L4_outerapproximation (:104-124, :171-200)."""
+    g = golden("ovehicle_l4")
+    T = int(g["T"])
+    off = 0
+    for c, n in enumerate(g["counts"]):
+        ps, yw = g["positions"][off:off + n], g["yaws"][off:off + n]
+        off += n
+        for t in range(T):
+            theta = np.mean(yw[:, t])
+            assert theta == g["yaw_mean"][c, t]
+            A, b = orc.compute_L4_outerapproximation(
+                theta, orc.vertices_of_bboxes(ps[:, t], yw[:, t], g["bbox"]))
+            np.testing.assert_array_equal(A, g["A"][c, t])
+            np.testing.assert_allclose(b, g["b"][c, t], rtol=1e-15)
+
+
+def ideal_ref_inputs(g):
+    """ideal_ref.npz -> (moments dict of the oracle's save_moments format, x0s, Zs)."""
+    import importlib.util
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "make_golden.py")
+    spec = importlib.util.spec_from_file_location("make_golden", here)
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    K, T = g["mean_in"].shape[0], int(g["T"])
+    mom = dict(mean_p0p1=[[g["mean_in"][k] for k in range(K)]],
+               cov_p0p1=[[g["cov_in"][k] for k in range(K)]],
+               cross_cov=[[g["xcov_in"][k] for k in range(K)]])
+    return mom, [list(g["x0"])], [mg.ideal_noise(int(g["zseed"]), K, T, int(g["n"]))], mg
+
+
+def test_predict_ideal_matches_reference_function(golden):
+    """The oracle's predict_ideal with injected draws against the reference's own
+    MidlevelAgent.predict_ideal (v8ideal/__init__.py:2620-2711, 1e6 samples as written)."""
+    g = golden("ideal_ref")
+    mom, x0s, Zs, _ = ideal_ref_inputs(g)
+    K, T, n = g["mean_in"].shape[0], int(g["T"]), int(g["n"])
+    traj = orc.predict_ideal(mom, [K], T, n, x0s=x0s, Zs=Zs)
+    for k in range(K):
+        np.testing.assert_allclose(traj[0][k][g["rows"]], g["traj_rows"][k], rtol=1e-13)
+        np.testing.assert_allclose(traj[0][k].mean(axis=0), g["traj_mean"][k], rtol=1e-12)
