@@ -16,6 +16,7 @@ ABI_VERSION = 1
 CCMPC_OK = 0
 CCMPC_F64 = 0
 CCMPC_F32 = 1
+GMM_PER_LATENT, GMM_PER_PARTICLE = 0, 1
 
 STATUS = {
     0: "ok", -1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
@@ -69,6 +70,8 @@ SIGNATURES = {
                                                    _P, _P, _P, _P, _P]),
     "ccmpc_sample_unicycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _D, _U64, _I64,
                                              _P, _P, _I64, _P]),
+    "ccmpc_sample_unicycle_ex": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P, _P, _I64, _I64, _I64,
+                                                _D, _U64, _I64, _P, _P, _I64, _P]),
     "ccmpc_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "ccmpc_bucket": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _I64, _P,
                                     _P, _P, _SZ, _P, _I64, _P, _P, _P, _P, _P]),

@@ -35,25 +35,40 @@ def global_cell_ids(cells_per_scene, begin, end):
     return list(range(first, first + n))
 
 
-def gather_records(rec, group=None):
+def record_counts(n_local, device, group=None):
+    """Every rank's cell count (one small all_gather; synchronises).  A planner whose shard
+    shapes are fixed exchanges them once and passes them to ``gather_records``."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([int(n_local)], dtype=torch.int64, device=device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    return [int(x.item()) for x in ns]
+
+
+def gather_records(rec, group=None, counts=None):
     """All-gather every rank's record block.
 
     rec: uint8 tensor (n_local, P, 128) on this rank's device (CPU under gloo).  Ranks may hold
     different numbers of cells; blocks are padded to the largest and trimmed after the
-    exchange.  Returns the (sum n, P, 128) block in rank order, i.e. the global cell order of
-    contiguous ``scene_range`` shards.
+    exchange.  ``counts`` (every rank's n_local, from ``record_counts``) skips the count
+    exchange, so the call enqueues without a host synchronisation.  Returns the (sum n, P, 128)
+    block in rank order, i.e. the global cell order of contiguous ``scene_range`` shards.
     """
     import torch.distributed as dist
     if rec.dtype != torch.uint8 or rec.dim() != 3 or rec.shape[2] != REC_BYTES:
         raise ValueError("rec must be a uint8 (cells, P, 128) record block")
     world = dist.get_world_size(group)
-    n = torch.tensor([rec.shape[0]], dtype=torch.int64, device=rec.device)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n, group=group)
-    counts = [int(x.item()) for x in ns]
+    if counts is None:
+        counts = record_counts(rec.shape[0], rec.device, group)
+    elif len(counts) != world or counts[dist.get_rank(group)] != rec.shape[0]:
+        raise ValueError(f"counts {counts} do not match this rank's {rec.shape[0]} cells")
     cap = max(counts)
-    padded = rec.new_zeros((cap,) + tuple(rec.shape[1:]))
-    padded[: rec.shape[0]] = rec
+    if rec.shape[0] == cap:
+        padded = rec.contiguous()
+    else:
+        padded = rec.new_zeros((cap,) + tuple(rec.shape[1:]))
+        padded[: rec.shape[0]] = rec
     out = [torch.empty_like(padded) for _ in range(world)]
-    dist.all_gather(out, padded.contiguous(), group=group)
+    dist.all_gather(out, padded, group=group)
     return torch.cat([o[:c] for o, c in zip(out, counts)], dim=0)

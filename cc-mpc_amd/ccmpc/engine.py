@@ -237,29 +237,61 @@ def l4(store, past_last, bbox, with_yaw=False, with_vertices=False):
     return out
 
 
-def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="cuda", ov_base=0):
-    """GMM-latent particle sampler.  init_state (O,4), latent_pmf (O,L), gmm (O,L,T,5).
-    ov_base = global id of the first OV (keys the RNG streams; see ccmpc.dist).
+def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="cuda", ov_base=0,
+                    z=None, eps=None, per_particle=False):
+    """GMM-latent particle sampler (ccmpc_sample_unicycle_ex).
+
+    init_state (O, 4); latent_pmf (O, L) p(z|x) (only used when z is drawn here; may be None
+    when z is given).  gmm: per (OV, latent, step) parameters (O, L, T, 5), or with
+    per_particle=True every sample's own parameters as p_y_xz's autoregressive decoder emits
+    them, (O, N, T, 5) -- host array or device tensor; (O, T, 5, N) device layout is built here.
+    z: injected latent ids (O, N) (torch's one-hot z argmax, prediction.py:103) or None for the
+    Philox draw; eps: injected standard-normal noise (O, N, T, 2) float32 or None for Philox.
+    ov_base = global id of the first OV (keys the Philox streams; see ccmpc.dist).
     Returns (z [O,N] int32, F32 ParticleStore in sample order: one cell per OV)."""
     lib = _lib.load()
     dev = require_device(device)
     init_state = np.asarray(init_state, np.float64).reshape(-1, 4)
     O = init_state.shape[0]
-    pmf = np.asarray(latent_pmf, np.float64).reshape(O, -1)
-    L = pmf.shape[1]
-    cdf = np.cumsum(pmf, axis=1)
-    gmm = np.ascontiguousarray(np.asarray(gmm, np.float32).reshape(O, L, T, 5))
+    t_z = t_eps = t_cdf = None
+    if z is not None:
+        t_z = torch.as_tensor(z, device=dev).to(torch.int32).reshape(O, N).contiguous()
+    if latent_pmf is not None:
+        pmf = np.asarray(latent_pmf, np.float64).reshape(O, -1)
+        L = pmf.shape[1]
+        t_cdf = torch.as_tensor(np.cumsum(pmf, axis=1), device=dev)
+    elif t_z is not None:
+        # the latent count: the per-latent table's, else any id below 64 (the kernel's bound)
+        L = (int(gmm.shape[1]) if hasattr(gmm, "shape") else len(gmm[0])) if not per_particle else 64
+    else:
+        raise ValueError("latent_pmf is needed when z is drawn by the sampler")
+    if t_z is not None and t_z.numel():
+        lo, hi = int(t_z.min().item()), int(t_z.max().item())
+        if lo < 0 or hi >= L:
+            raise ValueError(f"injected z outside [0, {L}): [{lo}, {hi}]")
+    if per_particle:
+        if t_z is None:
+            raise ValueError("per-particle GMM parameters need the injected z")
+        g = torch.as_tensor(gmm, device=dev).to(torch.float32).reshape(O, N, T, 5)
+        t_gmm = g.permute(0, 2, 3, 1).contiguous()           # (O, T, 5, N): particle-minor
+        layout = _lib.GMM_PER_PARTICLE
+    else:
+        t_gmm = torch.as_tensor(np.ascontiguousarray(np.asarray(
+            gmm.cpu() if torch.is_tensor(gmm) else gmm, np.float32).reshape(O, L, T, 5)),
+            device=dev)
+        layout = _lib.GMM_PER_LATENT
+    if eps is not None:
+        e = torch.as_tensor(eps, device=dev).to(torch.float32).reshape(O, N, T, 2)
+        t_eps = e.permute(0, 2, 3, 1).contiguous()           # (O, T, 2, N)
     store = ParticleStore(T, [N] * O, dtype=torch.float32, device=dev, origin=np.zeros((O, 2)))
-    z = torch.empty((O, N), dtype=torch.int32, device=dev)
+    out_z = torch.empty((O, N), dtype=torch.int32, device=dev)
     t_init = torch.as_tensor(init_state, device=dev)
-    t_cdf = torch.as_tensor(cdf, device=dev)
-    t_gmm = torch.as_tensor(gmm, device=dev)
-    _lib.check(lib.ccmpc_sample_unicycle(_p(t_init), _p(t_cdf), L, _p(t_gmm), O, N, T, float(dt),
-                                         int(seed) & (2**64 - 1), int(ov_base), _p(z),
-                                         _p(store.pos), store.ld,
-                                         _stream()), "ccmpc_sample_unicycle")
-    store._keepalive = (t_init, t_cdf, t_gmm)
-    return z, store
+    _lib.check(lib.ccmpc_sample_unicycle_ex(
+        _p(t_init), _p(t_cdf), L, _p(t_gmm), layout, _p(t_z), _p(t_eps), O, N, T, float(dt),
+        int(seed) & (2**64 - 1), int(ov_base), _p(out_z), _p(store.pos), store.ld, _stream()),
+        "ccmpc_sample_unicycle_ex")
+    store._keepalive = (t_init, t_cdf, t_gmm, t_z, t_eps)
+    return out_z, store
 
 
 def affine(mean, cov, ref_traj, cell_gamma, cell_ref=None, R=3.4, out_rec=None):

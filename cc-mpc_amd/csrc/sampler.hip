@@ -54,67 +54,149 @@ __device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, fl
   v = v + a * dt;
 }
 
+// One GMM2D component's reparametrised draw (Trajectron++ GMM2D.rsample with one component):
+// a = mu + L eps, L = [[s0, 0], [s1 rho, s1 sqrt(clamp(1 - rho^2, 1e-5, 1))]], s = exp(log s);
+// the matmul row is summed before mu is added, as `mus + squeeze(L @ eps)` does.
+__device__ __forceinline__ void gmm2d_action(float mu0, float mu1, float ls0, float ls1, float rho,
+                                             float e0, float e1, float &dphi, float &acc) {
+  const float s0 = exp_rn(ls0), s1 = exp_rn(ls1);
+  const float omr2 = fminf(fmaxf(1.0f - rho * rho, 1e-5f), 1.0f);
+  dphi = mu0 + s0 * e0;  // + 0 * e1: adds a signed zero, never changes s0 e0 unless it is 0
+  acc = mu1 + ((s1 * rho) * e0 + (s1 * sqrtf(omr2)) * e1);
+}
+
+// Where the draw's parameters and noise come from:
+//  PP    per-particle GMM parameters gmm[o][t][5][N] (what p_y_xz emits: its GRU decoder is
+//        autoregressive, so every sample carries its own parameters) instead of per (OV, latent,
+//        step) parameters gmm[o][L][T][5] selected by z;
+//  ZIN   latent ids injected (torch's one-hot z argmax, prediction.py:103) instead of the Philox
+//        inverse CDF;
+//  EPSIN noise injected eps[o][t][2][N] (torch's randn inside GMM2D.rsample) instead of Philox.
+// Per-particle arrays are particle-minor, so a wave's reads of one (t, k) are one contiguous run.
+template <bool PP, bool ZIN, bool EPSIN>
 __global__ __launch_bounds__(256) void sample_unicycle_kernel(
     const double *__restrict__ init_state, const double *__restrict__ latent_cdf, int n_latent,
-    const float *__restrict__ gmm, int64_t N, int T, float dt, uint64_t seed, uint32_t ov_base,
-    int32_t *__restrict__ out_z, float *__restrict__ out_pos, int64_t ld) {
+    const float *__restrict__ gmm, const int32_t *__restrict__ z_in,
+    const float *__restrict__ eps_in, int64_t N, int T, float dt, uint64_t seed,
+    uint32_t ov_base, int32_t *__restrict__ out_z, float *__restrict__ out_pos, int64_t ld) {
   const int ov = blockIdx.y;
   const uint32_t key = ov_base + static_cast<uint32_t>(ov);  // global OV id keys the streams
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= N) return;
-  const double *cdf = latent_cdf + static_cast<int64_t>(ov) * n_latent;
-  const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, key, STREAM_SAMPLER_Z, seed);
-  const double u = uniform53(w.x, w.y);
-  int z = n_latent - 1;
-  for (int k = 0; k < n_latent; ++k) {
-    if (cdf[k] > u) {  // numpy searchsorted(cdf, u, side='right')
-      z = k;
-      break;
+  int z;
+  if (ZIN) {
+    z = z_in[static_cast<int64_t>(ov) * N + i];
+    z = z < 0 ? 0 : (z >= n_latent ? n_latent - 1 : z);  // memory safety; the host validates
+  } else {
+    const double *cdf = latent_cdf + static_cast<int64_t>(ov) * n_latent;
+    const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, key, STREAM_SAMPLER_Z, seed);
+    const double u = uniform53(w.x, w.y);
+    z = n_latent - 1;
+    for (int k = 0; k < n_latent; ++k) {
+      if (cdf[k] > u) {  // numpy searchsorted(cdf, u, side='right')
+        z = k;
+        break;
+      }
     }
   }
   out_z[static_cast<int64_t>(ov) * N + i] = z;
   const double *st = init_state + 4 * ov;
   float x = static_cast<float>(st[0]), y = static_cast<float>(st[1]);
   float phi = static_cast<float>(st[2]), v = static_cast<float>(st[3]);
-  const float *g = gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
+  // per-latent: this particle's component row; per-particle: element (t, k) at g[(5t + k) N]
+  const float *g = PP ? gmm + static_cast<int64_t>(ov) * T * 5 * N + i
+                      : gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
+  const float *ep = EPSIN ? eps_in + static_cast<int64_t>(ov) * T * 2 * N + i : nullptr;
   float *o = out_pos + static_cast<int64_t>(ov) * ((N + 3) & ~int64_t(3)) + i;
   for (int t = 0; t < T; ++t) {
-    double e0d, e1d;
-    normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), key, STREAM_SAMPLER_EPS, seed,
-                e0d, e1d);
-    const float e0 = static_cast<float>(e0d), e1 = static_cast<float>(e1d);
-    const float mu0 = g[5 * t], mu1 = g[5 * t + 1];
-    const float s0 = exp_rn(g[5 * t + 2]), s1 = exp_rn(g[5 * t + 3]), rho = g[5 * t + 4];
-    const float dphi = mu0 + s0 * e0;
-    const float acc = (mu1 + (s1 * rho) * e0) + (s1 * sqrtf(1.0f - rho * rho)) * e1;
+    float e0, e1;
+    if (EPSIN) {
+      e0 = ep[(2 * t) * N];
+      e1 = ep[(2 * t + 1) * N];
+    } else {
+      double e0d, e1d;
+      normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), key, STREAM_SAMPLER_EPS,
+                  seed, e0d, e1d);
+      e0 = static_cast<float>(e0d);
+      e1 = static_cast<float>(e1d);
+    }
+    float p[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) p[k] = PP ? g[(5 * t + k) * N] : g[5 * t + k];
+    float dphi, acc;
+    gmm2d_action(p[0], p[1], p[2], p[3], p[4], e0, e1, dphi, acc);
     unicycle_step(x, y, phi, v, dphi, acc, dt);
     o[(2 * t) * ld] = x;
     o[(2 * t + 1) * ld] = y;
   }
 }
 
+template <bool PP, bool ZIN, bool EPSIN>
+static void launch_sampler(dim3 grid, hipStream_t s, const double *init_state,
+                           const double *latent_cdf, int n_latent, const float *gmm,
+                           const int32_t *z_in, const float *eps_in, int64_t N, int T, float dt,
+                           uint64_t seed, uint32_t ov_base, int32_t *out_z, float *out_pos,
+                           int64_t ld) {
+  hipLaunchKernelGGL((sample_unicycle_kernel<PP, ZIN, EPSIN>), grid, dim3(256), 0, s, init_state,
+                     latent_cdf, n_latent, gmm, z_in, eps_in, N, T, dt, seed, ov_base, out_z,
+                     out_pos, ld);
+}
+
 }  // namespace ccmpc
 
 using namespace ccmpc;
+
+extern "C" int ccmpc_sample_unicycle_ex(const double *init_state, const double *latent_cdf,
+                                        int64_t n_latent, const float *gmm, int32_t gmm_layout,
+                                        const int32_t *z_in, const float *eps_in, int64_t n_ov,
+                                        int64_t N, int64_t T, double dt, uint64_t seed,
+                                        int64_t ov_base, int32_t *out_z, float *out_pos,
+                                        int64_t ld, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
+  CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
+  CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536, "bad n_ov");
+  CCMPC_REQUIRE(N >= 1 && N < (int64_t(1) << 32), "bad N");
+  CCMPC_REQUIRE(ov_base >= 0 && ov_base + n_ov <= (int64_t(1) << 32), "bad ov_base");
+  CCMPC_REQUIRE(gmm_layout == CCMPC_GMM_PER_LATENT || gmm_layout == CCMPC_GMM_PER_PARTICLE,
+                "bad gmm_layout");
+  const bool pp = gmm_layout == CCMPC_GMM_PER_PARTICLE;
+  // per-particle parameters come from a decoder conditioned on each sample's z: z is an input
+  CCMPC_REQUIRE(!pp || z_in, "per-particle GMM parameters need the injected z_in");
+  CCMPC_REQUIRE(pp || n_ov * n_latent * T * 5 < (int64_t(1) << 40), "gmm too large");
+  CCMPC_REQUIRE(!pp || n_ov * T * 5 * N < (int64_t(1) << 40), "gmm too large");
+  if (n_ov == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(init_state && gmm && out_z && out_pos, "null pointer");
+  CCMPC_REQUIRE(z_in || latent_cdf, "latent_cdf is needed when z is drawn here");
+  CCMPC_REQUIRE(ld >= n_ov * ((N + 3) & ~int64_t(3)), "ld too small");
+  const dim3 grid(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(n_ov));
+  hipStream_t s = as_stream(stream);
+  const int L = static_cast<int>(n_latent), Ti = static_cast<int>(T);
+  const float fdt = static_cast<float>(dt);
+  const uint32_t base = static_cast<uint32_t>(ov_base);
+#define CCMPC_SAMPLER(PP, ZIN, EPSIN)                                                        \
+  launch_sampler<PP, ZIN, EPSIN>(grid, s, init_state, latent_cdf, L, gmm, z_in, eps_in, N, Ti, \
+                                 fdt, seed, base, out_z, out_pos, ld)
+  const int mode = (pp ? 4 : 0) | (z_in ? 2 : 0) | (eps_in ? 1 : 0);
+  switch (mode) {
+    case 0: CCMPC_SAMPLER(false, false, false); break;
+    case 1: CCMPC_SAMPLER(false, false, true); break;
+    case 2: CCMPC_SAMPLER(false, true, false); break;
+    case 3: CCMPC_SAMPLER(false, true, true); break;
+    case 6: CCMPC_SAMPLER(true, true, false); break;
+    default: CCMPC_SAMPLER(true, true, true); break;
+  }
+#undef CCMPC_SAMPLER
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}
 
 extern "C" int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf,
                                      int64_t n_latent, const float *gmm, int64_t n_ov, int64_t N,
                                      int64_t T, double dt, uint64_t seed, int64_t ov_base,
                                      int32_t *out_z, float *out_pos, int64_t ld,
                                      ccmpc_stream_t stream) {
-  CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
-  CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
-  CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536, "bad n_ov");
-  CCMPC_REQUIRE(N >= 1 && N < (int64_t(1) << 32), "bad N");
-  CCMPC_REQUIRE(ov_base >= 0 && ov_base + n_ov <= (int64_t(1) << 32), "bad ov_base");
-  if (n_ov == 0) return CCMPC_OK;
-  CCMPC_REQUIRE(init_state && latent_cdf && gmm && out_z && out_pos, "null pointer");
-  CCMPC_REQUIRE(ld >= n_ov * ((N + 3) & ~int64_t(3)), "ld too small");
-  const dim3 grid(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(n_ov));
-  hipLaunchKernelGGL(sample_unicycle_kernel, grid, dim3(256), 0, as_stream(stream), init_state,
-                     latent_cdf, static_cast<int>(n_latent), gmm, N, static_cast<int>(T),
-                     static_cast<float>(dt), seed, static_cast<uint32_t>(ov_base), out_z, out_pos,
-                     ld);
-  CCMPC_LAUNCH_CHECK();
-  return CCMPC_OK;
+  CCMPC_REQUIRE(latent_cdf, "null pointer");
+  return ccmpc_sample_unicycle_ex(init_state, latent_cdf, n_latent, gmm, CCMPC_GMM_PER_LATENT,
+                                  nullptr, nullptr, n_ov, N, T, dt, seed, ov_base, out_z, out_pos,
+                                  ld, stream);
 }

@@ -247,11 +247,35 @@ int ccmpc_ideal_minkowski_cycle(const double *prev_mean, const double *prev_cov,
  * g = ov_base + o the GLOBAL OV id, so a scene's draws do not depend on how scenes are sharded
  * over ranks or batched into calls.
  * PARITY UNPINNED upstream (absent submodule): checked against the repo's own restatement.
+ * This is the synthetic mode (Philox z and eps, per-latent parameters); the upstream-shaped
+ * boundary is ccmpc_sample_unicycle_ex below, of which this is the (PER_LATENT, NULL, NULL) case.
  * ------------------------------------------------------------------------------------- */
 int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf, int64_t n_latent,
                           const float *gmm, int64_t n_ov, int64_t N, int64_t T, double dt,
                           uint64_t seed, int64_t ov_base, int32_t *out_z, float *out_pos,
                           int64_t ld, ccmpc_stream_t stream);
+
+/* The sampler at the boundary Trajectron++ actually emits (prediction.py:81-86): torch draws
+ * z (latent.sample_p, one-hot -> argmax as :103 does) and the decoder's noise eps (randn inside
+ * GMM2D.rsample), and p_y_xz's GRU decoder is autoregressive, so every sample carries its OWN
+ * GMM parameters per step.  Replaces the action draw + Unicycle.integrate_samples tail of
+ * p_y_xz (:85) and the argmax of :103.
+ *  gmm_layout CCMPC_GMM_PER_LATENT:   gmm[o][L][T][5] selected by z (as ccmpc_sample_unicycle)
+ *             CCMPC_GMM_PER_PARTICLE: gmm[o][T][5][N] (particle-minor; needs z_in)
+ *  z_in[o][N]       injected latent ids in [0, n_latent) (ids outside are clamped for memory
+ *                   safety; the Python mirror rejects them), or NULL: Philox inverse CDF of
+ *                   latent_cdf (which may be NULL when z_in is given)
+ *  eps_in[o][T][2][N] injected standard-normal noise (float32), or NULL: Philox
+ * Per-step action a = mu + L eps with L = [[s0, 0], [s1 rho, s1 sqrt(clamp(1 - rho^2, 1e-5,
+ * 1))]] (GMM2D's clamp), the L eps row summed before mu is added.  out_z / out_pos as above.
+ * PARITY UNPINNED upstream (Trajectron++ absent): checked against the repo's restatement. */
+#define CCMPC_GMM_PER_LATENT 0
+#define CCMPC_GMM_PER_PARTICLE 1
+int ccmpc_sample_unicycle_ex(const double *init_state, const double *latent_cdf, int64_t n_latent,
+                             const float *gmm, int32_t gmm_layout, const int32_t *z_in,
+                             const float *eps_in, int64_t n_ov, int64_t N, int64_t T, double dt,
+                             uint64_t seed, int64_t ov_base, int32_t *out_z, float *out_pos,
+                             int64_t ld, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Particle bucketing by latent mode: make_ovehicles (v8ideal/__init__.py:469-505) +

@@ -670,13 +670,29 @@ def sample_latents(latent_cdf, n, ov, seed):
     return np.minimum(z, len(latent_cdf) - 1).astype(np.int32)
 
 
-def sample_unicycle(init_state, latent_cdf, gmm, n, T, dt, seed, ov=0):
-    """One OV's particle cloud: z draw, GMM2D reparametrised action per step
-    (a = mu + L eps, L = [[s0, 0], [s1 rho, s1 sqrt(1-rho^2)]]), Unicycle integration.
-    init_state: (x, y, phi, v) scene-relative; gmm: (Z, T, 5) = mu_dphi, mu_a, log_s_dphi,
-    log_s_a, rho.  Returns z (n,), positions (n, T, 2) float32."""
+def gmm2d_action(p, e0, e1):
+    """GMM2D.rsample with one component (Trajectron++ model/components/gmm2d.py): s = exp(log s),
+    L = [[s0, 0], [s1 rho, s1 sqrt(clamp(1 - rho^2, 1e-5, 1))]], a = mu + squeeze(L @ eps) --
+    the matmul row summed before mu is added.  p: (..., 5) float32 rows."""
     f = np.float32
-    z = sample_latents(latent_cdf, n, ov, seed)
+    s0, s1, rho = _rn32(np.exp, p[..., 2]), _rn32(np.exp, p[..., 3]), p[..., 4]
+    omr2 = np.clip(f(1) - rho * rho, f(1e-5), f(1)).astype(f)
+    dphi = (p[..., 0] + s0 * e0).astype(f)
+    acc = (p[..., 1] + ((s1 * rho) * e0 + (s1 * np.sqrt(omr2)) * e1)).astype(f)
+    return dphi, acc
+
+
+def sample_unicycle(init_state, latent_cdf, gmm, n, T, dt, seed, ov=0, z=None, eps=None,
+                    per_particle=False):
+    """One OV's particle cloud: z draw, GMM2D reparametrised action per step, Unicycle
+    integration.  init_state: (x, y, phi, v) scene-relative; gmm: (Z, T, 5) = mu_dphi, mu_a,
+    log_s_dphi, log_s_a, rho per latent, or with per_particle=True (n, T, 5) per sample (p_y_xz's
+    autoregressive decoder output).  z: injected ids (n,) or None (Philox inverse CDF of
+    latent_cdf); eps: injected noise (n, T, 2) or None (Philox).  Returns z (n,), positions
+    (n, T, 2) float32."""
+    f = np.float32
+    z = (sample_latents(latent_cdf, n, ov, seed) if z is None
+         else np.asarray(z, np.int32).reshape(n))
     x = np.full(n, init_state[0], dtype=f)
     y = np.full(n, init_state[1], dtype=f)
     phi = np.full(n, init_state[2], dtype=f)
@@ -685,13 +701,14 @@ def sample_unicycle(init_state, latent_cdf, gmm, n, T, dt, seed, ov=0):
     out = np.empty((n, T, 2), dtype=f)
     g = np.asarray(gmm, dtype=f)
     for t in range(T):
-        e0, e1 = philox.normal_pair(idx, t, ov, philox.STREAM_SAMPLER_EPS, seed)
-        e0, e1 = e0.astype(f), e1.astype(f)
-        p = g[z, t]
-        s0, s1, rho = _rn32(np.exp, p[:, 2]), _rn32(np.exp, p[:, 3]), p[:, 4]
-        dphi = p[:, 0] + s0 * e0
-        acc = p[:, 1] + (s1 * rho) * e0 + (s1 * np.sqrt(f(1) - rho * rho)) * e1
-        x, y, phi, v = unicycle_step(x, y, phi, v, dphi.astype(f), acc.astype(f), dt)
+        if eps is None:
+            e0, e1 = philox.normal_pair(idx, t, ov, philox.STREAM_SAMPLER_EPS, seed)
+            e0, e1 = e0.astype(f), e1.astype(f)
+        else:
+            e0, e1 = (np.asarray(eps, f)[:, t, c] for c in (0, 1))
+        p = g[:, t] if per_particle else g[z, t]
+        dphi, acc = gmm2d_action(p, e0, e1)
+        x, y, phi, v = unicycle_step(x, y, phi, v, dphi, acc, dt)
         out[:, t, 0] = x
         out[:, t, 1] = y
     return z, out

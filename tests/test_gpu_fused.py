@@ -214,3 +214,91 @@ def test_sampler_matches_restatement(gpu):
     # empirical latent frequencies follow p(z|x)
     freq = np.bincount(zc[0], minlength=L) / N
     assert np.max(np.abs(freq - pmf[0])) < 5 * np.sqrt(pmf[0].max() / N) + 1e-3
+
+
+def _torch_draws(pmf, N, T, seed):
+    """z and eps as the upstream boundary draws them in torch (latent.sample_p -> one-hot ->
+    argmax, prediction.py:81-83/:103; randn inside GMM2D.rsample)."""
+    g = torch.Generator().manual_seed(seed)
+    O = pmf.shape[0]
+    z = torch.multinomial(torch.as_tensor(pmf), N, replacement=True, generator=g).to(torch.int32)
+    eps = torch.randn((O, N, T, 2), generator=g, dtype=torch.float32)
+    return z.numpy(), eps.numpy()
+
+
+def _assert_cloud(got, want):
+    # float32 IEEE ops + float64-rounded transcendentals on both sides
+    assert np.mean(got != want) < 1e-4
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-3)
+
+
+def test_sampler_injected_latents_and_noise(gpu):
+    """Upstream-shaped boundary, per-latent parameters: torch-drawn z and eps injected
+    (ccmpc_sample_unicycle_ex).  PARITY UNPINNED upstream (Trajectron++ absent): vs the
+    restatement fed the same draws."""
+    e = eng()
+    O, L, T, N = 3, 25, 8, 6000
+    init, pmf, gmm = _sampler_inputs(O, L, T, seed=4)
+    z, eps = _torch_draws(pmf, N, T, seed=11)
+    zg, store = e.sample_unicycle(init, pmf, gmm, N, T, dt=0.5, device=gpu, z=z, eps=eps)
+    np.testing.assert_array_equal(zg.cpu().numpy(), z)
+    for o in range(O):
+        _, want = orc.sample_unicycle(init[o], None, gmm[o], N, T, 0.5, 0, ov=o, z=z[o],
+                                      eps=eps[o])
+        _assert_cloud(store.cell_positions(o), want)
+    # z injected, eps from Philox: the same eps stream as the synthetic mode
+    zg2, store2 = e.sample_unicycle(init, None, gmm, N, T, dt=0.5, seed=5, device=gpu, z=z)
+    for o in range(O):
+        _, want = orc.sample_unicycle(init[o], None, gmm[o], N, T, 0.5, 5, ov=o, z=z[o])
+        _assert_cloud(store2.cell_positions(o), want)
+
+
+def test_sampler_per_particle_parameters(gpu):
+    """p_y_xz's decoder is autoregressive: every sample has its own GMM parameters per step
+    (O, N, T, 5).  GPU vs restatement on the same draws; and the per-particle path fed the
+    per-latent table gathered by z reproduces the per-latent path bit for bit."""
+    e = eng()
+    O, L, T, N = 2, 6, 12, 5000
+    init, pmf, gmm = _sampler_inputs(O, L, T, seed=8)
+    z, eps = _torch_draws(pmf, N, T, seed=3)
+    rng = np.random.default_rng(1)
+    pp = np.stack([gmm[o][z[o]] for o in range(O)])                     # (O, N, T, 5)
+    jitter = pp.copy()
+    jitter[..., 0] += rng.normal(0, 0.05, jitter[..., 0].shape).astype(np.float32)
+    jitter[..., 4] = np.clip(jitter[..., 4] + rng.normal(0, 0.3, jitter[..., 4].shape),
+                             -1, 1).astype(np.float32)                   # |rho| = 1: the clamp
+    _, s_pp = e.sample_unicycle(init, None, jitter, N, T, device=gpu, z=z, eps=eps,
+                                per_particle=True)
+    for o in range(O):
+        _, want = orc.sample_unicycle(init[o], None, jitter[o], N, T, 0.5, 0, ov=o, z=z[o],
+                                      eps=eps[o], per_particle=True)
+        got = s_pp.cell_positions(o)
+        assert np.all(np.isfinite(got))
+        _assert_cloud(got, want)
+    _, s_gather = e.sample_unicycle(init, None, pp, N, T, device=gpu, z=z, eps=eps,
+                                    per_particle=True)
+    _, s_lat = e.sample_unicycle(init, pmf, gmm, N, T, device=gpu, z=z, eps=eps)
+    for o in range(O):
+        np.testing.assert_array_equal(s_gather.cell_positions(o), s_lat.cell_positions(o))
+    # device tensors are accepted as they come out of torch
+    _, s_dev = e.sample_unicycle(init, None, torch.as_tensor(jitter, device=gpu), N, T,
+                                 device=gpu, z=torch.as_tensor(z, device=gpu),
+                                 eps=torch.as_tensor(eps, device=gpu), per_particle=True)
+    np.testing.assert_array_equal(s_dev.cell_positions(1), s_pp.cell_positions(1))
+
+
+def test_sampler_rejects_bad_injections(gpu):
+    e = eng()
+    O, L, T, N = 1, 4, 3, 100
+    init, pmf, gmm = _sampler_inputs(O, L, T)
+    z = np.zeros((O, N), np.int32)
+    z[0, 7] = L
+    with pytest.raises(ValueError):
+        e.sample_unicycle(init, pmf, gmm, N, T, device=gpu, z=z)
+    with pytest.raises(ValueError):
+        e.sample_unicycle(init, pmf, np.zeros((O, N, T, 5), np.float32), N, T, device=gpu,
+                          per_particle=True)
+    lib = e._lib.load()
+    rc = lib.ccmpc_sample_unicycle_ex(None, None, L, None, 1, None, None, 1, N, T, 0.5, 0, 0,
+                                      None, None, N, None)
+    assert rc == -1                     # CCMPC_ERR_INVALID: per-particle parameters need z_in

@@ -250,3 +250,30 @@ def test_predict_ideal_matches_reference_function(golden):
     for k in range(K):
         np.testing.assert_allclose(traj[0][k][g["rows"]], g["traj_rows"][k], rtol=1e-13)
         np.testing.assert_allclose(traj[0][k].mean(axis=0), g["traj_mean"][k], rtol=1e-12)
+
+
+def test_sampler_restatement_modes_agree():
+    """The sampler restatement's upstream-shaped modes (injected z / eps, per-particle GMM
+    parameters as p_y_xz emits them) reduce to the synthetic mode on the same draws.
+    PARITY UNPINNED upstream (Trajectron++ absent)."""
+    rng = np.random.default_rng(0)
+    L, T, n = 5, 6, 400
+    gmm = np.zeros((L, T, 5), np.float32)
+    gmm[..., 0] = rng.normal(0, 0.2, (L, T))
+    gmm[..., 1] = rng.normal(0, 1, (L, T))
+    gmm[..., 2:4] = np.log(rng.uniform(0.05, 0.5, (L, T, 2)))
+    gmm[..., 4] = rng.uniform(-0.9, 0.9, (L, T))
+    init = np.array([10.0, -3.0, 0.4, 6.0])
+    cdf = np.cumsum(np.full(L, 1.0 / L))
+    z, pos = orc.sample_unicycle(init, cdf, gmm, n, T, 0.5, 17, ov=2)
+    z2, pos2 = orc.sample_unicycle(init, None, gmm, n, T, 0.5, 17, ov=2, z=z)
+    np.testing.assert_array_equal(pos2, pos)
+    eps = rng.standard_normal((n, T, 2)).astype(np.float32)
+    _, a = orc.sample_unicycle(init, None, gmm, n, T, 0.5, 0, z=z, eps=eps)
+    _, b = orc.sample_unicycle(init, None, gmm[z], n, T, 0.5, 0, z=z, eps=eps, per_particle=True)
+    np.testing.assert_array_equal(a, b)
+    # |rho| = 1 stays finite through GMM2D's clamp of 1 - rho^2
+    pp = gmm[z].copy()
+    pp[..., 4] = 1.0
+    _, c = orc.sample_unicycle(init, None, pp, n, T, 0.5, 0, z=z, eps=eps, per_particle=True)
+    assert np.all(np.isfinite(c))
