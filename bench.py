@@ -45,15 +45,19 @@ def parse():
     ap.add_argument("--cpu-cycles", type=int, default=200)
     ap.add_argument("--graph", action="store_true",
                     help="time hipGraph replays of the cycle instead of direct C-ABI calls")
-    ap.add_argument("--sweep", action="store_true",
-                    help="also time the same kernel at the larger BASELINE configs (C3/C4/C5, "
-                         "ideal rollout) and report their roofline in 'roofline_sweep'")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip 'roofline_sweep' (the same kernel at C3's particle sweep, C5 and "
+                         "the fused ideal rollout)")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip 'c4_sharded' (BASELINE configs[3] sharded over the ranks)")
     return ap.parse_args()
 
 
-def time_config(dev, seed, name, O, N, T, scenes):
+def time_config(dev, seed, name, O, N, T, scenes, cold=True):
     """Kernel time and algorithmic HBM rate of the one-launch cycle (and of the moment
-    reduction alone) for one synthetic configuration."""
+    reduction alone) for one synthetic configuration: back to back on one store (warm: the
+    Infinity Cache holds stores up to 256 MiB) and, for stores of >= 8 MB, rotating over
+    distinct copies so that every launch streams from HBM (cold)."""
     from ccmpc import cycle, engine, synthetic
     cells, K, refs = [], [], []
     for sc in range(scenes):
@@ -68,11 +72,17 @@ def time_config(dev, seed, name, O, N, T, scenes):
     tm = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev,
                           per_graph=10, replays=5)
     b = int(sum(store.counts)) * 2 * T * 8
-    return {"config": name, "particles": int(sum(store.counts)), "T": T,
-            "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
-            "alg_GBps": round(b / t / 1e9, 1), "frac": round(b / t / HBM_PEAK, 4),
-            "moments_only_us": round(tm * 1e6, 2),
-            "moments_only_frac": round(b / tm / HBM_PEAK, 4)}
+    row = {"config": name, "particles": int(sum(store.counts)), "T": T,
+           "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
+           "alg_GBps": round(b / t / 1e9, 1), "frac": round(b / t / HBM_PEAK, 4),
+           "moments_only_us": round(tm * 1e6, 2),
+           "moments_only_frac": round(b / tm / HBM_PEAK, 4)}
+    if cold:
+        tc, k = cold_time(cyc, dev, store.pos.numel() * store.pos.element_size())
+        if tc is not None:
+            row.update({"cold_kernel_us": round(tc * 1e6, 2),
+                        "cold_frac": round(b / tc / HBM_PEAK, 4), "cold_copies": k})
+    return row
 
 
 C4_GPU = ("C4/GPU@8: 8 scenes x 4 OVs np=20000 T=12", 4, 20000, 12, 8)
@@ -84,7 +94,7 @@ def sweep(dev, seed):
     from ccmpc import engine, risk, synthetic
     configs = [("C3 np=1000 O=1 T=8", 1, 1000, 8, 1), ("C3 np=5000 O=1 T=8", 1, 5000, 8, 1),
                ("C3 np=20000 O=1 T=8", 1, 20000, 8, 1), ("C3 np=100000 O=1 T=8", 1, 100000, 8, 1),
-               C4_GPU, ("C5 O=8 np=50000 T=40", 8, 50000, 40, 1)]
+               ("C5 O=8 np=50000 T=40", 8, 50000, 40, 1)]
     rows = [time_config(dev, seed, *c) for c in configs]
     # shrinking-horizon step: 1e6-sample ideal rollout fused with moments + half-spaces
     ovs, ref, _ = synthetic.scene(seed + 7, O=1, N=100000, T=8, K=2)
@@ -102,6 +112,88 @@ def sweep(dev, seed):
                  "particles": 2_000_000, "T": 7, "kernel_us": round(t * 1e6, 2),
                  "samples_per_s": round(2e6 * 7 / t, 1)})
     return rows
+
+
+C4_FULL = {"scenes": 64, "O": 4, "N": 20000, "T": 12}
+
+
+def c4_sharded(dev, seed, world, rank, steps=20, warmup=3):
+    """BASELINE.json configs[3] as the node runs it: 64 independent scenes x 4 OVs x np=20000,
+    ph=12, sharded over the ranks in contiguous scene blocks (ccmpc.dist.scene_range; strong
+    scaling: the batch is fixed).  One step = every rank's ccmpc_minkowski_cycle over its
+    scenes + the RCCL all-gather of the fixed-size half-space records (the north star's one
+    exchange), timed between barriers, max over ranks.  Also the rank's kernel alone, back to
+    back (warm) and rotating over distinct stores (cold HBM), as its HBM fraction."""
+    from ccmpc import cycle, dist as cdist, engine, synthetic
+    c = C4_FULL
+    b, e = cdist.scene_range(c["scenes"], rank, world)
+    cells, K, refs = [], [], []
+    for sc in range(b, e):
+        ovs, ref, _ = synthetic.scene(seed + 1000 + sc, O=c["O"], N=c["N"], T=c["T"])
+        cells += [x for o in ovs for x in o]
+        K.append([len(o) for o in ovs])
+        refs.append(ref)
+    store = engine.ParticleStore.from_cells(cells, device=dev)
+    cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], np.array(refs), scene_K=K)
+    launch = cyc.bind().launch
+    gather = None
+    if world > 1:
+        import torch.distributed as dist
+        gloo = dist.get_backend() == "gloo"
+        counts = cdist.record_counts(store.n_cells, "cpu" if gloo else dev)
+        gather = ((lambda: cdist.gather_records(cyc.rec.cpu(), counts=counts)) if gloo else
+                  (lambda: cdist.gather_records(cyc.rec, counts=counts)))
+
+    def step():
+        launch()
+        if gather is not None:
+            gather()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev) / steps
+    h = cyc.records().reshape(-1)
+    ok = bool(np.all(h["status"] == 0))
+    n_part = int(sum(store.counts))
+    alg = n_part * 2 * c["T"] * 8
+    t_warm = time_kernel_live(cyc.run, dev, per_graph=5, replays=4)
+    t_cold, k = cold_time(cyc, dev, store.pos.numel() * store.pos.element_size())
+    n_rec_local = cyc.n_constraints
+    n_rec = sum_over_ranks(n_rec_local, world, dev)
+    t_warm_max = max_over_ranks(t_warm, world, dev)
+    out = {
+        "config": "C4: 64 scenes x 4 OVs, np=20000/OV, ph=12, contiguous scene blocks per rank",
+        "scaling": "strong", "n_gpus": world, "scenes_per_rank": e - b,
+        "step_us": round(elapsed * 1e6, 2), "scenes_per_s": round(c["scenes"] / elapsed, 1),
+        "constraints_per_step": int(n_rec),
+        "constraints_per_s": round(n_rec / elapsed, 1),
+        "record_gather": ("none (N=1)" if world == 1 else
+                          ("RCCL" if _backend() == "nccl" else _backend())
+                          + " all_gather of every rank's records, inside the step"),
+        "rank0": {"particles": n_part, "cells": store.n_cells, "alg_bytes_per_launch": alg,
+                  "kernel_us_warm": round(t_warm * 1e6, 2),
+                  "hbm_frac_warm": round(alg / t_warm / HBM_PEAK, 4)},
+        "slowest_rank_kernel_us_warm": round(t_warm_max * 1e6, 2),
+        "records_ok": ok,
+    }
+    if t_cold is not None:
+        out["rank0"].update({"kernel_us_cold": round(t_cold * 1e6, 2),
+                             "hbm_frac_cold": round(alg / t_cold / HBM_PEAK, 4),
+                             "cold_copies": k})
+    return out
+
+
+def _backend():
+    import torch.distributed as dist
+    return dist.get_backend() if dist.is_initialized() else None
 
 
 def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True):
@@ -197,21 +289,35 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
+def sum_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    gloo = dist.get_backend() == "gloo"
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if gloo else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def time_kernel_live(fn, dev, per_graph=50, replays=20):
     """Average device time of one launch of `fn`: `per_graph` launches captured back to back
     into one hipGraph, replayed `replays` times between two HIP events on the capturing
     stream (no host launch overhead in the interval; each launch still pays its kernel
-    boundary, which rocprof's per-kernel duration does not include)."""
+    boundary, which rocprof's per-kernel duration does not include).  `fn` may be a list of
+    callables: launch i runs fn[i % len(fn)] (rotation over distinct buffers, cold_copies)."""
+    fns = list(fn) if isinstance(fn, (list, tuple)) else [fn]
+    per_graph = max(per_graph, len(fns))
     s = torch.cuda.Stream(device=dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
         for _ in range(3):
-            fn()
+            for f in fns:
+                f()
     torch.cuda.current_stream(dev).wait_stream(s)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        for _ in range(per_graph):
-            fn()
+        for i in range(per_graph):
+            fns[i % len(fns)]()
     g.replay()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -221,6 +327,48 @@ def time_kernel_live(fn, dev, per_graph=50, replays=20):
     ev1.record()
     ev1.synchronize()
     return ev0.elapsed_time(ev1) * 1e-3 / (per_graph * replays)
+
+
+MALL_BYTES = 256 << 20     # MI355X_MICROARCH.md: 256 MiB Infinity Cache in front of HBM
+
+
+def cold_copies(store_bytes, cap=64):
+    """Distinct copies of a store to rotate through so that every launch reads HBM, not the
+    Infinity Cache (FETCH_SIZE counts its hits): >= 3 copies and >= 2x the cache in total; None
+    when that would take more than `cap` copies (small stores are latency-bound anyway)."""
+    k = max(3, -(-2 * MALL_BYTES // max(int(store_bytes), 1)))
+    return k if k <= cap else None
+
+
+def clone_cycle(cyc):
+    """The same cycle over a fresh copy of its particle store (own buffers and workspace)."""
+    import copy
+    from ccmpc import cycle
+    st = copy.copy(cyc.store)
+    st.pos = cyc.store.pos.clone()
+    c = cycle.MinkowskiCycle.__new__(cycle.MinkowskiCycle)
+    c.__dict__.update(cyc.__dict__)
+    c.store = st
+    c.mean, c.cov = torch.empty_like(cyc.mean), torch.empty_like(cyc.cov)
+    c.rec, c.prob_lower = torch.empty_like(cyc.rec), torch.empty_like(cyc.prob_lower)
+    from ccmpc import engine
+    c.ws = engine.Workspace(st.device)
+    c.ws.get(cyc.ws.buf.numel())
+    c.graph = None
+    return c
+
+
+def cold_time(cyc, dev, store_bytes):
+    """Average launch time with every launch reading its particles from HBM (rotation over
+    cold_copies distinct stores), or None for stores too small to rotate."""
+    k = cold_copies(store_bytes)
+    if k is None:
+        return None, None
+    cycles = [cyc] + [clone_cycle(cyc) for _ in range(k - 1)]
+    t = time_kernel_live([c.run for c in cycles], dev, per_graph=4 * k, replays=3)
+    del cycles
+    torch.cuda.empty_cache()
+    return t, k
 
 
 def host_cpu():
@@ -491,28 +639,10 @@ def main():
                       "oracle restatement of v8ideal/__init__.py:881-947 (numpy/scipy)",
         }
         out["speedup_vs_cpu"] = round(value / (1.0 / med), 1)
-    if world > 1:
-        # the north star's one exchange: every rank's fixed-size half-space records gathered
-        # over RCCL (xGMI).  The QP of a scene stays on its owning rank, so this is reported
-        # beside `value`, not inside the timed step.
-        import torch.distributed as dist
-        from ccmpc import dist as cdist
-        rec2 = cyc.rec.view(cyc.rec.shape[0], -1, 128)
-        if dist.get_backend() == "gloo":
-            rec2 = rec2.cpu()
-        for _ in range(5):
-            cdist.gather_records(rec2)
-        torch.cuda.synchronize(dev)
-        barrier(world)
-        tg = time.perf_counter()
-        for _ in range(50):
-            cdist.gather_records(rec2)
-        torch.cuda.synchronize(dev)
-        tg = max_over_ranks((time.perf_counter() - tg) / 50, world, dev)
-        out["record_allgather"] = {"us": round(tg * 1e6, 2),
-                                   "bytes_per_rank": int(rec2.numel()),
-                                   "backend": "RCCL" if dist.get_backend() == "nccl" else
-                                   dist.get_backend()}
+    if not args.no_c4:
+        # BASELINE configs[3]: the 64-scene batch sharded over the ranks, the record gather
+        # (RCCL) inside the step; every rank takes part
+        out["c4_sharded"] = c4_sharded(dev, args.seed, world, rank)
     if rank == 0:
         # C2 is launch/latency-bound (2.56 MB per cycle); the HBM roofline of the
         # same kernel is meaningful at the per-GPU C4 batch, reported beside it
@@ -526,7 +656,7 @@ def main():
         with threadpool_limits(limits=1):
             out["episode_c1"] = episode_c1(dev, with_cpu=not args.no_cpu)
             out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
-    if args.sweep and rank == 0:
+    if not args.no_sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)
     if rank == 0:
         print(json.dumps(out), flush=True)
