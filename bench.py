@@ -473,6 +473,105 @@ def episode_c1(dev, cpu_steps=2, with_cpu=True):
     return out
 
 
+def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8):
+    """The drop-in planning step at C2's shape (O = 4 OVs, np = 5000, ph = 8) through
+    MidlevelAgent.predict_and_constrain: do_prediction (the sampler tail) + make_ovehicles +
+    compute_obstacle_constraints_GMM_Minkowski_idealprediction (v8ideal/__init__.py:414-505,
+    :781-964) -- one hipGraph replay per step with the packed input upload and the record /
+    moment / L4 download inside it, then the 9-tuple on the host (constraints built lazily).
+    A fresh Philox seed per step.  Beside it: the same step through the eager drop-in calls,
+    and the oracle's make_ovehicles + Minkowski generator (with vertices / L4) on the same
+    sampler output, on one host core."""
+    from ccmpc import engine, episode, ovehicle, planner
+    init, pmf, gmm = episode.synthetic_gmm(O, T=ph, seed=20251015)
+    minpos = np.array([150.0, -120.0])
+    pasts = [np.array([[minpos[0] + init[o, 0] - 2.0, minpos[1] + init[o, 1]]])
+             for o in range(O)]
+    K = [int(np.count_nonzero(pmf[o] > 0.1)) for o in range(O)]
+    eps = np.full((O, max(K)), 0.05 / O)
+    ego = np.array([165.0, -72.0])
+    ref = np.array([ego + [4.0 * (t + 1), 0.5 * (t + 1)] for t in range(ph)])
+    agent = planner.MidlevelAgent(prediction_horizon=ph, device=dev)
+    params = episode.Params(O, K, 0)
+
+    def graph_step(seed):
+        sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=seed)
+        return agent.predict_and_constrain(params, sampler, eps, ph, ref, minpos, pasts)
+
+    for i in range(20):
+        graph_step(i)
+    ts = []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        _, out = graph_step(1000 + i)
+        ts.append(time.perf_counter() - t0)
+    n_cons = len(out[0])
+    g = next(iter(agent._graphs.values()))
+    t_graph = time_graph_replay(g, dev)
+
+    eager = planner.MidlevelAgent(prediction_horizon=ph, device=dev)
+
+    def eager_step(seed):
+        z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=seed, device=dev)
+        ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, device=dev)
+        return eager.compute_obstacle_constraints_GMM_Minkowski_idealprediction(
+            params, ovs, None, None, None, eps, None, ph, ref)
+
+    for i in range(5):
+        eager_step(i)
+    te = []
+    for i in range(50):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        eager_step(2000 + i)
+        te.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    res = {"config": f"C2 shape drop-in step: {O} OVs x np={N} x ph={ph}, L=25 latent values, "
+                     f"K={K} kept modes; sampler -> bucketing -> Minkowski cycle -> L4 -> "
+                     "9-tuple (MidlevelAgent.predict_and_constrain)",
+           "steps": steps, "constraints_per_step": n_cons,
+           "dropin_step_us_median": round(med * 1e6, 1),
+           "dropin_step_us_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
+           "graph_replay_us": round(t_graph * 1e6, 1),
+           "eager_calls_step_us_median": round(statistics.median(te) * 1e6, 1),
+           "note": "wall clock per call on the host, inputs from host memory, outputs (records, "
+                   "moments, L4, statistics) on the host when it returns; graph_replay_us = "
+                   "HIP events around back-to-back replays (packed H2D + 5 kernels + packed D2H)"}
+    if with_cpu:
+        from oracle import ccmpc_oracle as orc
+        z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=7, device=dev)
+        zc = z.cpu().numpy()
+        pred = np.stack([store.cell_positions(o) for o in range(O)]).astype(np.float32)
+        tc = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            oovs = orc.make_ovehicles(pred, zc, pmf, minpos, pasts, [np.array([4.5, 2.5])] * O,
+                                      ph)
+            orc.minkowski_generator(oovs, ph, ph, ref, with_l4=True)
+            tc.append(time.perf_counter() - t0)
+        cpu = statistics.median(tc)
+        res["cpu_oracle_step_ms"] = round(cpu * 1e3, 2)
+        res["speedup_vs_cpu_step"] = round(cpu / med, 1)
+        res["cpu_note"] = ("oracle make_ovehicles + Minkowski generator with vertices/L4 on the "
+                           "same sampler output, median of 5, 1 BLAS thread (the reference "
+                           "path's own work; its Trajectron++ sampler is not counted)")
+    return res
+
+
+def time_graph_replay(g, dev, n=200):
+    """HIP-event time per replay of a captured step graph, back to back."""
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(10):
+        g.graph.replay()
+    torch.cuda.synchronize(dev)
+    ev0.record()
+    for _ in range(n):
+        g.graph.replay()
+    ev1.record()
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) * 1e-3 / n
+
+
 def pmc_traffic(kernel_prefix):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
     (kernel_prefix stops before the balanced-mode template flag, so both names match)
@@ -654,6 +753,7 @@ def main():
     if rank == 0 and world == 1:
         from threadpoolctl import threadpool_limits
         with threadpool_limits(limits=1):
+            out["dropin_step_c2"] = dropin_step(dev, with_cpu=not args.no_cpu)
             out["episode_c1"] = episode_c1(dev, with_cpu=not args.no_cpu)
             out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
     if not args.no_sweep and rank == 0:

@@ -56,6 +56,7 @@ SIGNATURES = {
     "ccmpc_abi_version": (ctypes.c_int, []),
     "ccmpc_last_error": (ctypes.c_char_p, []),
     "ccmpc_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "ccmpc_copy_async": (ctypes.c_int, [_P, _P, _SZ, _P]),
     "ccmpc_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "ccmpc_moments": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64, _I64, _P,
                                      _SZ, _P, _P, _P]),
@@ -71,7 +72,7 @@ SIGNATURES = {
     "ccmpc_sample_unicycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _D, _U64, _I64,
                                              _P, _P, _I64, _P]),
     "ccmpc_sample_unicycle_ex": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P, _P, _I64, _I64, _I64,
-                                                _D, _U64, _I64, _P, _P, _I64, _P]),
+                                                _D, _U64, _P, _I64, _P, _P, _I64, _P]),
     "ccmpc_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "ccmpc_bucket": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _I64, _P,
                                     _P, _P, _SZ, _P, _I64, _P, _P, _P, _P, _P]),

@@ -288,7 +288,8 @@ def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="c
     t_init = torch.as_tensor(init_state, device=dev)
     _lib.check(lib.ccmpc_sample_unicycle_ex(
         _p(t_init), _p(t_cdf), L, _p(t_gmm), layout, _p(t_z), _p(t_eps), O, N, T, float(dt),
-        int(seed) & (2**64 - 1), int(ov_base), _p(out_z), _p(store.pos), store.ld, _stream()),
+        int(seed) & (2**64 - 1), None, int(ov_base), _p(out_z), _p(store.pos), store.ld,
+        _stream()),
         "ccmpc_sample_unicycle_ex")
     store._keepalive = (t_init, t_cdf, t_gmm, t_z, t_eps)
     return out_z, store
@@ -425,7 +426,7 @@ def bucket(z, sample_store, latent_pmf, minpos, filter_pmf=0.1, max_k=None):
     pmf_out = torch.empty(n_cells, dtype=torch.float64, device=dev)
     centre = torch.empty((n_cells, 2), dtype=torch.float64, device=dev)
     need = lib.ccmpc_bucket_workspace_bytes(O, N, L, max_k)
-    ws = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(max(need, 16), dtype=torch.uint8, device=dev)   # zero-filled head: counters
     _lib.check(lib.ccmpc_bucket(_p(z), _p(sample_store.pos), sample_store.ld, T, O, N, L,
                                 _p(t_keep), _p(t_nk), _p(t_base), max_k, _p(t_min), _p(t_reg),
                                 _p(ws), ws.numel(), _p(out.pos), out.ld, _p(out.cell_off),

@@ -13,6 +13,10 @@ from . import engine
 DEFAULT_BBOX = np.array([4.5, 2.5])   # ovehicle.py:19
 
 
+def _host(x):
+    return x.cpu().numpy() if torch.is_tensor(x) else np.array(x)
+
+
 class ScenePredictions:
     """Bucketed particle clouds of all OVs of one planning step (cells in (ov, k) order)."""
 
@@ -80,14 +84,14 @@ class OVehicle:
             st.sync_counts() if st.counts is None else None
             n = np.array([st.counts[c] for c in self.cells], float)
             return n / n.sum()
-        return self.scene.cell_pmf[self.cells[0]:self.cells[-1] + 1].cpu().numpy()
+        return _host(self.scene.cell_pmf[self.cells[0]:self.cells[-1] + 1])
 
     @property
     def init_center(self):
         if self.scene.init_center is None:
             return np.array([self.pred_positions[k][:, self.T - 1].mean(0)
                              for k in range(self.n_states)])
-        return self.scene.init_center[self.cells[0]:self.cells[-1] + 1].cpu().numpy()
+        return _host(self.scene.init_center[self.cells[0]:self.cells[-1] + 1])
 
     @property
     def n_predictions(self):

@@ -113,6 +113,81 @@ class _VertTK:
         return v[8 * self.t:8 * self.t + 8, o:o + n].T.cpu().numpy().reshape(n, 4, 2)
 
 
+class HalfSpaceList:
+    """The generator's `constraints` list over one host copy of the record block: HalfSpace
+    objects are built when read (a planning step's records come back in one D2H; building
+    hundreds of Python objects per step would cost more than the whole GPU step).  Checking
+    the statuses happens up front, vectorised: the first failed record in the reference's
+    (cell, t, tau) order raises the reference's exception (_lib.record_error)."""
+
+    def __init__(self, h, cell_of, P, what="constraint"):
+        self._h = h.reshape(len(cell_of), -1)[:, :P]
+        self._cell_of = cell_of
+        self._P = self._h.shape[1]
+        st = self._h["status"].reshape(-1)
+        bad = np.flatnonzero(st != 0)
+        if bad.size:
+            c, p = divmod(int(bad[0]), self._P)
+            r = self._h[c, p]
+            o, k = cell_of[c]
+            raise engine._lib.record_error(
+                r["status"], f"{what} (ov={o}, k={k}, t={r['t_tau'] >> 16}, tau="
+                             f"{r['t_tau'] & 0xFFFF})")
+
+    def __len__(self):
+        return len(self._cell_of) * self._P
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        c, p = divmod(i, self._P)
+        r = self._h[c, p]
+        o, k = self._cell_of[c]
+        tt = int(r["t_tau"])
+        return HalfSpace(o, k, tt >> 16, tt & 0xFFFF, np.array([r["n0"], r["n1"]]),
+                         float(r["d"]), float(r["d"]), int(r["side"]), int(r["which"]))
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
+class UnionGrid:
+    """A_union / b_union [t][k][ov] (v8ideal/__init__.py:627-736) over a host array [cell, t,
+    ...]: None where OV `ov` has no mode k, as the reference's nested lists hold."""
+
+    def __init__(self, arr, K, ph):
+        self._arr, self._K, self._ph = arr, list(K), ph
+        self._first = np.concatenate([[0], np.cumsum(K)[:-1]]).astype(int)
+
+    def __len__(self):
+        return self._ph
+
+    def __getitem__(self, t):
+        if not 0 <= t < self._ph:
+            raise IndexError(t)
+        grid = self
+
+        class _K:
+            def __len__(self):
+                return max(grid._K)
+
+            def __getitem__(self, k):
+                class _O:
+                    def __len__(self):
+                        return len(grid._K)
+
+                    def __getitem__(self, ov):
+                        if k >= grid._K[ov]:
+                            return None
+                        return grid._arr[grid._first[ov] + k, t]
+                return _O()
+        return _K()
+
+
 def _match_modes(mean_loaded, x_init, cur_means, n_states, M_big):
     """Previous-frame mode per current mode: argmin of ||x_init - mean'_0|| + sum_t ||mean_t -
     mean'_{t+1}||, modes >= n_states (and missing ones) scored M_big, first minimum on ties
@@ -134,6 +209,11 @@ def _match_modes(mean_loaded, x_init, cur_means, n_states, M_big):
         md[n_states:] = M_big
         picks.append(int(np.argmin(md)))
     return picks
+
+
+def _host(x):
+    """NumPy view of a saved moment array (device tensor or host copy)."""
+    return x.cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
 
 
 def _object_grid(*shape):
@@ -230,8 +310,20 @@ class MidlevelAgent:
         self.mpc_params = mpc.MPCParams.reference_defaults()
         self._ltv = None                   # (x_init, T_full) -> (xbar, Gamma), first step's
         self._qp = {}
+        self._graphs = {}                  # (O, N, ph, L, K) -> step.MinkowskiStepGraph
+        self._risk_memo = {}
 
     # ------------------------------------------------------------------------------------
+    def _saved(self, frame):
+        """Saved moments of `frame` as device tensors (a graph step keeps host copies; they are
+        uploaded once, when a later step first needs them), or None."""
+        e = self._moments.get(frame)
+        if e is not None and not torch.is_tensor(e[0]):
+            e = (torch.as_tensor(e[0], device=self.device),
+                 torch.as_tensor(e[1], device=self.device), e[2], e[3])
+            self._moments[frame] = e
+        return e
+
     def _scene(self, ovehicles):
         """All OVs must share one ScenePredictions (the fast path); otherwise pack them."""
         scenes = {id(ov.scene) for ov in ovehicles}
@@ -243,8 +335,16 @@ class MidlevelAgent:
         return ScenePredictions(store, [len(c) for c in cells],
                                 [ov.past[-1] for ov in ovehicles], [ov.bbox for ov in ovehicles])
 
-    def _cell_risk(self, eps_ura, K):
-        """Per-cell (chi_r, chi_p, gamma) from the caller's eps_ura (:910-913)."""
+    def _cell_risk_host(self, eps_ura, K):
+        """Per-cell (chi_r, chi_p, gamma) from the caller's eps_ura (:910-913), host array
+        (memoised per (eps_ura, K): a planner asks for the same allocation every step)."""
+        key = (eps_ura.tobytes(), eps_ura.shape, tuple(K))
+        hit = self._risk_memo.get(key)
+        if hit is None:
+            hit = self._risk_memo[key] = self._cell_risk_rows(eps_ura, K)
+        return hit
+
+    def _cell_risk_rows(self, eps_ura, K):
         ph = self.prediction_horizon
         chi_p = risk._chi2_ppf2(risk.TARGET_P)
         rows = []
@@ -252,18 +352,25 @@ class MidlevelAgent:
             for k in range(k_o):
                 e = float(eps_ura[o, k]) / ph
                 rows.append((risk._chi2_ppf2(1 - e), chi_p, risk._norm_ppf(1 - e)))
-        return torch.as_tensor(np.asarray(rows, np.float64).reshape(-1, 3), device=self.device)
+        return np.asarray(rows, np.float64).reshape(-1, 3)
+
+    def _cell_risk(self, eps_ura, K):
+        return torch.as_tensor(self._cell_risk_host(eps_ura, K), device=self.device)
 
     def _ref(self, ref_traj, T):
         ref = np.asarray([[ref_traj[t][0], ref_traj[t][1]] for t in range(T)], np.float64)
         return torch.as_tensor(ref.reshape(1, T, 2), device=self.device)
 
-    def _state_stats(self, scene, mean0, cov0):
-        """ovStateMean/Cov_tau_1 (:864-875): t = 0 mean / variance of x, y, yaw per (ov, k)."""
+    def _state_stats(self, scene, mean0, cov0, yaw=None):
+        """ovStateMean/Cov_tau_1 (:864-875): t = 0 mean / variance of x, y, yaw per (ov, k).
+        yaw = (yaw_mean at t = 0 [C], yaw0_var [C]) when already on the host."""
         O, K = scene.O, scene.K
         maxK = max(K)
-        l4 = scene.l4()
-        ym, yv = l4["yaw_mean"][:, 0].cpu().numpy(), l4["yaw0_var"].cpu().numpy()
+        if yaw is None:
+            l4 = scene.l4()
+            ym, yv = l4["yaw_mean"][:, 0].cpu().numpy(), l4["yaw0_var"].cpu().numpy()
+        else:
+            ym, yv = yaw
         mx, my, myaw, vx, vy, vyaw = (_object_grid(O, maxK) for _ in range(6))
         c = 0
         for o in range(O):
@@ -312,20 +419,7 @@ class MidlevelAgent:
         return torch.as_tensor(np.asarray(src, np.int32), device=self.device)
 
     def _records_to_halfspaces(self, h, scene, T):
-        cons = []
-        P = T * (T - 1) // 2
-        for c, (o, k) in enumerate(scene.cell_of):
-            for p in range(P):
-                r = h[c, p]
-                if r["status"] != 0:
-                    raise engine._lib.record_error(
-                        r["status"], f"constraint (ov={o}, k={k}, t={r['t_tau'] >> 16}, tau="
-                                     f"{r['t_tau'] & 0xFFFF})")
-                n = np.array([r["n0"], r["n1"]])
-                cons.append(HalfSpace(o, k, int(r["t_tau"] >> 16), int(r["t_tau"] & 0xFFFF), n,
-                                      float(r["d"]), float(r["d"]), int(r["side"]),
-                                      int(r["which"])))
-        return cons
+        return HalfSpaceList(h, scene.cell_of, T * (T - 1) // 2)
 
     # ------------------------------------------------------------------------------------
     def compute_obstacle_constraints_GMM_Minkowski_idealprediction(
@@ -342,7 +436,7 @@ class MidlevelAgent:
         ref = self._ref(ref_traj, T)
         m_scene, c_scene = engine.moments(scene.store, workspace=self._ws) if T < ph else (None, None)
         if T < ph:
-            prev = self._moments.get(params.frame - self.record_interval)
+            prev = self._saved(params.frame - self.record_interval)
             if prev is None:
                 raise KeyError(f"no moments saved for frame {params.frame - self.record_interval}"
                                " (the reference fails to load its pickle here)")
@@ -439,7 +533,7 @@ class MidlevelAgent:
         m_scene, c_scene = engine.moments(scene.store, workspace=self._ws)
         tangent = const_idx = None
         if T < ph:
-            prev = self._moments.get(params.frame - self.record_interval)
+            prev = self._saved(params.frame - self.record_interval)
             if prev is None:
                 raise KeyError(f"no moments saved for frame {params.frame - self.record_interval}")
             src = self._src_cells(prev[2], K)
@@ -487,6 +581,74 @@ class MidlevelAgent:
         vertices, A_union, b_union = self._l4_lists(scene)
         return (cons, vertices, A_union, b_union, self._ov_in_junction(scene, mean0),
                 _object_grid(scene.O), st_mean, st_cov, meanNtangent)
+
+    def predict_and_constrain(self, params, sampler, eps_ura, Tsh, ref_traj, minpos, pasts,
+                              bboxes=None, filter_pmf=0.1):
+        """One planning frame's prediction + Minkowski constraint generation, as
+        do_highlevel_control runs them (v8ideal/__init__.py:2934-2976): do_prediction
+        (:414-467, the sampler tail of prediction.py:81-86), make_ovehicles (:469-505) and
+        compute_obstacle_constraints_GMM_Minkowski_idealprediction (:781-964).
+
+        sampler: dict(init_state (O, 4), latent_pmf (O, L), gmm (O, L, ph, 5), N, seed) -- the
+        per-latent sampler inputs.  At Tsh == ph the whole chain is ONE hipGraph replay
+        (ccmpc.step.MinkowskiStepGraph, cached per (O, N, ph, L, K)): inputs up in one copy, five
+        kernels, outputs down in one copy, then the 9-tuple over host views (constraints built
+        lazily).  Below ph the generator runs on the saved moments' ideal rollout, after the
+        same sampler and bucketing calls.  Returns (ovehicles, 9-tuple).  The OVehicles and the
+        device records stay valid until the next graph step of the same shape."""
+        from . import ovehicle, step
+        T, ph = int(Tsh), self.prediction_horizon
+        init = np.asarray(sampler["init_state"], np.float64)
+        pmf = np.asarray(sampler["latent_pmf"], np.float64)
+        O, L = pmf.shape
+        N, seed = int(sampler["N"]), int(sampler["seed"])
+        gmm = sampler["gmm"]
+        pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
+        past_last = np.array([p[-1] for p in pasts])
+        bboxes = (np.tile(ovehicle.DEFAULT_BBOX, (O, 1)) if bboxes is None
+                  else np.asarray(bboxes, np.float64).reshape(O, 2))
+        if T != ph:
+            z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=seed,
+                                              device=self.device)
+            ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, bboxes,
+                                          filter_pmf=filter_pmf, device=self.device)
+            out = self.compute_obstacle_constraints_GMM_Minkowski_idealprediction(
+                params, ovs, None, None, None, eps_ura, None, T, ref_traj)
+            return ovs, out
+        K = [int(np.count_nonzero(pmf[o] > filter_pmf)) for o in range(O)]
+        if min(K) == 0:
+            raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent "
+                             f"mode with p(z|x) > {filter_pmf} (ovehicle.py:96-97)")
+        key = (O, N, ph, L, tuple(K))
+        g = self._graphs.get(key)
+        if g is None:
+            g = step.MinkowskiStepGraph(O, N, ph, L, K, device=self.device, R=self.R)
+            self._graphs[key] = g
+        g.set_inputs(seed, init, pmf, gmm, minpos, ref_traj,
+                     self._cell_risk_host(np.asarray(eps_ura), K),
+                     np.repeat(past_last, K, axis=0), np.repeat(bboxes, K, axis=0),
+                     filter_pmf=filter_pmf)
+        g.replay()
+        o = g.out.snapshot()            # every output in one host copy (outlives the replay)
+        st = g.store
+        st.counts = o["cnt"].tolist()
+        st.offsets = o["off"].tolist()
+        scene = ovehicle.ScenePredictions(st, K, past_last, bboxes, o["pmf"], o["centre"])
+        ovs = [ovehicle.OVehicle(scene, j, past=pasts[j]) for j in range(O)]
+        h = o["rec"].reshape(-1).view(engine._lib.HALFSPACE_DTYPE).reshape(g.C, g.P)
+        constraints = HalfSpaceList(h, scene.cell_of, T * (T - 1) // 2)
+        self.last_records = h
+        self._last_rec = (g.out.d("rec"), mpc.REC_HALFSPACE, T)
+        mean, cov = o["mean"], o["cov"]
+        self._moments[params.frame] = (mean, cov, list(K), T)     # save_moments (:960)
+        self.prob_lower_save = list(o["pl"][-1])                  # last cell wins (:947, :961)
+        mean0, cov0 = mean[:, 0, :], cov[:, 0:2, 0:2]
+        st_mean, st_cov = self._state_stats(scene, mean0, cov0,
+                                            (o["yaw_mean"][:, 0], o["yaw0_var"]))
+        out = (constraints, LazyVertices(scene, ph), UnionGrid(o["A"], K, ph),
+               UnionGrid(o["b"], K, ph), self._ov_in_junction(scene, mean0),
+               _object_grid(O), st_mean, st_cov, 0)
+        return ovs, out
 
     def solve_planning_qp(self, x_init, goal, ref_traj, Tsh, u_prev=None, lon=3.7,
                           u_order=mpc.U_ORDER_F):
@@ -616,7 +778,7 @@ class MidlevelAgent:
         """The reference's pickle content for `frame`: dict(mean_p0p1, cov_p0p1, cross_cov)
         as nested lists [ov][k][t] (and [ov][k][t][tau])."""
         mean, cov, K, T = self._moments[frame]
-        mean, cov = mean.cpu().numpy(), cov.cpu().numpy()
+        mean, cov = _host(mean), _host(cov)
         O, maxK = len(K), max(K)
         mp, cp_, xc = _object_grid(O, maxK, T), _object_grid(O, maxK, T), _object_grid(O, maxK, T, T - 1)
         c = 0
@@ -633,7 +795,7 @@ class MidlevelAgent:
     def save_moments_npz(self, frame, path):
         """Write the saved moments of `frame` with the reference pickle's keys (flattened)."""
         mean, cov, K, T = self._moments[frame]
-        np.savez(path, mean=mean.cpu().numpy(), cov=cov.cpu().numpy(), K=np.asarray(K), T=T)
+        np.savez(path, mean=_host(mean), cov=_host(cov), K=np.asarray(K), T=T)
 
     def load_moments_npz(self, frame, path):
         d = np.load(path, allow_pickle=False)
@@ -644,7 +806,9 @@ class MidlevelAgent:
     def predict_ideal(self, ovehicles, T, ego_vehicle_id, params):
         """v8ideal/__init__.py:2620-2711, materialised: traj_all[ov][k] = (n_ideal, T, 2).
         (The generator never materialises these; it fuses the rollout with the moments.)"""
-        prev = self._moments[params.frame - self.record_interval]
+        prev = self._saved(params.frame - self.record_interval)
+        if prev is None:
+            raise KeyError(f"no moments saved for frame {params.frame - self.record_interval}")
         K = [ov.n_states for ov in ovehicles]
         src = self._src_cells(prev[2], K)
         seed = (self.seed * 1_000_003 + int(params.frame)) & (2**63 - 1)

@@ -1,0 +1,222 @@
+"""One planning step of v8ideal's prediction + constraint path as ONE hipGraph replay.
+
+Per planning frame the reference runs (v8ideal/__init__.py:2934-2976 -> :414-505, :781-964):
+
+    do_prediction       Trajectron++ sample (prediction.py:81-86)
+    make_ovehicles      bucketing by latent mode (:469-505, ovehicle.py:24-117)
+    generator           compute_obstacle_constraints_GMM_Minkowski_idealprediction at Tsh == ph
+                        (moments -> MVOE half-spaces, vertices / L4, t = 0 state statistics)
+
+For a fixed shape (OVs, particles, horizon, latent count and kept modes per OV) the whole chain
+is five kernels that need nothing from the host between them: the sampler, the bucketing, the
+one-launch Minkowski cycle and the L4 kernel read the bucketed cell counts on the device.  So
+``MinkowskiStepGraph`` captures
+
+    packed H2D of the step's host inputs  ->  sampler  ->  bucketing  ->  { cycle | L4 }
+    ->  packed D2H of every output the 9-tuple needs
+
+(the cycle and the L4 kernel are parallel branches of the graph: both only read the bucketed
+store)
+
+into one graph.  A step is: write the inputs into pinned memory, replay, wait for the stream,
+read the outputs through zero-copy NumPy views.  The Philox seed travels in the packed inputs
+(ccmpc_sample_unicycle_ex's seed_dev), so every replay draws a fresh particle set.
+
+Outputs live in the graph's buffers until the next replay of the same graph; what the caller
+keeps across steps (the saved moments) is copied out.
+"""
+import numpy as np
+import torch
+
+from . import _lib, engine, risk
+
+_ALIGN = 256
+
+
+class Pack:
+    """Named, 256-byte aligned fields of one flat device buffer, mirrored in pinned host memory
+    (one copy moves all of them)."""
+
+    def __init__(self, fields, device):
+        self.spec, off = {}, 0
+        for name, shape, dtype in fields:
+            shape = tuple(int(s) for s in shape)
+            n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+            off = -(-off // _ALIGN) * _ALIGN
+            self.spec[name] = (off, shape, dtype, n)
+            off += max(n, 1)
+        self.nbytes = -(-off // _ALIGN) * _ALIGN
+        self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=True)
+        raw = self.host.numpy()
+        self._d, self._h = {}, {}
+        for name, (off, shape, dtype, n) in self.spec.items():
+            self._d[name] = self.dev[off:off + n].view(dtype).view(shape)
+            npdt = torch.empty((), dtype=dtype).numpy().dtype
+            self._h[name] = raw[off:off + n].view(npdt).reshape(shape)
+
+    def d(self, name):
+        """Device view of a field."""
+        return self._d[name]
+
+    def h(self, name):
+        """Zero-copy NumPy view of the pinned host field."""
+        return self._h[name]
+
+    def snapshot(self):
+        """One copy of the whole host buffer; returns {field: view of the copy} (outputs that
+        must outlive the next replay, for one memcpy instead of one per field)."""
+        raw = self.host.numpy().copy()
+        out = {}
+        for name, (off, shape, dtype, n) in self.spec.items():
+            out[name] = raw[off:off + n].view(self._h[name].dtype).reshape(shape)
+        return out
+
+
+class MinkowskiStepGraph:
+    """Sampler -> bucketing -> Minkowski cycle -> L4 for a fixed shape, as one hipGraph.
+
+    O OVs with N particles each over T = ph steps; L latent values; K kept modes per OV (the
+    host decides them from p(z|x), as make_ovehicles does, so the shape is known before the
+    step runs).  gmm_shape is (O, L, T, 5) per-latent parameters (the synthetic / per-latent
+    mode of the sampler)."""
+
+    def __init__(self, O, N, T, L, K, device="cuda", dt=0.5, R=risk.R_COLLISION, tol=1e-8,
+                 maxiter=1000):
+        self.device = engine.require_device(device)
+        lib = _lib.load()
+        self.O, self.N, self.T, self.L = int(O), int(N), int(T), int(L)
+        self.K = [int(k) for k in K]
+        if len(self.K) != self.O or min(self.K) < 1:
+            raise ValueError("K must give >= 1 kept mode for each OV")
+        self.C = C = sum(self.K)
+        self.P = P = max(T * (T - 1) // 2, 1)
+        self.max_k = max(self.K)
+        self.dt, self.R, self.tol, self.maxiter = float(dt), float(R), float(tol), int(maxiter)
+        f64, f32, i32, i64, u8 = torch.float64, torch.float32, torch.int32, torch.int64, torch.uint8
+        self.inp = Pack([("seed", (1,), i64), ("init", (O, 4), f64), ("cdf", (O, L), f64),
+                         ("gmm", (O, L, T, 5), f32), ("keep", (O, L), i32), ("nk", (O,), i32),
+                         ("base", (O,), i32), ("minpos", (O, 2), f64), ("region", (O,), i64),
+                         ("origin", (C, 2), f64), ("ref", (1, T, 2), f64), ("risk", (C, 3), f64),
+                         ("past", (C, 2), f64), ("bbox", (C, 2), f64)], self.device)
+        self.out = Pack([("rec", (C, P, 128), u8), ("pl", (C, T), f64), ("mean", (C, T, 2), f64),
+                         ("cov", (C, 2 * T, 2 * T), f64), ("A", (C, T, 4, 2), f64),
+                         ("b", (C, T, 4), f64), ("yaw_mean", (C, T), f64),
+                         ("yaw0_var", (C,), f64), ("cnt", (C,), i64), ("off", (C,), i64),
+                         ("pmf", (C,), f64), ("centre", (C, 2), f64)], self.device)
+        # device-only intermediates: the sample-order store and the bucketed store
+        self.z = torch.empty((O, N), dtype=i32, device=self.device)
+        self.samples = engine.ParticleStore(T, [N] * O, dtype=f32, device=self.device,
+                                            origin=np.zeros((O, 2)))
+        region, cur = [], 0
+        for o in range(O):
+            region.append(cur)
+            cur = engine._round4(cur + N + 4 * self.K[o])
+        self.region = np.asarray(region, np.int64)
+        st = engine.ParticleStore(T, [0] * C, dtype=f32, device=self.device,
+                                  origin=np.zeros((C, 2)), capacity=cur)
+        st.cell_off, st.cell_cnt, st.origin = self.out.d("off"), self.out.d("cnt"), \
+            self.inp.d("origin")
+        st.counts = st.offsets = None
+        st.n_bound = cur
+        self.store = st
+        self.bucket_ws = torch.zeros(max(lib.ccmpc_bucket_workspace_bytes(O, N, L, self.max_k),
+                                         16), dtype=u8, device=self.device)
+        self.ws = engine.Workspace(self.device)
+        self.ws.get(lib.ccmpc_moments_workspace_bytes(T, C, st.n_bound))
+        self.side = torch.cuda.Stream(device=self.device)
+        self.graph = None
+        self._static_set = False
+
+    # ---------------------------------------------------------------------------------------
+    def _enqueue(self):
+        lib, p, s = _lib.load(), engine._p, engine._stream()
+        i, o, st, sm = self.inp, self.out, self.store, self.samples
+        O, N, T, L, C = self.O, self.N, self.T, self.L, self.C
+        chk = engine._lib.check
+        chk(lib.ccmpc_copy_async(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
+        chk(lib.ccmpc_sample_unicycle_ex(
+            p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None, None,
+            O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld, s),
+            "ccmpc_sample_unicycle_ex")
+        ws = self.bucket_ws
+        chk(lib.ccmpc_bucket(p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
+                             p(i.d("nk")), p(i.d("base")), self.max_k, p(i.d("minpos")),
+                             p(i.d("region")), p(ws), ws.numel(), p(st.pos), st.ld,
+                             p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")), p(o.d("centre")), s),
+            "ccmpc_bucket")
+        # the cycle and the L4 kernel only read the bucketed store: two graph branches
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            chk(lib.ccmpc_l4(p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
+                             p(o.d("cnt")), C, p(i.d("past")), p(i.d("bbox")), p(o.d("A")),
+                             p(o.d("b")), p(o.d("yaw_mean")), p(o.d("yaw0_var")), None, None,
+                             engine._stream()), "ccmpc_l4")
+        mws = self.ws.buf
+        chk(lib.ccmpc_minkowski_cycle(
+            p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
+            st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
+            self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")), p(o.d("pl")),
+            s), "ccmpc_minkowski_cycle")
+        main.wait_stream(self.side)
+        chk(lib.ccmpc_copy_async(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
+
+    def capture(self):
+        """Record the step into a hipGraph (after one eager run that warms every kernel)."""
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._enqueue()
+        s.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=s):
+            self._enqueue()
+        torch.cuda.synchronize(self.device)
+        return self
+
+    # ---------------------------------------------------------------------------------------
+    def set_inputs(self, seed, init_state, latent_pmf, gmm, minpos, ref_traj, cell_risk,
+                   past_last, bbox, filter_pmf=0.1):
+        """Write one step's host inputs into the pinned input pack (no device work).  The kept
+        modes implied by latent_pmf must match the graph's K."""
+        i, O, L = self.inp, self.O, self.L
+        pmf = np.asarray(latent_pmf, np.float64).reshape(O, L)
+        kept = pmf > filter_pmf
+        if not np.array_equal(kept.sum(1), self.K):
+            raise ValueError(f"kept modes per OV {kept.sum(1).tolist()}; this graph was built "
+                             f"for {self.K}")
+        keep = np.where(kept, np.cumsum(kept, axis=1) - 1, -1).astype(np.int32)
+        i.h("seed")[0] = np.int64(np.uint64(int(seed) & (2**64 - 1)).view(np.int64))
+        i.h("init")[:] = np.asarray(init_state, np.float64).reshape(O, 4)
+        i.h("cdf")[:] = np.cumsum(pmf, axis=1)
+        i.h("gmm")[:] = np.asarray(gmm, np.float32).reshape(O, L, self.T, 5)
+        i.h("keep")[:] = keep
+        if not self._static_set:       # shape-fixed fields: written once
+            i.h("nk")[:] = self.K
+            i.h("base")[:] = np.concatenate([[0], np.cumsum(self.K)[:-1]])
+            i.h("region")[:] = self.region
+            self._static_set = True
+        mp = np.asarray(minpos, np.float64)
+        if mp.size == 2:
+            i.h("minpos")[:] = mp.reshape(1, 2)
+            i.h("origin")[:] = mp.reshape(1, 2)
+        else:
+            mp = mp.reshape(O, 2)
+            i.h("minpos")[:] = mp
+            i.h("origin")[:] = np.repeat(mp, self.K, axis=0)
+        i.h("ref")[:] = np.asarray(ref_traj, np.float64)[:self.T].reshape(1, self.T, 2)
+        i.h("risk")[:] = np.asarray(cell_risk, np.float64).reshape(self.C, 3)
+        i.h("past")[:] = np.asarray(past_last, np.float64).reshape(self.C, 2)
+        i.h("bbox")[:] = np.asarray(bbox, np.float64).reshape(self.C, 2)
+
+    def replay(self):
+        """One step: the graph (inputs up, five kernels, outputs down); returns when the output
+        pack is on the host."""
+        if self.graph is None:
+            self.capture()
+        self.graph.replay()
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def records(self):
+        return self.out.h("rec").reshape(-1).view(_lib.HALFSPACE_DTYPE).reshape(self.C, self.P)

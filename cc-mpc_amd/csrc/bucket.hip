@@ -13,20 +13,24 @@
 // This is a stable counting sort on key = owner * (L + 1) + group, group = 0 for the native
 // mode and 1 + z for a rare latent.  Five short kernels:
 //   B1 stats   per block: latent counts (LDS int atomics, exact) and per-kept-mode sums of the
-//              final positions (fixed-order block reductions)
-//   B2 centres one block per OV: sums in block order -> centres
-//   B3 keys    per block: key histogram (LDS int atomics, exact)
-//   B4 scan    one block per OV: bin offsets (bin-major, block-minor), 4-aligned cell offsets
-//   B5 scatter per block: stable rank inside the block (wave ballots, waves in order) -> copy
+//              final positions (fixed-order block reductions), published write-through; the
+//              OV's last arriving block sums them in block order -> centres
+//   B2 keys    per block: key histogram (LDS int atomics, exact), published write-through; the
+//              OV's last arriving block scans them -> bin offsets (bin-major, block-minor),
+//              4-aligned cell offsets
+//   B3 scatter per block: stable rank inside the block (wave ballots, waves in order) -> copy
 //              the particle's 2T coordinates to its bucket slot
+// The last-arriver hand-off is the one of the moment reduction (gram.hpp: sc1 stores, drain,
+// agent-scope ticket, sc1 loads); its counters live at the head of the workspace, which must be
+// zero-filled once (every call leaves them zero).
 // Everything is integer-exact except the centre sums, whose fixed order makes them
 // deterministic; the bucketed store is bit-identical across runs.
-#include "ccmpc_common.hpp"
+#include "gram.hpp"
 
 namespace ccmpc {
 
 constexpr int kBucketBlock = 256;
-constexpr int kPerThread = 4;
+constexpr int kPerThread = 1;  // one round per block: many short blocks (C2 shape: 80, not 20)
 constexpr int kSpan = kBucketBlock * kPerThread;  // particles per block, in sample order
 constexpr int kMaxBins = 1024;
 constexpr int kMaxKept = 16;
@@ -44,8 +48,9 @@ struct BucketArgs {
   const double *minpos;     // [n_ov][2]
   int nb;                   // blocks per OV
   // workspace
-  int32_t *cnt_lat;         // [n_ov][nb][L]
-  double *sum_xy;           // [n_ov][nb][max_k][2]
+  int32_t *ctr;             // [2][n_ov] arrival counters (zero between calls)
+  double *part;             // [n_ov][nb][E1]: latent counts [L], then from S0 (even) the
+  int E1, S0;               // kept-mode sums [max_k][2]; E1 even
   double *centre;           // [n_ov][max_k][2]
   int32_t *hist;            // [n_ov][nb][nbins]
   int64_t *bin_off;         // [n_ov][nb][nbins]
@@ -95,10 +100,20 @@ __device__ __forceinline__ int key_of(const BucketArgs &a, int o, int64_t i) {
   return best * (a.L + 1) + 1 + zv;
 }
 
+__device__ __forceinline__ void st1_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, int32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(v), r, byte_off, 0, 16);
+}
+__device__ __forceinline__ int32_t ld1_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 16));
+}
+
 __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
   __shared__ int cnt[64];
   __shared__ double red[4];
+  __shared__ double pub[64 + 2 + 2 * kMaxKept];
+  __shared__ int flag;
   const int o = blockIdx.y, blk = blockIdx.x;
+  const int K = a.n_kept[o];
   for (int l = threadIdx.x; l < a.L; l += blockDim.x) cnt[l] = 0;
   __syncthreads();
   const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
@@ -115,7 +130,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
       final_world(a, o, i, xs[r], ys[r]);
     }
   }
-  for (int k = 0; k < a.n_kept[o]; ++k) {
+  for (int k = 0; k < K; ++k) {
     double sx = 0.0, sy = 0.0;
 #pragma unroll
     for (int r = 0; r < kPerThread; ++r) {
@@ -126,42 +141,77 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
     sx = block_sum256(sx, red);
     sy = block_sum256(sy, red);
     if (threadIdx.x == 0) {
-      double *d = a.sum_xy + ((static_cast<int64_t>(o) * a.nb + blk) * a.max_k + k) * 2;
-      d[0] = sx;
-      d[1] = sy;
+      pub[a.S0 + 2 * k] = sx;
+      pub[a.S0 + 2 * k + 1] = sy;
     }
   }
   __syncthreads();
-  for (int l = threadIdx.x; l < a.L; l += blockDim.x)
-    a.cnt_lat[(static_cast<int64_t>(o) * a.nb + blk) * a.L + l] = cnt[l];
-}
-
-__global__ __launch_bounds__(64) void bucket_centres(BucketArgs a) {
-  const int o = blockIdx.x;
-  for (int k = threadIdx.x; k < a.n_kept[o]; k += blockDim.x) {
-    int zv = 0;
-    for (int l = 0; l < a.L; ++l)
-      if (a.keep_map[o * a.L + l] == k) zv = l;
-    int64_t n = 0;
-    double sx = 0.0, sy = 0.0;
-    for (int b = 0; b < a.nb; ++b) {
-      n += a.cnt_lat[(static_cast<int64_t>(o) * a.nb + b) * a.L + zv];
-      const double *s = a.sum_xy + ((static_cast<int64_t>(o) * a.nb + b) * a.max_k + k) * 2;
-      sx += s[0];
-      sy += s[1];
+  for (int l = threadIdx.x; l < a.L; l += blockDim.x) pub[l] = static_cast<double>(cnt[l]);
+  __syncthreads();
+  // publish this block's partials write-through, then the OV's last arriver combines them
+  double *mine = a.part + (static_cast<int64_t>(o) * a.nb + blk) * a.E1;
+  const __amdgpu_buffer_rsrc_t rm = slab_rsrc(mine);
+  const int used = a.S0 + 2 * K;
+  for (int e = 2 * threadIdx.x; e < used; e += 2 * blockDim.x)
+    st2_sc1(rm, 8 * e, pub[e], e + 1 < used ? pub[e + 1] : 0.0);
+  if (!arrive_last(a.ctr + o, a.nb, &flag)) return;
+  // centres: kept mode k's own particles (latent zv_k), summed over blocks in a fixed order
+  // (this thread's blocks b = tid, tid + 256, ..., then the fixed block reduction); every
+  // mode's loads are issued before any is summed
+  __shared__ int zv_s[kMaxKept];
+  for (int l = threadIdx.x; l < a.L; l += blockDim.x) {
+    const int k = a.keep_map[o * a.L + l];
+    if (k >= 0) zv_s[k] = l;
+  }
+  __syncthreads();
+  const double *p0 = a.part + static_cast<int64_t>(o) * a.nb * a.E1;
+  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(p0);
+  constexpr int KB = 4;  // modes whose loads are in flight together
+  for (int k0 = 0; k0 < K; k0 += KB) {
+    double n[KB], sx[KB], sy[KB];
+#pragma unroll
+    for (int j = 0; j < KB; ++j) n[j] = sx[j] = sy[j] = 0.0;
+    for (int b = threadIdx.x; b < a.nb; b += blockDim.x) {
+      double2 c[KB], v[KB];
+#pragma unroll
+      for (int j = 0; j < KB; ++j) {
+        const int k = k0 + j < K ? k0 + j : K - 1;  // clamped: always a valid address
+        c[j] = ld2_sc1(rp, 8 * (b * a.E1 + (zv_s[k] & ~1)));
+        v[j] = ld2_sc1(rp, 8 * (b * a.E1 + a.S0 + 2 * k));
+      }
+#pragma unroll
+      for (int j = 0; j < KB; ++j) {
+        n[j] += (zv_s[k0 + j < K ? k0 + j : K - 1] & 1) ? c[j].y : c[j].x;
+        sx[j] += v[j].x;
+        sy[j] += v[j].y;
+      }
     }
-    a.centre[(o * a.max_k + k) * 2] = sx / static_cast<double>(n);
-    a.centre[(o * a.max_k + k) * 2 + 1] = sy / static_cast<double>(n);
-    const int cell = a.cell_base[o] + k;
-    a.init_center[2 * cell] = sx / static_cast<double>(n);
-    a.init_center[2 * cell + 1] = sy / static_cast<double>(n);
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      const int k = k0 + j;
+      if (k < K) {  // uniform: K is the OV's
+        const double nk = block_sum256(n[j], red);
+        const double xk = block_sum256(sx[j], red), yk = block_sum256(sy[j], red);
+        if (threadIdx.x == 0) {
+          a.centre[(o * a.max_k + k) * 2] = xk / nk;
+          a.centre[(o * a.max_k + k) * 2 + 1] = yk / nk;
+          const int cell = a.cell_base[o] + k;
+          a.init_center[2 * cell] = xk / nk;
+          a.init_center[2 * cell + 1] = yk / nk;
+        }
+      }
+    }
   }
 }
 
 __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
   __shared__ int h[kMaxBins];
+  __shared__ int64_t start[kMaxBins];
+  __shared__ int flag;
   const int o = blockIdx.y, blk = blockIdx.x;
-  const int nbins = a.n_kept[o] * (a.L + 1);
+  const int K = a.n_kept[o];
+  const int G = a.L + 1;
+  const int nbins = K * G;
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
@@ -171,33 +221,39 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
     if (i < a.N) atomicAdd(&h[key_of(a, o, i)], 1);
   }
   __syncthreads();
-  const int64_t stride = static_cast<int64_t>(a.max_k) * (a.L + 1);
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x)
-    a.hist[(static_cast<int64_t>(o) * a.nb + blk) * stride + b] = h[b];
-}
-
-__global__ __launch_bounds__(256) void bucket_scan(BucketArgs a) {
-  __shared__ int64_t tot[kMaxBins];
-  __shared__ int64_t start[kMaxBins];
-  const int o = blockIdx.x;
-  const int K = a.n_kept[o];
-  const int G = a.L + 1;
-  const int nbins = K * G;
   const int64_t stride = static_cast<int64_t>(a.max_k) * G;
-  const int32_t *hist = a.hist + static_cast<int64_t>(o) * a.nb * stride;
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+  int32_t *hist0 = a.hist + static_cast<int64_t>(o) * a.nb * stride;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hist0, 0, 0x7fffffff,
+                                                                       0x00020000);
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x)
+    st1_sc1(rh, 4 * static_cast<int>(blk * stride + b), h[b]);
+  if (!arrive_last(a.ctr + a.n_ov + o, a.nb, &flag)) return;
+  // the OV's scan: bin totals (blocks in order), bins in (kept mode, group) order
+  // (loads in batches of 8, all in flight together: a dependent chain of nb round trips
+  // was the kernel's whole latency)
+  auto column_sum = [&](int b, int k_end) {
     int64_t s = 0;
-    for (int blk = 0; blk < a.nb; ++blk) s += hist[blk * stride + b];
-    tot[b] = s;
-  }
+    int k = 0;
+    for (; k + 8 <= k_end; k += 8) {
+      int32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ld1_sc1(rh, 4 * static_cast<int>((k + j) * stride + b));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < k_end; ++k) s += ld1_sc1(rh, 4 * static_cast<int>(k * stride + b));
+    return s;
+  };
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) start[b] = column_sum(b, a.nb);
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t cur = a.region[o];
     for (int k = 0; k < K; ++k) {
       int64_t n = 0;
       for (int gi = 0; gi < G; ++gi) {
+        const int64_t c = start[k * G + gi];
         start[k * G + gi] = cur + n;
-        n += tot[k * G + gi];
+        n += c;
       }
       const int cell = a.cell_base[o] + k;
       a.cell_off[cell] = cur;
@@ -207,11 +263,20 @@ __global__ __launch_bounds__(256) void bucket_scan(BucketArgs a) {
     }
   }
   __syncthreads();
+  // every block's offset in each bin: the bin's start + the counts of the blocks before it
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
     int64_t s = start[b];
-    for (int blk = 0; blk < a.nb; ++blk) {
-      a.bin_off[(static_cast<int64_t>(o) * a.nb + blk) * stride + b] = s;
-      s += hist[blk * stride + b];
+    int64_t *dst = a.bin_off + static_cast<int64_t>(o) * a.nb * stride + b;
+    for (int k = 0; k < a.nb; k += 8) {
+      int32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = k + j < a.nb ? ld1_sc1(rh, 4 * static_cast<int>((k + j) * stride + b)) : 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (k + j < a.nb) dst[(k + j) * stride] = s;
+        s += v[j];
+      }
     }
   }
 }
@@ -262,17 +327,20 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
 inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  size_t cnt_lat, sum_xy, centre, hist, bin_off, total;
+  size_t ctr, part, centre, hist, bin_off, total;
+  int E1, S0;
 };
 
 inline WsLayout bucket_ws(int64_t n_ov, int64_t N, int64_t L, int64_t max_k) {
   const int64_t nb = (N + kSpan - 1) / kSpan;
   WsLayout w;
+  w.S0 = static_cast<int>((L + 1) & ~int64_t(1));
+  w.E1 = static_cast<int>(w.S0 + 2 * max_k);
   size_t o = 0;
-  w.cnt_lat = o;
-  o += align256(sizeof(int32_t) * n_ov * nb * L);
-  w.sum_xy = o;
-  o += align256(sizeof(double) * n_ov * nb * max_k * 2);
+  w.ctr = o;  // arrival counters first: the zero-filled head of the workspace
+  o += align256(sizeof(int32_t) * 2 * n_ov);
+  w.part = o;
+  o += align256(sizeof(double) * n_ov * nb * w.E1);
   w.centre = o;
   o += align256(sizeof(double) * n_ov * max_k * 2);
   w.hist = o;
@@ -332,8 +400,10 @@ extern "C" int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in
   a.region = region;
   a.minpos = minpos;
   a.nb = static_cast<int>((N + kSpan - 1) / kSpan);
-  a.cnt_lat = reinterpret_cast<int32_t *>(ws + L.cnt_lat);
-  a.sum_xy = reinterpret_cast<double *>(ws + L.sum_xy);
+  a.ctr = reinterpret_cast<int32_t *>(ws + L.ctr);
+  a.part = reinterpret_cast<double *>(ws + L.part);
+  a.E1 = L.E1;
+  a.S0 = L.S0;
   a.centre = reinterpret_cast<double *>(ws + L.centre);
   a.hist = reinterpret_cast<int32_t *>(ws + L.hist);
   a.bin_off = reinterpret_cast<int64_t *>(ws + L.bin_off);
@@ -346,9 +416,7 @@ extern "C" int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in
   hipStream_t s = as_stream(stream);
   const dim3 grid(static_cast<unsigned>(a.nb), static_cast<unsigned>(n_ov));
   hipLaunchKernelGGL(bucket_stats, grid, dim3(kBucketBlock), 0, s, a);
-  hipLaunchKernelGGL(bucket_centres, dim3(static_cast<unsigned>(n_ov)), dim3(64), 0, s, a);
   hipLaunchKernelGGL(bucket_hist, grid, dim3(kBucketBlock), 0, s, a);
-  hipLaunchKernelGGL(bucket_scan, dim3(static_cast<unsigned>(n_ov)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(bucket_scatter, grid, dim3(kBucketBlock), 0, s, a);
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;

@@ -27,3 +27,17 @@ extern "C" const char *ccmpc_status_string(int status) {
     default: return "unknown status";
   }
 }
+
+// Stream-ordered byte copy between host and device buffers (any direction; the runtime infers
+// it from the pointers).  Lets a captured planning-step graph carry its packed H2D input copy
+// and D2H output copy as graph nodes (ccmpc/step.py).
+extern "C" int ccmpc_copy_async(void *dst, const void *src, size_t bytes, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(dst && src, "null pointer");
+  if (bytes == 0) return CCMPC_OK;
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ccmpc::as_stream(stream));
+  if (e != hipSuccess) {
+    ccmpc::set_error(std::string("ccmpc_copy_async: ") + hipGetErrorString(e));
+    return CCMPC_ERR_LAUNCH;
+  }
+  return CCMPC_OK;
+}

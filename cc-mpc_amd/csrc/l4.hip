@@ -9,8 +9,9 @@
 //   t=0 yaw stats  v8ideal/__init__.py:872, :875 (mean and ddof=1 variance of yaw at t=0)
 //
 // One workgroup per (cell, t): pass 1 sums the headings (block reduction in a fixed order, so
-// the mean is bitwise reproducible), pass 2 re-reads the two steps and takes the max of the four
-// projections.  Max is order-independent, so b is exact whatever the reduction order.
+// the mean is bitwise reproducible), pass 2 takes the max of the four projections over every
+// corner, from registers for the particles pass 1 kept (re-reading the two steps beyond them).
+// Max is order-independent, so b is exact whatever the reduction order.
 #include "ccmpc_common.hpp"
 
 namespace ccmpc {
@@ -61,8 +62,26 @@ __device__ __forceinline__ double block_max(double v, double *red) {
   return s;
 }
 
+// A particle's heading and the (cos, sin) of it.  cos(atan2(dy, dx)) = dx / r and sin = dy / r
+// with r = hypot(dx, dy): two divisions instead of a second transcendental (within 2 ulp of
+// cos / sin of the rounded atan2, far below the 1e-13 vertex tolerance); a zero step keeps
+// sincos of atan2, whose signed-zero cases the ratio cannot express.
+__device__ __forceinline__ void heading_cs(double dx, double dy, double &yaw, double &S, double &C) {
+  yaw = atan2(dy, dx);
+  const double r = sqrt(dx * dx + dy * dy);
+  if (r > 0.0 && isfinite(r)) {
+    C = dx / r;
+    S = dy / r;
+  } else {
+    sincos(yaw, &S, &C);
+  }
+}
+
+constexpr int kL4Threads = 512;  // 8 waves: 2 per SIMD, so the f64 transcendental chains overlap
+constexpr int kL4Cache = 8;      // headings kept in registers between the passes (4096 particles)
+
 template <typename P>
-__global__ __launch_bounds__(256) void l4_kernel(
+__global__ __launch_bounds__(kL4Threads) void l4_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
     const double *__restrict__ past_last, const double *__restrict__ bbox,
@@ -76,12 +95,24 @@ __global__ __launch_bounds__(256) void l4_kernel(
   const double px = past_last[2 * cell], py = past_last[2 * cell + 1];
   const double lon = bbox[2 * cell], lat = bbox[2 * cell + 1];
   const P *base = pos + off;
+  const int nth = blockDim.x;
 
-  // pass 1: headings, mean (and the t = 0 variance, shifted by the first particle's heading)
+  // the step delta of particle i (step 0 measured from past[-1], ovehicle.py:72-76)
+  auto delta = [&](int64_t i, double &x, double &y, double &dx, double &dy) {
+    x = world(base, ld, 2 * t, i, o0);
+    y = world(base, ld, 2 * t + 1, i, o1);
+    const double xp = t == 0 ? px : world(base, ld, 2 * t - 2, i, o0);
+    const double yp = t == 0 ? py : world(base, ld, 2 * t - 1, i, o1);
+    dx = x - xp;
+    dy = y - yp;
+  };
+
+  // pass 1: headings, mean (and the t = 0 variance, shifted by the first particle's heading);
+  // the first kL4Cache headings of each thread (and their cos / sin) stay in registers
   double s = 0.0, s1 = 0.0, s2 = 0.0;
   const double shift = (t == 0 && n > 0) ? heading(base, ld, 0, 0, o0, o1, px, py) : 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const double y = heading(base, ld, t, i, o0, o1, px, py);
+  double yc[kL4Cache], sc[kL4Cache], cc[kL4Cache], xc[kL4Cache], vc[kL4Cache];
+  auto take = [&](int64_t i, double y) {
     s += y;
     if (t == 0) {
       const double d = y - shift;
@@ -89,6 +120,21 @@ __global__ __launch_bounds__(256) void l4_kernel(
       s2 += d * d;
     }
     if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + off + i] = y;
+  };
+#pragma unroll
+  for (int j = 0; j < kL4Cache; ++j) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(j) * nth;
+    if (i < n) {
+      double dx, dy;
+      delta(i, xc[j], vc[j], dx, dy);
+      heading_cs(dx, dy, yc[j], sc[j], cc[j]);
+      take(i, yc[j]);
+    }
+  }
+  for (int64_t i = threadIdx.x + static_cast<int64_t>(kL4Cache) * nth; i < n; i += nth) {
+    double x, y, dx, dy;
+    delta(i, x, y, dx, dy);
+    take(i, atan2(dy, dx));
   }
   const double nn = static_cast<double>(n);
   const double theta = block_sum(s, red) / nn;
@@ -101,11 +147,7 @@ __global__ __launch_bounds__(256) void l4_kernel(
   const double ct = cos(theta), st = sin(theta);
   const double A[4][2] = {{ct, st}, {-st, ct}, {-ct, -st}, {st, -ct}};
   double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const double yaw = heading(base, ld, t, i, o0, o1, px, py);
-    const double x = world(base, ld, 2 * t, i, o0), y = world(base, ld, 2 * t + 1, i, o1);
-    double S, C;
-    sincos(yaw, &S, &C);
+  auto corners = [&](int64_t i, double x, double y, double S, double C) {
     // rows of Rot per corner (midlevel/util.py:109-118), disp = 0.5 * Rot @ [lon, lat]
     const double dx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
                           0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
@@ -122,6 +164,17 @@ __global__ __launch_bounds__(256) void l4_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) mx[r] = fmax(mx[r], A[r][0] * vx + A[r][1] * vy);
     }
+  };
+#pragma unroll
+  for (int j = 0; j < kL4Cache; ++j) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(j) * nth;
+    if (i < n) corners(i, xc[j], vc[j], sc[j], cc[j]);
+  }
+  for (int64_t i = threadIdx.x + static_cast<int64_t>(kL4Cache) * nth; i < n; i += nth) {
+    double x, y, dx, dy, yaw, S, C;
+    delta(i, x, y, dx, dy);
+    heading_cs(dx, dy, yaw, S, C);
+    corners(i, x, y, S, C);
   }
   double bm[4];
 #pragma unroll
@@ -156,12 +209,12 @@ extern "C" int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T,
   CCMPC_REQUIRE(dtype == CCMPC_F64 || dtype == CCMPC_F32, "bad dtype");
   const dim3 grid(static_cast<unsigned>(n_cells * T));
   if (dtype == CCMPC_F64)
-    hipLaunchKernelGGL((l4_kernel<double>), grid, dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL((l4_kernel<double>), grid, dim3(kL4Threads), 0, as_stream(stream),
                        static_cast<const double *>(positions), ld, static_cast<int>(T), origin,
                        cell_off, cell_cnt, past_last, bbox, out_A, out_b, out_yaw_mean,
                        out_yaw0_var, out_yaw, out_vertices);
   else
-    hipLaunchKernelGGL((l4_kernel<float>), grid, dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL((l4_kernel<float>), grid, dim3(kL4Threads), 0, as_stream(stream),
                        static_cast<const float *>(positions), ld, static_cast<int>(T), origin,
                        cell_off, cell_cnt, past_last, bbox, out_A, out_b, out_yaw_mean,
                        out_yaw0_var, out_yaw, out_vertices);

@@ -33,23 +33,28 @@ __device__ __forceinline__ float exp_rn(float a) {
   return static_cast<float>(exp(static_cast<double>(a)));
 }
 
-__device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, float &v, float dphi,
-                                              float a, float dt) {
+// One Unicycle.dynamic step.  (s0, c0) = sin / cos of the current heading, carried from the
+// previous step: the heading after a turning step IS that step's phi + w dt, whose sin / cos
+// it already evaluated, and a straight step keeps phi -- so each step evaluates one sincos
+// (none when straight) with exactly the values of a fresh sincos_rn(phi).
+__device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, float &v, float &s0,
+                                              float &c0, float dphi, float a, float dt) {
   const bool straight = fabsf(dphi) <= 1e-2f;
-  const float w = straight ? 1.0f : dphi;
-  const float phi1 = phi + w * dt;
-  float s0, c0, s1, c1;
-  sincos_rn(phi, s0, c0);
-  sincos_rn(phi1, s1, c1);
   if (straight) {
     x = x + v * c0 * dt + (a / 2.0f) * c0 * dt * dt;
     y = y + v * s0 * dt + (a / 2.0f) * s0 * dt * dt;
   } else {
+    const float w = dphi;
+    const float phi1 = phi + w * dt;
+    float s1, c1;
+    sincos_rn(phi1, s1, c1);
     const float dsin = (s1 - s0) / w, dcos = (c1 - c0) / w;
     const float aw = a / w;
     x = x + aw * dcos + v * dsin + aw * s1 * dt;
     y = y - v * dcos + aw * dsin - aw * c1 * dt;
     phi = phi1;
+    s0 = s1;
+    c0 = c1;
   }
   v = v + a * dt;
 }
@@ -73,59 +78,100 @@ __device__ __forceinline__ void gmm2d_action(float mu0, float mu1, float ls0, fl
 //        inverse CDF;
 //  EPSIN noise injected eps[o][t][2][N] (torch's randn inside GMM2D.rsample) instead of Philox.
 // Per-particle arrays are particle-minor, so a wave's reads of one (t, k) are one contiguous run.
+//
+// Two phases per block of kSampP particles: the per-step actions do not depend on the state
+// (the noise and the parameters are fixed by (particle, t, z)), so kSlots waves draw the T
+// actions of the block's particles in parallel into LDS (the Philox / Box-Muller / exp work),
+// then one wave runs the Unicycle chain, one lane per particle -- the serial part is just the
+// integration.
+constexpr int kSampP = 64;       // particles per block (one wave in the chain phase)
+constexpr int kSlots = 8;        // waves drawing actions
+constexpr int kSampThreads = kSampP * kSlots;
+
 template <bool PP, bool ZIN, bool EPSIN>
-__global__ __launch_bounds__(256) void sample_unicycle_kernel(
+__global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
     const double *__restrict__ init_state, const double *__restrict__ latent_cdf, int n_latent,
     const float *__restrict__ gmm, const int32_t *__restrict__ z_in,
-    const float *__restrict__ eps_in, int64_t N, int T, float dt, uint64_t seed,
-    uint32_t ov_base, int32_t *__restrict__ out_z, float *__restrict__ out_pos, int64_t ld) {
+    const float *__restrict__ eps_in, int64_t N, int T, float dt, uint64_t seed_arg,
+    const uint64_t *__restrict__ seed_dev, uint32_t ov_base, int32_t *__restrict__ out_z,
+    float *__restrict__ out_pos, int64_t ld) {
+  __shared__ float act[2][40][kSampP];  // (dphi, a) per (t, particle); T <= 40
+  __shared__ int zs[kSampP];
+  __shared__ double cdf_s[64];           // this OV's latent CDF, one coalesced read
+  __shared__ float gmm_s[PP ? 1 : 64 * 40 * 5 / 4];  // per-latent rows, staged when they fit
   const int ov = blockIdx.y;
+  const int lane = threadIdx.x & (kSampP - 1), slot = threadIdx.x / kSampP;
+  // a seed in device memory lets a captured graph draw fresh particles on every replay
+  const uint64_t seed = seed_dev ? *seed_dev : seed_arg;
   const uint32_t key = ov_base + static_cast<uint32_t>(ov);  // global OV id keys the streams
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  int z;
-  if (ZIN) {
-    z = z_in[static_cast<int64_t>(ov) * N + i];
-    z = z < 0 ? 0 : (z >= n_latent ? n_latent - 1 : z);  // memory safety; the host validates
-  } else {
-    const double *cdf = latent_cdf + static_cast<int64_t>(ov) * n_latent;
-    const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, key, STREAM_SAMPLER_Z, seed);
-    const double u = uniform53(w.x, w.y);
-    z = n_latent - 1;
-    for (int k = 0; k < n_latent; ++k) {
-      if (cdf[k] > u) {  // numpy searchsorted(cdf, u, side='right')
-        z = k;
-        break;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kSampP + lane;
+  const bool valid = i < N;
+  if (!ZIN && threadIdx.x < n_latent)
+    cdf_s[threadIdx.x] = latent_cdf[static_cast<int64_t>(ov) * n_latent + threadIdx.x];
+  // the OV's per-latent parameter table (L x T x 5 floats) read once, in parallel with the CDF,
+  // so the z-dependent parameter reads below are LDS reads, not a dependent global round trip
+  const int gsz = n_latent * T * 5;
+  const bool staged = !PP && gsz <= static_cast<int>(sizeof(gmm_s) / sizeof(float));
+  if (staged)
+    for (int e = threadIdx.x; e < gsz; e += blockDim.x)
+      gmm_s[e] = gmm[static_cast<int64_t>(ov) * gsz + e];
+  __syncthreads();
+  if (slot == 0 && valid) {
+    int z;
+    if (ZIN) {
+      z = z_in[static_cast<int64_t>(ov) * N + i];
+      z = z < 0 ? 0 : (z >= n_latent ? n_latent - 1 : z);  // memory safety; the host validates
+    } else {
+      const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, key, STREAM_SAMPLER_Z, seed);
+      const double u = uniform53(w.x, w.y);
+      z = n_latent - 1;
+      for (int k = 0; k < n_latent; ++k) {
+        if (cdf_s[k] > u) {  // numpy searchsorted(cdf, u, side='right')
+          z = k;
+          break;
+        }
       }
     }
+    zs[lane] = z;
+    out_z[static_cast<int64_t>(ov) * N + i] = z;
   }
-  out_z[static_cast<int64_t>(ov) * N + i] = z;
+  __syncthreads();
+  if (valid) {
+    const int z = zs[lane];
+    // per-latent: this particle's component row; per-particle: element (t, k) at g[(5t + k) N]
+    const float *g = PP ? gmm + static_cast<int64_t>(ov) * T * 5 * N + i
+                        : gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
+    const float *ep = EPSIN ? eps_in + static_cast<int64_t>(ov) * T * 2 * N + i : nullptr;
+    for (int t = slot; t < T; t += kSlots) {
+      float e0, e1;
+      if (EPSIN) {
+        e0 = ep[(2 * t) * N];
+        e1 = ep[(2 * t + 1) * N];
+      } else {
+        double e0d, e1d;
+        normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), key, STREAM_SAMPLER_EPS,
+                    seed, e0d, e1d);
+        e0 = static_cast<float>(e0d);
+        e1 = static_cast<float>(e1d);
+      }
+      float p[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        p[k] = PP ? g[(5 * t + k) * N]
+                  : (staged ? gmm_s[(z * T + t) * 5 + k] : g[5 * t + k]);
+      gmm2d_action(p[0], p[1], p[2], p[3], p[4], e0, e1, act[0][t][lane], act[1][t][lane]);
+    }
+  }
+  __syncthreads();
+  if (slot != 0 || !valid) return;
   const double *st = init_state + 4 * ov;
   float x = static_cast<float>(st[0]), y = static_cast<float>(st[1]);
   float phi = static_cast<float>(st[2]), v = static_cast<float>(st[3]);
-  // per-latent: this particle's component row; per-particle: element (t, k) at g[(5t + k) N]
-  const float *g = PP ? gmm + static_cast<int64_t>(ov) * T * 5 * N + i
-                      : gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
-  const float *ep = EPSIN ? eps_in + static_cast<int64_t>(ov) * T * 2 * N + i : nullptr;
+  float s0, c0;
+  sincos_rn(phi, s0, c0);
   float *o = out_pos + static_cast<int64_t>(ov) * ((N + 3) & ~int64_t(3)) + i;
   for (int t = 0; t < T; ++t) {
-    float e0, e1;
-    if (EPSIN) {
-      e0 = ep[(2 * t) * N];
-      e1 = ep[(2 * t + 1) * N];
-    } else {
-      double e0d, e1d;
-      normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), key, STREAM_SAMPLER_EPS,
-                  seed, e0d, e1d);
-      e0 = static_cast<float>(e0d);
-      e1 = static_cast<float>(e1d);
-    }
-    float p[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) p[k] = PP ? g[(5 * t + k) * N] : g[5 * t + k];
-    float dphi, acc;
-    gmm2d_action(p[0], p[1], p[2], p[3], p[4], e0, e1, dphi, acc);
-    unicycle_step(x, y, phi, v, dphi, acc, dt);
+    unicycle_step(x, y, phi, v, s0, c0, act[0][t][lane], act[1][t][lane], dt);
     o[(2 * t) * ld] = x;
     o[(2 * t + 1) * ld] = y;
   }
@@ -135,11 +181,11 @@ template <bool PP, bool ZIN, bool EPSIN>
 static void launch_sampler(dim3 grid, hipStream_t s, const double *init_state,
                            const double *latent_cdf, int n_latent, const float *gmm,
                            const int32_t *z_in, const float *eps_in, int64_t N, int T, float dt,
-                           uint64_t seed, uint32_t ov_base, int32_t *out_z, float *out_pos,
-                           int64_t ld) {
-  hipLaunchKernelGGL((sample_unicycle_kernel<PP, ZIN, EPSIN>), grid, dim3(256), 0, s, init_state,
-                     latent_cdf, n_latent, gmm, z_in, eps_in, N, T, dt, seed, ov_base, out_z,
-                     out_pos, ld);
+                           uint64_t seed, const uint64_t *seed_dev, uint32_t ov_base,
+                           int32_t *out_z, float *out_pos, int64_t ld) {
+  hipLaunchKernelGGL((sample_unicycle_kernel<PP, ZIN, EPSIN>), grid, dim3(kSampThreads), 0, s,
+                     init_state, latent_cdf, n_latent, gmm, z_in, eps_in, N, T, dt, seed,
+                     seed_dev, ov_base, out_z, out_pos, ld);
 }
 
 }  // namespace ccmpc
@@ -150,8 +196,9 @@ extern "C" int ccmpc_sample_unicycle_ex(const double *init_state, const double *
                                         int64_t n_latent, const float *gmm, int32_t gmm_layout,
                                         const int32_t *z_in, const float *eps_in, int64_t n_ov,
                                         int64_t N, int64_t T, double dt, uint64_t seed,
-                                        int64_t ov_base, int32_t *out_z, float *out_pos,
-                                        int64_t ld, ccmpc_stream_t stream) {
+                                        const uint64_t *seed_dev, int64_t ov_base,
+                                        int32_t *out_z, float *out_pos, int64_t ld,
+                                        ccmpc_stream_t stream) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
   CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536, "bad n_ov");
@@ -168,14 +215,14 @@ extern "C" int ccmpc_sample_unicycle_ex(const double *init_state, const double *
   CCMPC_REQUIRE(init_state && gmm && out_z && out_pos, "null pointer");
   CCMPC_REQUIRE(z_in || latent_cdf, "latent_cdf is needed when z is drawn here");
   CCMPC_REQUIRE(ld >= n_ov * ((N + 3) & ~int64_t(3)), "ld too small");
-  const dim3 grid(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(n_ov));
+  const dim3 grid(static_cast<unsigned>((N + kSampP - 1) / kSampP), static_cast<unsigned>(n_ov));
   hipStream_t s = as_stream(stream);
   const int L = static_cast<int>(n_latent), Ti = static_cast<int>(T);
   const float fdt = static_cast<float>(dt);
   const uint32_t base = static_cast<uint32_t>(ov_base);
 #define CCMPC_SAMPLER(PP, ZIN, EPSIN)                                                        \
   launch_sampler<PP, ZIN, EPSIN>(grid, s, init_state, latent_cdf, L, gmm, z_in, eps_in, N, Ti, \
-                                 fdt, seed, base, out_z, out_pos, ld)
+                                 fdt, seed, seed_dev, base, out_z, out_pos, ld)
   const int mode = (pp ? 4 : 0) | (z_in ? 2 : 0) | (eps_in ? 1 : 0);
   switch (mode) {
     case 0: CCMPC_SAMPLER(false, false, false); break;
@@ -197,6 +244,6 @@ extern "C" int ccmpc_sample_unicycle(const double *init_state, const double *lat
                                      ccmpc_stream_t stream) {
   CCMPC_REQUIRE(latent_cdf, "null pointer");
   return ccmpc_sample_unicycle_ex(init_state, latent_cdf, n_latent, gmm, CCMPC_GMM_PER_LATENT,
-                                  nullptr, nullptr, n_ov, N, T, dt, seed, ov_base, out_z, out_pos,
-                                  ld, stream);
+                                  nullptr, nullptr, n_ov, N, T, dt, seed, nullptr, ov_base, out_z,
+                                  out_pos, ld, stream);
 }

@@ -97,6 +97,12 @@ int ccmpc_abi_version(void);
 const char *ccmpc_last_error(void);
 const char *ccmpc_status_string(int status);
 
+/* Stream-ordered copy of `bytes` between host (pinned) and device buffers, direction inferred
+ * from the pointers (hipMemcpyDefault).  Graph plumbing with no reference counterpart: a
+ * captured planning step (ccmpc/step.py) carries its packed input upload and output download
+ * as graph nodes, so one replay is the whole step. */
+int ccmpc_copy_async(void *dst, const void *src, size_t bytes, ccmpc_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Moment (Gram) reduction.  Replaces every np.mean / np.cov over particle clouds on the path:
  *   v8ideal/__init__.py:864-875 (t=0 stats), :896 + makeconstraint.py:41-70 predict_moments
@@ -266,6 +272,8 @@ int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf, in
  *                   safety; the Python mirror rejects them), or NULL: Philox inverse CDF of
  *                   latent_cdf (which may be NULL when z_in is given)
  *  eps_in[o][T][2][N] injected standard-normal noise (float32), or NULL: Philox
+ *  seed_dev         device copy of the Philox seed (read at launch, so a captured graph draws
+ *                   fresh particles per replay), or NULL: `seed`
  * Per-step action a = mu + L eps with L = [[s0, 0], [s1 rho, s1 sqrt(clamp(1 - rho^2, 1e-5,
  * 1))]] (GMM2D's clamp), the L eps row summed before mu is added.  out_z / out_pos as above.
  * PARITY UNPINNED upstream (Trajectron++ absent): checked against the repo's restatement. */
@@ -274,8 +282,8 @@ int ccmpc_sample_unicycle(const double *init_state, const double *latent_cdf, in
 int ccmpc_sample_unicycle_ex(const double *init_state, const double *latent_cdf, int64_t n_latent,
                              const float *gmm, int32_t gmm_layout, const int32_t *z_in,
                              const float *eps_in, int64_t n_ov, int64_t N, int64_t T, double dt,
-                             uint64_t seed, int64_t ov_base, int32_t *out_z, float *out_pos,
-                             int64_t ld, ccmpc_stream_t stream);
+                             uint64_t seed, const uint64_t *seed_dev, int64_t ov_base,
+                             int32_t *out_z, float *out_pos, int64_t ld, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Particle bucketing by latent mode: make_ovehicles (v8ideal/__init__.py:469-505) +
@@ -292,6 +300,8 @@ int ccmpc_sample_unicycle_ex(const double *init_state, const double *latent_cdf,
  *       cell_off/cell_cnt [n_cells], cell_pmf = N_k / N, init_center [n_cells][2] (world)
  * Rare particles go to the kept mode whose centre (mean final position) is nearest, first
  * index on ties (scipy.spatial.distance_matrix + np.argmin).  Deterministic.
+ * Workspace: ccmpc_bucket_workspace_bytes; its head holds per-OV arrival counters, so
+ * zero-fill it once (every call leaves them zero).  Three launches.
  * ------------------------------------------------------------------------------------- */
 size_t ccmpc_bucket_workspace_bytes(int64_t n_ov, int64_t N, int64_t n_latent, int64_t max_k);
 int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T, int64_t n_ov,

@@ -299,6 +299,6 @@ def test_sampler_rejects_bad_injections(gpu):
         e.sample_unicycle(init, pmf, np.zeros((O, N, T, 5), np.float32), N, T, device=gpu,
                           per_particle=True)
     lib = e._lib.load()
-    rc = lib.ccmpc_sample_unicycle_ex(None, None, L, None, 1, None, None, 1, N, T, 0.5, 0, 0,
-                                      None, None, N, None)
+    rc = lib.ccmpc_sample_unicycle_ex(None, None, L, None, 1, None, None, 1, N, T, 0.5, 0, None,
+                                      0, None, None, N, None)
     assert rc == -1                     # CCMPC_ERR_INVALID: per-particle parameters need z_in

@@ -1,0 +1,126 @@
+"""GPU tests of the graph-captured planning step (ccmpc.step.MinkowskiStepGraph behind
+MidlevelAgent.predict_and_constrain): one replay = sampler -> bucketing -> Minkowski cycle -> L4
+with packed input/output copies.  It must give exactly what the eager drop-in calls give
+(do_prediction + make_ovehicles + the Minkowski generator, v8ideal/__init__.py:414-505,
+:781-964), step after step, and its records must meet the oracle."""
+import numpy as np
+import pytest
+
+from oracle import ccmpc_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+O, N, PH = 4, 3000, 8
+
+
+def _inputs():
+    from ccmpc import episode
+    init, pmf, gmm = episode.synthetic_gmm(O, T=PH, seed=4242)
+    minpos = np.array([150.0, -120.0])
+    pasts = [np.array([[minpos[0] + init[o, 0] - 2.0, minpos[1] + init[o, 1]]])
+             for o in range(O)]
+    K = [int(np.count_nonzero(pmf[o] > 0.1)) for o in range(O)]
+    eps = np.full((O, max(K)), 0.05 / O)
+    return init, pmf, gmm, minpos, pasts, K, eps
+
+
+def _ref(frame):
+    ego = np.array([165.0 + 0.2 * frame, -72.0])
+    return np.array([ego + [4.0 * (t + 1), 0.5 * (t + 1)] for t in range(PH)])
+
+
+def _eager(agent, init, pmf, gmm, seed, minpos, pasts, params, eps, T, ref, gpu):
+    from ccmpc import engine, ovehicle
+    z, store = engine.sample_unicycle(init, pmf, gmm, N, PH, seed=seed, device=gpu)
+    ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, device=gpu)
+    out = agent.compute_obstacle_constraints_GMM_Minkowski_idealprediction(
+        params, ovs, None, None, None, eps, None, T, ref)
+    return ovs, out
+
+
+def _same(out_g, out_e, ovs_g, ovs_e, K, T):
+    cons_g, cons_e = out_g[0], out_e[0]
+    assert len(cons_g) == len(cons_e) == sum(K) * T * (T - 1) // 2
+    for a, b in zip(cons_g, cons_e):
+        assert (a.ov, a.k, a.t, a.tau, a.side, a.which) == (b.ov, b.k, b.t, b.tau, b.side,
+                                                            b.which)
+        assert a.d == b.d and np.array_equal(a.n, b.n)
+    for t in range(PH):
+        for o in range(O):
+            for k in range(max(K)):
+                ag, ae = out_g[2][t][k][o], out_e[2][t][k][o]
+                assert (ag is None) == (ae is None)
+                if ag is not None:
+                    np.testing.assert_array_equal(ag, ae)
+                    np.testing.assert_array_equal(out_g[3][t][k][o], out_e[3][t][k][o])
+    assert out_g[4] == out_e[4]
+    for i in range(3):
+        for o in range(O):
+            for k in range(K[o]):
+                assert out_g[6][i][o][k] == out_e[6][i][o][k]
+                assert out_g[7][i][o][k] == out_e[7][i][o][k]
+    for og, oe in zip(ovs_g, ovs_e):
+        assert og.n_states == oe.n_states
+        np.testing.assert_array_equal(og.latent_pmf, oe.latent_pmf)
+        np.testing.assert_array_equal(og.init_center, oe.init_center)
+        for pg, pe in zip(og.pred_positions, oe.pred_positions):
+            np.testing.assert_array_equal(pg, pe)
+
+
+def test_graph_step_equals_eager_drop_in_calls(gpu):
+    from ccmpc import episode, planner
+    init, pmf, gmm, minpos, pasts, K, eps = _inputs()
+    ag = planner.MidlevelAgent(prediction_horizon=PH, n_ideal=200_000, device=gpu)
+    ae = planner.MidlevelAgent(prediction_horizon=PH, n_ideal=200_000, device=gpu)
+    # two full-horizon frames through ONE captured graph (fresh Philox draws per replay), then
+    # a shrinking frame on the graph step's saved moments
+    for frame, seed in ((0, 11), (100, 12), (110, 13)):
+        T = PH if frame != 110 else PH - 1
+        params = episode.Params(O, K, frame)
+        sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=seed)
+        ovs_g, out_g = ag.predict_and_constrain(params, sampler, eps, T, _ref(frame), minpos,
+                                                pasts)
+        ovs_e, out_e = _eager(ae, init, pmf, gmm, seed, minpos, pasts, params, eps, T,
+                              _ref(frame), gpu)
+        _same(out_g, out_e, ovs_g, ovs_e, K, T)
+        np.testing.assert_array_equal(ag.last_records.view(np.uint8),
+                                      ae.last_records.view(np.uint8))
+        if T == PH:
+            assert ag.prob_lower_save == ae.prob_lower_save
+    assert len(ag._graphs) == 1
+
+
+def test_graph_step_records_meet_the_oracle(gpu):
+    from ccmpc import episode, planner
+    init, pmf, gmm, minpos, pasts, K, eps = _inputs()
+    agent = planner.MidlevelAgent(prediction_horizon=PH, device=gpu)
+    params = episode.Params(O, K, 0)
+    sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=5)
+    ovs, out = agent.predict_and_constrain(params, sampler, eps, PH, _ref(0), minpos, pasts)
+    oovs = [orc.OVehicle(PH, pasts[o], ov.latent_pmf, ov.pred_positions,
+                         [orc._step_yaws(c, pasts[o][-1], PH) for c in ov.pred_positions],
+                         ov.init_center, ov.bbox) for o, ov in enumerate(ovs)]
+    want = orc.minkowski_generator(oovs, PH, PH, _ref(0))
+    cons = out[0]
+    assert len(cons) == len(want["records"])
+    for c, r in zip(cons, want["records"]):
+        assert (c.ov, c.k, c.t, c.tau, c.which) == (r["ov"], r["k"], r["t"], r["tau"],
+                                                    r["which"])
+        assert c.side == r["side"]
+        assert abs(c.d - r["d"]) <= 1e-9 * max(1.0, abs(r["d"]))
+    for t in range(PH):
+        for o in range(O):
+            for k in range(K[o]):
+                np.testing.assert_allclose(out[2][t][k][o], want["A_union"][t][k][o],
+                                           rtol=1e-12, atol=1e-12)
+                np.testing.assert_allclose(out[3][t][k][o], want["b_union"][t][k][o],
+                                           rtol=1e-9)
+
+
+def test_graph_step_refuses_a_different_mode_split(gpu):
+    from ccmpc import step
+    init, pmf, gmm, minpos, pasts, K, eps = _inputs()
+    g = step.MinkowskiStepGraph(O, N, PH, pmf.shape[1], [k + 1 for k in K], device=gpu)
+    with pytest.raises(ValueError):
+        g.set_inputs(1, init, pmf, gmm, minpos, _ref(0), np.zeros((sum(K) + O, 3)),
+                     np.zeros((sum(K) + O, 2)), np.zeros((sum(K) + O, 2)))
