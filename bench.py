@@ -572,18 +572,25 @@ def time_graph_replay(g, dev, n=200):
     return ev0.elapsed_time(ev1) * 1e-3 / n
 
 
-def pmc_traffic(kernel_prefix):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
-    (kernel_prefix stops before the balanced-mode template flag, so both names match)
-    (profiles/<round>/summary.json, written by profiles/collect.sh on this same default
-    workload: FETCH_SIZE x2 (gfx950) + WRITE_SIZE).  None when no summary is committed."""
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")))
-    for path in reversed(paths):
-        with open(path) as f:
-            summ = json.load(f)
-        for name, d in summ.items():
-            if name.startswith(kernel_prefix) and "hbm_bytes_avg" in d:
-                return int(d["hbm_bytes_avg"]), os.path.relpath(path, ROOT)
+def pmc_traffic(kernel_prefix, config=None):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary: the
+    per-configuration one (profiles/<round>/configs/<config>_summary.json, written by
+    profiles/collect_configs.sh: that configuration's launches only) when `config` is given and
+    one exists, else profiles/<round>/summary.json (profiles/collect.sh).  FETCH_SIZE x2
+    (gfx950) + WRITE_SIZE.  kernel_prefix stops before the balanced-mode template flag, so both
+    names match.  (None, None) when nothing is committed."""
+    rounds = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))
+    for rdir in reversed(rounds):
+        paths = ([os.path.join(rdir, "configs", f"{config}_summary.json")] if config else [])
+        paths.append(os.path.join(rdir, "summary.json"))
+        for path in paths:
+            if not os.path.exists(path):
+                continue
+            with open(path) as f:
+                summ = json.load(f)
+            for name, d in summ.items():
+                if name.startswith(kernel_prefix) and "hbm_bytes_avg" in d:
+                    return int(d["hbm_bytes_avg"]), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -687,7 +694,7 @@ def main():
     t_mom = time_kernel_live(lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws), dev)
 
     pcie = pcie_inclusive(cyc, step, dev)
-    traffic, traffic_src = pmc_traffic("void ccmpc::moments_kernel<double, 1, true")
+    traffic, traffic_src = pmc_traffic("void ccmpc::moments_kernel<double, 1, true", "C2")
     value = world * args.steps / elapsed
     out = {
         "metric": METRIC,
@@ -747,7 +754,7 @@ def main():
         # same kernel is meaningful at the per-GPU C4 batch, reported beside it
         c4 = time_config(dev, args.seed, *C4_GPU)
         c4["traffic"], c4["traffic_source"] = pmc_traffic(
-            "void ccmpc::moments4_kernel<double, 6, true")
+            "void ccmpc::moments4_kernel<double, 6, true", "C4")
         c4["alg_bytes_per_launch"] = c4["particles"] * 2 * C4_GPU[3] * 8
         out["roofline_c4_batch"] = c4
     if rank == 0 and world == 1:

@@ -285,7 +285,11 @@ __device__ void minkowski_cell(const double *C, const double *mu, int T, int cel
   const int rows = 2 * T;
   const int P = T * (T - 1) / 2;
   ccmpc_halfspace *rec = mp.out_rec + static_cast<int64_t>(cell) * P;
-  const int half = (nthreads >= 128) ? nthreads / 2 : 0;  // wave-aligned when blockDim % 128 == 0
+  // lower bounds on the other half of the group (other waves: truly concurrent with the MVOE
+  // chains) while the records fit half the threads; beyond that every thread takes whole pairs
+  // (a record's chain is the tail's critical path, so fewer rounds of chains win: T = 40's 780
+  // pairs on 512 threads take 2 rounds instead of 4)
+  const int half = (nthreads >= 128 && P <= nthreads / 2) ? nthreads / 2 : 0;
   const bool lb_side = half && tid >= half;
   const int base = lb_side ? tid - half : tid, stride = half ? half : nthreads;
   for (int p = base; p < P; p += stride) {

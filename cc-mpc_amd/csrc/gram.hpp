@@ -46,12 +46,28 @@ struct Geo {
 // MFMA work over many CUs.  Large inputs are bandwidth-bound: 256 per wave means fewer slabs
 // and a shallower tree.  (64 at RB >= 3 balances the f64 matrix pipes better per wave but
 // pays the per-workgroup combine ~3x more often: C5 went from 94 to 134 us.)
+#ifndef CCMPC_LGWQ_SMALL  // build-time knobs (tools/build_variant.sh experiments)
+#define CCMPC_LGWQ_SMALL 6
+#endif
+#ifndef CCMPC_LGWQ_MID
+#define CCMPC_LGWQ_MID CCMPC_LGWQ_SMALL
+#endif
+#ifndef CCMPC_LGWQ_LARGE
+#define CCMPC_LGWQ_LARGE 9
+#endif
+#ifndef CCMPC_LG_TINY_INPUT
+#define CCMPC_LG_TINY_INPUT 15
+#endif
+#ifndef CCMPC_LG_SMALL_INPUT
+#define CCMPC_LG_SMALL_INPUT 18
+#endif
 inline int store_lg_wave_quota(int /*rb*/, int64_t n_bound) {
 #if CCMPC_PROBE & 8  // diagnostic build only: CCMPC_LG_WQ overrides the large-input quota
   static const int ov = [] { const char *e = getenv("CCMPC_LG_WQ"); return e ? atoi(e) : 0; }();
-  if (ov && n_bound > (int64_t(1) << 18)) return ov;
+  if (ov && n_bound > (int64_t(1) << CCMPC_LG_SMALL_INPUT)) return ov;
 #endif
-  return n_bound <= (int64_t(1) << 18) ? 6 : 8;
+  if (n_bound <= (int64_t(1) << CCMPC_LG_TINY_INPUT)) return CCMPC_LGWQ_SMALL;
+  return n_bound <= (int64_t(1) << CCMPC_LG_SMALL_INPUT) ? CCMPC_LGWQ_MID : CCMPC_LGWQ_LARGE;
 }
 
 inline int lg_waves_per_item(int rb) { return rb <= 2 ? 2 : 3; }
@@ -138,7 +154,9 @@ __device__ __forceinline__ bool locate_item(int32_t item, const int64_t *__restr
 // always fits (sum_c ceil(n_c / chunk) <= total / chunk + n_cells <= G), and no CU streams
 // more than its slots x chunk.  (A binary search for the smallest fitting chunk cost ~3 us of
 // wave reductions per launch on C4, more than the ~5% shorter stream it bought.)
-inline bool balanced_mode(int64_t n_bound) { return n_bound > (int64_t(1) << 18); }
+inline bool balanced_mode(int64_t n_bound) {
+  return n_bound > (int64_t(1) << CCMPC_LG_SMALL_INPUT);
+}
 constexpr int kChunkAlign = 16;  // item boundaries: whole 128-byte f64 lines, aligned quads
 
 // ceil(n / d) for n >= 0, d > 0: 32-bit when both fit (every realistic cell), else 64-bit.
@@ -337,46 +355,64 @@ __device__ __forceinline__ void decode_entry(int e, int RB, int &i, int &j) {
   j = 16 * (bi + t) + col;
 }
 
-// Combine the NW waves' accumulators in a fixed order (wave 0 + 1 + ... + NW-1), tile by tile
-// through `xch` ((NW-1) x 256 doubles, >= 16 NW), and let wave 0 write the item's slab: to
-// global memory write-through (to_lds = false) or to the LDS slab `dst` (to_lds = true).
-// Every thread of the workgroup must call it.
+// Tiles exchanged per round of combine_waves, and the LDS it needs (doubles).  Up to 5 tiles
+// per round: T = 40's 15 tiles in 3 rounds, 80 KB of LDS at 8 waves.
+__host__ __device__ constexpr int combine_tiles_per_round(int rb) {
+  return n_tiles(rb) < 5 ? n_tiles(rb) : 5;
+}
+__host__ __device__ constexpr int combine_xch_doubles(int rb, int nw) {
+  return nw * combine_tiles_per_round(rb) * 256 > 16 * nw ? nw * combine_tiles_per_round(rb) * 256
+                                                          : 16 * nw;
+}
+
+// Combine the NW waves' accumulators in a fixed order (wave 0 + 1 + ... + NW-1) and write the
+// item's slab: to global memory write-through (to_lds = false) or to the LDS slab `dst`
+// (to_lds = true).  Rounds of up to combine_tiles_per_round tiles: every wave parks its tiles
+// in `xch` (combine_xch_doubles(RB, NW) doubles), then EVERY thread sums entry pairs over the
+// waves and stores them -- the sum and the stores are spread over the whole workgroup (with
+// wave 0 alone doing them tile by tile, T = 40's 15 tiles took 28 us).  Every thread of the
+// workgroup must call it.
 template <int RB, int NACC, int NW>
 __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)],
                                               const double (&s1)[RB], double *xch, double *dst,
                                               bool to_lds) {
   constexpr int NT = n_tiles(RB);
+  constexpr int TB = combine_tiles_per_round(RB);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(dst);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    d4 s = acc[0][t];
-    if (NACC == 2) s += acc[NACC - 1][t];
-    if (NW > 1) {
-      if (w > 0) {
+  for (int t0 = 0; t0 < NT; t0 += TB) {
+    // park: xch[((w TB + tb) 4 + k) 64 + lane] = this wave's register k of tile t0 + tb
 #pragma unroll
-        for (int k = 0; k < 4; ++k) xch[(w - 1) * 256 + k * 64 + lane] = s[k];
+    for (int tb = 0; tb < TB; ++tb) {
+      if (t0 + tb < NT) {
+        d4 s = acc[0][t0 + tb];
+        if (NACC == 2) s += acc[NACC - 1][t0 + tb];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xch[((w * TB + tb) * 4 + k) * 64 + lane] = s[k];
       }
-      __syncthreads();
     }
-    if (w == 0) {
-      double v[4];
+    __syncthreads();
+    // slab entry t*256 + 4 l + k <-> (tile t, lane l, register k); pairs (k, k+1), k even
+    const int n_e = (NT - t0 < TB ? NT - t0 : TB) * 256;
+    for (int e = 2 * threadIdx.x; e < n_e; e += 2 * blockDim.x) {
+      const int tb = e >> 8, l = (e >> 2) & 63, k = e & 3;
+      const double *x = xch + (tb * 4 + k) * 64 + l;
+      double a = x[0], b = x[64];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[k] = s[k];
-#pragma unroll
-        for (int o = 0; o < NW - 1; ++o) v[k] += xch[o * 256 + k * 64 + lane];
+      for (int o = 1; o < NW; ++o) {
+        a += x[o * TB * 256];
+        b += x[o * TB * 256 + 64];
       }
-      const int e = t * 256 + 4 * lane;
+      const int ge = t0 * 256 + e;
       if (to_lds) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dst[e + k] = v[k];
+        dst[ge] = a;
+        dst[ge + 1] = b;
       } else {
-        st2_sc1(rs, 8 * e, v[0], v[1]);
-        st2_sc1(rs, 8 * (e + 2), v[2], v[3]);
+        st2_sc1(rs, 8 * ge, a, b);
       }
     }
-    if (NW > 1) __syncthreads();
+    __syncthreads();
   }
 #pragma unroll
   for (int b = 0; b < RB; ++b) {
@@ -446,7 +482,10 @@ __device__ __forceinline__ int32_t tree_next_first(int32_t first_l, int cell) {
 // A level with at most kRootFanIn nodes is combined by ONE last arriver (the root); larger
 // levels are reduced in fixed groups of kFanIn first.  Cells up to 64 items thus need a single
 // arrival round trip.
-constexpr int kRootFanIn = 64;
+#ifndef CCMPC_ROOT_FANIN
+#define CCMPC_ROOT_FANIN 64
+#endif
+constexpr int kRootFanIn = CCMPC_ROOT_FANIN;
 
 // Host: capacity of level l (nodes) for n_cells cells holding <= max_items items in total.
 inline int64_t level_capacity(int64_t max_items, int64_t n_cells, int l) {

@@ -55,6 +55,16 @@ __device__ unsigned long long g_probe_ts[kProbeMaxWG * kProbeSlots];
 
 namespace ccmpc {
 
+// Load groups in flight per wave (a ring: DEPTH - 1 groups stream while one is multiplied).
+#ifndef CCMPC_DEPTH
+#define CCMPC_DEPTH 2
+#endif
+#ifndef CCMPC_DEPTH4
+#define CCMPC_DEPTH4 CCMPC_DEPTH
+#endif
+constexpr int kDepth = CCMPC_DEPTH;
+constexpr int kDepth4 = CCMPC_DEPTH4;
+
 // Loads are pure loads, branch-free: every lane always issues its 16-byte loads, the address
 // clamped to the wave's last aligned quad (addressable because cell offsets and ld are
 // multiples of 4).  Masking (out-of-range particles, dead rows) happens in mfma_group, so a
@@ -210,7 +220,7 @@ void moments_kernel(
   constexpr int S = G::S;
   constexpr int E = slab_doubles(RB);
   constexpr bool COV_IN_LDS = MINK && RB <= 2;
-  __shared__ double xch[(G::NW - 1) * 256];
+  __shared__ double xch[combine_xch_doubles(RB, G::NW)];
   __shared__ double slab_lds[E];
   __shared__ double shift_lds[D];
   __shared__ double S_lds[D];
@@ -260,22 +270,28 @@ void moments_kernel(
     // sched_barrier(0) fences keep the four phases in program order, so each MFMA group waits
     // (vmcnt) only for its own buffer while the other buffer's loads stay in flight.
     const int64_t ngroups = wr.ngroups, st = wr.stride;
-    Quad<P> va[S][RB], vb[S][RB];
+    constexpr int DP = kDepth;
+    Quad<P> buf[DP][S][RB];
     if (ngroups > 0) {
-      load_group<P, RB, S>(va, rowp, wr.p0, p1, g);
+      // ring of DP load groups: group g lives in buf[g % DP]; DP - 1 groups are in flight
+      // while one is multiplied
+#pragma unroll
+      for (int d = 0; d < DP - 1; ++d) load_group<P, RB, S>(buf[d], rowp, wr.p0 + d * st, p1, g);
       int64_t gi = 0;
-      for (; gi + 2 <= ngroups; gi += 2) {
-        const int64_t ga = wr.p0 + gi * st, gb = ga + st;
-        load_group<P, RB, S>(vb, rowp, gb, p1, g);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_group<P, RB, S, NACC>(va, sh, live, ga, p1, g, acc, s1);
-        __builtin_amdgcn_sched_barrier(0);
-        load_group<P, RB, S>(va, rowp, gb + st, p1, g);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_group<P, RB, S, NACC>(vb, sh, live, gb, p1, g, acc, s1);
-        __builtin_amdgcn_sched_barrier(0);
+      for (; gi + DP <= ngroups; gi += DP) {
+#pragma unroll
+        for (int d = 0; d < DP; ++d) {
+          load_group<P, RB, S>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1,
+                               g);
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-      if (gi < ngroups) mfma_group<P, RB, S, NACC>(va, sh, live, wr.p0 + gi * st, p1, g, acc, s1);
+#pragma unroll
+      for (int d = 0; d < DP - 1; ++d)  // the < DP groups left were loaded ahead
+        if (gi + d < ngroups)
+          mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
     }
     PROBE_TS(2);
 
@@ -428,22 +444,24 @@ __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
     for (int I = 0; I < NB; ++I) s1[I] = 0.0;
 
     const int64_t ngroups = wr.ngroups, st = wr.stride;
-    Pair<P> va[NB], vb[NB];
+    constexpr int DP = kDepth4;
+    Pair<P> buf[DP][NB];
     if (ngroups > 0) {
-      load_group4<P, NB>(va, rowp, wr.p0, p1, m);
+#pragma unroll
+      for (int d = 0; d < DP - 1; ++d) load_group4<P, NB>(buf[d], rowp, wr.p0 + d * st, p1, m);
       int64_t gi = 0;
-      for (; gi + 2 <= ngroups; gi += 2) {
-        const int64_t ga = wr.p0 + gi * st, gb = ga + st;
-        load_group4<P, NB>(vb, rowp, gb, p1, m);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_group4<P, NB>(va, sh, live, ga, p1, m, acc, s1);
-        __builtin_amdgcn_sched_barrier(0);
-        load_group4<P, NB>(va, rowp, gb + st, p1, m);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_group4<P, NB>(vb, sh, live, gb, p1, m, acc, s1);
-        __builtin_amdgcn_sched_barrier(0);
+      for (; gi + DP <= ngroups; gi += DP) {
+#pragma unroll
+        for (int d = 0; d < DP; ++d) {
+          load_group4<P, NB>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1, m);
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_group4<P, NB>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, m, acc, s1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-      if (gi < ngroups) mfma_group4<P, NB>(va, sh, live, wr.p0 + gi * st, p1, m, acc, s1);
+#pragma unroll
+      for (int d = 0; d < DP - 1; ++d)
+        if (gi + d < ngroups) mfma_group4<P, NB>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, m, acc, s1);
     }
     PROBE_TS(2);
 

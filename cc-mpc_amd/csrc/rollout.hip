@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
   constexpr int NW = ideal_waves(RB);
   __shared__ StepPlan plan[40];
   __shared__ double stage_all[NW * D * kStageStride];
-  __shared__ double xch[(NW - 1) * 256 > 64 ? (NW - 1) * 256 : 64];
+  __shared__ double xch[combine_xch_doubles(RB, NW)];
   __shared__ double shift_s[D];
   __shared__ double S_lds[D];
   __shared__ double mean_lds[D];

@@ -3,6 +3,8 @@
     python tools/probe_moments.py C4 moments 200
     python tools/probe_moments.py C5 cycle 100
     python tools/probe_moments.py ALL time 0      (graph-timed us per launch, every config)
+    ROTATE=3 python tools/probe_moments.py C4full cycle 30   (launches rotate over 3 copies of
+                                                              the store: every launch from HBM)
 """
 import os
 import sys
@@ -15,7 +17,8 @@ import torch  # noqa: E402
 from ccmpc import cycle, engine, synthetic  # noqa: E402
 
 CONFIGS = {"C2": (4, 5000, 8, 1), "C3": (1, 100000, 8, 1), "C4": (4, 20000, 12, 8),
-           "C5": (8, 50000, 40, 1)}
+           "C5": (8, 50000, 40, 1), "C3-1e3": (1, 1000, 8, 1), "C3-2e4": (1, 20000, 8, 1),
+           "C4full": (4, 20000, 12, 64)}
 
 
 def build(name, dev):
@@ -56,10 +59,15 @@ def main():
         refs.append(ref)
     store = engine.ParticleStore.from_cells(cells, device=dev)
     cyc = cycle.MinkowskiCycle(store, K, refs[0])
-    fn = cyc.run if what == "cycle" else (
-        lambda: engine.moments(store, cyc.mean, cyc.cov, cyc.ws))
-    for _ in range(iters):
-        fn()
+    cycles = [cyc]
+    for _ in range(int(os.environ.get("ROTATE", "1")) - 1):
+        sys.path.insert(0, ROOT)
+        from bench import clone_cycle
+        cycles.append(clone_cycle(cyc))
+    fns = [c.run if what == "cycle" else
+           (lambda c=c: engine.moments(c.store, c.mean, c.cov, c.ws)) for c in cycles]
+    for i in range(iters):
+        fns[i % len(fns)]()
     torch.cuda.synchronize()
     print(f"{name} {what} x{iters}: {sum(store.counts)} particles, {store.n_cells} cells")
 

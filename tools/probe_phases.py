@@ -61,20 +61,21 @@ def one(name, what, dev, lib, back_to_back=1):
     if what == "cycle":
         print("  halfspaces ", stats((rel[:, 6] - rel[:, 5])[fin]))
         order = np.argsort(rel[:, 0])
-        print("  start by block (block:us):",
-              " ".join(f"{int(b)}:{rel[b, 0] / 100:.2f}" for b in range(len(rel))))
         print("  slowest starters:", [int(b) for b in order[-10:]])
     print("  end at     ", stats(np.maximum(rel[:, 4], rel[:, 6])))
 
 
 def main():
+    """python tools/probe_phases.py [NAME:moments|cycle ...] (default: every config's moments,
+    then the C2 cycle)."""
     dev = torch.device("cuda:0")
     lib = _lib.load()
     lib.ccmpc_probe_timestamps.restype = ctypes.c_int
     lib.ccmpc_probe_timestamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    for name in CONFIGS:
-        one(name, "moments", dev, lib, back_to_back=5)
-    one("C2", "cycle", dev, lib, back_to_back=5)
+    jobs = [a.split(":") for a in sys.argv[1:]] or (
+        [(n, "moments") for n in CONFIGS] + [("C2", "cycle")])
+    for name, what in jobs:
+        one(name, what, dev, lib, back_to_back=5)
 
 
 if __name__ == "__main__":

@@ -7,5 +7,5 @@ OUT=$ROOT/gpurun_out/variants
 mkdir -p "$OUT"
 cp "$LIB" /tmp/libccmpc.real.so
 cp "$ROOT/cc-mpc_amd/csrc/${PROBE_LIB:-build_p4}/libccmpc.so" "$LIB"
-timeout -k 10 300 python3 "$ROOT/tools/probe_phases.py" > "$OUT/timeline.txt" 2>&1
+timeout -k 10 300 python3 "$ROOT/tools/probe_phases.py" $JOBS > "$OUT/timeline.txt" 2>&1
 cp /tmp/libccmpc.real.so "$LIB"
