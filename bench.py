@@ -117,7 +117,7 @@ def sweep(dev, seed):
 C4_FULL = {"scenes": 64, "O": 4, "N": 20000, "T": 12}
 
 
-def c4_sharded(dev, seed, world, rank, steps=20, warmup=3):
+def c4_sharded(dev, seed, world, rank, steps=20, warmup=3, cfg=None, return_records=False):
     """BASELINE.json configs[3] as the node runs it: 64 independent scenes x 4 OVs x np=20000,
     ph=12, sharded over the ranks in contiguous scene blocks (ccmpc.dist.scene_range; strong
     scaling: the batch is fixed).  One step = every rank's ccmpc_minkowski_cycle over its
@@ -125,7 +125,7 @@ def c4_sharded(dev, seed, world, rank, steps=20, warmup=3):
     exchange), timed between barriers, max over ranks.  Also the rank's kernel alone, back to
     back (warm) and rotating over distinct stores (cold HBM), as its HBM fraction."""
     from ccmpc import cycle, dist as cdist, engine, synthetic
-    c = C4_FULL
+    c = C4_FULL if cfg is None else cfg
     b, e = cdist.scene_range(c["scenes"], rank, world)
     cells, K, refs = [], [], []
     for sc in range(b, e):
@@ -143,11 +143,12 @@ def c4_sharded(dev, seed, world, rank, steps=20, warmup=3):
         counts = cdist.record_counts(store.n_cells, "cpu" if gloo else dev)
         gather = ((lambda: cdist.gather_records(cyc.rec.cpu(), counts=counts)) if gloo else
                   (lambda: cdist.gather_records(cyc.rec, counts=counts)))
+    gathered = [cyc.rec]
 
     def step():
         launch()
         if gather is not None:
-            gather()
+            gathered[0] = gather()
 
     for _ in range(warmup):
         step()
@@ -188,6 +189,8 @@ def c4_sharded(dev, seed, world, rank, steps=20, warmup=3):
         out["rank0"].update({"kernel_us_cold": round(t_cold * 1e6, 2),
                              "hbm_frac_cold": round(alg / t_cold / HBM_PEAK, 4),
                              "cold_copies": k})
+    if return_records:       # every scene's records, as the timed step's gather left them
+        return out, gathered[0]
     return out
 
 

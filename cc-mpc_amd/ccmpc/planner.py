@@ -364,21 +364,20 @@ class MidlevelAgent:
     def _state_stats(self, scene, mean0, cov0, yaw=None):
         """ovStateMean/Cov_tau_1 (:864-875): t = 0 mean / variance of x, y, yaw per (ov, k).
         yaw = (yaw_mean at t = 0 [C], yaw0_var [C]) when already on the host."""
-        O, K = scene.O, scene.K
+        K = scene.K
         maxK = max(K)
         if yaw is None:
             l4 = scene.l4()
             ym, yv = l4["yaw_mean"][:, 0].cpu().numpy(), l4["yaw0_var"].cpu().numpy()
         else:
             ym, yv = yaw
-        mx, my, myaw, vx, vy, vyaw = (_object_grid(O, maxK) for _ in range(6))
-        c = 0
-        for o in range(O):
-            for k in range(K[o]):
-                mx[o][k], my[o][k], myaw[o][k] = mean0[c, 0], mean0[c, 1], ym[c]
-                vx[o][k], vy[o][k], vyaw[o][k] = cov0[c, 0, 0], cov0[c, 1, 1], yv[c]
-                c += 1
-        return (mx, my, myaw), (vx, vy, vyaw)
+        first = np.concatenate([[0], np.cumsum(K)[:-1]]).astype(int)
+
+        def grid(col):          # [o][k] lists, None where OV o has no mode k
+            vals = col.tolist()
+            return [vals[f:f + k] + [None] * (maxK - k) for f, k in zip(first, K)]
+        return ((grid(mean0[:, 0]), grid(mean0[:, 1]), grid(np.asarray(ym))),
+                (grid(cov0[:, 0, 0]), grid(cov0[:, 1, 1]), grid(np.asarray(yv))))
 
     def _l4_lists(self, scene):
         ph = self.prediction_horizon
@@ -628,13 +627,17 @@ class MidlevelAgent:
                      self._cell_risk_host(np.asarray(eps_ura), K),
                      np.repeat(past_last, K, axis=0), np.repeat(bboxes, K, axis=0),
                      filter_pmf=filter_pmf)
-        g.replay()
-        o = g.out.snapshot()            # every output in one host copy (outlives the replay)
+        g.launch()
+        # host objects that need no output are built while the graph runs
         st = g.store
+        scene = ovehicle.ScenePredictions(st, K, past_last, bboxes)
+        ovs = [ovehicle.OVehicle(scene, j, past=pasts[j]) for j in range(O)]
+        vertices, direct = LazyVertices(scene, ph), _object_grid(O)
+        g.wait()
+        o = g.out.snapshot()            # every output in one host copy (outlives the replay)
         st.counts = o["cnt"].tolist()
         st.offsets = o["off"].tolist()
-        scene = ovehicle.ScenePredictions(st, K, past_last, bboxes, o["pmf"], o["centre"])
-        ovs = [ovehicle.OVehicle(scene, j, past=pasts[j]) for j in range(O)]
+        scene.cell_pmf, scene.init_center = o["pmf"], o["centre"]
         h = o["rec"].reshape(-1).view(engine._lib.HALFSPACE_DTYPE).reshape(g.C, g.P)
         constraints = HalfSpaceList(h, scene.cell_of, T * (T - 1) // 2)
         self.last_records = h
@@ -645,9 +648,8 @@ class MidlevelAgent:
         mean0, cov0 = mean[:, 0, :], cov[:, 0:2, 0:2]
         st_mean, st_cov = self._state_stats(scene, mean0, cov0,
                                             (o["yaw_mean"][:, 0], o["yaw0_var"]))
-        out = (constraints, LazyVertices(scene, ph), UnionGrid(o["A"], K, ph),
-               UnionGrid(o["b"], K, ph), self._ov_in_junction(scene, mean0),
-               _object_grid(O), st_mean, st_cov, 0)
+        out = (constraints, vertices, UnionGrid(o["A"], K, ph), UnionGrid(o["b"], K, ph),
+               self._ov_in_junction(scene, mean0), direct, st_mean, st_cov, 0)
         return ovs, out
 
     def solve_planning_qp(self, x_init, goal, ref_traj, Tsh, u_prev=None, lon=3.7,

@@ -210,13 +210,60 @@ class MinkowskiStepGraph:
         i.h("past")[:] = np.asarray(past_last, np.float64).reshape(self.C, 2)
         i.h("bbox")[:] = np.asarray(bbox, np.float64).reshape(self.C, 2)
 
-    def replay(self):
-        """One step: the graph (inputs up, five kernels, outputs down); returns when the output
-        pack is on the host."""
+    def bind(self):
+        """Pre-convert every argument of the step's C-ABI calls for the current stream (the
+        direct-launch alternative to the graph: one foreign call per stage, the cycle and L4
+        back to back on one stream)."""
+        lib, p, s = _lib.load(), engine._p, engine._stream()
+        i, o, st, sm = self.inp, self.out, self.store, self.samples
+        O, N, T, L, C = self.O, self.N, self.T, self.L, self.C
+        ws, mws = self.bucket_ws, self.ws.buf
+        self._calls = [
+            (lib.ccmpc_copy_async, (p(i.dev), p(i.host), i.nbytes, s)),
+            (lib.ccmpc_sample_unicycle_ex, (
+                p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None,
+                None, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld, s)),
+            (lib.ccmpc_bucket, (p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
+                                p(i.d("nk")), p(i.d("base")), self.max_k, p(i.d("minpos")),
+                                p(i.d("region")), p(ws), ws.numel(), p(st.pos), st.ld,
+                                p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")), p(o.d("centre")),
+                                s)),
+            (lib.ccmpc_minkowski_cycle, (
+                p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
+                st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
+                self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")),
+                p(o.d("pl")), s)),
+            (lib.ccmpc_l4, (p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
+                            p(o.d("cnt")), C, p(i.d("past")), p(i.d("bbox")), p(o.d("A")),
+                            p(o.d("b")), p(o.d("yaw_mean")), p(o.d("yaw0_var")), None, None,
+                            s)),
+            (lib.ccmpc_copy_async, (p(o.host), p(o.dev), o.nbytes, s)),
+        ]
+        return self
+
+    def launch(self, direct=False):
+        """Enqueue one step (inputs up, the kernels, outputs down) without waiting: one graph
+        replay, or (direct) the bound C-ABI calls."""
+        if direct:
+            if getattr(self, "_calls", None) is None:
+                self.bind()
+            for fn, args in self._calls:
+                rc = fn(*args)
+                if rc != 0:
+                    _lib.check(rc, fn.__name__)
+            return
         if self.graph is None:
             self.capture()
         self.graph.replay()
+
+    def wait(self):
+        """Return when the launched step's output pack is on the host."""
         torch.cuda.current_stream(self.device).synchronize()
+
+    def replay(self):
+        """One step; returns when the output pack is on the host."""
+        self.launch()
+        self.wait()
 
     def records(self):
         return self.out.h("rec").reshape(-1).view(_lib.HALFSPACE_DTYPE).reshape(self.C, self.P)

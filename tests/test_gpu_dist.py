@@ -64,3 +64,41 @@ def test_two_ranks_shard_a_multi_scene_cycle(gpu, tmp_path):
     from ccmpc import _lib
     recs = got.numpy().view(_lib.HALFSPACE_DTYPE).reshape(got.shape[:2])
     assert np.all(recs["status"] == 0)
+
+
+BENCH_CFG = {"scenes": 5, "O": 3, "N": 1200, "T": 12}
+
+
+def _bench_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "cc-mpc_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        out, full = bench.c4_sharded(torch.device("cuda:0"), 77, world, rank, steps=2, warmup=1,
+                                     cfg=BENCH_CFG, return_records=True)
+        if rank == 0:
+            torch.save(full.cpu(), os.path.join(out_dir, "bench_gathered.pt"))
+            assert out["records_ok"] and out["n_gpus"] == world
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_c4_shard_path_gathers_every_scene(gpu, tmp_path):
+    """bench.py's c4_sharded (what the driver's SCALE run times at N > 1) on two gloo ranks:
+    the records gathered inside the timed step are the single-rank batch's, bit for bit."""
+    import sys
+    import torch.multiprocessing as mp
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    mp.start_processes(_bench_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2,
+                       join=True, start_method="spawn")
+    got = torch.load(os.path.join(tmp_path, "bench_gathered.pt"), weights_only=True)
+    _, want = bench.c4_sharded(gpu, 77, 1, 0, steps=1, warmup=1, cfg=BENCH_CFG,
+                               return_records=True)
+    assert torch.equal(got, want.cpu())

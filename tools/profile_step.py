@@ -48,6 +48,25 @@ def main():
         g.graph.replay()
         torch.cuda.current_stream().synchronize()
     print(f"replay + sync: {(time.perf_counter() - t0) / a.steps * 1e6:.1f} us")
+    g.bind()
+    for i in range(10):
+        g.launch(direct=True)
+        g.wait()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        g.launch(direct=True)
+        g.wait()
+    print(f"direct launches + sync: {(time.perf_counter() - t0) / a.steps * 1e6:.1f} us")
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        g.launch(direct=True)
+    torch.cuda.current_stream().synchronize()
+    print(f"direct launches, host only: {(time.perf_counter() - t0) / a.steps * 1e6:.1f} us")
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        g.graph.replay()
+    torch.cuda.current_stream().synchronize()
+    print(f"graph replays, host only: {(time.perf_counter() - t0) / a.steps * 1e6:.1f} us")
     t0 = time.perf_counter()
     for i in range(a.steps):
         g.set_inputs(i, init, pmf, gmm, minpos, ref, np.zeros((sum(K), 3)) + 1,
