@@ -16,6 +16,25 @@
 
 namespace ccmpc {
 
+#ifndef CCMPC_PROBE
+#define CCMPC_PROBE 0
+#endif
+// CCMPC_PROBE & 4 (diagnostic build only): per-workgroup phase timestamps (s_memrealtime,
+// 100 MHz) read back by ccmpc_probe_l4_timestamps (tools/probe_l4.py).
+#if CCMPC_PROBE & 4
+constexpr int kL4ProbeSlots = 8, kL4ProbeMaxWG = 4096;
+__device__ unsigned long long g_l4_ts[kL4ProbeMaxWG * kL4ProbeSlots];
+#define L4_TS(k)                                                                               \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kL4ProbeMaxWG)                                        \
+      g_l4_ts[blockIdx.x * kL4ProbeSlots + (k)] = __builtin_amdgcn_s_memrealtime();            \
+  } while (0)
+#else
+#define L4_TS(k) \
+  do {           \
+  } while (0)
+#endif
+
 template <typename P>
 __device__ __forceinline__ double world(const P *pos, int64_t ld, int row, int64_t i, double o) {
   return static_cast<double>(pos[static_cast<int64_t>(row) * ld + i]) + o;
@@ -67,7 +86,11 @@ __device__ __forceinline__ double block_max(double v, double *red) {
 // cos / sin of the rounded atan2, far below the 1e-13 vertex tolerance); a zero step keeps
 // sincos of atan2, whose signed-zero cases the ratio cannot express.
 __device__ __forceinline__ void heading_cs(double dx, double dy, double &yaw, double &S, double &C) {
+#if CCMPC_L4_PROBE_NOATAN  // diagnostic build only: the transcendental's share of the kernel
+  yaw = dy * dx;
+#else
   yaw = atan2(dy, dx);
+#endif
   const double r = sqrt(dx * dx + dy * dy);
   if (r > 0.0 && isfinite(r)) {
     C = dx / r;
@@ -77,8 +100,11 @@ __device__ __forceinline__ void heading_cs(double dx, double dy, double &yaw, do
   }
 }
 
-constexpr int kL4Threads = 512;  // 8 waves: 2 per SIMD, so the f64 transcendental chains overlap
-constexpr int kL4Cache = 8;      // headings kept in registers between the passes (4096 particles)
+#ifndef CCMPC_L4_THREADS
+#define CCMPC_L4_THREADS 512
+#endif
+constexpr int kL4Threads = CCMPC_L4_THREADS;  // 8 waves: 2 per SIMD, f64 chains overlap
+constexpr int kL4Cache = 12;     // headings kept in registers between the passes (6144 particles)
 
 template <typename P>
 __global__ __launch_bounds__(kL4Threads) void l4_kernel(
@@ -89,6 +115,7 @@ __global__ __launch_bounds__(kL4Threads) void l4_kernel(
     double *__restrict__ out_yaw0_var, double *__restrict__ out_yaw,
     double *__restrict__ out_vertices) {
   __shared__ double red[16];
+  L4_TS(0);
   const int cell = blockIdx.x / T, t = blockIdx.x % T;
   const int64_t off = cell_off[cell], n = cell_cnt[cell];
   const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
@@ -136,13 +163,16 @@ __global__ __launch_bounds__(kL4Threads) void l4_kernel(
     delta(i, x, y, dx, dy);
     take(i, atan2(dy, dx));
   }
+  L4_TS(1);
   const double nn = static_cast<double>(n);
   const double theta = block_sum(s, red) / nn;
+  L4_TS(2);
   if (t == 0) {
     const double a = block_sum(s1, red), b2 = block_sum(s2, red);
     if (threadIdx.x == 0) out_yaw0_var[cell] = (b2 - a * a / nn) / (nn - 1.0);
   }
 
+  L4_TS(3);
   // pass 2: corners and the four support values of A = [I; -I] R(theta)
   const double ct = cos(theta), st = sin(theta);
   const double A[4][2] = {{ct, st}, {-st, ct}, {-ct, -st}, {st, -ct}};
@@ -171,14 +201,22 @@ __global__ __launch_bounds__(kL4Threads) void l4_kernel(
     if (i < n) corners(i, xc[j], vc[j], sc[j], cc[j]);
   }
   for (int64_t i = threadIdx.x + static_cast<int64_t>(kL4Cache) * nth; i < n; i += nth) {
-    double x, y, dx, dy, yaw, S, C;
+    double x, y, dx, dy, S, C;
     delta(i, x, y, dx, dy);
-    heading_cs(dx, dy, yaw, S, C);
+    const double r = sqrt(dx * dx + dy * dy);
+    if (r > 0.0 && isfinite(r)) {  // cos / sin of the heading without the atan2 (heading_cs)
+      C = dx / r;
+      S = dy / r;
+    } else {
+      sincos(atan2(dy, dx), &S, &C);
+    }
     corners(i, x, y, S, C);
   }
+  L4_TS(4);
   double bm[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) bm[r] = block_max(mx[r], red);
+  L4_TS(5);
   if (threadIdx.x == 0) {
     const int64_t ct_idx = static_cast<int64_t>(cell) * T + t;
     for (int r = 0; r < 4; ++r) {
@@ -193,6 +231,17 @@ __global__ __launch_bounds__(kL4Threads) void l4_kernel(
 }  // namespace ccmpc
 
 using namespace ccmpc;
+
+#if CCMPC_PROBE & 4
+extern "C" int ccmpc_probe_l4_timestamps(void *host, int reset) {
+  const size_t bytes = sizeof(g_l4_ts);
+  if (reset) {
+    static unsigned long long zeros[kL4ProbeMaxWG * kL4ProbeSlots];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_l4_ts), zeros, bytes) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_l4_ts), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T,
                         const double *origin, const int64_t *cell_off, const int64_t *cell_cnt,

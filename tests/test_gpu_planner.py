@@ -120,12 +120,13 @@ def test_affine_generator(gpu):
         assert not c.holds(np.array([r["mean"][0], r["mean"][1]]))
 
 
-def test_make_ovehicles_matches_reference_bucketing(gpu):
+@pytest.mark.parametrize("N", [6000, 12000])   # one-workgroup path (<= 8192) / three launches
+def test_make_ovehicles_matches_reference_bucketing(gpu, N):
     """Sampler output -> buckets: same membership, same order, same pmf / init_center as
     make_ovehicles + OVehicle.from_trajectron (v8ideal/__init__.py:469-505, ovehicle.py:24-117)."""
     from ccmpc import engine, ovehicle
     rng = np.random.default_rng(7)
-    O, L, T, N = 3, 25, 8, 6000
+    O, L, T = 3, 25, 8
     pmf = np.stack([np.exp(rng.normal(0, 1.6, L)) for _ in range(O)])
     pmf /= pmf.sum(1, keepdims=True)
     for o in range(O):                       # make sure every OV keeps >= 1 mode
