@@ -34,9 +34,12 @@ inline int row_blocks(int64_t T) { return static_cast<int>((2 * T + 15) / 16); }
 // (one CU's 4 matrix pipes need ~4 us for a 2000-particle T=8 cell), so latency-bound sizes
 // use WQ = 64 (one load group per wave, one tree level); bandwidth-bound sizes use WQ = 256
 // (fewer slabs, shallower tree).  A cell that fits one item never leaves its workgroup.
+#ifndef CCMPC_LG_NW1  // log2 waves per work item at RB = 1 (T <= 8); build-time knob
+#define CCMPC_LG_NW1 3
+#endif
 template <int RB>
 struct Geo {
-  static constexpr int NW = RB <= 2 ? 4 : 8;
+  static constexpr int NW = RB == 1 ? (1 << CCMPC_LG_NW1) : (RB <= 2 ? 4 : 8);
   static constexpr int S = RB == 1 ? 4 : (RB == 2 ? 2 : 1);
   static constexpr int NACC = (n_tiles(RB) == 1) ? 2 : 1;  // 2 chains when there is one tile
   static constexpr int MIN_WAVES_PER_SIMD = RB == 1 ? 4 : 2;
@@ -70,7 +73,9 @@ inline int store_lg_wave_quota(int /*rb*/, int64_t n_bound) {
   return n_bound <= (int64_t(1) << CCMPC_LG_SMALL_INPUT) ? CCMPC_LGWQ_MID : CCMPC_LGWQ_LARGE;
 }
 
-inline int lg_waves_per_item(int rb) { return rb <= 2 ? 2 : 3; }
+__host__ __device__ inline int lg_waves_per_item(int rb) {
+  return rb == 1 ? CCMPC_LG_NW1 : (rb <= 2 ? 2 : 3);
+}
 
 inline int store_lg_chunk(int rb, int64_t n_bound) {
   return lg_waves_per_item(rb) + store_lg_wave_quota(rb, n_bound);

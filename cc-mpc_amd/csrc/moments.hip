@@ -233,7 +233,7 @@ void moments_kernel(
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int rows = 2 * T;
-  const int lg_chunk = lg_wq + (G::NW == 4 ? 2 : 3);
+  const int lg_chunk = lg_wq + lg_waves_per_item(RB);
 
   // one work item: the cell's particles [a, b) -> partial Gram -> combine tree / finalise
   auto item = [=](const ItemLoc &loc, int32_t nit, int64_t a, int64_t b) {
