@@ -83,6 +83,9 @@ SIGNATURES = {
     "ccmpc_ideal_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "ccmpc_l4": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64, _P, _P, _P, _P,
                                 _P, _P, _P, _P, _P]),
+    "ccmpc_l4_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
+    "ccmpc_l4_split": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64, _I64, _P,
+                                      _P, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ccmpc_ideal_moments": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _U64, _P,
                                            _P, _SZ, _P, _P, _P, _P]),
     "ccmpc_mpc_ltv": (ctypes.c_int, [_P, _I64, _I64, _D, _D, _D, _P, _P, _P]),

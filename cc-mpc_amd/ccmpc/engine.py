@@ -215,9 +215,12 @@ def ideal_minkowski_cycle(prev_mean, prev_cov, src_cell, T, n_samples, ref_traj,
     return out_mean, out_cov, status, rec, pl
 
 
-def l4(store, past_last, bbox, with_yaw=False, with_vertices=False):
-    """Headings, L4 outer approximation and t=0 yaw stats per (cell, t) (ccmpc_l4).
-    Returns dict(A [C,T,4,2], b [C,T,4], yaw_mean [C,T], yaw0_var [C], yaw?, vertices?)."""
+def l4(store, past_last, bbox, with_yaw=False, with_vertices=False, split=True,
+       workspace=None):
+    """Headings, L4 outer approximation and t=0 yaw stats per (cell, t): ccmpc_l4_split (every
+    (cell, t) over several workgroups, two launches) or, split=False, ccmpc_l4 (one workgroup
+    per (cell, t)).  Returns dict(A [C,T,4,2], b [C,T,4], yaw_mean [C,T], yaw0_var [C], yaw?,
+    vertices?)."""
     lib = _lib.load()
     C, T, dev = store.n_cells, store.T, store.device
     out = dict(A=torch.empty((C, T, 4, 2), dtype=torch.float64, device=dev),
@@ -230,10 +233,21 @@ def l4(store, past_last, bbox, with_yaw=False, with_vertices=False):
                        if with_vertices else None)
     past_last = torch.as_tensor(np.asarray(past_last, np.float64).reshape(C, 2), device=dev)
     bbox = torch.as_tensor(np.asarray(bbox, np.float64).reshape(C, 2), device=dev)
+    if split:
+        need = lib.ccmpc_l4_workspace_bytes(T, C, store.n_bound)
+        ws = (workspace or Workspace(dev)).get(need)
+        _lib.check(lib.ccmpc_l4_split(
+            _p(store.pos), store.ccmpc_dtype, store.ld, T, _p(store.origin), _p(store.cell_off),
+            _p(store.cell_cnt), C, store.n_bound, _p(past_last), _p(bbox), _p(ws), ws.numel(),
+            _p(out["A"]), _p(out["b"]), _p(out["yaw_mean"]), _p(out["yaw0_var"]),
+            _p(out["yaw"]), _p(out["vertices"]), _stream()), "ccmpc_l4_split")
+        out["_keepalive"] = (past_last, bbox, ws)
+        return out
     _lib.check(lib.ccmpc_l4(_p(store.pos), store.ccmpc_dtype, store.ld, T, _p(store.origin),
                             _p(store.cell_off), _p(store.cell_cnt), C, _p(past_last), _p(bbox),
                             _p(out["A"]), _p(out["b"]), _p(out["yaw_mean"]), _p(out["yaw0_var"]),
                             _p(out["yaw"]), _p(out["vertices"]), _stream()), "ccmpc_l4")
+    out["_keepalive"] = (past_last, bbox)
     return out
 
 

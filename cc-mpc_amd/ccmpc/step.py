@@ -124,6 +124,8 @@ class MinkowskiStepGraph:
                                          16), dtype=u8, device=self.device)
         self.ws = engine.Workspace(self.device)
         self.ws.get(lib.ccmpc_moments_workspace_bytes(T, C, st.n_bound))
+        self.l4_ws = engine.Workspace(self.device)      # its own: layouts differ
+        self.l4_ws.get(lib.ccmpc_l4_workspace_bytes(T, C, st.n_bound))
         self.side = torch.cuda.Stream(device=self.device)
         self.graph = None
         self._static_set = False
@@ -149,10 +151,12 @@ class MinkowskiStepGraph:
         main = torch.cuda.current_stream(self.device)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
-            chk(lib.ccmpc_l4(p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
-                             p(o.d("cnt")), C, p(i.d("past")), p(i.d("bbox")), p(o.d("A")),
-                             p(o.d("b")), p(o.d("yaw_mean")), p(o.d("yaw0_var")), None, None,
-                             engine._stream()), "ccmpc_l4")
+            lws = self.l4_ws.buf
+            chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
+                                   p(o.d("cnt")), C, st.n_bound, p(i.d("past")), p(i.d("bbox")),
+                                   p(lws), lws.numel(), p(o.d("A")), p(o.d("b")),
+                                   p(o.d("yaw_mean")), p(o.d("yaw0_var")), None, None,
+                                   engine._stream()), "ccmpc_l4_split")
         mws = self.ws.buf
         chk(lib.ccmpc_minkowski_cycle(
             p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
@@ -233,10 +237,11 @@ class MinkowskiStepGraph:
                 st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
                 self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")),
                 p(o.d("pl")), s)),
-            (lib.ccmpc_l4, (p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
-                            p(o.d("cnt")), C, p(i.d("past")), p(i.d("bbox")), p(o.d("A")),
-                            p(o.d("b")), p(o.d("yaw_mean")), p(o.d("yaw0_var")), None, None,
-                            s)),
+            (lib.ccmpc_l4_split, (p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
+                                  p(o.d("cnt")), C, st.n_bound, p(i.d("past")), p(i.d("bbox")),
+                                  p(self.l4_ws.buf), self.l4_ws.buf.numel(), p(o.d("A")),
+                                  p(o.d("b")), p(o.d("yaw_mean")), p(o.d("yaw0_var")), None,
+                                  None, s)),
             (lib.ccmpc_copy_async, (p(o.host), p(o.dev), o.nbytes, s)),
         ]
         return self

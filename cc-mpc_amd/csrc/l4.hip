@@ -12,7 +12,7 @@
 // the mean is bitwise reproducible), pass 2 takes the max of the four projections over every
 // corner, from registers for the particles pass 1 kept (re-reading the two steps beyond them).
 // Max is order-independent, so b is exact whatever the reduction order.
-#include "ccmpc_common.hpp"
+#include "gram.hpp"
 
 namespace ccmpc {
 
@@ -228,6 +228,181 @@ __global__ __launch_bounds__(kL4Threads) void l4_kernel(
   }
 }
 
+// ---- split over workgroups: every (cell, t) on S workgroups ------------------------------------
+// One workgroup per (cell, t) is issue-bound on its f64 atan2 / division work for large clouds
+// (a 5000-particle cell: 17 us on one CU; 100k particles would take ~0.3 ms), and uses one CU of
+// 256.  The split form runs two launches of (cell, t, chunk) workgroups:
+//   pass 1  headings of the chunk, partial sums (heading, shifted heading and its square for
+//           t = 0) published write-through; the (cell, t)'s last arriver sums them in chunk order
+//           -> theta, the yaw statistics, and theta for pass 2 in the workspace;
+//   pass 2  the chunk's corners and the four support-value maxima, published the same way; the
+//           last arriver takes the max over chunks (order-free) -> b.
+// The hand-off is the moment reduction's (gram.hpp: sc1 stores, drain, agent-scope ticket, sc1
+// loads); the counters at the head of the zero-filled workspace return to zero every call.
+struct L4Split {
+  int S;              // workgroups per (cell, t)
+  int32_t *ctr;       // [2][n_cells T] arrival counters
+  double *part1;      // [n_cells T][S][4]: sum yaw, sum (yaw - shift), sum (yaw - shift)^2, 0
+  double *part2;      // [n_cells T][S][4]: the four maxima
+  double *theta;      // [n_cells T]
+};
+
+inline size_t l4_split_bytes(int64_t T, int64_t n_cells, int S, size_t *o1, size_t *o2,
+                             size_t *o3) {
+  const int64_t ct = T * n_cells;
+  size_t o = ((2 * ct * sizeof(int32_t) + 255) / 256) * 256;
+  *o1 = o;
+  o += ct * S * 4 * sizeof(double);
+  *o2 = o;
+  o += ct * S * 4 * sizeof(double);
+  *o3 = o;
+  o += ct * sizeof(double);
+  return (o + 255) / 256 * 256;
+}
+
+inline int l4_split_factor(int64_t n_cells, int64_t n_bound) {
+  const int64_t per = n_cells > 0 ? (n_bound + n_cells - 1) / n_cells : 0;
+  const int64_t S = (per + 1023) / 1024;  // ~1024 particles per workgroup on the average cell
+  return static_cast<int>(S < 1 ? 1 : (S > 64 ? 64 : S));
+}
+
+template <typename P>
+__global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
+    const double *__restrict__ past_last, L4Split sp, double *__restrict__ out_yaw_mean,
+    double *__restrict__ out_yaw0_var, double *__restrict__ out_yaw) {
+  __shared__ double red[16];
+  __shared__ int flag;
+  const int ct = blockIdx.x / sp.S, part = blockIdx.x % sp.S;
+  const int cell = ct / T, t = ct % T;
+  const int64_t off = cell_off[cell], n = cell_cnt[cell];
+  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
+  const double px = past_last[2 * cell], py = past_last[2 * cell + 1];
+  const P *base = pos + off;
+  const int64_t chunk = (n + sp.S - 1) / sp.S;
+  const int64_t i0 = part * chunk, i1 = min(n, i0 + chunk);
+  const double shift = (t == 0 && n > 0) ? heading(base, ld, 0, 0, o0, o1, px, py) : 0.0;
+  double s = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const double y = heading(base, ld, t, i, o0, o1, px, py);
+    s += y;
+    if (t == 0) {
+      const double d = y - shift;
+      s1 += d;
+      s2 += d * d;
+    }
+    if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + off + i] = y;
+  }
+  s = block_sum(s, red);
+  if (t == 0) {
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+  }
+  double *mine = sp.part1 + (static_cast<int64_t>(ct) * sp.S + part) * 4;
+  const __amdgpu_buffer_rsrc_t rm = slab_rsrc(mine);
+  if (threadIdx.x == 0) {
+    st2_sc1(rm, 0, s, s1);
+    st2_sc1(rm, 16, s2, 0.0);
+  }
+  if (!arrive_last(sp.ctr + ct, sp.S, &flag)) return;
+  if (threadIdx.x == 0) {  // chunk order: deterministic
+    const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part1 + static_cast<int64_t>(ct) * sp.S * 4);
+    double a = 0.0, b1 = 0.0, b2 = 0.0;
+    for (int k = 0; k < sp.S; ++k) {
+      const double2 u = ld2_sc1(rp, 32 * k), v = ld2_sc1(rp, 32 * k + 16);
+      a += u.x;
+      b1 += u.y;
+      b2 += v.x;
+    }
+    const double nn = static_cast<double>(n);
+    const double theta = a / nn;
+    sp.theta[ct] = theta;
+    out_yaw_mean[ct] = theta;
+    if (t == 0) out_yaw0_var[cell] = (b2 - b1 * b1 / nn) / (nn - 1.0);
+  }
+}
+
+template <typename P>
+__global__ __launch_bounds__(kL4Threads) void l4_pass2_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
+    const double *__restrict__ past_last, const double *__restrict__ bbox, L4Split sp,
+    double *__restrict__ out_A, double *__restrict__ out_b, double *__restrict__ out_vertices) {
+  __shared__ double red[16];
+  __shared__ int flag;
+  const int ct = blockIdx.x / sp.S, part = blockIdx.x % sp.S;
+  const int cell = ct / T, t = ct % T;
+  const int64_t off = cell_off[cell], n = cell_cnt[cell];
+  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
+  const double px = past_last[2 * cell], py = past_last[2 * cell + 1];
+  const double lon = bbox[2 * cell], lat = bbox[2 * cell + 1];
+  const P *base = pos + off;
+  const int64_t chunk = (n + sp.S - 1) / sp.S;
+  const int64_t i0 = part * chunk, i1 = min(n, i0 + chunk);
+  const double theta = sp.theta[ct];  // written by pass 1 (an earlier launch)
+  const double ct_ = cos(theta), st_ = sin(theta);
+  const double A[4][2] = {{ct_, st_}, {-st_, ct_}, {-ct_, -st_}, {st_, -ct_}};
+  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const double x = world(base, ld, 2 * t, i, o0), y = world(base, ld, 2 * t + 1, i, o1);
+    const double xp = t == 0 ? px : world(base, ld, 2 * t - 2, i, o0);
+    const double yp = t == 0 ? py : world(base, ld, 2 * t - 1, i, o1);
+    const double dx = x - xp, dy = y - yp;
+    double S, C;
+    const double r = sqrt(dx * dx + dy * dy);
+    if (r > 0.0 && isfinite(r)) {  // cos / sin of the heading without the atan2 (heading_cs)
+      C = dx / r;
+      S = dy / r;
+    } else {
+      sincos(atan2(dy, dx), &S, &C);
+    }
+    // rows of Rot per corner (midlevel/util.py:109-118), disp = 0.5 * Rot @ [lon, lat]
+    const double ddx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
+                           0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
+    const double ddy[4] = {0.5 * (S * lon - C * lat), 0.5 * (S * lon + C * lat),
+                           0.5 * (-S * lon + C * lat), 0.5 * (-S * lon - C * lat)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double vx = x + ddx[c], vy = y + ddy[c];
+      if (out_vertices) {
+        double *vp = out_vertices + (static_cast<int64_t>(t) * 8 + 2 * c) * ld + off + i;
+        vp[0] = vx;
+        vp[ld] = vy;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mx[q] = fmax(mx[q], A[q][0] * vx + A[q][1] * vy);
+    }
+  }
+  double bm[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bm[q] = block_max(mx[q], red);
+  double *mine = sp.part2 + (static_cast<int64_t>(ct) * sp.S + part) * 4;
+  const __amdgpu_buffer_rsrc_t rm = slab_rsrc(mine);
+  if (threadIdx.x == 0) {
+    st2_sc1(rm, 0, bm[0], bm[1]);
+    st2_sc1(rm, 16, bm[2], bm[3]);
+  }
+  const int nct = gridDim.x / sp.S;
+  if (!arrive_last(sp.ctr + nct + ct, sp.S, &flag)) return;
+  if (threadIdx.x == 0) {
+    const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part2 + static_cast<int64_t>(ct) * sp.S * 4);
+    double b[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < sp.S; ++k) {
+      const double2 u = ld2_sc1(rp, 32 * k), v = ld2_sc1(rp, 32 * k + 16);
+      b[0] = fmax(b[0], u.x);
+      b[1] = fmax(b[1], u.y);
+      b[2] = fmax(b[2], v.x);
+      b[3] = fmax(b[3], v.y);
+    }
+    for (int q = 0; q < 4; ++q) {
+      out_A[static_cast<int64_t>(ct) * 8 + 2 * q] = A[q][0];
+      out_A[static_cast<int64_t>(ct) * 8 + 2 * q + 1] = A[q][1];
+      out_b[static_cast<int64_t>(ct) * 4 + q] = b[q];
+    }
+  }
+}
+
 }  // namespace ccmpc
 
 using namespace ccmpc;
@@ -267,6 +442,57 @@ extern "C" int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T,
                        static_cast<const float *>(positions), ld, static_cast<int>(T), origin,
                        cell_off, cell_cnt, past_last, bbox, out_A, out_b, out_yaw_mean,
                        out_yaw0_var, out_yaw, out_vertices);
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}
+
+extern "C" size_t ccmpc_l4_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_particles_bound) {
+  if (T < 1 || T > 40 || n_cells < 0 || n_particles_bound < 0) return 0;
+  size_t o1, o2, o3;
+  return l4_split_bytes(T, n_cells, l4_split_factor(n_cells, n_particles_bound), &o1, &o2, &o3);
+}
+
+extern "C" int ccmpc_l4_split(const void *positions, int dtype, int64_t ld, int64_t T,
+                              const double *origin, const int64_t *cell_off,
+                              const int64_t *cell_cnt, int64_t n_cells,
+                              int64_t n_particles_bound, const double *past_last,
+                              const double *bbox, void *workspace, size_t workspace_bytes,
+                              double *out_A, double *out_b, double *out_yaw_mean,
+                              double *out_yaw0_var, double *out_yaw, double *out_vertices,
+                              ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
+  CCMPC_REQUIRE(n_cells >= 0 && n_cells * T * 64 < (int64_t(1) << 31), "bad n_cells");
+  if (n_cells == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(positions && cell_off && cell_cnt && past_last && bbox && out_A && out_b &&
+                    out_yaw_mean && out_yaw0_var,
+                "null pointer");
+  CCMPC_REQUIRE(dtype == CCMPC_F64 || dtype == CCMPC_F32, "bad dtype");
+  CCMPC_REQUIRE(workspace && aligned(workspace, 256), "workspace must be 256-byte aligned");
+  const int S = l4_split_factor(n_cells, n_particles_bound);
+  size_t o1, o2, o3;
+  if (workspace_bytes < l4_split_bytes(T, n_cells, S, &o1, &o2, &o3)) {
+    set_error("ccmpc_l4_split: workspace too small");
+    return CCMPC_ERR_WORKSPACE;
+  }
+  char *w = static_cast<char *>(workspace);
+  const L4Split sp{S, reinterpret_cast<int32_t *>(w), reinterpret_cast<double *>(w + o1),
+                   reinterpret_cast<double *>(w + o2), reinterpret_cast<double *>(w + o3)};
+  const dim3 grid(static_cast<unsigned>(n_cells * T * S));
+  hipStream_t s = as_stream(stream);
+  const int Ti = static_cast<int>(T);
+  if (dtype == CCMPC_F64) {
+    const double *p = static_cast<const double *>(positions);
+    hipLaunchKernelGGL((l4_pass1_kernel<double>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
+                       cell_off, cell_cnt, past_last, sp, out_yaw_mean, out_yaw0_var, out_yaw);
+    hipLaunchKernelGGL((l4_pass2_kernel<double>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
+                       cell_off, cell_cnt, past_last, bbox, sp, out_A, out_b, out_vertices);
+  } else {
+    const float *p = static_cast<const float *>(positions);
+    hipLaunchKernelGGL((l4_pass1_kernel<float>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
+                       cell_off, cell_cnt, past_last, sp, out_yaw_mean, out_yaw0_var, out_yaw);
+    hipLaunchKernelGGL((l4_pass2_kernel<float>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
+                       cell_off, cell_cnt, past_last, bbox, sp, out_A, out_b, out_vertices);
+  }
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

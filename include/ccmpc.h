@@ -328,6 +328,20 @@ int ccmpc_l4(const void *positions, int dtype, int64_t ld, int64_t T, const doub
              double *out_yaw_mean, double *out_yaw0_var, double *out_yaw, double *out_vertices,
              ccmpc_stream_t stream);
 
+/* The same outputs with every (cell, t) split over ~n_particles_bound / (n_cells 1024) workgroups
+ * in two launches (pass 1: headings and their sums; pass 2: corners and maxima; each
+ * (cell, t)'s last arriving workgroup combines the chunks, sums in chunk order, so the result is
+ * deterministic).  One workgroup per (cell, t) is issue-bound on its f64 atan2 / division work
+ * for large clouds; this form spreads it over the chip.  Workspace: ccmpc_l4_workspace_bytes,
+ * 256-byte aligned, its head (arrival counters) zero-filled once; every call leaves it zero. */
+size_t ccmpc_l4_workspace_bytes(int64_t T, int64_t n_cells, int64_t n_particles_bound);
+int ccmpc_l4_split(const void *positions, int dtype, int64_t ld, int64_t T, const double *origin,
+                   const int64_t *cell_off, const int64_t *cell_cnt, int64_t n_cells,
+                   int64_t n_particles_bound, const double *past_last, const double *bbox,
+                   void *workspace, size_t workspace_bytes, double *out_A, double *out_b,
+                   double *out_yaw_mean, double *out_yaw0_var, double *out_yaw,
+                   double *out_vertices, ccmpc_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * The caller of the path: the planning step's quadratic program,
  * batched over scenes.  Replaces the cvxpy + CPLEX problem of do_highlevel_control

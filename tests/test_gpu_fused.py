@@ -302,3 +302,34 @@ def test_sampler_rejects_bad_injections(gpu):
     rc = lib.ccmpc_sample_unicycle_ex(None, None, L, None, 1, None, None, 1, N, T, 0.5, 0, None,
                                       0, None, None, N, None)
     assert rc == -1                     # CCMPC_ERR_INVALID: per-particle parameters need z_in
+
+
+@pytest.mark.parametrize("dtype,T,N", [(torch.float64, 8, 3000), (torch.float32, 12, 40000)])
+def test_l4_split_equals_one_workgroup_form(gpu, dtype, T, N):
+    """ccmpc_l4_split (each (cell, t) over several workgroups, chunk-ordered sums) against
+    ccmpc_l4 (one workgroup per (cell, t)): same headings, same corners; the mean heading's sum
+    order differs, so A / b / yaw statistics agree to rounding; repeated calls are bitwise
+    stable (deterministic chunk order, counters back to zero)."""
+    from ccmpc import engine, synthetic
+    ovs, _, pasts = synthetic.scene(91, O=3, N=N, T=T)
+    cells = [c for o in ovs for c in o]
+    origin = np.array([c[:, 0].mean(0) for c in cells]) if dtype == torch.float32 else None
+    store = engine.ParticleStore.from_cells(cells, device=gpu, dtype=dtype, origin=origin)
+    past = np.repeat(pasts, [len(o) for o in ovs], axis=0)
+    bbox = np.tile([4.5, 2.5], (store.n_cells, 1))
+    one = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, split=False)
+    ws = engine.Workspace(gpu)
+    a = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, workspace=ws)
+    b = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, workspace=ws)
+    cols = torch.as_tensor(np.concatenate([np.arange(o, o + n) for o, n in
+                                           zip(store.offsets, store.counts)]), device=gpu)
+    for x in (one, a, b):       # the per-particle outputs, at the particles' slots only
+        x["yaw"], x["vertices"] = x["yaw"][:, cols], x["vertices"][:, cols]
+    for k in ("A", "b", "yaw_mean", "yaw0_var", "yaw", "vertices"):
+        assert torch.equal(a[k], b[k]), k
+    torch.testing.assert_close(a["yaw"], one["yaw"], rtol=0, atol=0)
+    torch.testing.assert_close(a["yaw_mean"], one["yaw_mean"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(a["yaw0_var"], one["yaw0_var"], rtol=1e-10, atol=1e-14)
+    torch.testing.assert_close(a["A"], one["A"], rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(a["b"], one["b"], rtol=1e-12, atol=1e-10)
+    torch.testing.assert_close(a["vertices"], one["vertices"], rtol=1e-13, atol=1e-12)

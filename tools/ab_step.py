@@ -38,7 +38,37 @@ def child():
             p(i.d("past")), p(i.d("bbox")), p(o.d("A")), p(o.d("b")), p(o.d("yaw_mean")),
             p(o.d("yaw0_var")), None, None, engine._stream()), "ccmpc_l4")
     t_l4 = bench.time_kernel_live(l4, dev, per_graph=20, replays=5)
-    print(f"  graph replay {t_graph * 1e6:7.2f} us   l4 {t_l4 * 1e6:7.2f} us", flush=True)
+    lws = g.l4_ws.buf
+
+    def l4s():
+        engine._lib.check(lib.ccmpc_l4_split(
+            p(st.pos), engine.F32, st.ld, ph, p(st.origin), p(o.d("off")), p(o.d("cnt")), g.C,
+            st.n_bound, p(i.d("past")), p(i.d("bbox")), p(lws), lws.numel(), p(o.d("A")),
+            p(o.d("b")), p(o.d("yaw_mean")), p(o.d("yaw0_var")), None, None, engine._stream()),
+            "ccmpc_l4_split")
+    t_l4s = bench.time_kernel_live(l4s, dev, per_graph=20, replays=5)
+    print(f"  graph replay {t_graph * 1e6:7.2f} us   l4 {t_l4 * 1e6:7.2f} us   "
+          f"l4_split {t_l4s * 1e6:7.2f} us", flush=True)
+    # a C1-sized cloud (one OV, 2 modes, 1e5 particles, ph = 8): both forms
+    from ccmpc import synthetic
+    ovs, _, pasts = synthetic.scene(5, O=1, N=100_000, T=ph, K=2)
+    big = engine.ParticleStore.from_cells(ovs[0], device=dev)
+    past = np.repeat(pasts, 2, axis=0)
+    bb = np.tile([4.5, 2.5], (2, 1))
+    ws = engine.Workspace(dev)
+    for split in (False, True):
+        fn = lambda: engine.l4(big, past, bb, split=split, workspace=ws)
+        fn()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(20):
+            fn()
+        ev1.record()
+        ev1.synchronize()
+        print(f"  1e5-particle cells x 2, T = {ph}: {'split' if split else 'one workgroup'} "
+              f"{ev0.elapsed_time(ev1) / 20 * 1e3:8.2f} us (with the wrapper's H2D copies)",
+              flush=True)
 
 
 def main():
