@@ -63,6 +63,9 @@ namespace ccmpc {
 #define CCMPC_DEPTH4 CCMPC_DEPTH
 #endif
 constexpr int kDepth = CCMPC_DEPTH;
+#ifndef CCMPC_PRIO
+#define CCMPC_PRIO 0
+#endif
 constexpr int kDepth4 = CCMPC_DEPTH4;
 
 // Loads are pure loads, branch-free: every lane always issues its 16-byte loads, the address
@@ -219,13 +222,15 @@ void moments_kernel(
   constexpr int D = 16 * RB;
   constexpr int S = G::S;
   constexpr int E = slab_doubles(RB);
-  constexpr bool COV_IN_LDS = MINK && RB <= 2;
+  // the fused tail reads the covariance from LDS; it lives in the cross-wave exchange buffer,
+  // which is free once the item is combined (so T = 40 keeps its 80 x 80 covariance on chip too)
+  constexpr bool COV_IN_LDS = MINK;
+  static_assert(combine_xch_doubles(RB, G::NW) >= D * D, "xch must hold the covariance");
   __shared__ double xch[combine_xch_doubles(RB, G::NW)];
   __shared__ double slab_lds[E];
   __shared__ double shift_lds[D];
   __shared__ double S_lds[D];
   __shared__ double mean_lds[D];
-  __shared__ double cov_lds[COV_IN_LDS ? D * D : 1];
   __shared__ double lb_s[MINK ? 40 * 39 / 2 : 1];
   __shared__ double ref_lds[MINK ? D + 3 : 1];  // reference trajectory [T][2], then risk[3]
   __shared__ int flag;
@@ -270,6 +275,9 @@ void moments_kernel(
     // sched_barrier(0) fences keep the four phases in program order, so each MFMA group waits
     // (vmcnt) only for its own buffer while the other buffer's loads stay in flight.
     const int64_t ngroups = wr.ngroups, st = wr.stride;
+#if CCMPC_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md)
+    if (G::NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(CCMPC_PRIO);
+#endif
     constexpr int DP = kDepth;
     Quad<P> buf[DP][S][RB];
     if (ngroups > 0) {
@@ -294,13 +302,16 @@ void moments_kernel(
           mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
     }
     PROBE_TS(2);
+#if CCMPC_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
 
     if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
 #pragma unroll
     for (int bb = 0; bb < RB; ++bb) {
       if (w == 0 && g == 0) shift_lds[16 * bb + r] = sh[bb];
     }
-    const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
+    const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, xch, lb_s, ref_lds, &flag};
     cell_epilogue<Scheme16<RB>, MINK, COV_IN_LDS>(
         [&](double *dst, bool to_lds) {
           combine_waves<RB, NACC, G::NW>(acc, s1, xch, dst, to_lds);
@@ -409,7 +420,6 @@ __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
   __shared__ double shift_lds[D];
   __shared__ double S_lds[D];
   __shared__ double mean_lds[D];
-  __shared__ double cov_lds[MINK ? D * D : 1];
   __shared__ double lb_s[MINK ? 12 * 11 / 2 : 1];
   __shared__ double ref_lds[MINK ? D + 3 : 1];  // reference trajectory [T][2], then risk[3]
   __shared__ int flag;
@@ -469,7 +479,9 @@ __global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
 #pragma unroll
     for (int I = 0; I < NB; ++I)
       if (w == 0 && m == 0) shift_lds[4 * I + c] = sh[I];
-    const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, cov_lds, lb_s, ref_lds, &flag};
+    // the covariance for the tail reuses the exchange buffer (free after combine4)
+    static_assert(kNW4 * Combine4Layout<NB>::XS >= D * D, "xch must hold the covariance");
+    const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, xch, lb_s, ref_lds, &flag};
     cell_epilogue<Sch, MINK, MINK>(
         [&](double *dst, bool to_lds) { combine4<NB, kNW4>(acc, s1, xch, dst, to_lds); }, loc,
         nit, T, tree, origin, out_mean, out_cov, mp, L);
