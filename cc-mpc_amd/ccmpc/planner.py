@@ -155,6 +155,28 @@ class HalfSpaceList:
         return (self[i] for i in range(len(self)))
 
 
+class CellGrid:
+    """A per-cell value as the reference's [ov][k] nested list (None where OV `ov` has no mode
+    k), over a host array in (ov, k) cell order; rows are built on access."""
+
+    def __init__(self, values, K, first=None):
+        self._v, self._K = values, K
+        self._first = first if first is not None else [sum(K[:o]) for o in range(len(K))]
+        self._maxK = max(K)
+
+    def __len__(self):
+        return len(self._K)
+
+    def __getitem__(self, o):
+        if not 0 <= o < len(self._K):
+            raise IndexError(o)
+        f, k = self._first[o], self._K[o]
+        return [float(x) for x in self._v[f:f + k]] + [None] * (self._maxK - k)
+
+    def __iter__(self):
+        return (self[o] for o in range(len(self._K)))
+
+
 class UnionGrid:
     """A_union / b_union [t][k][ov] (v8ideal/__init__.py:627-736) over a host array [cell, t,
     ...]: None where OV `ov` has no mode k, as the reference's nested lists hold."""
@@ -365,19 +387,16 @@ class MidlevelAgent:
         """ovStateMean/Cov_tau_1 (:864-875): t = 0 mean / variance of x, y, yaw per (ov, k).
         yaw = (yaw_mean at t = 0 [C], yaw0_var [C]) when already on the host."""
         K = scene.K
-        maxK = max(K)
         if yaw is None:
             l4 = scene.l4()
             ym, yv = l4["yaw_mean"][:, 0].cpu().numpy(), l4["yaw0_var"].cpu().numpy()
         else:
             ym, yv = yaw
-        first = np.concatenate([[0], np.cumsum(K)[:-1]]).astype(int)
-
-        def grid(col):          # [o][k] lists, None where OV o has no mode k
-            vals = col.tolist()
-            return [vals[f:f + k] + [None] * (maxK - k) for f, k in zip(first, K)]
-        return ((grid(mean0[:, 0]), grid(mean0[:, 1]), grid(np.asarray(ym))),
-                (grid(cov0[:, 0, 0]), grid(cov0[:, 1, 1]), grid(np.asarray(yv))))
+        K = list(K)
+        first = [sum(K[:o]) for o in range(len(K))]
+        return tuple(tuple(CellGrid(v, K, first) for v in vals) for vals in (
+            (mean0[:, 0], mean0[:, 1], np.asarray(ym)),
+            (cov0[:, 0, 0], cov0[:, 1, 1], np.asarray(yv))))
 
     def _l4_lists(self, scene):
         ph = self.prediction_horizon
@@ -393,15 +412,9 @@ class MidlevelAgent:
 
     def _ov_in_junction(self, scene, mean0):
         """OVconstraint (:831-851): the Town03 scene-4 T-intersection test, last mode wins."""
-        flag = False
-        c = 0
-        for o in range(scene.O):
-            inj = None
-            for k in range(scene.K[o]):
-                inj = not (mean0[c, 0] >= 190 or mean0[c, 1] <= -80)
-                c += 1
-            flag = flag or bool(inj)
-        return flag
+        inj = ~((mean0[:, 0] >= 190) | (mean0[:, 1] <= -80))      # per cell
+        last = np.cumsum(scene.K) - 1                               # each OV's last mode
+        return bool(np.any(inj[last]))
 
     def _src_cells(self, prev_K, K):
         """data_idx fallback (:2648-2656): mode k reads saved mode k, or the last saved slot."""
@@ -614,7 +627,7 @@ class MidlevelAgent:
             out = self.compute_obstacle_constraints_GMM_Minkowski_idealprediction(
                 params, ovs, None, None, None, eps_ura, None, T, ref_traj)
             return ovs, out
-        K = [int(np.count_nonzero(pmf[o] > filter_pmf)) for o in range(O)]
+        K = (pmf > filter_pmf).sum(1).tolist()
         if min(K) == 0:
             raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent "
                              f"mode with p(z|x) > {filter_pmf} (ovehicle.py:96-97)")

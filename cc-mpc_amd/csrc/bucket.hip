@@ -79,25 +79,24 @@ __device__ __forceinline__ void final_world(const BucketArgs &a, int o, int64_t 
   y = static_cast<double>(p[(2 * (a.T - 1) + 1) * a.ld_in]) + a.minpos[2 * o + 1];
 }
 
-// bucket key of particle i of OV o (needs centres for rare latents)
-__device__ __forceinline__ int key_of(const BucketArgs &a, int o, int64_t i) {
-  const int zv = a.z[o * a.N + i];
-  const int k = a.keep_map[o * a.L + zv];
-  if (k >= 0) return k * (a.L + 1);
-  double x, y;
-  final_world(a, o, i, x, y);
-  const int K = a.n_kept[o];
+// Bucket key of a particle from values staged in LDS / registers (keep_map and the centres read once per
+// block, z and the final position loaded up front with everything else the block needs: the
+// global reads of key_of are a chain of dependent round trips in a kernel this small).
+__device__ __forceinline__ int key_staged(int zv, double x, double y, const int *keep_s,
+                                          const double (*cen_s)[2], int K, int L) {
+  const int k = keep_s[zv];
+  if (k >= 0) return k * (L + 1);
   int best = 0;
   double bd = INFINITY;
   for (int j = 0; j < K; ++j) {
-    const double dx = x - a.centre[(o * a.max_k + j) * 2], dy = y - a.centre[(o * a.max_k + j) * 2 + 1];
+    const double dx = x - cen_s[j][0], dy = y - cen_s[j][1];
     const double d = sqrt(dx * dx + dy * dy);
     if (d < bd) {
       bd = d;
       best = j;
     }
   }
-  return best * (a.L + 1) + 1 + zv;
+  return best * (L + 1) + 1 + zv;
 }
 
 __device__ __forceinline__ void st1_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, int32_t v) {
@@ -112,29 +111,35 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
   __shared__ double red[4];
   __shared__ double pub[64 + 2 + 2 * kMaxKept];
   __shared__ int flag;
+  __shared__ int keep_s[64];
   const int o = blockIdx.y, blk = blockIdx.x;
   const int K = a.n_kept[o];
-  for (int l = threadIdx.x; l < a.L; l += blockDim.x) cnt[l] = 0;
-  __syncthreads();
   const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
   int zs[kPerThread];
   double xs[kPerThread], ys[kPerThread];
 #pragma unroll
-  for (int r = 0; r < kPerThread; ++r) {
+  for (int r = 0; r < kPerThread; ++r) {  // every load of the block issued together
     const int64_t i = i0 + r * kBucketBlock + threadIdx.x;
     zs[r] = -1;
     xs[r] = ys[r] = 0.0;
     if (i < a.N) {
       zs[r] = a.z[o * a.N + i];
-      atomicAdd(&cnt[zs[r]], 1);
       final_world(a, o, i, xs[r], ys[r]);
     }
   }
+  for (int l = threadIdx.x; l < a.L; l += blockDim.x) {
+    cnt[l] = 0;
+    keep_s[l] = a.keep_map[o * a.L + l];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kPerThread; ++r)
+    if (zs[r] >= 0) atomicAdd(&cnt[zs[r]], 1);
   for (int k = 0; k < K; ++k) {
     double sx = 0.0, sy = 0.0;
 #pragma unroll
     for (int r = 0; r < kPerThread; ++r) {
-      const bool mine = zs[r] >= 0 && a.keep_map[o * a.L + zs[r]] == k;
+      const bool mine = zs[r] >= 0 && keep_s[zs[r]] == k;
       sx += mine ? xs[r] : 0.0;
       sy += mine ? ys[r] : 0.0;
     }
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
   // mode's loads are issued before any is summed
   __shared__ int zv_s[kMaxKept];
   for (int l = threadIdx.x; l < a.L; l += blockDim.x) {
-    const int k = a.keep_map[o * a.L + l];
+    const int k = keep_s[l];
     if (k >= 0) zv_s[k] = l;
   }
   __syncthreads();
@@ -208,18 +213,33 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
   __shared__ int h[kMaxBins];
   __shared__ int64_t start[kMaxBins];
   __shared__ int flag;
+  __shared__ int keep_s[64];
+  __shared__ double cen_s[kMaxKept][2];
   const int o = blockIdx.y, blk = blockIdx.x;
   const int K = a.n_kept[o];
   const int G = a.L + 1;
   const int nbins = K * G;
+  const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
+  int zs[kPerThread];
+  double xs[kPerThread], ys[kPerThread];
+#pragma unroll
+  for (int r = 0; r < kPerThread; ++r) {  // every load of the block issued together
+    const int64_t i = i0 + r * kBucketBlock + threadIdx.x;
+    zs[r] = -1;
+    xs[r] = ys[r] = 0.0;
+    if (i < a.N) {
+      zs[r] = a.z[o * a.N + i];
+      final_world(a, o, i, xs[r], ys[r]);
+    }
+  }
+  for (int l = threadIdx.x; l < a.L; l += blockDim.x) keep_s[l] = a.keep_map[o * a.L + l];
+  for (int j = threadIdx.x; j < 2 * K; j += blockDim.x)
+    cen_s[j >> 1][j & 1] = a.centre[(o * a.max_k + (j >> 1)) * 2 + (j & 1)];
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) h[b] = 0;
   __syncthreads();
-  const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
 #pragma unroll
-  for (int r = 0; r < kPerThread; ++r) {
-    const int64_t i = i0 + r * kBucketBlock + threadIdx.x;
-    if (i < a.N) atomicAdd(&h[key_of(a, o, i)], 1);
-  }
+  for (int r = 0; r < kPerThread; ++r)
+    if (zs[r] >= 0) atomicAdd(&h[key_staged(zs[r], xs[r], ys[r], keep_s, cen_s, K, a.L)], 1);
   __syncthreads();
   const int64_t stride = static_cast<int64_t>(a.max_k) * G;
   int32_t *hist0 = a.hist + static_cast<int64_t>(o) * a.nb * stride;
@@ -284,20 +304,45 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
 __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
   __shared__ int run[kMaxBins];        // particles of each bin in earlier rounds of this block
   __shared__ int wcnt[4][kMaxBins];    // per wave counts of the current round
+  __shared__ int keep_s[64];
+  __shared__ double cen_s[kMaxKept][2];
+  __shared__ int64_t boff_s[kMaxBins];
   const int o = blockIdx.y, blk = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int nbins = a.n_kept[o] * (a.L + 1);
+  const int K = a.n_kept[o];
+  const int nbins = K * (a.L + 1);
   const int64_t stride = static_cast<int64_t>(a.max_k) * (a.L + 1);
   const int64_t *boff = a.bin_off + (static_cast<int64_t>(o) * a.nb + blk) * stride;
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) run[b] = 0;
   const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
+  // kPerThread == 1: this thread's particle, its key inputs and its 2T coordinates, every load
+  // issued together with the block's tables
+  static_assert(kPerThread == 1, "one particle per thread");
+  const int64_t i = i0 + threadIdx.x;  // sample order = (wave, lane)
+  const bool valid = i < a.N;
+  int zv = 0;
+  double xf = 0.0, yf = 0.0;
+  if (valid) {
+    zv = a.z[o * a.N + i];
+    final_world(a, o, i, xf, yf);
+  }
+  const int rows = 2 * a.T;
+  const float *src = a.pos + o * a.S_in + (valid ? i : 0);
+  float v[80];
+#pragma unroll
+  for (int rr = 0; rr < 80; ++rr)
+    if (rr < rows) v[rr] = src[static_cast<int64_t>(rr) * a.ld_in];
+  for (int l = threadIdx.x; l < a.L; l += blockDim.x) keep_s[l] = a.keep_map[o * a.L + l];
+  for (int j = threadIdx.x; j < 2 * K; j += blockDim.x)
+    cen_s[j >> 1][j & 1] = a.centre[(o * a.max_k + (j >> 1)) * 2 + (j & 1)];
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+    run[b] = 0;
+    boff_s[b] = boff[b];
+  }
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int r = 0; r < kPerThread; ++r) {
     for (int b = threadIdx.x; b < 4 * nbins; b += blockDim.x) wcnt[b / nbins][b % nbins] = 0;
     __syncthreads();
-    const int64_t i = i0 + r * kBucketBlock + threadIdx.x;  // sample order = (round, wave, lane)
-    const bool valid = i < a.N;
-    const int key = valid ? key_of(a, o, i) : -1;
+    const int key = valid ? key_staged(zv, xf, yf, keep_s, cen_s, K, a.L) : -1;
     // rank among equal keys of this wave (lanes in order)
     int rank = 0;
     unsigned long long todo = __ballot(valid);
@@ -312,10 +357,11 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
     __syncthreads();
     if (valid) {
       int before = run[key];
-      for (int v = 0; v < w; ++v) before += wcnt[v][key];
-      const int64_t dst = boff[key] + before + rank;
-      const float *src = a.pos + o * a.S_in + i;
-      for (int row = 0; row < 2 * a.T; ++row) a.out[row * a.ld_out + dst] = src[row * a.ld_in];
+      for (int u = 0; u < w; ++u) before += wcnt[u][key];
+      const int64_t dst = boff_s[key] + before + rank;
+#pragma unroll
+      for (int rr = 0; rr < 80; ++rr)
+        if (rr < rows) a.out[static_cast<int64_t>(rr) * a.ld_out + dst] = v[rr];
     }
     __syncthreads();
     for (int b = threadIdx.x; b < nbins; b += blockDim.x)
