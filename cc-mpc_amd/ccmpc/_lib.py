@@ -76,6 +76,10 @@ SIGNATURES = {
     "ccmpc_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "ccmpc_bucket": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _I64, _P,
                                     _P, _P, _SZ, _P, _I64, _P, _P, _P, _P, _P]),
+    "ccmpc_sample_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
+    "ccmpc_sample_bucket": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P, _P, _I64, _I64, _I64, _D,
+                                           _U64, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P,
+                                           _P, _I64, _P, _P, _P, _P, _P]),
     "ccmpc_affine_scale": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _D, _I32, _P, _P, _P,
                                           _P]),
     "ccmpc_ideal_rollout": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _P, _U64,

@@ -265,6 +265,21 @@ def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="c
     Returns (z [O,N] int32, F32 ParticleStore in sample order: one cell per OV)."""
     lib = _lib.load()
     dev = require_device(device)
+    O, L, t_init, t_cdf, t_gmm, layout, t_z, t_eps = _sampler_inputs(
+        init_state, latent_pmf, gmm, N, T, dev, z, eps, per_particle)
+    store = ParticleStore(T, [N] * O, dtype=torch.float32, device=dev, origin=np.zeros((O, 2)))
+    out_z = torch.empty((O, N), dtype=torch.int32, device=dev)
+    _lib.check(lib.ccmpc_sample_unicycle_ex(
+        _p(t_init), _p(t_cdf), L, _p(t_gmm), layout, _p(t_z), _p(t_eps), O, N, T, float(dt),
+        int(seed) & (2**64 - 1), None, int(ov_base), _p(out_z), _p(store.pos), store.ld,
+        _stream()),
+        "ccmpc_sample_unicycle_ex")
+    store._keepalive = (t_init, t_cdf, t_gmm, t_z, t_eps)
+    return out_z, store
+
+
+def _sampler_inputs(init_state, latent_pmf, gmm, N, T, dev, z, eps, per_particle):
+    """Device copies of a sampler call's inputs (ccmpc_sample_unicycle_ex's layouts)."""
     init_state = np.asarray(init_state, np.float64).reshape(-1, 4)
     O = init_state.shape[0]
     t_z = t_eps = t_cdf = None
@@ -297,16 +312,84 @@ def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="c
     if eps is not None:
         e = torch.as_tensor(eps, device=dev).to(torch.float32).reshape(O, N, T, 2)
         t_eps = e.permute(0, 2, 3, 1).contiguous()           # (O, T, 2, N)
-    store = ParticleStore(T, [N] * O, dtype=torch.float32, device=dev, origin=np.zeros((O, 2)))
-    out_z = torch.empty((O, N), dtype=torch.int32, device=dev)
     t_init = torch.as_tensor(init_state, device=dev)
-    _lib.check(lib.ccmpc_sample_unicycle_ex(
+    return O, L, t_init, t_cdf, t_gmm, layout, t_z, t_eps
+
+
+def _bucket_plan(pmf, filter_pmf, max_k):
+    """Kept modes of every OV (p(z|x) > filter, host data as in prediction.py:77-79): K per
+    OV, max_k, keep_map [O, L] (kept index or -1), cell_base [O]."""
+    O, L = pmf.shape
+    keep = [np.argwhere(pmf[o] > filter_pmf).ravel() for o in range(O)]
+    K = [int(k.size) for k in keep]
+    if min(K) == 0:
+        raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent mode "
+                         f"with p(z|x) > {filter_pmf} (ovehicle.py:96-97 fails the same way)")
+    max_k = max(K) if max_k is None else max_k
+    keep_map = -np.ones((O, L), np.int32)
+    for o in range(O):
+        keep_map[o, keep[o]] = np.arange(K[o], dtype=np.int32)
+    cell_base = np.concatenate([[0], np.cumsum(K)[:-1]]).astype(np.int32)
+    return K, max_k, keep_map, cell_base
+
+
+FUSED_MAX_N = 8192
+
+
+def sample_bucket(init_state, latent_pmf, gmm, N, T, minpos, dt=0.5, seed=0, device="cuda",
+                  ov_base=0, z=None, eps=None, per_particle=False, filter_pmf=0.1, max_k=None,
+                  with_z=False, workspace=None):
+    """Sampler + bucketing in one launch (ccmpc_sample_bucket, N <= 8192): the draws of
+    sample_unicycle with the same arguments, bucketed as bucket() buckets them (each cell the
+    same particles in the same order, the same pmf / init_center bits; only the cell offsets
+    differ).  latent_pmf (O, L) is required (it decides the kept modes).
+
+    Returns (bucketed F32 ParticleStore, K per OV, cell_pmf [n_cells] device, init_center
+    [n_cells, 2] device), and the sample-order z [O, N] first when with_z.  workspace: an
+    optional uint8 device tensor, zero-filled once by the caller and reused across calls."""
+    lib = _lib.load()
+    dev = require_device(device)
+    if latent_pmf is None:
+        raise ValueError("latent_pmf decides the kept modes: it is required")
+    if not 1 <= int(N) <= FUSED_MAX_N:
+        raise ValueError(f"sample_bucket takes N in [1, {FUSED_MAX_N}]: use sample_unicycle + "
+                         "bucket beyond")
+    O, L, t_init, t_cdf, t_gmm, layout, t_z, t_eps = _sampler_inputs(
+        init_state, latent_pmf, gmm, N, T, dev, z, eps, per_particle)
+    pmf = np.asarray(latent_pmf, np.float64).reshape(O, L)
+    K, max_k, keep_map, cell_base = _bucket_plan(pmf, filter_pmf, max_k)
+    region, cur, n_bound = [], 0, 0
+    for o in range(O):
+        region.append(cur)
+        cur = _round4(cur + K[o] * (N + 4))          # room for every cell's worst case
+        n_bound = _round4(n_bound + N + 4 * K[o])    # the particles themselves (+ alignment)
+    n_cells = int(sum(K))
+    origin = np.repeat(np.asarray(minpos, np.float64).reshape(-1, 2), K, axis=0)
+    out = ParticleStore(T, [0] * n_cells, dtype=torch.float32, device=dev, origin=origin,
+                        capacity=cur)
+    out.counts = None                                   # device-side until sync_counts()
+    out.n_bound = n_bound
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)
+    t_keep, t_nk, t_base = t(keep_map), t(np.asarray(K, np.int32)), t(cell_base)
+    t_min = t(np.asarray(minpos, np.float64).reshape(-1, 2))
+    t_reg = t(np.asarray(region, np.int64))
+    pmf_out = torch.empty(n_cells, dtype=torch.float64, device=dev)
+    centre = torch.empty((n_cells, 2), dtype=torch.float64, device=dev)
+    out_z = torch.empty((O, N), dtype=torch.int32, device=dev) if with_z else None
+    need = lib.ccmpc_sample_bucket_workspace_bytes(O, N, T, max_k)
+    if need == 0:
+        raise ValueError("shape not supported by ccmpc_sample_bucket")
+    ws = workspace if workspace is not None else torch.zeros(need, dtype=torch.uint8, device=dev)
+    _lib.check(lib.ccmpc_sample_bucket(
         _p(t_init), _p(t_cdf), L, _p(t_gmm), layout, _p(t_z), _p(t_eps), O, N, T, float(dt),
-        int(seed) & (2**64 - 1), None, int(ov_base), _p(out_z), _p(store.pos), store.ld,
-        _stream()),
-        "ccmpc_sample_unicycle_ex")
-    store._keepalive = (t_init, t_cdf, t_gmm, t_z, t_eps)
-    return out_z, store
+        int(seed) & (2**64 - 1), None, int(ov_base), _p(t_keep), _p(t_nk), _p(t_base), max_k,
+        _p(t_min), _p(t_reg), _p(ws), ws.numel(), _p(out_z), _p(out.pos), out.ld,
+        _p(out.cell_off), _p(out.cell_cnt), _p(pmf_out), _p(centre), _stream()),
+        "ccmpc_sample_bucket")
+    out._keepalive = (t_init, t_cdf, t_gmm, t_z, t_eps, t_keep, t_nk, t_base, t_min, t_reg, ws)
+    if with_z:
+        return out_z, out, K, pmf_out, centre
+    return out, K, pmf_out, centre
 
 
 def affine(mean, cov, ref_traj, cell_gamma, cell_ref=None, R=3.4, out_rec=None):
@@ -413,16 +496,7 @@ def bucket(z, sample_store, latent_pmf, minpos, filter_pmf=0.1, max_k=None):
     O, L = pmf.shape
     N = int(z.shape[1])
     T = sample_store.T
-    keep = [np.argwhere(pmf[o] > filter_pmf).ravel() for o in range(O)]
-    K = [int(k.size) for k in keep]
-    if min(K) == 0:
-        raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent mode "
-                         f"with p(z|x) > {filter_pmf} (ovehicle.py:96-97 fails the same way)")
-    max_k = max(K) if max_k is None else max_k
-    keep_map = -np.ones((O, L), np.int32)
-    for o in range(O):
-        keep_map[o, keep[o]] = np.arange(K[o], dtype=np.int32)
-    cell_base = np.concatenate([[0], np.cumsum(K)[:-1]]).astype(np.int32)
+    K, max_k, keep_map, cell_base = _bucket_plan(pmf, filter_pmf, max_k)
     region, cur = [], 0
     for o in range(O):
         region.append(cur)

@@ -104,24 +104,34 @@ class MinkowskiStepGraph:
                          ("b", (C, T, 4), f64), ("yaw_mean", (C, T), f64),
                          ("yaw0_var", (C,), f64), ("cnt", (C,), i64), ("off", (C,), i64),
                          ("pmf", (C,), f64), ("centre", (C, 2), f64)], self.device)
-        # device-only intermediates: the sample-order store and the bucketed store
-        self.z = torch.empty((O, N), dtype=i32, device=self.device)
-        self.samples = engine.ParticleStore(T, [N] * O, dtype=f32, device=self.device,
-                                            origin=np.zeros((O, 2)))
-        region, cur = [], 0
+        # small clouds: sampler + bucketing in one launch (ccmpc_sample_bucket), whose cells need
+        # K (N + 4) slots per OV; else the sampler's sample-order store + ccmpc_bucket
+        fused_ws = lib.ccmpc_sample_bucket_workspace_bytes(O, N, T, self.max_k) \
+            if self.max_k * (L + 1) <= 512 else 0
+        self.fused = fused_ws > 0
+        region, cur, n_bound = [], 0, 0
         for o in range(O):
             region.append(cur)
-            cur = engine._round4(cur + N + 4 * self.K[o])
+            cur = engine._round4(cur + (self.K[o] * (N + 4) if self.fused
+                                        else N + 4 * self.K[o]))
+            n_bound = engine._round4(n_bound + N + 4 * self.K[o])
         self.region = np.asarray(region, np.int64)
         st = engine.ParticleStore(T, [0] * C, dtype=f32, device=self.device,
                                   origin=np.zeros((C, 2)), capacity=cur)
         st.cell_off, st.cell_cnt, st.origin = self.out.d("off"), self.out.d("cnt"), \
             self.inp.d("origin")
         st.counts = st.offsets = None
-        st.n_bound = cur
+        st.n_bound = n_bound
         self.store = st
-        self.bucket_ws = torch.zeros(max(lib.ccmpc_bucket_workspace_bytes(O, N, L, self.max_k),
-                                         16), dtype=u8, device=self.device)
+        if self.fused:
+            self.bucket_ws = torch.zeros(fused_ws, dtype=u8, device=self.device)
+        else:
+            self.z = torch.empty((O, N), dtype=i32, device=self.device)
+            self.samples = engine.ParticleStore(T, [N] * O, dtype=f32, device=self.device,
+                                                origin=np.zeros((O, 2)))
+            self.bucket_ws = torch.zeros(
+                max(lib.ccmpc_bucket_workspace_bytes(O, N, L, self.max_k), 16), dtype=u8,
+                device=self.device)
         self.ws = engine.Workspace(self.device)
         self.ws.get(lib.ccmpc_moments_workspace_bytes(T, C, st.n_bound))
         self.l4_ws = engine.Workspace(self.device)      # its own: layouts differ
@@ -131,22 +141,38 @@ class MinkowskiStepGraph:
         self._static_set = False
 
     # ---------------------------------------------------------------------------------------
+    def _sample_calls(self, s):
+        """The sampling + bucketing stage's C-ABI calls: [(fn, args)]."""
+        lib, p = _lib.load(), engine._p
+        i, o, st = self.inp, self.out, self.store
+        O, N, T, L = self.O, self.N, self.T, self.L
+        ws = self.bucket_ws
+        if self.fused:
+            return [(lib.ccmpc_sample_bucket, (
+                p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None, None,
+                O, N, T, self.dt, 0, p(i.d("seed")), 0, p(i.d("keep")), p(i.d("nk")),
+                p(i.d("base")), self.max_k, p(i.d("minpos")), p(i.d("region")), p(ws),
+                ws.numel(), None, p(st.pos), st.ld, p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")),
+                p(o.d("centre")), s))]
+        sm = self.samples
+        return [(lib.ccmpc_sample_unicycle_ex, (
+                    p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None,
+                    None, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld,
+                    s)),
+                (lib.ccmpc_bucket, (p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
+                                    p(i.d("nk")), p(i.d("base")), self.max_k,
+                                    p(i.d("minpos")), p(i.d("region")), p(ws), ws.numel(),
+                                    p(st.pos), st.ld, p(o.d("off")), p(o.d("cnt")),
+                                    p(o.d("pmf")), p(o.d("centre")), s))]
+
     def _enqueue(self):
         lib, p, s = _lib.load(), engine._p, engine._stream()
-        i, o, st, sm = self.inp, self.out, self.store, self.samples
-        O, N, T, L, C = self.O, self.N, self.T, self.L, self.C
+        i, o, st = self.inp, self.out, self.store
+        T, C = self.T, self.C
         chk = engine._lib.check
         chk(lib.ccmpc_copy_async(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
-        chk(lib.ccmpc_sample_unicycle_ex(
-            p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None, None,
-            O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld, s),
-            "ccmpc_sample_unicycle_ex")
-        ws = self.bucket_ws
-        chk(lib.ccmpc_bucket(p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
-                             p(i.d("nk")), p(i.d("base")), self.max_k, p(i.d("minpos")),
-                             p(i.d("region")), p(ws), ws.numel(), p(st.pos), st.ld,
-                             p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")), p(o.d("centre")), s),
-            "ccmpc_bucket")
+        for fn, args in self._sample_calls(s):
+            chk(fn(*args), fn.__name__)
         # the cycle and the L4 kernel only read the bucketed store: two graph branches
         main = torch.cuda.current_stream(self.device)
         self.side.wait_stream(main)
@@ -219,19 +245,11 @@ class MinkowskiStepGraph:
         direct-launch alternative to the graph: one foreign call per stage, the cycle and L4
         back to back on one stream)."""
         lib, p, s = _lib.load(), engine._p, engine._stream()
-        i, o, st, sm = self.inp, self.out, self.store, self.samples
-        O, N, T, L, C = self.O, self.N, self.T, self.L, self.C
-        ws, mws = self.bucket_ws, self.ws.buf
-        self._calls = [
-            (lib.ccmpc_copy_async, (p(i.dev), p(i.host), i.nbytes, s)),
-            (lib.ccmpc_sample_unicycle_ex, (
-                p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None,
-                None, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld, s)),
-            (lib.ccmpc_bucket, (p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
-                                p(i.d("nk")), p(i.d("base")), self.max_k, p(i.d("minpos")),
-                                p(i.d("region")), p(ws), ws.numel(), p(st.pos), st.ld,
-                                p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")), p(o.d("centre")),
-                                s)),
+        i, o, st = self.inp, self.out, self.store
+        T, C = self.T, self.C
+        mws = self.ws.buf
+        self._calls = [(lib.ccmpc_copy_async, (p(i.dev), p(i.host), i.nbytes, s))] + \
+            self._sample_calls(s) + [
             (lib.ccmpc_minkowski_cycle, (
                 p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
                 st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,

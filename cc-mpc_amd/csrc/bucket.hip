@@ -11,10 +11,11 @@
 //                  reference's np.concatenate order
 //   pmf_k        = N_k / N
 // This is a stable counting sort on key = owner * (L + 1) + group, group = 0 for the native
-// mode and 1 + z for a rare latent.  Five short kernels:
-//   B1 stats   per block: latent counts (LDS int atomics, exact) and per-kept-mode sums of the
-//              final positions (fixed-order block reductions), published write-through; the
-//              OV's last arriving block sums them in block order -> centres
+// mode and 1 + z for a rare latent.  Three short kernels:
+//   B1 stats   per block: latent counts (LDS int atomics, exact) and, per wave, the kept-mode
+//              sums of its 64 final positions (bucket.hpp's centre groups), published
+//              write-through; the OV's last arriving block sums them in the canonical order
+//              (bucket.hpp) -> centres
 //   B2 keys    per block: key histogram (LDS int atomics, exact), published write-through; the
 //              OV's last arriving block scans them -> bin offsets (bin-major, block-minor),
 //              4-aligned cell offsets
@@ -24,16 +25,22 @@
 // agent-scope ticket, sc1 loads); its counters live at the head of the workspace, which must be
 // zero-filled once (every call leaves them zero).
 // Everything is integer-exact except the centre sums, whose fixed order makes them
-// deterministic; the bucketed store is bit-identical across runs.
-#include "gram.hpp"
+// deterministic; the bucketed store is bit-identical across runs, and to the fused sampler +
+// bucketing kernel's (sample_bucket.hip) up to where each cell starts.
+#include "bucket.hpp"
 
 namespace ccmpc {
 
 constexpr int kBucketBlock = 256;
 constexpr int kPerThread = 1;  // one round per block: many short blocks (C2 shape: 80, not 20)
 constexpr int kSpan = kBucketBlock * kPerThread;  // particles per block, in sample order
-constexpr int kMaxBins = 1024;
-constexpr int kMaxKept = 16;
+
+#if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
+__device__ unsigned long long g_bkt_ts[3][kStepProbeWG * kStepProbeSlots];
+#define BKT_TS(kern, k) CCMPC_STEP_TS(g_bkt_ts[kern], k)
+#else
+#define BKT_TS(kern, k) CCMPC_STEP_TS(nullptr, k)
+#endif
 
 struct BucketArgs {
   const int32_t *z;        // [n_ov][N]
@@ -49,8 +56,10 @@ struct BucketArgs {
   int nb;                   // blocks per OV
   // workspace
   int32_t *ctr;             // [2][n_ov] arrival counters (zero between calls)
-  double *part;             // [n_ov][nb][E1]: latent counts [L], then from S0 (even) the
-  int E1, S0;               // kept-mode sums [max_k][2]; E1 even
+  double *part;             // [n_ov][nb][E1]: latent counts [L] (as doubles; E1 even)
+  int E1;
+  double *gpart;            // [n_ov][G][max_k][2]: per 64-particle group kept-mode sums
+  int G;                    // groups per OV = ceil(N / 64)
   double *centre;           // [n_ov][max_k][2]
   int32_t *hist;            // [n_ov][nb][nbins]
   int64_t *bin_off;         // [n_ov][nb][nbins]
@@ -79,137 +88,114 @@ __device__ __forceinline__ void final_world(const BucketArgs &a, int o, int64_t 
   y = static_cast<double>(p[(2 * (a.T - 1) + 1) * a.ld_in]) + a.minpos[2 * o + 1];
 }
 
-// Bucket key of a particle from values staged in LDS / registers (keep_map and the centres read once per
-// block, z and the final position loaded up front with everything else the block needs: the
-// global reads of key_of are a chain of dependent round trips in a kernel this small).
-__device__ __forceinline__ int key_staged(int zv, double x, double y, const int *keep_s,
-                                          const double (*cen_s)[2], int K, int L) {
-  const int k = keep_s[zv];
-  if (k >= 0) return k * (L + 1);
-  int best = 0;
-  double bd = INFINITY;
-  for (int j = 0; j < K; ++j) {
-    const double dx = x - cen_s[j][0], dy = y - cen_s[j][1];
-    const double d = sqrt(dx * dx + dy * dy);
-    if (d < bd) {
-      bd = d;
-      best = j;
-    }
-  }
-  return best * (L + 1) + 1 + zv;
-}
-
-__device__ __forceinline__ void st1_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, int32_t v) {
-  __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(v), r, byte_off, 0, 16);
-}
-__device__ __forceinline__ int32_t ld1_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  return static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 16));
-}
-
 __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
+  BKT_TS(0, 0);
   __shared__ int cnt[64];
   __shared__ double red[4];
-  __shared__ double pub[64 + 2 + 2 * kMaxKept];
   __shared__ int flag;
   __shared__ int keep_s[64];
+  __shared__ int zv_s[kMaxKept];
+  __shared__ double nk_s[kMaxKept];
+  __shared__ double2 sup_s[kMaxKept][kCentreSuper];
   const int o = blockIdx.y, blk = blockIdx.x;
+  const int lane = threadIdx.x & 63;
   const int K = a.n_kept[o];
   const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
-  int zs[kPerThread];
-  double xs[kPerThread], ys[kPerThread];
-#pragma unroll
-  for (int r = 0; r < kPerThread; ++r) {  // every load of the block issued together
-    const int64_t i = i0 + r * kBucketBlock + threadIdx.x;
-    zs[r] = -1;
-    xs[r] = ys[r] = 0.0;
-    if (i < a.N) {
-      zs[r] = a.z[o * a.N + i];
-      final_world(a, o, i, xs[r], ys[r]);
-    }
+  static_assert(kPerThread == 1 && kBucketBlock % kCentreGroup == 0, "one group per wave");
+  const int64_t i = i0 + threadIdx.x;
+  int zv = -1;
+  double xf = 0.0, yf = 0.0;
+  if (i < a.N) {
+    zv = a.z[o * a.N + i];
+    final_world(a, o, i, xf, yf);
   }
   for (int l = threadIdx.x; l < a.L; l += blockDim.x) {
     cnt[l] = 0;
     keep_s[l] = a.keep_map[o * a.L + l];
   }
   __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kPerThread; ++r)
-    if (zs[r] >= 0) atomicAdd(&cnt[zs[r]], 1);
+  BKT_TS(0, 1);
+  if (zv >= 0) atomicAdd(&cnt[zv], 1);
+  // this wave's 64 particles are centre group g (bucket.hpp): its kept-mode sums
+  const int g = blk * (kBucketBlock / kCentreGroup) + (threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t rg =
+      slab_rsrc(a.gpart + static_cast<int64_t>(o) * a.G * a.max_k * 2);
   for (int k = 0; k < K; ++k) {
-    double sx = 0.0, sy = 0.0;
-#pragma unroll
-    for (int r = 0; r < kPerThread; ++r) {
-      const bool mine = zs[r] >= 0 && keep_s[zs[r]] == k;
-      sx += mine ? xs[r] : 0.0;
-      sy += mine ? ys[r] : 0.0;
-    }
-    sx = block_sum256(sx, red);
-    sy = block_sum256(sy, red);
-    if (threadIdx.x == 0) {
-      pub[a.S0 + 2 * k] = sx;
-      pub[a.S0 + 2 * k + 1] = sy;
-    }
+    const bool mine = zv >= 0 && keep_s[zv] == k;
+    const double sx = group_sum64(mine ? xf : 0.0), sy = group_sum64(mine ? yf : 0.0);
+    if (lane == 0 && g < a.G) st2_sc1(rg, 16 * (g * a.max_k + k), sx, sy);
   }
   __syncthreads();
-  for (int l = threadIdx.x; l < a.L; l += blockDim.x) pub[l] = static_cast<double>(cnt[l]);
-  __syncthreads();
-  // publish this block's partials write-through, then the OV's last arriver combines them
+  // latent counts, published write-through; the OV's last arriver combines them
   double *mine = a.part + (static_cast<int64_t>(o) * a.nb + blk) * a.E1;
   const __amdgpu_buffer_rsrc_t rm = slab_rsrc(mine);
-  const int used = a.S0 + 2 * K;
-  for (int e = 2 * threadIdx.x; e < used; e += 2 * blockDim.x)
-    st2_sc1(rm, 8 * e, pub[e], e + 1 < used ? pub[e + 1] : 0.0);
+  for (int e = 2 * threadIdx.x; e < a.L; e += 2 * blockDim.x)
+    st2_sc1(rm, 8 * e, static_cast<double>(cnt[e]),
+            e + 1 < a.L ? static_cast<double>(cnt[e + 1]) : 0.0);
+  BKT_TS(0, 2);
   if (!arrive_last(a.ctr + o, a.nb, &flag)) return;
-  // centres: kept mode k's own particles (latent zv_k), summed over blocks in a fixed order
-  // (this thread's blocks b = tid, tid + 256, ..., then the fixed block reduction); every
-  // mode's loads are issued before any is summed
-  __shared__ int zv_s[kMaxKept];
+  BKT_TS(0, 3);
   for (int l = threadIdx.x; l < a.L; l += blockDim.x) {
     const int k = keep_s[l];
     if (k >= 0) zv_s[k] = l;
   }
   __syncthreads();
-  const double *p0 = a.part + static_cast<int64_t>(o) * a.nb * a.E1;
-  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(p0);
-  constexpr int KB = 4;  // modes whose loads are in flight together
+  // n_k: kept mode k's own particles (integer-exact in any order); every mode's loads together
+  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(a.part + static_cast<int64_t>(o) * a.nb * a.E1);
+  constexpr int KB = 4;
   for (int k0 = 0; k0 < K; k0 += KB) {
-    double n[KB], sx[KB], sy[KB];
+    double n[KB];
 #pragma unroll
-    for (int j = 0; j < KB; ++j) n[j] = sx[j] = sy[j] = 0.0;
+    for (int j = 0; j < KB; ++j) n[j] = 0.0;
     for (int b = threadIdx.x; b < a.nb; b += blockDim.x) {
-      double2 c[KB], v[KB];
+      double2 c[KB];
 #pragma unroll
       for (int j = 0; j < KB; ++j) {
         const int k = k0 + j < K ? k0 + j : K - 1;  // clamped: always a valid address
         c[j] = ld2_sc1(rp, 8 * (b * a.E1 + (zv_s[k] & ~1)));
-        v[j] = ld2_sc1(rp, 8 * (b * a.E1 + a.S0 + 2 * k));
       }
 #pragma unroll
-      for (int j = 0; j < KB; ++j) {
-        n[j] += (zv_s[k0 + j < K ? k0 + j : K - 1] & 1) ? c[j].y : c[j].x;
-        sx[j] += v[j].x;
-        sy[j] += v[j].y;
-      }
+      for (int j = 0; j < KB; ++j) n[j] += (zv_s[k0 + j < K ? k0 + j : K - 1] & 1) ? c[j].y : c[j].x;
     }
 #pragma unroll
     for (int j = 0; j < KB; ++j) {
-      const int k = k0 + j;
-      if (k < K) {  // uniform: K is the OV's
-        const double nk = block_sum256(n[j], red);
-        const double xk = block_sum256(sx[j], red), yk = block_sum256(sy[j], red);
-        if (threadIdx.x == 0) {
-          a.centre[(o * a.max_k + k) * 2] = xk / nk;
-          a.centre[(o * a.max_k + k) * 2 + 1] = yk / nk;
-          const int cell = a.cell_base[o] + k;
-          a.init_center[2 * cell] = xk / nk;
-          a.init_center[2 * cell + 1] = yk / nk;
-        }
-      }
+      const double s = block_sum256(n[j], red);
+      if (k0 + j < K && threadIdx.x == 0) nk_s[k0 + j] = s;
     }
   }
+  // the canonical centre sums (bucket.hpp): superblocks in parallel, then left to right
+  const int J = (a.G + kCentreSuper - 1) / kCentreSuper;
+  double2 tot = {0.0, 0.0};  // thread k's running sum of mode k
+  for (int j0 = 0; j0 < J; j0 += kCentreSuper) {
+    const int nj = min(kCentreSuper, J - j0);
+    for (int u = threadIdx.x; u < K * nj; u += blockDim.x) {
+      const int k = u / nj, j = j0 + u % nj;
+      sup_s[k][j - j0] = superblock_sum(j, a.G, [&](int gg) {
+        return ld2_sc1(rg, 16 * (gg * a.max_k + k));
+      });
+    }
+    __syncthreads();
+    if (threadIdx.x < K)
+      for (int j = 0; j < nj; ++j) {
+        tot.x += sup_s[threadIdx.x][j].x;
+        tot.y += sup_s[threadIdx.x][j].y;
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    const double cx = tot.x / nk_s[k], cy = tot.y / nk_s[k];
+    a.centre[(o * a.max_k + k) * 2] = cx;
+    a.centre[(o * a.max_k + k) * 2 + 1] = cy;
+    const int cell = a.cell_base[o] + k;
+    a.init_center[2 * cell] = cx;
+    a.init_center[2 * cell + 1] = cy;
+  }
+  BKT_TS(0, 4);
 }
 
 __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
+  BKT_TS(1, 0);
   __shared__ int h[kMaxBins];
   __shared__ int64_t start[kMaxBins];
   __shared__ int flag;
@@ -237,6 +223,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
     cen_s[j >> 1][j & 1] = a.centre[(o * a.max_k + (j >> 1)) * 2 + (j & 1)];
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) h[b] = 0;
   __syncthreads();
+  BKT_TS(1, 1);
 #pragma unroll
   for (int r = 0; r < kPerThread; ++r)
     if (zs[r] >= 0) atomicAdd(&h[key_staged(zs[r], xs[r], ys[r], keep_s, cen_s, K, a.L)], 1);
@@ -247,7 +234,9 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
                                                                        0x00020000);
   for (int b = threadIdx.x; b < nbins; b += blockDim.x)
     st1_sc1(rh, 4 * static_cast<int>(blk * stride + b), h[b]);
+  BKT_TS(1, 2);
   if (!arrive_last(a.ctr + a.n_ov + o, a.nb, &flag)) return;
+  BKT_TS(1, 3);
   // the OV's scan: bin totals (blocks in order), bins in (kept mode, group) order
   // (loads in batches of 8, all in flight together: a dependent chain of nb round trips
   // was the kernel's whole latency)
@@ -299,9 +288,11 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
       }
     }
   }
+  BKT_TS(1, 4);
 }
 
 __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
+  BKT_TS(2, 0);
   __shared__ int run[kMaxBins];        // particles of each bin in earlier rounds of this block
   __shared__ int wcnt[4][kMaxBins];    // per wave counts of the current round
   __shared__ int keep_s[64];
@@ -342,6 +333,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
   for (int r = 0; r < kPerThread; ++r) {
     for (int b = threadIdx.x; b < 4 * nbins; b += blockDim.x) wcnt[b / nbins][b % nbins] = 0;
     __syncthreads();
+    BKT_TS(2, 1);
     const int key = valid ? key_staged(zv, xf, yf, keep_s, cen_s, K, a.L) : -1;
     // rank among equal keys of this wave (lanes in order)
     int rank = 0;
@@ -368,25 +360,28 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
       run[b] += wcnt[0][b] + wcnt[1][b] + wcnt[2][b] + wcnt[3][b];
     __syncthreads();
   }
+  BKT_TS(2, 2);
 }
 
 inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  size_t ctr, part, centre, hist, bin_off, total;
-  int E1, S0;
+  size_t ctr, part, gpart, centre, hist, bin_off, total;
+  int E1, G;
 };
 
 inline WsLayout bucket_ws(int64_t n_ov, int64_t N, int64_t L, int64_t max_k) {
   const int64_t nb = (N + kSpan - 1) / kSpan;
   WsLayout w;
-  w.S0 = static_cast<int>((L + 1) & ~int64_t(1));
-  w.E1 = static_cast<int>(w.S0 + 2 * max_k);
+  w.E1 = static_cast<int>((L + 1) & ~int64_t(1));
+  w.G = static_cast<int>((N + kCentreGroup - 1) / kCentreGroup);
   size_t o = 0;
   w.ctr = o;  // arrival counters first: the zero-filled head of the workspace
   o += align256(sizeof(int32_t) * 2 * n_ov);
   w.part = o;
   o += align256(sizeof(double) * n_ov * nb * w.E1);
+  w.gpart = o;
+  o += align256(sizeof(double) * n_ov * w.G * max_k * 2);
   w.centre = o;
   o += align256(sizeof(double) * n_ov * max_k * 2);
   w.hist = o;
@@ -400,6 +395,22 @@ inline WsLayout bucket_ws(int64_t n_ov, int64_t N, int64_t L, int64_t max_k) {
 }  // namespace ccmpc
 
 using namespace ccmpc;
+
+#if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
+// which: 0 stats (slots 0 start, 1 loaded, 2 published, 3 last arriver, 4 done), 1 hist (same),
+// 2 scatter (0 start, 1 loaded, 2 done)  (tools/probe_step.py)
+extern "C" int ccmpc_probe_bucket_timestamps(void *host, int which, int reset) {
+  if (which < 0 || which > 2) return -1;
+  const size_t bytes = sizeof(g_bkt_ts[0]);
+  if (reset) {
+    static unsigned long long zeros[kStepProbeWG * kStepProbeSlots];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_bkt_ts), zeros, bytes, which * bytes) == hipSuccess
+               ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bkt_ts), bytes, which * bytes) == hipSuccess
+             ? 0 : -1;
+}
+#endif
 
 extern "C" size_t ccmpc_bucket_workspace_bytes(int64_t n_ov, int64_t N, int64_t n_latent,
                                                int64_t max_k) {
@@ -449,7 +460,8 @@ extern "C" int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in
   a.ctr = reinterpret_cast<int32_t *>(ws + L.ctr);
   a.part = reinterpret_cast<double *>(ws + L.part);
   a.E1 = L.E1;
-  a.S0 = L.S0;
+  a.gpart = reinterpret_cast<double *>(ws + L.gpart);
+  a.G = L.G;
   a.centre = reinterpret_cast<double *>(ws + L.centre);
   a.hist = reinterpret_cast<int32_t *>(ws + L.hist);
   a.bin_off = reinterpret_cast<int64_t *>(ws + L.bin_off);

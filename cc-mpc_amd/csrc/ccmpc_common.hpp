@@ -84,6 +84,24 @@ __device__ __forceinline__ void normal_pair(uint32_t c0, uint32_t c1, uint32_t c
   z1 = r * s;
 }
 
+// ---- diagnostic timestamps (PROBE=4 builds only) -------------------------------------------
+// CCMPC_STEP_TS(table, k): workgroup (blockIdx.y * gridDim.x + blockIdx.x)'s slot k of a
+// [4096][8] table gets s_memrealtime (100 MHz, one clock for every kernel of a step, so the
+// gaps between kernels show).  Each file defines its own table and reader.
+constexpr int kStepProbeWG = 4096, kStepProbeSlots = 8;
+#if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
+#define CCMPC_STEP_TS(tab, k)                                                                 \
+  do {                                                                                        \
+    const unsigned wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                 \
+    if (threadIdx.x == 0 && wg_ < ::ccmpc::kStepProbeWG)                                      \
+      (tab)[wg_ * ::ccmpc::kStepProbeSlots + (k)] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
+#else
+#define CCMPC_STEP_TS(tab, k) \
+  do {                        \
+  } while (0)
+#endif
+
 // ---- 2x2 symmetric helpers -----------------------------------------------------------------
 struct Sym2 {
   double a, b, c;  // [[a, b], [b, c]]

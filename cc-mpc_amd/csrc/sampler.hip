@@ -15,60 +15,13 @@
 // GRU decoder that produce them are upstream of this boundary (absent submodule).
 // Float32 arithmetic throughout, as torch runs it; the noise and the transcendentals are
 // evaluated in float64 and rounded to float32.
-#include "ccmpc_common.hpp"
+#include "sampler.hpp"
 
 namespace ccmpc {
 
-// float32 sin/cos/exp evaluated in float64 and rounded once: correctly rounded in practice, so
-// the result does not depend on which libm computes it (the oracle does the same), and the
-// (sin(phi + w dt) - sin(phi)) / w cancellation cannot amplify a 1-ulp libm difference.
-__device__ __forceinline__ void sincos_rn(float a, float &s, float &c) {
-  double sd, cd;
-  sincos(static_cast<double>(a), &sd, &cd);
-  s = static_cast<float>(sd);
-  c = static_cast<float>(cd);
-}
-
-__device__ __forceinline__ float exp_rn(float a) {
-  return static_cast<float>(exp(static_cast<double>(a)));
-}
-
-// One Unicycle.dynamic step.  (s0, c0) = sin / cos of the current heading, carried from the
-// previous step: the heading after a turning step IS that step's phi + w dt, whose sin / cos
-// it already evaluated, and a straight step keeps phi -- so each step evaluates one sincos
-// (none when straight) with exactly the values of a fresh sincos_rn(phi).
-__device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, float &v, float &s0,
-                                              float &c0, float dphi, float a, float dt) {
-  const bool straight = fabsf(dphi) <= 1e-2f;
-  if (straight) {
-    x = x + v * c0 * dt + (a / 2.0f) * c0 * dt * dt;
-    y = y + v * s0 * dt + (a / 2.0f) * s0 * dt * dt;
-  } else {
-    const float w = dphi;
-    const float phi1 = phi + w * dt;
-    float s1, c1;
-    sincos_rn(phi1, s1, c1);
-    const float dsin = (s1 - s0) / w, dcos = (c1 - c0) / w;
-    const float aw = a / w;
-    x = x + aw * dcos + v * dsin + aw * s1 * dt;
-    y = y - v * dcos + aw * dsin - aw * c1 * dt;
-    phi = phi1;
-    s0 = s1;
-    c0 = c1;
-  }
-  v = v + a * dt;
-}
-
-// One GMM2D component's reparametrised draw (Trajectron++ GMM2D.rsample with one component):
-// a = mu + L eps, L = [[s0, 0], [s1 rho, s1 sqrt(clamp(1 - rho^2, 1e-5, 1))]], s = exp(log s);
-// the matmul row is summed before mu is added, as `mus + squeeze(L @ eps)` does.
-__device__ __forceinline__ void gmm2d_action(float mu0, float mu1, float ls0, float ls1, float rho,
-                                             float e0, float e1, float &dphi, float &acc) {
-  const float s0 = exp_rn(ls0), s1 = exp_rn(ls1);
-  const float omr2 = fminf(fmaxf(1.0f - rho * rho, 1e-5f), 1.0f);
-  dphi = mu0 + s0 * e0;  // + 0 * e1: adds a signed zero, never changes s0 e0 unless it is 0
-  acc = mu1 + ((s1 * rho) * e0 + (s1 * sqrtf(omr2)) * e1);
-}
+#if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
+__device__ unsigned long long g_samp_ts[kStepProbeWG * kStepProbeSlots];
+#endif
 
 // Where the draw's parameters and noise come from:
 //  PP    per-particle GMM parameters gmm[o][t][5][N] (what p_y_xz emits: its GRU decoder is
@@ -99,6 +52,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
   __shared__ int zs[kSampP];
   __shared__ double cdf_s[64];           // this OV's latent CDF, one coalesced read
   __shared__ float gmm_s[PP ? 1 : 64 * 40 * 5 / 4];  // per-latent rows, staged when they fit
+  CCMPC_STEP_TS(g_samp_ts, 0);
   const int ov = blockIdx.y;
   const int lane = threadIdx.x & (kSampP - 1), slot = threadIdx.x / kSampP;
   // a seed in device memory lets a captured graph draw fresh particles on every replay
@@ -116,53 +70,26 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
     for (int e = threadIdx.x; e < gsz; e += blockDim.x)
       gmm_s[e] = gmm[static_cast<int64_t>(ov) * gsz + e];
   __syncthreads();
+  CCMPC_STEP_TS(g_samp_ts, 1);
   if (slot == 0 && valid) {
     int z;
     if (ZIN) {
       z = z_in[static_cast<int64_t>(ov) * N + i];
       z = z < 0 ? 0 : (z >= n_latent ? n_latent - 1 : z);  // memory safety; the host validates
     } else {
-      const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, key, STREAM_SAMPLER_Z, seed);
-      const double u = uniform53(w.x, w.y);
-      z = n_latent - 1;
-      for (int k = 0; k < n_latent; ++k) {
-        if (cdf_s[k] > u) {  // numpy searchsorted(cdf, u, side='right')
-          z = k;
-          break;
-        }
-      }
+      z = draw_latent(i, key, seed, cdf_s, n_latent);
     }
     zs[lane] = z;
     out_z[static_cast<int64_t>(ov) * N + i] = z;
   }
   __syncthreads();
-  if (valid) {
-    const int z = zs[lane];
-    // per-latent: this particle's component row; per-particle: element (t, k) at g[(5t + k) N]
-    const float *g = PP ? gmm + static_cast<int64_t>(ov) * T * 5 * N + i
-                        : gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
-    const float *ep = EPSIN ? eps_in + static_cast<int64_t>(ov) * T * 2 * N + i : nullptr;
-    for (int t = slot; t < T; t += kSlots) {
-      float e0, e1;
-      if (EPSIN) {
-        e0 = ep[(2 * t) * N];
-        e1 = ep[(2 * t + 1) * N];
-      } else {
-        double e0d, e1d;
-        normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), key, STREAM_SAMPLER_EPS,
-                    seed, e0d, e1d);
-        e0 = static_cast<float>(e0d);
-        e1 = static_cast<float>(e1d);
-      }
-      float p[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        p[k] = PP ? g[(5 * t + k) * N]
-                  : (staged ? gmm_s[(z * T + t) * 5 + k] : g[5 * t + k]);
-      gmm2d_action(p[0], p[1], p[2], p[3], p[4], e0, e1, act[0][t][lane], act[1][t][lane]);
-    }
-  }
+  CCMPC_STEP_TS(g_samp_ts, 2);
+  if (valid)
+    for (int t = slot; t < T; t += kSlots)
+      draw_action<PP, EPSIN>(t, i, zs[lane], ov, T, n_latent, N, key, seed, gmm, gmm_s, staged,
+                             eps_in, act[0][t][lane], act[1][t][lane]);
   __syncthreads();
+  CCMPC_STEP_TS(g_samp_ts, 3);
   if (slot != 0 || !valid) return;
   const double *st = init_state + 4 * ov;
   float x = static_cast<float>(st[0]), y = static_cast<float>(st[1]);
@@ -175,6 +102,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
     o[(2 * t) * ld] = x;
     o[(2 * t + 1) * ld] = y;
   }
+  CCMPC_STEP_TS(g_samp_ts, 4);
 }
 
 template <bool PP, bool ZIN, bool EPSIN>
@@ -191,6 +119,18 @@ static void launch_sampler(dim3 grid, hipStream_t s, const double *init_state,
 }  // namespace ccmpc
 
 using namespace ccmpc;
+
+#if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
+// slots: 0 start, 1 tables staged, 2 z drawn, 3 actions drawn, 4 chain done (tools/probe_step.py)
+extern "C" int ccmpc_probe_sampler_timestamps(void *host, int reset) {
+  const size_t bytes = sizeof(g_samp_ts);
+  if (reset) {
+    static unsigned long long zeros[kStepProbeWG * kStepProbeSlots];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_samp_ts), zeros, bytes) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_samp_ts), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int ccmpc_sample_unicycle_ex(const double *init_state, const double *latent_cdf,
                                         int64_t n_latent, const float *gmm, int32_t gmm_layout,

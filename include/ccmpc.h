@@ -312,6 +312,30 @@ int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T
                  double *init_center, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Sampler + bucketing in ONE launch, for clouds of N <= 8192 particles per OV: the same draws
+ * as ccmpc_sample_unicycle_ex (same Philox streams, same float32 arithmetic) bucketed as
+ * ccmpc_bucket buckets them -- every cell holds the same particles in the same order and the
+ * same init_center / pmf bits.  Replaces prediction.py:81-86 + v8ideal/__init__.py:469-505 +
+ * ovehicle.py:24-117 on the drop-in step's shape.
+ * Differences from ccmpc_bucket's output: only where the cells start.  Cell k of OV o starts at
+ *   region[o] + sum_{j<k} round4(n_j + R_o)   (n_j = mode j's own particles, R_o = rare ones)
+ * so region[o] needs n_kept[o] * (N + 4) free slots of pos_out.  out_z (optional, may be NULL)
+ * gets the sample-order latent ids.  N > 8192: use the sampler + ccmpc_bucket.
+ * Workspace: ccmpc_sample_bucket_workspace_bytes (0 = shape not supported), 256-byte aligned;
+ * its head holds per-OV arrival counters: zero-fill once (every call leaves them zero).
+ * ------------------------------------------------------------------------------------- */
+size_t ccmpc_sample_bucket_workspace_bytes(int64_t n_ov, int64_t N, int64_t T, int64_t max_k);
+int ccmpc_sample_bucket(const double *init_state, const double *latent_cdf, int64_t n_latent,
+                        const float *gmm, int32_t gmm_layout, const int32_t *z_in,
+                        const float *eps_in, int64_t n_ov, int64_t N, int64_t T, double dt,
+                        uint64_t seed, const uint64_t *seed_dev, int64_t ov_base,
+                        const int32_t *keep_map, const int32_t *n_kept, const int32_t *cell_base,
+                        int64_t max_k, const double *minpos, const int64_t *region,
+                        void *workspace, size_t workspace_bytes, int32_t *out_z, float *pos_out,
+                        int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
+                        double *init_center, ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Headings, bounding-box vertices and L4 outer approximation for every (cell, t).
  * Replaces ovehicle.py:72-76 (yaws = atan2 of step deltas, step 0 from past[-1]),
  * v8ideal/__init__.py:627-640 (vertices_of_bboxes, restated from midlevel/util.py:104-124),

@@ -120,7 +120,7 @@ def test_affine_generator(gpu):
         assert not c.holds(np.array([r["mean"][0], r["mean"][1]]))
 
 
-@pytest.mark.parametrize("N", [6000, 12000])   # one-workgroup path (<= 8192) / three launches
+@pytest.mark.parametrize("N", [6000, 12000])
 def test_make_ovehicles_matches_reference_bucketing(gpu, N):
     """Sampler output -> buckets: same membership, same order, same pmf / init_center as
     make_ovehicles + OVehicle.from_trajectron (v8ideal/__init__.py:469-505, ovehicle.py:24-117)."""
