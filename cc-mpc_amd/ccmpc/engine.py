@@ -339,7 +339,7 @@ FUSED_MAX_N = 8192
 def sample_bucket(init_state, latent_pmf, gmm, N, T, minpos, dt=0.5, seed=0, device="cuda",
                   ov_base=0, z=None, eps=None, per_particle=False, filter_pmf=0.1, max_k=None,
                   with_z=False, workspace=None):
-    """Sampler + bucketing in one launch (ccmpc_sample_bucket, N <= 8192): the draws of
+    """Sampler + bucketing in three short launches (ccmpc_sample_bucket, N <= 8192): the draws of
     sample_unicycle with the same arguments, bucketed as bucket() buckets them (each cell the
     same particles in the same order, the same pmf / init_center bits; only the cell offsets
     differ).  latent_pmf (O, L) is required (it decides the kept modes).

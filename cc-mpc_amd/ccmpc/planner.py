@@ -23,6 +23,7 @@ Differences from the reference, all at the boundary:
   * the unseeded RNG of predict_ideal (:2664, :2699) is a Philox stream keyed by
     (seed, frame, cell), so runs are reproducible.
 """
+import functools
 import os
 
 import numpy as np
@@ -181,9 +182,10 @@ class UnionGrid:
     """A_union / b_union [t][k][ov] (v8ideal/__init__.py:627-736) over a host array [cell, t,
     ...]: None where OV `ov` has no mode k, as the reference's nested lists hold."""
 
-    def __init__(self, arr, K, ph):
+    def __init__(self, arr, K, ph, first=None):
         self._arr, self._K, self._ph = arr, list(K), ph
-        self._first = np.concatenate([[0], np.cumsum(K)[:-1]]).astype(int)
+        self._first = (first if first is not None
+                       else np.concatenate([[0], np.cumsum(K)[:-1]]).astype(int))
 
     def __len__(self):
         return self._ph
@@ -236,6 +238,18 @@ def _match_modes(mean_loaded, x_init, cur_means, n_states, M_big):
 def _host(x):
     """NumPy view of a saved moment array (device tensor or host copy)."""
     return x.cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+
+
+@functools.lru_cache(maxsize=64)
+def _first_cells(K):
+    """First cell of each OV for kept-mode counts K (a tuple)."""
+    return [sum(K[:o]) for o in range(len(K))]
+
+
+@functools.lru_cache(maxsize=64)
+def _last_cells(K):
+    """Last cell (mode) of each OV."""
+    return np.cumsum(K) - 1
 
 
 def _object_grid(*shape):
@@ -393,7 +407,7 @@ class MidlevelAgent:
         else:
             ym, yv = yaw
         K = list(K)
-        first = [sum(K[:o]) for o in range(len(K))]
+        first = _first_cells(tuple(K))
         return tuple(tuple(CellGrid(v, K, first) for v in vals) for vals in (
             (mean0[:, 0], mean0[:, 1], np.asarray(ym)),
             (cov0[:, 0, 0], cov0[:, 1, 1], np.asarray(yv))))
@@ -412,9 +426,8 @@ class MidlevelAgent:
 
     def _ov_in_junction(self, scene, mean0):
         """OVconstraint (:831-851): the Town03 scene-4 T-intersection test, last mode wins."""
-        inj = ~((mean0[:, 0] >= 190) | (mean0[:, 1] <= -80))      # per cell
-        last = np.cumsum(scene.K) - 1                               # each OV's last mode
-        return bool(np.any(inj[last]))
+        m = mean0[_last_cells(tuple(scene.K))]                      # each OV's last mode
+        return bool(np.any(~((m[:, 0] >= 190) | (m[:, 1] <= -80))))
 
     def _src_cells(self, prev_K, K):
         """data_idx fallback (:2648-2656): mode k reads saved mode k, or the last saved slot."""
@@ -637,8 +650,7 @@ class MidlevelAgent:
             g = step.MinkowskiStepGraph(O, N, ph, L, K, device=self.device, R=self.R)
             self._graphs[key] = g
         g.set_inputs(seed, init, pmf, gmm, minpos, ref_traj,
-                     self._cell_risk_host(np.asarray(eps_ura), K),
-                     np.repeat(past_last, K, axis=0), np.repeat(bboxes, K, axis=0),
+                     self._cell_risk_host(np.asarray(eps_ura), K), past_last, bboxes,
                      filter_pmf=filter_pmf)
         g.launch()
         # host objects that need no output are built while the graph runs
@@ -661,7 +673,9 @@ class MidlevelAgent:
         mean0, cov0 = mean[:, 0, :], cov[:, 0:2, 0:2]
         st_mean, st_cov = self._state_stats(scene, mean0, cov0,
                                             (o["yaw_mean"][:, 0], o["yaw0_var"]))
-        out = (constraints, vertices, UnionGrid(o["A"], K, ph), UnionGrid(o["b"], K, ph),
+        first = _first_cells(tuple(K))
+        out = (constraints, vertices, UnionGrid(o["A"], K, ph, first),
+               UnionGrid(o["b"], K, ph, first),
                self._ov_in_junction(scene, mean0), direct, st_mean, st_cov, 0)
         return ovs, out
 

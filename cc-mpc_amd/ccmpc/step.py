@@ -25,6 +25,8 @@ read the outputs through zero-copy NumPy views.  The Philox seed travels in the 
 Outputs live in the graph's buffers until the next replay of the same graph; what the caller
 keeps across steps (the saved moments) is copied out.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -54,6 +56,8 @@ class Pack:
             self._d[name] = self.dev[off:off + n].view(dtype).view(shape)
             npdt = torch.empty((), dtype=dtype).numpy().dtype
             self._h[name] = raw[off:off + n].view(npdt).reshape(shape)
+        self._views = [(name, shape, self._h[name].dtype, off)
+                       for name, (off, shape, dtype, n) in self.spec.items()]
 
     def d(self, name):
         """Device view of a field."""
@@ -67,10 +71,8 @@ class Pack:
         """One copy of the whole host buffer; returns {field: view of the copy} (outputs that
         must outlive the next replay, for one memcpy instead of one per field)."""
         raw = self.host.numpy().copy()
-        out = {}
-        for name, (off, shape, dtype, n) in self.spec.items():
-            out[name] = raw[off:off + n].view(self._h[name].dtype).reshape(shape)
-        return out
+        nd = np.ndarray
+        return {name: nd(shape, dt, raw, off) for name, shape, dt, off in self._views}
 
 
 class MinkowskiStepGraph:
@@ -104,7 +106,7 @@ class MinkowskiStepGraph:
                          ("b", (C, T, 4), f64), ("yaw_mean", (C, T), f64),
                          ("yaw0_var", (C,), f64), ("cnt", (C,), i64), ("off", (C,), i64),
                          ("pmf", (C,), f64), ("centre", (C, 2), f64)], self.device)
-        # small clouds: sampler + bucketing in one launch (ccmpc_sample_bucket), whose cells need
+        # small clouds: sampler + bucketing in three short launches (ccmpc_sample_bucket), whose cells need
         # K (N + 4) slots per OV; else the sampler's sample-order store + ccmpc_bucket
         fused_ws = lib.ccmpc_sample_bucket_workspace_bytes(O, N, T, self.max_k) \
             if self.max_k * (L + 1) <= 512 else 0
@@ -137,6 +139,9 @@ class MinkowskiStepGraph:
         self.l4_ws = engine.Workspace(self.device)      # its own: layouts differ
         self.l4_ws.get(lib.ccmpc_l4_workspace_bytes(T, C, st.n_bound))
         self.side = torch.cuda.Stream(device=self.device)
+        # the cycle and the L4 kernel as parallel graph branches, or (CCMPC_STEP_LINEAR=1) one
+        # after the other on one stream
+        self.branch = os.environ.get("CCMPC_STEP_LINEAR", "0") != "1"
         self.graph = None
         self._static_set = False
 
@@ -175,8 +180,9 @@ class MinkowskiStepGraph:
             chk(fn(*args), fn.__name__)
         # the cycle and the L4 kernel only read the bucketed store: two graph branches
         main = torch.cuda.current_stream(self.device)
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
+        side = self.side if self.branch else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
             lws = self.l4_ws.buf
             chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
                                    p(o.d("cnt")), C, st.n_bound, p(i.d("past")), p(i.d("bbox")),
@@ -189,7 +195,7 @@ class MinkowskiStepGraph:
             st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
             self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")), p(o.d("pl")),
             s), "ccmpc_minkowski_cycle")
-        main.wait_stream(self.side)
+        main.wait_stream(side)
         chk(lib.ccmpc_copy_async(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
 
     def capture(self):
@@ -208,25 +214,29 @@ class MinkowskiStepGraph:
     # ---------------------------------------------------------------------------------------
     def set_inputs(self, seed, init_state, latent_pmf, gmm, minpos, ref_traj, cell_risk,
                    past_last, bbox, filter_pmf=0.1):
-        """Write one step's host inputs into the pinned input pack (no device work).  The kept
-        modes implied by latent_pmf must match the graph's K."""
-        i, O, L = self.inp, self.O, self.L
-        pmf = np.asarray(latent_pmf, np.float64).reshape(O, L)
-        kept = pmf > filter_pmf
-        if not np.array_equal(kept.sum(1), self.K):
-            raise ValueError(f"kept modes per OV {kept.sum(1).tolist()}; this graph was built "
-                             f"for {self.K}")
-        keep = np.where(kept, np.cumsum(kept, axis=1) - 1, -1).astype(np.int32)
-        i.h("seed")[0] = np.int64(np.uint64(int(seed) & (2**64 - 1)).view(np.int64))
-        i.h("init")[:] = np.asarray(init_state, np.float64).reshape(O, 4)
-        i.h("cdf")[:] = np.cumsum(pmf, axis=1)
-        i.h("gmm")[:] = np.asarray(gmm, np.float32).reshape(O, L, self.T, 5)
-        i.h("keep")[:] = keep
-        if not self._static_set:       # shape-fixed fields: written once
+        """Write one step's host inputs into the pinned input pack (no device work; every field
+        written in place, no temporaries).  The kept modes implied by latent_pmf must match the
+        graph's K.  past_last / bbox: per cell (C, 2) or per OV (O, 2)."""
+        i, O, L, C = self.inp, self.O, self.L, self.C
+        if not self._static_set:       # shape-fixed fields and helpers: once
             i.h("nk")[:] = self.K
             i.h("base")[:] = np.concatenate([[0], np.cumsum(self.K)[:-1]])
             i.h("region")[:] = self.region
+            self._K_arr = np.asarray(self.K)
+            self._ov_of_cell = np.repeat(np.arange(O), self.K)
             self._static_set = True
+        pmf = np.asarray(latent_pmf, np.float64).reshape(O, L)
+        kept = pmf > filter_pmf
+        kc = np.cumsum(kept, axis=1)
+        if not np.array_equal(kc[:, -1], self._K_arr):
+            raise ValueError(f"kept modes per OV {kc[:, -1].tolist()}; this graph was built "
+                             f"for {self.K}")
+        np.subtract(kc, 1, out=i.h("keep"), casting="unsafe")
+        i.h("keep")[~kept] = -1
+        i.h("seed")[0] = np.int64(np.uint64(int(seed) & (2**64 - 1)).view(np.int64))
+        i.h("init").reshape(-1)[:] = np.asarray(init_state, np.float64).reshape(-1)
+        np.cumsum(pmf, axis=1, out=i.h("cdf"))
+        np.copyto(i.h("gmm").reshape(-1), np.asarray(gmm).reshape(-1), casting="same_kind")
         mp = np.asarray(minpos, np.float64)
         if mp.size == 2:
             i.h("minpos")[:] = mp.reshape(1, 2)
@@ -234,11 +244,15 @@ class MinkowskiStepGraph:
         else:
             mp = mp.reshape(O, 2)
             i.h("minpos")[:] = mp
-            i.h("origin")[:] = np.repeat(mp, self.K, axis=0)
-        i.h("ref")[:] = np.asarray(ref_traj, np.float64)[:self.T].reshape(1, self.T, 2)
-        i.h("risk")[:] = np.asarray(cell_risk, np.float64).reshape(self.C, 3)
-        i.h("past")[:] = np.asarray(past_last, np.float64).reshape(self.C, 2)
-        i.h("bbox")[:] = np.asarray(bbox, np.float64).reshape(self.C, 2)
+            np.take(mp, self._ov_of_cell, axis=0, out=i.h("origin"))
+        i.h("ref").reshape(-1)[:] = np.asarray(ref_traj, np.float64)[:self.T].reshape(-1)
+        i.h("risk").reshape(-1)[:] = np.asarray(cell_risk, np.float64).reshape(3 * C)
+        for name, v in (("past", past_last), ("bbox", bbox)):
+            v = np.asarray(v, np.float64)
+            if v.size == 2 * C:
+                i.h(name).reshape(-1)[:] = v.reshape(-1)
+            else:
+                np.take(v.reshape(O, 2), self._ov_of_cell, axis=0, out=i.h(name))
 
     def bind(self):
         """Pre-convert every argument of the step's C-ABI calls for the current stream (the

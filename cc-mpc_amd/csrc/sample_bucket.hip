@@ -1,30 +1,34 @@
-// Fused sampler + bucketing for small clouds (N <= 8192 particles per OV): the drop-in step's
+// Sampler + bucketing for small clouds (N <= 8192 particles per OV): the drop-in step's
 // do_prediction -> make_ovehicles (prediction.py:81-86, v8ideal/__init__.py:469-505,
-// ovehicle.py:24-117) in ONE launch instead of the sampler and bucket.hip's three kernels.
+// ovehicle.py:24-117) in three short launches instead of the sampler and bucket.hip's three.
 //
-// What made the four-launch form slow was not work but dependent memory round trips: each of
+// What makes the four-launch form slow is not work but dependent memory round trips: each of
 // bucket.hip's kernels re-reads the particles, exchanges partials through memory and ends, and
-// the next starts cold (measured, tools/probe_step.py: ~10 us per kernel, 35 us for the three).
-// Here the bucketing rides on the sampler's blocks (64 particles, 512 threads each):
+// the next starts cold (tools/probe_step.py: ~10 us per kernel).  Here:
 //
-//   counts   every block redraws the latent ids of its whole OV (one Philox + CDF search per
-//            particle; or reads the injected z) and counts them per category -- kept mode k or
-//            "rare" -- before its own first particle and in total.  No exchange is needed to know
-//            where a kept mode's own particles go: cell k of the OV starts at
-//                region + sum_{j < k} round4(n_j + R)       (R = the OV's rare count)
-//            so it can take its n_j natives AND, in the worst case, every rare particle; its
-//            natives go to  start_k + (natives of k before this block) + (rank in the block).
-//   sample   the sampler's two phases (actions in parallel, then the Unicycle chain on one wave);
-//            the chain writes a native particle's 2T coordinates straight into its cell, and a
-//            rare particle's into a rare list in sample order (write-through), with its final
-//            position and latent id.
-//   centres  per block (= one 64-particle centre group, bucket.hpp), the kept-mode sums of the
-//            final world positions, published write-through.
-//   rares    the OV's last arriving block: centres in the canonical order (bucket.hpp, so they
-//            equal bucket.hip's bit for bit), the owner of every rare particle, a stable counting
-//            sort of the rare list by (owner, latent) in sample order, and the copy of each rare
-//            particle's coordinates into its owner's cell after the natives; cell offsets,
-//            counts, pmf and centres.
+//  P0 latents  one latent id per particle (Philox + CDF count, or the injected z) and each
+//              64-particle group's count per category -- kept mode k or "rare".
+//  P1 place    per block of 64 particles (512 threads): the category counts of the groups before
+//              its own and in total (a few KB of reads summed in LDS; an earlier form redrew every
+//              latent of the OV in every block: 13-20 us of Philox).  No exchange is needed to
+//              know where a kept mode's own particles go: cell k of the OV starts at
+//                  region + sum_{j < k} round4(n_j + R)       (R = the OV's rare count)
+//              so it can take its n_j natives AND, in the worst case, every rare particle; its
+//              natives go to  start_k + (natives of k before this block) + (rank in the block).
+//              Then the sampler's two phases (actions in parallel, then the Unicycle chain on
+//              one wave); the chain writes a native particle's 2T coordinates straight into its
+//              cell, and a rare particle's into a rare list in sample order, with its final
+//              position and latent id; and the block's kept-mode sums of the final world
+//              positions (= one 64-particle centre group, bucket.hpp).
+//  P2 rares    per block of 256 rare-list slots: the centres in the canonical order (bucket.hpp,
+//              so they equal bucket.hip's bit for bit), the key (owner, latent) of EVERY rare
+//              particle of the OV -- a few KB of L2 reads -- counted per bin in LDS in total and
+//              before the block's first slot, so the block knows each bin's start and its own
+//              particles' stable ranks in sample order without any exchange; then the copy of
+//              its rare particles' coordinates into the owners' cells after the natives.  Block
+//              0 writes cell offsets, counts, pmf and centres.
+// (A single launch whose last arriving block ranked and copied every rare particle of the OV
+// was measured at 120 us: that tail is one CU's serial work.)
 //
 // Each cell holds exactly what bucket.hip's does, in the same order (natives in sample order,
 // then the rare latents ascending, each in sample order), so every later kernel -- whose work
@@ -37,16 +41,20 @@ namespace ccmpc {
 
 constexpr int kFusedMaxN = 8192;
 constexpr int kFusedMaxBins = 512;
-constexpr int kFP = 64;                       // particles per block (the chain wave)
+constexpr int kFP = 64;                       // particles per P1 block (the chain wave)
 constexpr int kFThreads = 512;                // 8 waves
 constexpr int kFWaves = kFThreads / 64;
-constexpr int kFGroups = kFusedMaxN / kFP;    // centre groups (blocks) per OV at most
+constexpr int kFGroups = kFusedMaxN / kFP;    // centre groups (P1 blocks) per OV at most
+constexpr int kRThreads = 256;                // P2: rare-list slots per block
+constexpr int kRWaves = kRThreads / 64;
+constexpr int kHdrInts = 64;
+constexpr int kCntStride = 32;                // >= kMaxKept + 1                  // per-OV header: tot[kMaxKept + 1], cstart[kMaxKept]
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
-__device__ unsigned long long g_fused_ts[kStepProbeWG * kStepProbeSlots];
+__device__ unsigned long long g_fused_ts[3][kStepProbeWG * kStepProbeSlots];
+#define FUSED_TS(kern, k) CCMPC_STEP_TS(g_fused_ts[kern], k)
+#else
+#define FUSED_TS(kern, k) CCMPC_STEP_TS(nullptr, k)
 #endif
-#define FUSED_TS(k) CCMPC_STEP_TS(g_fused_ts, k)
-
-constexpr int kFPrefetch = 32;                // rare-copy elements per thread loaded up front
 
 struct FusedArgs {
   // sampler (sampler.hip)
@@ -64,8 +72,10 @@ struct FusedArgs {
   int max_k;
   const double *minpos;
   const int64_t *region;
-  // workspace
-  int32_t *ctr;    // [n_ov] arrival counters (zero between calls)
+  // workspace (written by P1, read by P2; the kernel boundary orders them)
+  int32_t *zbuf;   // [n_ov][Npad]: latent ids (P0)
+  int32_t *gcnt;   // [n_ov][G][kCntStride]: per 64-particle group category counts (P0)
+  int32_t *hdr;    // [n_ov][kHdrInts]: category totals [K + 1], then cell starts (int64) [K]
   double *gpart;   // [n_ov][G][max_k][2]
   float *rinfo;    // [n_ov][Npad][4]: rare particle's final (x, y), latent id (bits), 0
   float *rstore;   // [n_ov][2T][Npad]: rare particles' coordinates, rare-list order
@@ -79,32 +89,58 @@ struct FusedArgs {
   double *cell_pmf, *init_center;
 };
 
-union FusedSmem {
-  struct {
-    float act[2][40][kFP];
-    float gmm[64 * 40 * 5 / 4];
-  } s;                                  // sampling
-  double2 gp[kFGroups * kMaxKept];      // last arriver: the centre groups' partials
-  struct {
-    int32_t rk[kFusedMaxN];             // rare r: its key, then key << 16 | rank in its bin
-    int32_t run[kFusedMaxBins];         // rare particles of each bin in earlier rounds
-    int32_t wcnt[kFWaves][kFusedMaxBins];
-    int32_t bstart[kFusedMaxBins];      // bin start relative to the region
-  } r;                                  // rare ranking
-};
+__device__ __forceinline__ int64_t *hdr_starts(int32_t *h) {
+  return reinterpret_cast<int64_t *>(h + 2 * kMaxKept);
+}
 
-template <bool PP, bool ZIN, bool EPSIN>
-__global__ __launch_bounds__(kFThreads) void sample_bucket_kernel(FusedArgs a) {
-  __shared__ FusedSmem sm;
+// P0: one latent id per particle (Philox inverse CDF, or the injected z) into the workspace, and
+// each 64-particle group's count per category (kept mode k, or K = rare) -- one wave = one group.
+template <bool ZIN>
+__global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
   __shared__ double cdf_s[64];
   __shared__ int keep_s[64];
+  FUSED_TS(0, 0);
+  const int o = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int K = a.n_kept[o], L = a.L;
+  const int64_t N = a.N;
+  if (!ZIN && tid < L) cdf_s[tid] = a.latent_cdf[static_cast<int64_t>(o) * L + tid];
+  if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kFThreads + tid;
+  const bool v = i < N;
+  int z = 0;
+  if (ZIN && v) {
+    z = a.z_in[static_cast<int64_t>(o) * N + i];
+    z = z < 0 ? 0 : (z >= L ? L - 1 : z);  // memory safety; the host validates
+  }
+  __syncthreads();
+  if (!ZIN && v)
+    z = draw_latent(i, a.ov_base + static_cast<uint32_t>(o), a.seed_dev ? *a.seed_dev : a.seed,
+                    cdf_s, L);
+  if (v) {
+    a.zbuf[static_cast<int64_t>(o) * a.Npad + i] = z;
+    if (a.out_z) a.out_z[static_cast<int64_t>(o) * N + i] = z;
+  }
+  const int kk = keep_s[z];
+  const int cat = kk >= 0 ? kk : K;
+  const int g = blockIdx.x * kFWaves + w;
+  int mine = 0;
+  for (int c = 0; c <= K; ++c) {
+    const int n = __popcll(__ballot(v && cat == c));
+    if (lane == c) mine = n;
+  }
+  if (g < a.G && lane <= K) a.gcnt[(static_cast<int64_t>(o) * a.G + g) * kCntStride + lane] = mine;
+  FUSED_TS(0, 1);
+}
+
+template <bool PP, bool EPSIN>
+__global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
+  __shared__ float act[2][40][kFP];
+  __shared__ float gmm_s[64 * 40 * 5 / 4];
+  __shared__ int keep_s[64];
   __shared__ int zs[kFP];
-  __shared__ int wc[kFWaves][2][kMaxKept + 1];
   __shared__ int before_s[kMaxKept + 1], total_s[kMaxKept + 1];
   __shared__ int64_t cstart_s[kMaxKept];
-  __shared__ double cen_s[kMaxKept][2];
-  __shared__ int flag;
-  FUSED_TS(0);
+  FUSED_TS(1, 0);
   const int o = blockIdx.y, blk = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int K = a.n_kept[o], L = a.L, T = a.T;
@@ -113,53 +149,34 @@ __global__ __launch_bounds__(kFThreads) void sample_bucket_kernel(FusedArgs a) {
   const uint32_t key = a.ov_base + static_cast<uint32_t>(o);
   const int64_t i0 = static_cast<int64_t>(blk) * kFP;
   const double mx = a.minpos[2 * o], my = a.minpos[2 * o + 1];
-  if (!ZIN && tid < L) cdf_s[tid] = a.latent_cdf[static_cast<int64_t>(o) * L + tid];
+  // every load issued together: own latent ids, the groups' category counts, the tables
+  if (tid < kFP && i0 + tid < N) zs[tid] = a.zbuf[static_cast<int64_t>(o) * a.Npad + i0 + tid];
+  const int nu = a.G * (K + 1);
+  constexpr int kU = kFGroups * (kMaxKept + 1) / kFThreads + 1;
+  int cv[kU];
+#pragma unroll
+  for (int j = 0; j < kU; ++j) {
+    const int u = tid + j * kFThreads;
+    cv[j] = u < nu ? a.gcnt[(static_cast<int64_t>(o) * a.G + u / (K + 1)) * kCntStride +
+                            u % (K + 1)]
+                   : 0;
+  }
   if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
   const int gsz = L * T * 5;
-  const bool staged = !PP && gsz <= static_cast<int>(sizeof(sm.s.gmm) / sizeof(float));
+  const bool staged = !PP && gsz <= static_cast<int>(sizeof(gmm_s) / sizeof(float));
   if (staged)
-    for (int e = tid; e < gsz; e += kFThreads) sm.s.gmm[e] = a.gmm[static_cast<int64_t>(o) * gsz + e];
+    for (int e = tid; e < gsz; e += kFThreads) gmm_s[e] = a.gmm[static_cast<int64_t>(o) * gsz + e];
+  if (tid <= K) before_s[tid] = total_s[tid] = 0;
   __syncthreads();
-
-  // ---- counts: the OV's latent ids, per category, before this block and in total ------------
-  if (tid < kFWaves * 2 * (kMaxKept + 1)) (&wc[0][0][0])[tid] = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < N; base += kFThreads) {
-    const int64_t i = base + tid;
-    const bool v = i < N;
-    int z = 0;
-    if (v) {
-      if (ZIN) {
-        z = a.z_in[static_cast<int64_t>(o) * N + i];
-        z = z < 0 ? 0 : (z >= L ? L - 1 : z);  // memory safety; the host validates
-      } else {
-        z = draw_latent(i, key, seed, cdf_s, L);
-      }
-      if (i >= i0 && i < i0 + kFP) {
-        zs[i - i0] = z;
-        if (a.out_z) a.out_z[static_cast<int64_t>(o) * N + i] = z;
-      }
+  // category counts before this block's group and in total (integer-exact in any order)
+#pragma unroll
+  for (int j = 0; j < kU; ++j) {
+    const int u = tid + j * kFThreads;
+    if (u < nu && cv[j] != 0) {
+      const int c = u % (K + 1);
+      atomicAdd(&total_s[c], cv[j]);
+      if (u / (K + 1) < blk) atomicAdd(&before_s[c], cv[j]);
     }
-    const int kk = keep_s[z];
-    const int cat = kk >= 0 ? kk : K;
-    for (int c = 0; c <= K; ++c) {  // wave counts by ballot, kept in this wave's LDS row
-      const int nt = __popcll(__ballot(v && cat == c));
-      const int nb = __popcll(__ballot(v && cat == c && i < i0));
-      if (lane == 0) {
-        wc[w][0][c] += nb;
-        wc[w][1][c] += nt;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid <= K) {
-    int b = 0, t = 0;
-    for (int u = 0; u < kFWaves; ++u) {
-      b += wc[u][0][tid];
-      t += wc[u][1][tid];
-    }
-    before_s[tid] = b;
-    total_s[tid] = t;
   }
   __syncthreads();
   if (tid == 0) {
@@ -170,211 +187,200 @@ __global__ __launch_bounds__(kFThreads) void sample_bucket_kernel(FusedArgs a) {
       cur += (static_cast<int64_t>(total_s[k]) + R + 3) & ~int64_t(3);
     }
   }
+  FUSED_TS(1, 1);
 
-  FUSED_TS(1);
   // ---- actions (all waves), then the chain (wave 0) ------------------------------------------
   const int64_t ip = i0 + lane;
   const bool valid = ip < N;
   if (valid)
     for (int t = w; t < T; t += kFWaves)
-      draw_action<PP, EPSIN>(t, ip, zs[lane], o, T, L, N, key, seed, a.gmm, sm.s.gmm, staged,
-                             a.eps_in, sm.s.act[0][t][lane], sm.s.act[1][t][lane]);
+      draw_action<PP, EPSIN>(t, ip, zs[lane], o, T, L, N, key, seed, a.gmm, gmm_s, staged,
+                             a.eps_in, act[0][t][lane], act[1][t][lane]);
   __syncthreads();
-  const __amdgpu_buffer_rsrc_t rrs = raw_rsrc(a.rstore + static_cast<int64_t>(o) * 2 * T * a.Npad);
-  const __amdgpu_buffer_rsrc_t rri = raw_rsrc(a.rinfo + static_cast<int64_t>(o) * a.Npad * 4);
-  const __amdgpu_buffer_rsrc_t rg =
-      slab_rsrc(a.gpart + static_cast<int64_t>(o) * a.G * a.max_k * 2);
+  if (blk == 0 && tid <= K) {  // the OV's header for P2 (every block computed the same values)
+    int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
+    h[tid] = total_s[tid];
+    if (tid < K) hdr_starts(h)[tid] = cstart_s[tid];
+  }
+  if (w != 0) return;
   const int npad = static_cast<int>(a.Npad);
-  if (w == 0) {
-    const int z = valid ? zs[lane] : 0;
-    const int kk = keep_s[z];
-    const int cat = kk >= 0 ? kk : K;
-    const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    int rank = 0;
-    for (int c = 0; c <= K; ++c) {
-      const unsigned long long m = __ballot(valid && cat == c);
-      if (cat == c) rank = __popcll(m & below);
+  float *rst = a.rstore + static_cast<int64_t>(o) * 2 * T * a.Npad;
+  const int z = valid ? zs[lane] : 0;
+  const int kk = keep_s[z];
+  const int cat = kk >= 0 ? kk : K;
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int rank = 0;
+  for (int c = 0; c <= K; ++c) {
+    const unsigned long long m = __ballot(valid && cat == c);
+    if (cat == c) rank = __popcll(m & below);
+  }
+  const bool native = kk >= 0;
+  const int64_t dst = native ? cstart_s[kk] + before_s[kk] + rank : 0;
+  const int rs = native ? 0 : before_s[K] + rank;  // slot in the rare list
+  float x = 0.0f, y = 0.0f;
+  if (valid) {
+    const double *st = a.init_state + 4 * o;
+    x = static_cast<float>(st[0]);
+    y = static_cast<float>(st[1]);
+    float phi = static_cast<float>(st[2]), v = static_cast<float>(st[3]);
+    float s0, c0;
+    sincos_rn(phi, s0, c0);
+    float *op = native ? a.out + dst : rst + rs;
+    const int64_t ld = native ? a.ld_out : a.Npad;
+    for (int t = 0; t < T; ++t) {
+      unicycle_step(x, y, phi, v, s0, c0, act[0][t][lane], act[1][t][lane], a.dt);
+      op[(2 * t) * ld] = x;
+      op[(2 * t + 1) * ld] = y;
     }
-    const bool native = kk >= 0;
-    const int64_t dst = native ? cstart_s[kk] + before_s[kk] + rank : 0;
-    const int rs = native ? 0 : before_s[K] + rank;  // slot in the rare list
-    float x = 0.0f, y = 0.0f;
-    if (valid) {
-      const double *st = a.init_state + 4 * o;
-      x = static_cast<float>(st[0]);
-      y = static_cast<float>(st[1]);
-      float phi = static_cast<float>(st[2]), v = static_cast<float>(st[3]);
-      float s0, c0;
-      sincos_rn(phi, s0, c0);
-      float *op = a.out + dst;
-      for (int t = 0; t < T; ++t) {
-        unicycle_step(x, y, phi, v, s0, c0, sm.s.act[0][t][lane], sm.s.act[1][t][lane], a.dt);
-        if (native) {
-          op[(2 * t) * a.ld_out] = x;
-          op[(2 * t + 1) * a.ld_out] = y;
-        } else {
-          stf_sc1(rrs, 4 * ((2 * t) * npad + rs), x);
-          stf_sc1(rrs, 4 * ((2 * t + 1) * npad + rs), y);
-        }
-      }
-      if (!native) {
-        const float4 info = {x, y, __builtin_bit_cast(float, z), 0.0f};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128_t, info), rri, 16 * rs, 0,
-                                               16);
-      }
-    }
-    // this block is centre group blk: its kept-mode sums of the final world positions
-    const double xw = static_cast<double>(x) + mx, yw = static_cast<double>(y) + my;
-    for (int k = 0; k < K; ++k) {
-      const bool mine = valid && cat == k;
-      const double sx = group_sum64(mine ? xw : 0.0), sy = group_sum64(mine ? yw : 0.0);
-      if (lane == 0) st2_sc1(rg, 16 * (blk * a.max_k + k), sx, sy);
+    if (!native) {
+      const float4 info = {x, y, __builtin_bit_cast(float, z), 0.0f};
+      reinterpret_cast<float4 *>(a.rinfo)[static_cast<int64_t>(o) * npad + rs] = info;
     }
   }
-  FUSED_TS(2);
-  if (!arrive_last(a.ctr + o, a.G, &flag)) return;
-  FUSED_TS(3);
+  // this block is centre group blk: its kept-mode sums of the final world positions
+  const double xw = static_cast<double>(x) + mx, yw = static_cast<double>(y) + my;
+  double2 *gp = reinterpret_cast<double2 *>(a.gpart) + (static_cast<int64_t>(o) * a.G + blk) * a.max_k;
+  for (int k = 0; k < K; ++k) {
+    const bool mine = valid && cat == k;
+    const double sx = group_sum64(mine ? xw : 0.0), sy = group_sum64(mine ? yw : 0.0);
+    if (lane == 0) gp[k] = double2{sx, sy};
+  }
+  FUSED_TS(1, 2);
+}
 
-  // ---- the OV's last arriver: centres, then the rare particles --------------------------------
-  const int R = total_s[K];
-  const int rows = 2 * T;
-  const int E = R * rows;
-  // every load the rest needs is issued here: the centre partials, and the first kFPrefetch
-  // copy elements of this thread (element e = row * R + r, e = tid + 512 j)
+__global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
+  __shared__ double2 gp_s[kFGroups * kMaxKept];   // the OV's centre partials [g][k]
+  __shared__ int hist[kFusedMaxBins];             // rare particles per bin, all of the OV
+  __shared__ int pre[kFusedMaxBins];              // ... in rare-list slots before this block's
+  __shared__ int bstart[kFusedMaxBins];           // bin start relative to the region
+  __shared__ int wcnt[kRWaves][kFusedMaxBins];
+  __shared__ int okey[kRThreads];
+  __shared__ int keep_s[64], tot_s[kMaxKept + 1];
+  __shared__ int64_t cst_s[kMaxKept];
+  __shared__ double cen_s[kMaxKept][2];
+  FUSED_TS(2, 0);
+  const int o = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int K = a.n_kept[o], L = a.L, T = a.T, rows = 2 * T;
+  const int r0 = blockIdx.x * kRThreads;
+  const int npad = static_cast<int>(a.Npad);
+  // every load that needs nothing from another is issued at once: the header, the tables, this
+  // thread's rare-slot coordinates (slot clamped into the list's storage, used only if < R) and
+  // the centre partials
+  const int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
+  if (tid <= K) tot_s[tid] = h[tid];
+  if (tid < K) cst_s[tid] = hdr_starts(const_cast<int32_t *>(h))[tid];
+  if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
+  const int r = r0 + tid;
+  const float *src = a.rstore + static_cast<int64_t>(o) * 2 * T * a.Npad + (r < npad ? r : npad - 1);
+  float v[80];
+#pragma unroll
+  for (int rr = 0; rr < 80; ++rr)
+    if (rr < rows) v[rr] = src[static_cast<int64_t>(rr) * npad];
   const int ng = a.G * K;
-  double2 gpv[kFGroups * kMaxKept / kFThreads];
-#pragma unroll
-  for (int q = 0; q < kFGroups * kMaxKept / kFThreads; ++q) {
-    const int u = tid + q * kFThreads;  // u = g K + k
-    if (u < ng) gpv[q] = ld2_sc1(rg, 16 * ((u / K) * a.max_k + u % K));
-  }
-  const int dr = R > 0 ? kFThreads % R : 0, drow = R > 0 ? kFThreads / R : 0;
-  int row0 = R > 0 ? tid / R : rows, r0 = R > 0 ? tid % R : 0;
-  float v[kFPrefetch];
-  {
-    int row = row0, r = r0;
-#pragma unroll
-    for (int j = 0; j < kFPrefetch; ++j) {
-      v[j] = row < rows ? ldf_sc1(rrs, 4 * (row * npad + r)) : 0.0f;
-      r += dr;
-      row += drow;
-      if (r >= R) {
-        r -= R;
-        ++row;
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < kFGroups * kMaxKept / kFThreads; ++q) {
-    const int u = tid + q * kFThreads;
-    if (u < ng) sm.gp[u] = gpv[q];
-  }
+  const double2 *gp = reinterpret_cast<const double2 *>(a.gpart) + static_cast<int64_t>(o) * a.G * a.max_k;
+  for (int u = tid; u < ng; u += kRThreads) gp_s[u] = gp[(u / K) * a.max_k + u % K];
+  const int nbins = K * (L + 1);
+  for (int b = tid; b < nbins; b += kRThreads) hist[b] = pre[b] = 0;
   __syncthreads();
-  // centres, canonical order (bucket.hpp): superblocks (at most 2 here), then left to right
+  FUSED_TS(2, 1);
+  const int R = tot_s[K];
+  if (r0 >= R && blockIdx.x != 0) return;  // uniform: no rare slots here (block 0 writes cells)
+  const bool own = r < R;
+  const int64_t reg = a.region[o];
+  const double mx = a.minpos[2 * o], my = a.minpos[2 * o + 1];
+  // the first batch of rare records in flight while the centres are summed
+  const float4 *info = reinterpret_cast<const float4 *>(a.rinfo) + static_cast<int64_t>(o) * npad;
+  constexpr int kB = 8;
+  float4 f[kB];
+  auto load_batch = [&](int q0) {
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const int q = q0 + j * kRThreads + tid;
+      f[j] = info[q < R ? q : (R > 0 ? R - 1 : 0)];
+    }
+  };
+  load_batch(0);
+  // centres, canonical order (bucket.hpp): superblocks, then left to right
   if (tid < K) {
     const int k = tid;
     double2 tot = {0.0, 0.0};
     for (int j = 0; j * kCentreSuper < a.G; ++j) {
-      const double2 s = superblock_sum(j, a.G, [&](int g) { return sm.gp[g * K + k]; });
+      const double2 s = superblock_sum(j, a.G, [&](int g) { return gp_s[g * K + k]; });
       tot.x += s.x;
       tot.y += s.y;
     }
-    const double nk = static_cast<double>(total_s[k]);
+    const double nk = static_cast<double>(tot_s[k]);
     cen_s[k][0] = tot.x / nk;
     cen_s[k][1] = tot.y / nk;
   }
-  __syncthreads();  // sm.gp is dead from here
-  FUSED_TS(4);
-  // keys of the rare list: owner (L + 1) + 1 + z
-  const int nbins = K * (L + 1);
-  for (int r = tid; r < R; r += kFThreads) {
-    const float4 info = __builtin_bit_cast(
-        float4, __builtin_amdgcn_raw_buffer_load_b128(rri, 16 * r, 0, 16));
-    const int z = __builtin_bit_cast(int, info.z);
-    sm.r.rk[r] = key_staged(z, static_cast<double>(info.x) + mx,
-                            static_cast<double>(info.y) + my, keep_s, cen_s, K, L);
-  }
-  for (int b = tid; b < nbins; b += kFThreads) sm.r.run[b] = 0;
-  // stable ranks in sample order: rounds of 512 rare particles, waves in order
-  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (int base = 0; base < R; base += kFThreads) {
-    for (int b = tid; b < kFWaves * nbins; b += kFThreads) sm.r.wcnt[b / nbins][b % nbins] = 0;
-    __syncthreads();
-    const int r = base + tid;
-    const bool ok = r < R;
-    const int kr = ok ? sm.r.rk[r] : -1;
-    int rank = 0;
-    unsigned long long todo = __ballot(ok);
-    while (todo) {
-      const int leader = __ffsll(static_cast<long long>(todo)) - 1;
-      const int kl = __shfl(kr, leader, 64);
-      const unsigned long long m = __ballot(ok && kr == kl);
-      if (ok && kr == kl) rank = __popcll(m & below);
-      if (lane == leader) sm.r.wcnt[w][kl] = __popcll(m);
-      todo &= ~m;
-    }
-    __syncthreads();
-    if (ok) {
-      int before = sm.r.run[kr];
-      for (int u = 0; u < w; ++u) before += sm.r.wcnt[u][kr];
-      sm.r.rk[r] = (kr << 16) | (before + rank);
-    }
-    __syncthreads();
-    for (int b = tid; b < nbins; b += kFThreads) {
-      int s = sm.r.run[b];
-      for (int u = 0; u < kFWaves; ++u) s += sm.r.wcnt[u][b];
-      sm.r.run[b] = s;
-    }
-    __syncthreads();  // before the next round clears wcnt
-  }
-  FUSED_TS(5);
-  // bins of kept mode k start after its natives; the cells' outputs
-  if (tid < K) {
-    const int k = tid;
-    const int64_t reg = a.region[o];
-    int s = static_cast<int>(cstart_s[k] - reg) + total_s[k];
-    for (int z = 0; z < L; ++z) {
-      const int b = k * (L + 1) + 1 + z;
-      sm.r.bstart[b] = s;
-      s += sm.r.run[b];
-    }
-    const int64_t n = s - (cstart_s[k] - reg);
-    const int cell = a.cell_base[o] + k;
-    a.cell_off[cell] = cstart_s[k];
-    a.cell_cnt[cell] = n;
-    a.cell_pmf[cell] = static_cast<double>(n) / static_cast<double>(N);
-    a.init_center[2 * cell] = cen_s[k][0];
-    a.init_center[2 * cell + 1] = cen_s[k][1];
-  }
   __syncthreads();
-  // the copy: element (row, r) -> row `row` of the owner's cell, slot bstart + rank
-  float *out = a.out + a.region[o];
-  auto dst_of = [&](int r) {
-    const int p = sm.r.rk[r];
-    return static_cast<int64_t>(sm.r.bstart[p >> 16] + (p & 0xffff));
-  };
-  {
-    int row = row0, r = r0;
+  FUSED_TS(2, 2);
+  // every rare particle's key (owner (L + 1) + 1 + z), counted per bin: in total, and before
+  // this block's first slot; this block's own keys kept
+  for (int q0 = 0; q0 < R; q0 += kB * kRThreads) {
+    if (q0 > 0) load_batch(q0);
 #pragma unroll
-    for (int j = 0; j < kFPrefetch; ++j) {
-      if (row < rows) out[row * a.ld_out + dst_of(r)] = v[j];
-      r += dr;
-      row += drow;
-      if (r >= R) {
-        r -= R;
-        ++row;
+    for (int j = 0; j < kB; ++j) {
+      const int q = q0 + j * kRThreads + tid;
+      if (q < R) {
+        const int kq = key_staged(__builtin_bit_cast(int, f[j].z), static_cast<double>(f[j].x) + mx,
+                                  static_cast<double>(f[j].y) + my, keep_s, cen_s, K, L);
+        atomicAdd(&hist[kq], 1);
+        if (q < r0) atomicAdd(&pre[kq], 1);
+        if (q >= r0 && q < r0 + kRThreads) okey[q - r0] = kq;
       }
     }
   }
-  for (int e = tid + kFPrefetch * kFThreads; e < E; e += kFThreads) {  // beyond the prefetch
-    const int row = e / R, r = e % R;
-    out[row * a.ld_out + dst_of(r)] = ldf_sc1(rrs, 4 * (row * npad + r));
+  for (int b = tid; b < kRWaves * nbins; b += kRThreads) wcnt[b / nbins][b % nbins] = 0;
+  __syncthreads();
+  FUSED_TS(2, 3);
+  // bins of kept mode k start after its natives, latents ascending (one thread per bin, its
+  // prefix summed over independent LDS reads); block 0: the cells' outputs
+  for (int b = tid; b < nbins; b += kRThreads) {
+    const int k = b / (L + 1), gi = b - k * (L + 1), hb = k * (L + 1) + 1;
+    const int upto = gi == 0 ? L : gi - 1;  // gi == 0 (the natives' bin): every rare bin of k
+    int s = 0;
+#pragma unroll 8
+    for (int zz = 0; zz < upto; ++zz) s += hist[hb + zz];
+    if (gi > 0) {
+      bstart[b] = static_cast<int>(cst_s[k] - reg) + tot_s[k] + s;
+    } else if (blockIdx.x == 0) {
+      const int64_t n = tot_s[k] + s;
+      const int cell = a.cell_base[o] + k;
+      a.cell_off[cell] = cst_s[k];
+      a.cell_cnt[cell] = n;
+      a.cell_pmf[cell] = static_cast<double>(n) / static_cast<double>(a.N);
+      a.init_center[2 * cell] = cen_s[k][0];
+      a.init_center[2 * cell + 1] = cen_s[k][1];
+    }
   }
-  FUSED_TS(6);
+  // this block's stable ranks: lanes in order within a wave, waves in order
+  const int kr = own ? okey[tid] : -1;
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int rank = 0;
+  unsigned long long todo = __ballot(own);
+  while (todo) {
+    const int leader = __ffsll(static_cast<long long>(todo)) - 1;
+    const int kl = __shfl(kr, leader, 64);
+    const unsigned long long m = __ballot(own && kr == kl);
+    if (own && kr == kl) rank = __popcll(m & below);
+    if (lane == leader) wcnt[w][kl] = __popcll(m);
+    todo &= ~m;
+  }
+  __syncthreads();
+  if (own) {
+    int before = pre[kr] + rank;
+    for (int u = 0; u < w; ++u) before += wcnt[u][kr];
+    float *out = a.out + reg + bstart[kr] + before;
+#pragma unroll
+    for (int rr = 0; rr < 80; ++rr)
+      if (rr < rows) out[static_cast<int64_t>(rr) * a.ld_out] = v[rr];
+  }
+  FUSED_TS(2, 4);
 }
 
 struct FusedWs {
-  size_t ctr, gpart, rinfo, rstore, total;
+  size_t zbuf, gcnt, hdr, gpart, rinfo, rstore, total;
 };
 
 inline size_t a256(size_t b) { return (b + 255) / 256 * 256; }
@@ -383,8 +389,12 @@ inline FusedWs fused_ws(int64_t n_ov, int64_t N, int64_t T, int64_t max_k) {
   const int64_t G = (N + kFP - 1) / kFP, Npad = (N + 3) & ~int64_t(3);
   FusedWs w;
   size_t o = 0;
-  w.ctr = o;  // arrival counters first: the zero-filled head of the workspace
-  o += a256(sizeof(int32_t) * n_ov);
+  w.zbuf = o;
+  o += a256(sizeof(int32_t) * n_ov * Npad);
+  w.gcnt = o;
+  o += a256(sizeof(int32_t) * n_ov * G * kCntStride);
+  w.hdr = o;
+  o += a256(sizeof(int32_t) * kHdrInts * n_ov);
   w.gpart = o;
   o += a256(sizeof(double) * 2 * n_ov * G * max_k);
   w.rinfo = o;
@@ -400,15 +410,18 @@ inline FusedWs fused_ws(int64_t n_ov, int64_t N, int64_t T, int64_t max_k) {
 using namespace ccmpc;
 
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
-// slots: 0 start, 1 counted, 2 sampled + published, 3 last arriver, 4 centres, 5 ranked,
-// 6 copied (tools/probe_step.py)
-extern "C" int ccmpc_probe_fused_timestamps(void *host, int reset) {
-  const size_t bytes = sizeof(g_fused_ts);
+// which 0: P0 latents (slots 0 start, 1 done); 1: P1 place (0 start, 1 counted, 2 sampled +
+// published); 2: P2 rares (0 start, 1 loaded, 2 centres, 3 keyed, 4 copied)  (tools/probe_step.py)
+extern "C" int ccmpc_probe_fused_timestamps(void *host, int which, int reset) {
+  if (which < 0 || which > 2) return -1;
+  const size_t bytes = sizeof(g_fused_ts[0]);
   if (reset) {
     static unsigned long long zeros[kStepProbeWG * kStepProbeSlots];
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_fused_ts), zeros, bytes) == hipSuccess ? 0 : -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fused_ts), zeros, bytes, which * bytes) == hipSuccess
+               ? 0 : -1;
   }
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_ts), bytes) == hipSuccess ? 0 : -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_ts), bytes, which * bytes) == hipSuccess
+             ? 0 : -1;
 }
 #endif
 
@@ -472,7 +485,9 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
   a.max_k = static_cast<int>(max_k);
   a.minpos = minpos;
   a.region = region;
-  a.ctr = reinterpret_cast<int32_t *>(ws + L.ctr);
+  a.zbuf = reinterpret_cast<int32_t *>(ws + L.zbuf);
+  a.gcnt = reinterpret_cast<int32_t *>(ws + L.gcnt);
+  a.hdr = reinterpret_cast<int32_t *>(ws + L.hdr);
   a.gpart = reinterpret_cast<double *>(ws + L.gpart);
   a.rinfo = reinterpret_cast<float *>(ws + L.rinfo);
   a.rstore = reinterpret_cast<float *>(ws + L.rstore);
@@ -485,20 +500,27 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
   a.cell_cnt = cell_cnt;
   a.cell_pmf = cell_pmf;
   a.init_center = init_center;
-  const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
   hipStream_t s = as_stream(stream);
-  const int mode = (pp ? 4 : 0) | (z_in ? 2 : 0) | (eps_in ? 1 : 0);
-#define CCMPC_FUSED(PP, ZIN, EPSIN) \
-  hipLaunchKernelGGL((sample_bucket_kernel<PP, ZIN, EPSIN>), grid, dim3(kFThreads), 0, s, a)
+  const dim3 zgrid(static_cast<unsigned>((N + kFThreads - 1) / kFThreads),
+                   static_cast<unsigned>(n_ov));
+  if (z_in)
+    hipLaunchKernelGGL(latent_count_kernel<true>, zgrid, dim3(kFThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(latent_count_kernel<false>, zgrid, dim3(kFThreads), 0, s, a);
+  const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
+  const int mode = (pp ? 2 : 0) | (eps_in ? 1 : 0);
+#define CCMPC_FUSED(PP, EPSIN) \
+  hipLaunchKernelGGL((sample_place_kernel<PP, EPSIN>), grid, dim3(kFThreads), 0, s, a)
   switch (mode) {
-    case 0: CCMPC_FUSED(false, false, false); break;
-    case 1: CCMPC_FUSED(false, false, true); break;
-    case 2: CCMPC_FUSED(false, true, false); break;
-    case 3: CCMPC_FUSED(false, true, true); break;
-    case 6: CCMPC_FUSED(true, true, false); break;
-    default: CCMPC_FUSED(true, true, true); break;
+    case 0: CCMPC_FUSED(false, false); break;
+    case 1: CCMPC_FUSED(false, true); break;
+    case 2: CCMPC_FUSED(true, false); break;
+    default: CCMPC_FUSED(true, true); break;
   }
 #undef CCMPC_FUSED
+  const dim3 rgrid(static_cast<unsigned>((N + kRThreads - 1) / kRThreads),
+                   static_cast<unsigned>(n_ov));
+  hipLaunchKernelGGL(rare_place_kernel, rgrid, dim3(kRThreads), 0, s, a);
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

@@ -58,18 +58,17 @@ __device__ __forceinline__ void gmm2d_action(float mu0, float mu1, float ls0, fl
 }
 
 // Latent id of particle i by inverse CDF of its Philox uniform (DiscreteLatent.sample_p:
-// numpy searchsorted(cdf, u, side='right')); cdf in LDS.
+// numpy searchsorted(cdf, u, side='right'), clamped to the last latent); cdf in LDS.  The cdf is
+// a cumulative sum (non-decreasing), so the first k with cdf[k] > u is the number of entries
+// <= u: a count over independent LDS reads, not a search whose every step waits on the last
+// read (the early-exit loop was a chain of up to L dependent LDS round trips per draw).
 __device__ __forceinline__ int draw_latent(int64_t i, uint32_t key, uint64_t seed,
                                            const double *cdf, int n_latent) {
   const u32x4 w = philox4x32(static_cast<uint32_t>(i), 0u, key, STREAM_SAMPLER_Z, seed);
   const double u = uniform53(w.x, w.y);
-  int z = n_latent - 1;
-  for (int k = 0; k < n_latent; ++k) {
-    if (cdf[k] > u) {
-      z = k;
-      break;
-    }
-  }
+  int z = 0;
+#pragma unroll 8
+  for (int k = 0; k < n_latent - 1; ++k) z += cdf[k] <= u ? 1 : 0;
   return z;
 }
 

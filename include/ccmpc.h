@@ -312,7 +312,7 @@ int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T
                  double *init_center, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
- * Sampler + bucketing in ONE launch, for clouds of N <= 8192 particles per OV: the same draws
+ * Sampler + bucketing in three short launches, for clouds of N <= 8192 particles per OV: the same draws
  * as ccmpc_sample_unicycle_ex (same Philox streams, same float32 arithmetic) bucketed as
  * ccmpc_bucket buckets them -- every cell holds the same particles in the same order and the
  * same init_center / pmf bits.  Replaces prediction.py:81-86 + v8ideal/__init__.py:469-505 +
@@ -322,7 +322,7 @@ int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T
  * so region[o] needs n_kept[o] * (N + 4) free slots of pos_out.  out_z (optional, may be NULL)
  * gets the sample-order latent ids.  N > 8192: use the sampler + ccmpc_bucket.
  * Workspace: ccmpc_sample_bucket_workspace_bytes (0 = shape not supported), 256-byte aligned;
- * its head holds per-OV arrival counters: zero-fill once (every call leaves them zero).
+ * no initialisation needed (the first launch writes everything the second reads).
  * ------------------------------------------------------------------------------------- */
 size_t ccmpc_sample_bucket_workspace_bytes(int64_t n_ov, int64_t N, int64_t T, int64_t max_k);
 int ccmpc_sample_bucket(const double *init_state, const double *latent_cdf, int64_t n_latent,

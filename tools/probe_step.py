@@ -50,14 +50,15 @@ def main():
             init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=s), eps, ph, ref, minpos, pasts)
     g = next(iter(agent._graphs.values()))
     lib = engine._lib.load()
-    for name, nargs in (("ccmpc_probe_sampler_timestamps", 2), ("ccmpc_probe_fused_timestamps", 2),
+    for name, nargs in (("ccmpc_probe_sampler_timestamps", 2), ("ccmpc_probe_fused_timestamps", 3),
                         ("ccmpc_probe_bucket_timestamps", 3), ("ccmpc_probe_timestamps", 2)):
         f = getattr(lib, name)
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * (nargs - 1)
     for rep in range(a.reps):
         assert lib.ccmpc_probe_sampler_timestamps(None, 1) == 0
-        assert lib.ccmpc_probe_fused_timestamps(None, 1) == 0
+        for w in range(3):
+            assert lib.ccmpc_probe_fused_timestamps(None, w, 1) == 0
         for w in range(3):
             assert lib.ccmpc_probe_bucket_timestamps(None, w, 1) == 0
         assert lib.ccmpc_probe_timestamps(None, 1) == 0
@@ -67,8 +68,10 @@ def main():
         torch.cuda.synchronize()
         ks = [("sampler", table(lib.ccmpc_probe_sampler_timestamps, 0),
                ["staged", "z", "actions", "chain"]),
-              ("fused", table(lib.ccmpc_probe_fused_timestamps, 0),
-               ["counted", "sampled", "last", "centres", "ranked", "copied"]),
+              ("latents", table(lib.ccmpc_probe_fused_timestamps, 0, 0), ["drawn"]),
+              ("place", table(lib.ccmpc_probe_fused_timestamps, 1, 0), ["counted", "sampled"]),
+              ("rares", table(lib.ccmpc_probe_fused_timestamps, 2, 0),
+               ["loaded", "centres", "keyed", "copied"]),
               ("b.stats", table(lib.ccmpc_probe_bucket_timestamps, 0, 0),
                ["loaded", "published", "last", "done"]),
               ("b.hist", table(lib.ccmpc_probe_bucket_timestamps, 1, 0),
