@@ -406,9 +406,12 @@ __device__ __forceinline__ void mfma_group4(const Pair<P> (&raw)[NB], const doub
 }
 
 constexpr int kNW4 = 4;  // waves per Scheme4 work item
+#ifndef CCMPC_M4_OCC  // Scheme4 workgroups per CU the register budget must allow (build knob)
+#define CCMPC_M4_OCC(NB) ((NB) <= 5 ? 3 : 2)
+#endif
 
 template <typename P, int NB, bool MINK, bool BAL>
-__global__ __launch_bounds__(kNW4 * 64, NB <= 5 ? 3 : 2) void moments4_kernel(
+__global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
     const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off,
     const int32_t *__restrict__ cell_ref, int n_cells, const P *__restrict__ pos, int64_t ld,
     int T, const double *__restrict__ origin, int lg_wq, TreeLayout tree,
