@@ -3,8 +3,10 @@
 //
 // One lane per (cell, t, tau) pair for the Minkowski generator: the work per pair is scalar
 // float64 arithmetic on 2x2 matrices plus the MVOE fixed point (median ~10 iterations), so the
-// kernel is latency-bound and tiny next to the moment reduction.  One workgroup per cell keeps
-// the cell's pairs together so the per-t minimum of the lower bound is a local reduction.
+// kernel is latency-bound and tiny next to the moment reduction.  One wave per (cell, t): its
+// lanes tau < t are the row's pairs, all in flight at once (one chain deep, at any T), and the
+// per-t minimum of the lower bound is a wave reduction.  (One workgroup per cell ran T = 40's
+// 780 pairs in four rounds of chains.)
 //
 // Every step follows the reference's operation order (which matrix is formed first, the
 // strict '<' tie-break, the side test n.mean <= d) so that the integer outputs (which, side)
@@ -13,15 +15,29 @@
 
 namespace ccmpc {
 
-__global__ __launch_bounds__(256) void minkowski_kernel(const double *__restrict__ mean,
-                                                       const double *__restrict__ cov, int T,
-                                                       MinkParams mp) {
-  __shared__ double lb_s[40 * 39 / 2];
-  const int cell = blockIdx.x;
+__global__ __launch_bounds__(64) void minkowski_rows_kernel(const double *__restrict__ mean,
+                                                            const double *__restrict__ cov, int T,
+                                                            MinkParams mp) {
+  const int cell = blockIdx.x, t = blockIdx.y, tau = threadIdx.x;
   const int rows = 2 * T;
-  minkowski_cell(cov + static_cast<int64_t>(cell) * rows * rows,
-                 mean + static_cast<int64_t>(cell) * rows, T, cell, mp, lb_s, threadIdx.x,
-                 blockDim.x);
+  const int rsel = mp.cell_ref ? mp.cell_ref[cell] : 0;
+  const double *ref = mp.ref_traj + static_cast<int64_t>(rsel) * rows;
+  const double *C = cov + static_cast<int64_t>(cell) * rows * rows;
+  const double *mu = mean + static_cast<int64_t>(cell) * rows;
+  double lb = 1.0;
+  if (tau < t) {
+    const int p = t * (t - 1) / 2 + tau;
+    ccmpc_halfspace *rec = mp.out_rec + static_cast<int64_t>(cell) * (T * (T - 1) / 2) + p;
+    const double *risk = mp.cell_risk + 3 * cell;
+    lb = pair_lower_bound(pair_moments(C, rows, t, tau), risk[2]);
+    rec->lower_bound = lb;
+    minkowski_pair(C, mu, ref, rows, t, tau, risk[0], risk[1], mp.R, mp.tol, mp.maxiter, rec);
+  }
+  // prob_lower[t] = fmin over the row from 1.0 (:946; fmin ignores NaN in any order, and the
+  // lanes tau >= t hold the 1.0 start)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lb = fmin(lb, __shfl_xor(lb, o, 64));
+  if (tau == 0) mp.out_prob_lower[static_cast<int64_t>(cell) * T + t] = lb;
 }
 
 __global__ __launch_bounds__(64) void affine_kernel(
@@ -189,6 +205,13 @@ __global__ __launch_bounds__(256) void affine_scale_kernel(
   }
 }
 
+void launch_minkowski_rows(const double *mean, const double *cov, int T, int n_cells,
+                           const MinkParams &mp, hipStream_t s) {
+  hipLaunchKernelGGL(minkowski_rows_kernel,
+                     dim3(static_cast<unsigned>(n_cells), static_cast<unsigned>(T)), dim3(64), 0,
+                     s, mean, cov, T, mp);
+}
+
 }  // namespace ccmpc
 
 using namespace ccmpc;
@@ -203,11 +226,9 @@ extern "C" int ccmpc_minkowski(const double *mean, const double *cov, int64_t T,
   if (n_cells == 0) return CCMPC_OK;
   CCMPC_REQUIRE(mean && cov && ref_traj && cell_risk && out_rec && out_prob_lower, "null pointer");
   CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
-  const int P = static_cast<int>(T * (T - 1) / 2);
-  const int threads = P <= 64 ? 64 : 256;
   const MinkParams mp{ref_traj, cell_ref, cell_risk, R, tol, maxiter, out_rec, out_prob_lower};
-  hipLaunchKernelGGL(minkowski_kernel, dim3(static_cast<unsigned>(n_cells)), dim3(threads), 0,
-                     as_stream(stream), mean, cov, static_cast<int>(T), mp);
+  launch_minkowski_rows(mean, cov, static_cast<int>(T), static_cast<int>(n_cells), mp,
+                        as_stream(stream));
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

@@ -320,4 +320,8 @@ __device__ void minkowski_cell(const double *C, const double *mu, int T, int cel
                  mp.cell_risk[3 * cell + 2], mp, lb_s, tid, nthreads);
 }
 
+// The unfused half-space launch (constraints.hip): one wave per (cell, t), lanes = the row's pairs.
+void launch_minkowski_rows(const double *mean, const double *cov, int T, int n_cells,
+                           const MinkParams &mp, hipStream_t s);
+
 }  // namespace ccmpc

@@ -37,12 +37,18 @@ inline int row_blocks(int64_t T) { return static_cast<int>((2 * T + 15) / 16); }
 #ifndef CCMPC_LG_NW1  // log2 waves per work item at RB = 1 (T <= 8); build-time knob
 #define CCMPC_LG_NW1 3
 #endif
+#ifndef CCMPC_LG_NW_BIG  // log2 waves per work item at RB >= 3 (T > 24); build-time knob
+#define CCMPC_LG_NW_BIG 3
+#endif
+#ifndef CCMPC_MINW_BIG  // waves per SIMD the RB >= 3 register budget must allow; build knob
+#define CCMPC_MINW_BIG 2
+#endif
 template <int RB>
 struct Geo {
-  static constexpr int NW = RB == 1 ? (1 << CCMPC_LG_NW1) : (RB <= 2 ? 4 : 8);
+  static constexpr int NW = RB == 1 ? (1 << CCMPC_LG_NW1) : (RB <= 2 ? 4 : (1 << CCMPC_LG_NW_BIG));
   static constexpr int S = RB == 1 ? 4 : (RB == 2 ? 2 : 1);
   static constexpr int NACC = (n_tiles(RB) == 1) ? 2 : 1;  // 2 chains when there is one tile
-  static constexpr int MIN_WAVES_PER_SIMD = RB == 1 ? 4 : 2;
+  static constexpr int MIN_WAVES_PER_SIMD = RB == 1 ? 4 : (RB <= 2 ? 2 : CCMPC_MINW_BIG);
 };
 
 // log2 of the particles per wave.  Small inputs are latency-bound: 64 per wave spreads the
@@ -74,7 +80,7 @@ inline int store_lg_wave_quota(int /*rb*/, int64_t n_bound) {
 }
 
 __host__ __device__ inline int lg_waves_per_item(int rb) {
-  return rb == 1 ? CCMPC_LG_NW1 : (rb <= 2 ? 2 : 3);
+  return rb == 1 ? CCMPC_LG_NW1 : (rb <= 2 ? 2 : CCMPC_LG_NW_BIG);
 }
 
 inline int store_lg_chunk(int rb, int64_t n_bound) {

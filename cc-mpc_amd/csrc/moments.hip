@@ -63,6 +63,9 @@ namespace ccmpc {
 #define CCMPC_DEPTH4 CCMPC_DEPTH
 #endif
 constexpr int kDepth = CCMPC_DEPTH;
+#ifndef CCMPC_DEPTH_BIG  // the ring at RB >= 3 (T > 24)
+#define CCMPC_DEPTH_BIG CCMPC_DEPTH
+#endif
 #ifndef CCMPC_PRIO
 #define CCMPC_PRIO 0
 #endif
@@ -225,8 +228,9 @@ void moments_kernel(
   // the fused tail reads the covariance from LDS; it lives in the cross-wave exchange buffer,
   // which is free once the item is combined (so T = 40 keeps its 80 x 80 covariance on chip too)
   constexpr bool COV_IN_LDS = MINK;
-  static_assert(combine_xch_doubles(RB, G::NW) >= D * D, "xch must hold the covariance");
-  __shared__ double xch[combine_xch_doubles(RB, G::NW)];
+  constexpr int XCH = combine_xch_doubles(RB, G::NW) > (MINK ? D * D : 0)
+                          ? combine_xch_doubles(RB, G::NW) : D * D;
+  __shared__ double xch[XCH];
   __shared__ double slab_lds[E];
   __shared__ double shift_lds[D];
   __shared__ double S_lds[D];
@@ -278,7 +282,7 @@ void moments_kernel(
 #if CCMPC_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md)
     if (G::NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(CCMPC_PRIO);
 #endif
-    constexpr int DP = kDepth;
+    constexpr int DP = RB >= 3 ? CCMPC_DEPTH_BIG : kDepth;
     Quad<P> buf[DP][S][RB];
     if (ngroups > 0) {
       // ring of DP load groups: group g lives in buf[g % DP]; DP - 1 groups are in flight
@@ -598,6 +602,11 @@ static int dispatch(const P *pos, int64_t ld, int T, const double *origin, const
 #undef CCMPC_ARGS
 }
 
+#ifndef CCMPC_SPLIT_TAIL_T  // ccmpc_minkowski_cycle above this T: moments, then the rows launch
+#define CCMPC_SPLIT_TAIL_T 24
+#endif
+constexpr int kSplitTailT = CCMPC_SPLIT_TAIL_T;
+
 template <bool MINK>
 static int run(const void *positions, int dtype, int64_t ld, int64_t T, const double *origin,
                const int64_t *cell_off, const int64_t *cell_cnt, int64_t n_cells,
@@ -605,6 +614,22 @@ static int run(const void *positions, int dtype, int64_t ld, int64_t T, const do
                double *out_cov, const MinkParams &mp, ccmpc_stream_t stream, const char *who) {
   hipStream_t s = as_stream(stream);
   const int Ti = static_cast<int>(T), nc = static_cast<int>(n_cells);
+  if (MINK && T > kSplitTailT) {
+    // long horizons: the moments launch, then the half-spaces as a launch of their own with one
+    // wave per (cell, t) -- the fused tail runs T(T-1)/2 chains on the cell's one finalising
+    // workgroup (T = 40: 780 chains, two rounds, ~12 us), while this runs every row at once.
+    // Same device functions on the same covariance values, so the same records.
+    const int rc = run<false>(positions, dtype, ld, T, origin, cell_off, cell_cnt, n_cells,
+                              n_bound, workspace, ws_bytes, out_mean, out_cov, mp, stream, who);
+    if (rc != CCMPC_OK) return rc;
+    launch_minkowski_rows(out_mean, out_cov, Ti, nc, mp, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error(std::string(who) + ": launch failed: " + hipGetErrorString(e));
+      return CCMPC_ERR_LAUNCH;
+    }
+    return CCMPC_OK;
+  }
   int rc;
   if (dtype == CCMPC_F64)
     rc = dispatch<double, MINK>(static_cast<const double *>(positions), ld, Ti, origin, cell_off,

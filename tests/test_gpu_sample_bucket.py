@@ -75,7 +75,8 @@ def _assert_same(got, want):
     (2, 9, 40, 700, 5, None),        # T = 40 (80 coordinate rows)
     (3, 25, 8, 3000, 6, 1),          # one kept mode: every rare particle is its
     (2, 10, 8, 2000, 7, 8),          # eight kept modes, few rare particles
-    (2, 25, 8, 8192, 9, "heavy"),    # ~7000 rare particles: 14 ranking rounds
+    (2, 25, 8, 8192, 9, "heavy"),    # ~7000 rare particles: 28 rare-slot blocks per OV
+    (2, 5, 8, 1000, 10, 5),          # every latent kept: no rare particle at all
     (1, 3, 6, 1, 8, None),           # a single particle
 ])
 def test_fused_equals_sampler_then_bucketing(gpu, O, L, T, N, seed, kept):
