@@ -279,6 +279,16 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   const int ng = a.G * K;
   const double2 *gp = reinterpret_cast<const double2 *>(a.gpart) + static_cast<int64_t>(o) * a.G * a.max_k;
   for (int u = tid; u < ng; u += kRThreads) gp_s[u] = gp[(u / K) * a.max_k + u % K];
+  // the first batch of rare records too: R is not known yet, so the slots are clamped into the
+  // list's storage (a launch's first kB * 256 records cover the C2 shape's whole rare list)
+  const float4 *info = reinterpret_cast<const float4 *>(a.rinfo) + static_cast<int64_t>(o) * npad;
+  constexpr int kB = 8;
+  float4 f[kB];
+#pragma unroll
+  for (int j = 0; j < kB; ++j) {
+    const int q = j * kRThreads + tid;
+    f[j] = info[q < npad ? q : npad - 1];
+  }
   const int nbins = K * (L + 1);
   for (int b = tid; b < nbins; b += kRThreads) hist[b] = pre[b] = 0;
   __syncthreads();
@@ -288,10 +298,6 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   const bool own = r < R;
   const int64_t reg = a.region[o];
   const double mx = a.minpos[2 * o], my = a.minpos[2 * o + 1];
-  // the first batch of rare records in flight while the centres are summed
-  const float4 *info = reinterpret_cast<const float4 *>(a.rinfo) + static_cast<int64_t>(o) * npad;
-  constexpr int kB = 8;
-  float4 f[kB];
   auto load_batch = [&](int q0) {
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
@@ -299,7 +305,6 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
       f[j] = info[q < R ? q : (R > 0 ? R - 1 : 0)];
     }
   };
-  load_batch(0);
   // centres, canonical order (bucket.hpp): superblocks, then left to right
   if (tid < K) {
     const int k = tid;

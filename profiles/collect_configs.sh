@@ -13,8 +13,10 @@ ROUND=${1:-r02}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
 cd /tmp
-for spec in "C2 1 400" "C3-1e3 1 400" "C3-2e4 1 400" "C3 1 400" "C4 1 200" "C4full 3 30" "C5 3 60"; do
+ALL=("C2 1 400" "C3-1e3 1 400" "C3-2e4 1 400" "C3 1 400" "C4 1 200" "C4full 3 30" "C5 3 60")
+for spec in "${ALL[@]}"; do
   set -- $spec
+  if [ -n "${ONLY:-}" ] && [[ ",$ONLY," != *",$1,"* ]]; then continue; fi
   CFG=$1; ROT=$2; IT=$3
   OUT=$ROOT/gpurun_out/prof_${ROUND}_${CFG}
   mkdir -p "$OUT"
