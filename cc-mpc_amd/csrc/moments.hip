@@ -384,12 +384,57 @@ __device__ __forceinline__ void load_group4(Pair<P> (&v)[NB], const P *const (&r
   for (int I = 0; I < NB; ++I) load_pair(rowp[I] + qc, v[I]);
 }
 
+// Row-contiguous loads (CCMPC_ROWLOAD4): the matrix-core layout puts 4 rows in every 4
+// consecutive lanes, so a load instruction in that layout walks 4 rows megabytes apart lane by
+// lane and the address-translation unit sees one request per 16-byte lane (UTCL1 counters,
+// profiles/r02/utcl1_counters_C4_C5.txt: 72M requests per C4 launch = one per 13.6 bytes).
+// Instead, lane l loads row 4I + (l >> 4), particles 2 (l & 15) + {0, 1}: 16 lanes cover 256
+// contiguous bytes of one row.  One ds_bpermute per dword then hands lane (c + 4 m) the value
+// of lane (16 c + m).  Measured (profiles/r02/ab10_rowload4.log): the 64-scene C4 batch 212.8
+// -> 209.6 us cold, the per-GPU batch at 8 GPUs 33.9 -> 34.9 us warm -- so translation is not
+// what holds the stream back; off by default, kept as a build knob.
+#ifndef CCMPC_ROWLOAD4
+#define CCMPC_ROWLOAD4 0
+#endif
+__device__ __forceinline__ double bperm_f64(int addr, double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = static_cast<uint32_t>(
+      __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(static_cast<uint32_t>(u))));
+  const uint32_t hi = static_cast<uint32_t>(
+      __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(static_cast<uint32_t>(u >> 32))));
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+__device__ __forceinline__ float bperm_f32(int addr, float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, x)));
+}
+__device__ __forceinline__ Pair<double> bperm_pair(int addr, const Pair<double> &p) {
+  Pair<double> r;
+  r.v.x = bperm_f64(addr, p.v.x);
+  r.v.y = bperm_f64(addr, p.v.y);
+  return r;
+}
+__device__ __forceinline__ Pair<float> bperm_pair(int addr, const Pair<float> &p) {
+  Pair<float> r;
+  r.v.x = bperm_f32(addr, p.v.x);
+  r.v.y = bperm_f32(addr, p.v.y);
+  return r;
+}
+
 template <typename P, int NB>
-__device__ __forceinline__ void mfma_group4(const Pair<P> (&raw)[NB], const double (&sh)[NB],
+__device__ __forceinline__ void mfma_group4(const Pair<P> (&loaded)[NB], const double (&sh)[NB],
                                             const bool (&live)[NB], int64_t gbase, int64_t p1,
-                                            int m, double (&acc)[n_pairs(NB)],
+                                            int m, int paddr, double (&acc)[n_pairs(NB)],
                                             double (&s1)[NB]) {
   const int64_t q = gbase + 2 * m;
+#if CCMPC_ROWLOAD4
+  Pair<P> raw[NB];
+#pragma unroll
+  for (int I = 0; I < NB; ++I) raw[I] = bperm_pair(paddr, loaded[I]);
+#else
+  const Pair<P>(&raw)[NB] = loaded;
+  (void)paddr;
+#endif
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     double v[NB];  // sub-step j: shifted; out-of-range slots and dead rows become 0
@@ -438,20 +483,27 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
 
   auto item = [=](const ItemLoc &loc, int32_t nit, int64_t a, int64_t b) {
     const int c = lane & 3, m = lane >> 2;
+#if CCMPC_ROWLOAD4
+    const int rl = lane >> 4, ml = lane & 15;  // the loading lane's row in the block, pair
+#else
+    const int rl = c, ml = m;
+#endif
+    const int paddr = 4 * (16 * c + m);        // matrix lane (c, m) <- loading lane 16 c + m
     const int64_t cnt = loc.cnt;
     const double pre = MINK ? prefetch_tail(mp, loc, rows) : 0.0;
     const WaveRange wr = wave_range<BAL>(a, b, w, kNW4, int64_t(1) << lg_wq, 32);
     const int64_t p1 = wr.p1;
 
     double sh[NB];
-    const P *rowp[NB];
-    bool live[NB];
+    const P *rowp[NB];  // the loading lane's rows (dead rows clamped to row 0)
+    bool live[NB];      // the matrix lane's rows
 #pragma unroll
     for (int I = 0; I < NB; ++I) {
-      const int R = 4 * I + c;
+      const int R = 4 * I + c, RL = 4 * I + rl;
       live[I] = R < rows;
-      rowp[I] = pos + static_cast<int64_t>(live[I] ? R : 0) * ld + loc.off;
-      sh[I] = (live[I] && cnt > 0) ? static_cast<double>(rowp[I][0]) : 0.0;
+      rowp[I] = pos + static_cast<int64_t>(RL < rows ? RL : 0) * ld + loc.off;
+      sh[I] = (live[I] && cnt > 0)
+                  ? static_cast<double>(pos[static_cast<int64_t>(R) * ld + loc.off]) : 0.0;
     }
     double acc[NP];
 #pragma unroll
@@ -465,20 +517,21 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
     Pair<P> buf[DP][NB];
     if (ngroups > 0) {
 #pragma unroll
-      for (int d = 0; d < DP - 1; ++d) load_group4<P, NB>(buf[d], rowp, wr.p0 + d * st, p1, m);
+      for (int d = 0; d < DP - 1; ++d) load_group4<P, NB>(buf[d], rowp, wr.p0 + d * st, p1, ml);
       int64_t gi = 0;
       for (; gi + DP <= ngroups; gi += DP) {
 #pragma unroll
         for (int d = 0; d < DP; ++d) {
-          load_group4<P, NB>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1, m);
+          load_group4<P, NB>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1, ml);
           __builtin_amdgcn_sched_barrier(0);
-          mfma_group4<P, NB>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, m, acc, s1);
+          mfma_group4<P, NB>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, m, paddr, acc, s1);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
 #pragma unroll
       for (int d = 0; d < DP - 1; ++d)
-        if (gi + d < ngroups) mfma_group4<P, NB>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, m, acc, s1);
+        if (gi + d < ngroups)
+          mfma_group4<P, NB>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, m, paddr, acc, s1);
     }
     PROBE_TS(2);
 
