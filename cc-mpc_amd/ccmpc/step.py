@@ -142,6 +142,7 @@ class MinkowskiStepGraph:
         # the cycle and the L4 kernel as parallel graph branches, or (CCMPC_STEP_LINEAR=1) one
         # after the other on one stream
         self.branch = os.environ.get("CCMPC_STEP_LINEAR", "0") != "1"
+        self.cycle_first = os.environ.get("CCMPC_STEP_CYCLE_FIRST", "0") == "1"
         self.graph = None
         self._static_set = False
 
@@ -178,23 +179,32 @@ class MinkowskiStepGraph:
         chk(lib.ccmpc_copy_async(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
         for fn, args in self._sample_calls(s):
             chk(fn(*args), fn.__name__)
-        # the cycle and the L4 kernel only read the bucketed store: two graph branches
+        # the cycle and the L4 kernel only read the bucketed store: two graph branches (the
+        # fork is taken after the sampling; which branch is captured first is a knob)
         main = torch.cuda.current_stream(self.device)
         side = self.side if self.branch else main
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            lws = self.l4_ws.buf
-            chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
-                                   p(o.d("cnt")), C, st.n_bound, p(i.d("past")), p(i.d("bbox")),
-                                   p(lws), lws.numel(), p(o.d("A")), p(o.d("b")),
-                                   p(o.d("yaw_mean")), p(o.d("yaw0_var")), None, None,
-                                   engine._stream()), "ccmpc_l4_split")
-        mws = self.ws.buf
-        chk(lib.ccmpc_minkowski_cycle(
-            p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
-            st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
-            self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")), p(o.d("pl")),
-            s), "ccmpc_minkowski_cycle")
+
+        def l4():
+            with torch.cuda.stream(side):
+                lws = self.l4_ws.buf
+                chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, T, p(st.origin),
+                                       p(o.d("off")), p(o.d("cnt")), C, st.n_bound,
+                                       p(i.d("past")), p(i.d("bbox")), p(lws), lws.numel(),
+                                       p(o.d("A")), p(o.d("b")), p(o.d("yaw_mean")),
+                                       p(o.d("yaw0_var")), None, None, engine._stream()),
+                    "ccmpc_l4_split")
+
+        def cycle():
+            mws = self.ws.buf
+            chk(lib.ccmpc_minkowski_cycle(
+                p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
+                st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
+                self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")),
+                p(o.d("pl")), s), "ccmpc_minkowski_cycle")
+
+        for stage in ((cycle, l4) if self.cycle_first else (l4, cycle)):
+            stage()
         main.wait_stream(side)
         chk(lib.ccmpc_copy_async(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
 
