@@ -57,6 +57,7 @@ SIGNATURES = {
     "ccmpc_last_error": (ctypes.c_char_p, []),
     "ccmpc_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "ccmpc_copy_async": (ctypes.c_int, [_P, _P, _SZ, _P]),
+    "ccmpc_copy_kernel_async": (ctypes.c_int, [_P, _P, _SZ, _P]),
     "ccmpc_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "ccmpc_moments": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64, _I64, _P,
                                      _SZ, _P, _P, _P]),

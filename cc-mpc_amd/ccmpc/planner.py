@@ -241,6 +241,15 @@ def _host(x):
 
 
 @functools.lru_cache(maxsize=64)
+def _default_bboxes(O):
+    """ovehicle.py:19's bbox for every OV (read-only: shared between calls)."""
+    from . import ovehicle
+    b = np.tile(ovehicle.DEFAULT_BBOX, (O, 1))
+    b.setflags(write=False)
+    return b
+
+
+@functools.lru_cache(maxsize=64)
 def _first_cells(K):
     """First cell of each OV for kept-mode counts K (a tuple)."""
     return [sum(K[:o]) for o in range(len(K))]
@@ -630,7 +639,7 @@ class MidlevelAgent:
         gmm = sampler["gmm"]
         pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
         past_last = np.array([p[-1] for p in pasts])
-        bboxes = (np.tile(ovehicle.DEFAULT_BBOX, (O, 1)) if bboxes is None
+        bboxes = (_default_bboxes(O) if bboxes is None
                   else np.asarray(bboxes, np.float64).reshape(O, 2))
         if T != ph:
             z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=seed,

@@ -143,6 +143,10 @@ class MinkowskiStepGraph:
         # after the other on one stream
         self.branch = os.environ.get("CCMPC_STEP_LINEAR", "0") != "1"
         self.cycle_first = os.environ.get("CCMPC_STEP_CYCLE_FIRST", "0") == "1"
+        # the packed copies as copy kernels that read / write the pinned pack directly, or
+        # (CCMPC_STEP_COPY_KERNEL=0) as memcpy nodes (a runtime blit of ~4.8 us each): the
+        # kernels take ~8 us off a step (profiles/r02/v33_step_copy_kernel.txt)
+        self.copy_kernel = os.environ.get("CCMPC_STEP_COPY_KERNEL", "1") == "1"
         self.graph = None
         self._static_set = False
 
@@ -176,7 +180,8 @@ class MinkowskiStepGraph:
         i, o, st = self.inp, self.out, self.store
         T, C = self.T, self.C
         chk = engine._lib.check
-        chk(lib.ccmpc_copy_async(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
+        copy = lib.ccmpc_copy_kernel_async if self.copy_kernel else lib.ccmpc_copy_async
+        chk(copy(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
         for fn, args in self._sample_calls(s):
             chk(fn(*args), fn.__name__)
         # the cycle and the L4 kernel only read the bucketed store: two graph branches (the
@@ -206,7 +211,7 @@ class MinkowskiStepGraph:
         for stage in ((cycle, l4) if self.cycle_first else (l4, cycle)):
             stage()
         main.wait_stream(side)
-        chk(lib.ccmpc_copy_async(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
+        chk(copy(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
 
     def capture(self):
         """Record the step into a hipGraph (after one eager run that warms every kernel)."""
@@ -243,7 +248,8 @@ class MinkowskiStepGraph:
                              f"for {self.K}")
         np.subtract(kc, 1, out=i.h("keep"), casting="unsafe")
         i.h("keep")[~kept] = -1
-        i.h("seed")[0] = np.int64(np.uint64(int(seed) & (2**64 - 1)).view(np.int64))
+        sd = int(seed) & (2**64 - 1)
+        i.h("seed")[0] = sd - (1 << 64) if sd >= (1 << 63) else sd
         i.h("init").reshape(-1)[:] = np.asarray(init_state, np.float64).reshape(-1)
         np.cumsum(pmf, axis=1, out=i.h("cdf"))
         np.copyto(i.h("gmm").reshape(-1), np.asarray(gmm).reshape(-1), casting="same_kind")

@@ -102,6 +102,9 @@ const char *ccmpc_status_string(int status);
  * captured planning step (ccmpc/step.py) carries its packed input upload and output download
  * as graph nodes, so one replay is the whole step. */
 int ccmpc_copy_async(void *dst, const void *src, size_t bytes, ccmpc_stream_t stream);
+/* The same copy as a device kernel reading / writing the pinned host buffer directly (a graph
+ * kernel node rather than a memcpy node); bytes and both pointers 16-byte aligned. */
+int ccmpc_copy_kernel_async(void *dst, const void *src, size_t bytes, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Moment (Gram) reduction.  Replaces every np.mean / np.cov over particle clouds on the path:
