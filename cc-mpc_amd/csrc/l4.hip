@@ -260,19 +260,79 @@ inline size_t l4_split_bytes(int64_t T, int64_t n_cells, int S, size_t *o1, size
   return (o + 255) / 256 * 256;
 }
 
+// Average particles per cell up to which ccmpc_l4_split is ONE launch (pass 2 in the (cell, t)'s
+// last arriver of pass 1).  Measured at the drop-in step's C2 shape (~2200 particles per cell):
+// 139.6 us per step against 136.2 with the two launches (profiles/r02/v35_l4_one_launch.txt) --
+// the last arriver's whole-cell pass costs more than the second launch saves.  Off (0).
+#ifndef CCMPC_L4_TAIL2_MAX
+#define CCMPC_L4_TAIL2_MAX 0
+#endif
+constexpr int64_t kL4Tail2Max = CCMPC_L4_TAIL2_MAX;
+
 inline int l4_split_factor(int64_t n_cells, int64_t n_bound) {
   const int64_t per = n_cells > 0 ? (n_bound + n_cells - 1) / n_cells : 0;
   const int64_t S = (per + 1023) / 1024;  // ~1024 particles per workgroup on the average cell
   return static_cast<int>(S < 1 ? 1 : (S > 64 ? 64 : S));
 }
 
+// Pass 2's per-particle work over [i0, i1) of one (cell, t): the bbox corners at the particle's
+// own heading and the running maxima of the four support values of A (midlevel/util.py:109-124,
+// :171-200).  fmax is exact and order-free, so any split of the particles gives the same b.
 template <typename P>
+__device__ __forceinline__ void corner_maxima(const P *base, int64_t ld, int t, int64_t i0,
+                                              int64_t i1, int64_t off, double o0, double o1,
+                                              double px, double py, double lon, double lat,
+                                              const double (&A)[4][2], double (&mx)[4],
+                                              double *__restrict__ out_vertices) {
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const double x = world(base, ld, 2 * t, i, o0), y = world(base, ld, 2 * t + 1, i, o1);
+    const double xp = t == 0 ? px : world(base, ld, 2 * t - 2, i, o0);
+    const double yp = t == 0 ? py : world(base, ld, 2 * t - 1, i, o1);
+    const double dx = x - xp, dy = y - yp;
+    double S, C;
+    const double r = sqrt(dx * dx + dy * dy);
+    if (r > 0.0 && isfinite(r)) {  // cos / sin of the heading without the atan2 (heading_cs)
+      C = dx / r;
+      S = dy / r;
+    } else {
+      sincos(atan2(dy, dx), &S, &C);
+    }
+    // rows of Rot per corner (midlevel/util.py:109-118), disp = 0.5 * Rot @ [lon, lat]
+    const double ddx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
+                           0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
+    const double ddy[4] = {0.5 * (S * lon - C * lat), 0.5 * (S * lon + C * lat),
+                           0.5 * (-S * lon + C * lat), 0.5 * (-S * lon - C * lat)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double vx = x + ddx[c], vy = y + ddy[c];
+      if (out_vertices) {
+        double *vp = out_vertices + (static_cast<int64_t>(t) * 8 + 2 * c) * ld + off + i;
+        vp[0] = vx;
+        vp[ld] = vy;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mx[q] = fmax(mx[q], A[q][0] * vx + A[q][1] * vy);
+    }
+  }
+}
+
+__device__ __forceinline__ void support_rows(double theta, double (&A)[4][2]) {
+  const double ct_ = cos(theta), st_ = sin(theta);
+  A[0][0] = ct_; A[0][1] = st_;
+  A[1][0] = -st_; A[1][1] = ct_;
+  A[2][0] = -ct_; A[2][1] = -st_;
+  A[3][0] = st_; A[3][1] = -ct_;
+}
+
+template <typename P, bool TAIL2>
 __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
-    const double *__restrict__ past_last, L4Split sp, double *__restrict__ out_yaw_mean,
-    double *__restrict__ out_yaw0_var, double *__restrict__ out_yaw) {
+    const double *__restrict__ past_last, const double *__restrict__ bbox, L4Split sp,
+    double *__restrict__ out_yaw_mean, double *__restrict__ out_yaw0_var,
+    double *__restrict__ out_yaw, double *__restrict__ out_A, double *__restrict__ out_b) {
   __shared__ double red[16];
+  __shared__ double theta_s;
   __shared__ int flag;
   const int ct = blockIdx.x / sp.S, part = blockIdx.x % sp.S;
   const int cell = ct / T, t = ct % T;
@@ -318,9 +378,28 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
     const double nn = static_cast<double>(n);
     const double theta = a / nn;
     sp.theta[ct] = theta;
+    theta_s = theta;
     out_yaw_mean[ct] = theta;
     if (t == 0) out_yaw0_var[cell] = (b2 - b1 * b1 / nn) / (nn - 1.0);
   }
+  if (!TAIL2) return;
+  // small cells: the (cell, t)'s last arriver runs pass 2 over the whole cell itself (no second
+  // launch, no second hand-off; the maxima are order-free, so b is the two-pass b bit for bit)
+  __syncthreads();
+  double A[4][2];
+  support_rows(theta_s, A);
+  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  corner_maxima(base, ld, t, 0, n, off, o0, o1, px, py, bbox[2 * cell], bbox[2 * cell + 1], A, mx,
+                static_cast<double *>(nullptr));
+  double bm[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bm[q] = block_max(mx[q], red);
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 4; ++q) {
+      out_A[static_cast<int64_t>(ct) * 8 + 2 * q] = A[q][0];
+      out_A[static_cast<int64_t>(ct) * 8 + 2 * q + 1] = A[q][1];
+      out_b[static_cast<int64_t>(ct) * 4 + q] = bm[q];
+    }
 }
 
 template <typename P>
@@ -341,39 +420,10 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass2_kernel(
   const int64_t chunk = (n + sp.S - 1) / sp.S;
   const int64_t i0 = part * chunk, i1 = min(n, i0 + chunk);
   const double theta = sp.theta[ct];  // written by pass 1 (an earlier launch)
-  const double ct_ = cos(theta), st_ = sin(theta);
-  const double A[4][2] = {{ct_, st_}, {-st_, ct_}, {-ct_, -st_}, {st_, -ct_}};
+  double A[4][2];
+  support_rows(theta, A);
   double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const double x = world(base, ld, 2 * t, i, o0), y = world(base, ld, 2 * t + 1, i, o1);
-    const double xp = t == 0 ? px : world(base, ld, 2 * t - 2, i, o0);
-    const double yp = t == 0 ? py : world(base, ld, 2 * t - 1, i, o1);
-    const double dx = x - xp, dy = y - yp;
-    double S, C;
-    const double r = sqrt(dx * dx + dy * dy);
-    if (r > 0.0 && isfinite(r)) {  // cos / sin of the heading without the atan2 (heading_cs)
-      C = dx / r;
-      S = dy / r;
-    } else {
-      sincos(atan2(dy, dx), &S, &C);
-    }
-    // rows of Rot per corner (midlevel/util.py:109-118), disp = 0.5 * Rot @ [lon, lat]
-    const double ddx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
-                           0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
-    const double ddy[4] = {0.5 * (S * lon - C * lat), 0.5 * (S * lon + C * lat),
-                           0.5 * (-S * lon + C * lat), 0.5 * (-S * lon - C * lat)};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double vx = x + ddx[c], vy = y + ddy[c];
-      if (out_vertices) {
-        double *vp = out_vertices + (static_cast<int64_t>(t) * 8 + 2 * c) * ld + off + i;
-        vp[0] = vx;
-        vp[ld] = vy;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) mx[q] = fmax(mx[q], A[q][0] * vx + A[q][1] * vy);
-    }
-  }
+  corner_maxima(base, ld, t, i0, i1, off, o0, o1, px, py, lon, lat, A, mx, out_vertices);
   double bm[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) bm[q] = block_max(mx[q], red);
@@ -480,19 +530,28 @@ extern "C" int ccmpc_l4_split(const void *positions, int dtype, int64_t ld, int6
   const dim3 grid(static_cast<unsigned>(n_cells * T * S));
   hipStream_t s = as_stream(stream);
   const int Ti = static_cast<int>(T);
-  if (dtype == CCMPC_F64) {
-    const double *p = static_cast<const double *>(positions);
-    hipLaunchKernelGGL((l4_pass1_kernel<double>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
-                       cell_off, cell_cnt, past_last, sp, out_yaw_mean, out_yaw0_var, out_yaw);
-    hipLaunchKernelGGL((l4_pass2_kernel<double>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
+  // small cells (<= kL4Tail2Max particles on average, no vertex output): one launch, pass 2 in
+  // the (cell, t)'s last arriver of pass 1
+  const bool tail2 = !out_vertices && n_particles_bound <= kL4Tail2Max * n_cells;
+  auto run = [&](auto tag) {
+    using P = decltype(tag);
+    const P *p = static_cast<const P *>(positions);
+    if (tail2) {
+      hipLaunchKernelGGL((l4_pass1_kernel<P, true>), grid, dim3(kL4Threads), 0, s, p, ld, Ti,
+                         origin, cell_off, cell_cnt, past_last, bbox, sp, out_yaw_mean,
+                         out_yaw0_var, out_yaw, out_A, out_b);
+      return;
+    }
+    hipLaunchKernelGGL((l4_pass1_kernel<P, false>), grid, dim3(kL4Threads), 0, s, p, ld, Ti,
+                       origin, cell_off, cell_cnt, past_last, bbox, sp, out_yaw_mean,
+                       out_yaw0_var, out_yaw, out_A, out_b);
+    hipLaunchKernelGGL((l4_pass2_kernel<P>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
                        cell_off, cell_cnt, past_last, bbox, sp, out_A, out_b, out_vertices);
-  } else {
-    const float *p = static_cast<const float *>(positions);
-    hipLaunchKernelGGL((l4_pass1_kernel<float>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
-                       cell_off, cell_cnt, past_last, sp, out_yaw_mean, out_yaw0_var, out_yaw);
-    hipLaunchKernelGGL((l4_pass2_kernel<float>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
-                       cell_off, cell_cnt, past_last, bbox, sp, out_A, out_b, out_vertices);
-  }
+  };
+  if (dtype == CCMPC_F64)
+    run(double{});
+  else
+    run(float{});
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }
