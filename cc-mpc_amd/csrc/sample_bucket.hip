@@ -267,6 +267,9 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   // thread's rare-slot coordinates (slot clamped into the list's storage, used only if < R) and
   // the centre partials
   const int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
+  // (a load issued after a __syncthreads is a fresh round trip the next barrier waits for)
+  const int64_t reg = a.region[o];
+  const double mx = a.minpos[2 * o], my = a.minpos[2 * o + 1];
   if (tid <= K) tot_s[tid] = h[tid];
   if (tid < K) cst_s[tid] = hdr_starts(const_cast<int32_t *>(h))[tid];
   if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
@@ -296,8 +299,6 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   const int R = tot_s[K];
   if (r0 >= R && blockIdx.x != 0) return;  // uniform: no rare slots here (block 0 writes cells)
   const bool own = r < R;
-  const int64_t reg = a.region[o];
-  const double mx = a.minpos[2 * o], my = a.minpos[2 * o + 1];
   auto load_batch = [&](int q0) {
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
@@ -359,6 +360,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
       a.init_center[2 * cell + 1] = cen_s[k][1];
     }
   }
+  FUSED_TS(2, 4);
   // this block's stable ranks: lanes in order within a wave, waves in order
   const int kr = own ? okey[tid] : -1;
   const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
     todo &= ~m;
   }
   __syncthreads();
+  FUSED_TS(2, 5);
   if (own) {
     int before = pre[kr] + rank;
     for (int u = 0; u < w; ++u) before += wcnt[u][kr];
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
     for (int rr = 0; rr < 80; ++rr)
       if (rr < rows) out[static_cast<int64_t>(rr) * a.ld_out] = v[rr];
   }
-  FUSED_TS(2, 4);
+  FUSED_TS(2, 6);
 }
 
 struct FusedWs {
@@ -416,7 +419,8 @@ using namespace ccmpc;
 
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
 // which 0: P0 latents (slots 0 start, 1 done); 1: P1 place (0 start, 1 counted, 2 sampled +
-// published); 2: P2 rares (0 start, 1 loaded, 2 centres, 3 keyed, 4 copied)  (tools/probe_step.py)
+// published); 2: P2 rares (0 start, 1 loaded, 2 centres, 3 keyed, 4 bin starts, 5 ranked,
+// 6 copied)  (tools/probe_step.py)
 extern "C" int ccmpc_probe_fused_timestamps(void *host, int which, int reset) {
   if (which < 0 || which > 2) return -1;
   const size_t bytes = sizeof(g_fused_ts[0]);

@@ -71,7 +71,7 @@ def main():
               ("latents", table(lib.ccmpc_probe_fused_timestamps, 0, 0), ["drawn"]),
               ("place", table(lib.ccmpc_probe_fused_timestamps, 1, 0), ["counted", "sampled"]),
               ("rares", table(lib.ccmpc_probe_fused_timestamps, 2, 0),
-               ["loaded", "centres", "keyed", "copied"]),
+               ["loaded", "centres", "keyed", "bins", "ranked", "copied"]),
               ("b.stats", table(lib.ccmpc_probe_bucket_timestamps, 0, 0),
                ["loaded", "published", "last", "done"]),
               ("b.hist", table(lib.ccmpc_probe_bucket_timestamps, 1, 0),
