@@ -135,12 +135,23 @@ __device__ __forceinline__ void mfma_group(const Quad<P> (&raw)[S][RB], const do
 // partial Gram (publish(dst, to_lds) = the scheme's cross-wave combine), then either finalise
 // in LDS (the cell is this one item) or climb the combine tree, and as the cell's last arriver
 // gather the root, finalise and (MINK) build the cell's half-spaces.
+// Long horizons (16x16 tiles, RB >= 4, i.e. T > 24) in balanced mode, moments only: a cell's
+// root gather is up to kRootFanIn slabs of 10-31 KB, ~1 MB on ONE CU for T = 40 (8 us at the
+// CU's L2 bandwidth).  Such cells skip the arrival; root_finalize_kernel then sums them in the
+// root gather's order, one workgroup per (cell, tile), so the values are the same bits.
+#ifndef CCMPC_DEFER_ROOT
+#define CCMPC_DEFER_ROOT 1
+#endif
+__host__ __device__ constexpr bool defer_root(int rb, bool mink, bool bal) {
+  return CCMPC_DEFER_ROOT && bal && !mink && rb >= 4;
+}
+
 struct EpilogueLds {
   double *slab, *shift, *S, *mean, *cov, *lb, *ref;
   int *flag;
 };
 
-template <typename Sch, bool MINK, bool COV_IN_LDS, typename Publish>
+template <typename Sch, bool MINK, bool COV_IN_LDS, bool DEFER, typename Publish>
 __device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &loc, int32_t nit,
                                               int T, const TreeLayout &tree,
                                               const double *__restrict__ origin,
@@ -160,6 +171,8 @@ __device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &lo
   } else {
     publish(tree.slabs[0] + static_cast<int64_t>(loc.first + loc.chunk_idx) * E, false);
     PROBE_TS(3);
+    // deferred root: root_finalize_kernel sums this cell's item slabs, spread over workgroups
+    if (DEFER && nit <= kRootFanIn) return;
     const double *root;
     int32_t root_n;
     const bool last = tree_climb<E>(tree, loc.chunk_idx, nit, loc.first, cell, L.flag, &root,
@@ -228,6 +241,7 @@ void moments_kernel(
   // the fused tail reads the covariance from LDS; it lives in the cross-wave exchange buffer,
   // which is free once the item is combined (so T = 40 keeps its 80 x 80 covariance on chip too)
   constexpr bool COV_IN_LDS = MINK;
+  constexpr bool DEFER = defer_root(RB, MINK, BAL);
   constexpr int XCH = combine_xch_doubles(RB, G::NW) > (MINK ? D * D : 0)
                           ? combine_xch_doubles(RB, G::NW) : D * D;
   __shared__ double xch[XCH];
@@ -316,7 +330,7 @@ void moments_kernel(
       if (w == 0 && g == 0) shift_lds[16 * bb + r] = sh[bb];
     }
     const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, xch, lb_s, ref_lds, &flag};
-    cell_epilogue<Scheme16<RB>, MINK, COV_IN_LDS>(
+    cell_epilogue<Scheme16<RB>, MINK, COV_IN_LDS, DEFER>(
         [&](double *dst, bool to_lds) {
           combine_waves<RB, NACC, G::NW>(acc, s1, xch, dst, to_lds);
         },
@@ -542,7 +556,7 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
     // the covariance for the tail reuses the exchange buffer (free after combine4)
     static_assert(kNW4 * Combine4Layout<NB>::XS >= D * D, "xch must hold the covariance");
     const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, xch, lb_s, ref_lds, &flag};
-    cell_epilogue<Sch, MINK, MINK>(
+    cell_epilogue<Sch, MINK, MINK, false>(
         [&](double *dst, bool to_lds) { combine4<NB, kNW4>(acc, s1, xch, dst, to_lds); }, loc,
         nit, T, tree, origin, out_mean, out_cov, mp, L);
   };
@@ -570,6 +584,113 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
   item(loc, items_of(loc.cnt, lg_chunk), i0, i1);
 }
 
+// A balanced launch's cell -> (first item, item count), as locate_balanced deals them (same
+// chunk from the same exact count sum).  Every lane of the wave gets the result.
+__device__ __forceinline__ void cell_items_balanced(int cell, int G, const int64_t *__restrict__ cnt,
+                                                    int n_cells, int32_t &first, int32_t &nit,
+                                                    int64_t &n) {
+  const int lane = threadIdx.x & 63;
+  double part = 0.0;  // exact: counts and their sum < 2^53
+  for (int base = 0; base < n_cells; base += 64)
+    part += base + lane < n_cells ? static_cast<double>(cnt[base + lane]) : 0.0;
+  const double td = wave_sum_dpp_f64(part);
+  const int64_t A = kChunkAlign;
+  const int64_t chunk =
+      (static_cast<int64_t>(td / (static_cast<double>(G - n_cells) * A)) + 1) * A;
+  int32_t before = 0;
+  first = 0;
+  nit = 0;
+  n = 0;
+  for (int base = 0; base < n_cells; base += 64) {
+    const int c = base + lane;
+    const int64_t nn = c < n_cells ? cnt[c] : 0;
+    const int32_t mine =
+        c < n_cells ? static_cast<int32_t>(nn > 0 ? ceil_div_fast(nn, chunk) : 1) : 0;
+    int32_t incl = mine;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const int32_t y = __shfl_up(incl, s, 64);
+      if (lane >= s) incl += y;
+    }
+    if (cell < base + 64) {
+      const int l = cell - base;
+      first = before + __shfl(incl - mine, l, 64);
+      nit = __shfl(mine, l, 64);
+      n = __shfl(nn, l, 64);
+      return;
+    }
+    before += __shfl(incl, 63, 64);
+  }
+}
+
+// The deferred root (defer_root): one workgroup per (cell, 16x16 tile).  Threads 0..127 sum one
+// entry pair of the tile over the cell's item slabs, threads 128.. the row sums and the shift,
+// all loads in one round; then the tile's covariance entries (and, in tile 0, the mean) by
+// finalize_cell's expressions.  Cells of one item were finalised by the moments launch, cells
+// past kRootFanIn items by its combine tree.
+constexpr int kRootThreads = 256;
+template <typename P, int RB>
+__global__ __launch_bounds__(kRootThreads) void root_finalize_kernel(
+    const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off, int n_cells, int G,
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const double *__restrict__ slabs0, double *__restrict__ out_mean,
+    double *__restrict__ out_cov) {
+  constexpr int NT = n_tiles(RB), D = 16 * RB, E = slab_doubles(RB), GRAM = NT * 256;
+  static_assert(128 + D / 2 + D <= kRootThreads, "thread roles");
+  __shared__ double S_lds[D];
+  __shared__ double shift_lds[D];
+  const int cell = blockIdx.x / NT, tile = blockIdx.x % NT, tid = threadIdx.x;
+  const int rows = 2 * T;
+  int32_t first, nit;
+  int64_t cnt;
+  cell_items_balanced(cell, G, cell_cnt, n_cells, first, nit, cnt);
+  if (nit <= 1 || nit > kRootFanIn) return;  // uniform
+  const double *root = slabs0 + static_cast<int64_t>(first) * E;
+  auto gather = [&](int e) {  // gather_root's order for one entry pair
+    double2 s = sum_group2(root, min(nit, kFanIn), E, e);
+    for (int k = kFanIn; k < nit; k += kFanIn) {
+      const double2 t = sum_group2(root + static_cast<int64_t>(k) * E, min(nit - k, kFanIn), E, e);
+      s.x += t.x;
+      s.y += t.y;
+    }
+    return s;
+  };
+  const int e = tile * 256 + 2 * tid;
+  double2 g{0.0, 0.0};
+  if (tid < 128) {
+    g = gather(e);
+  } else if (tid < 128 + D / 2) {
+    const int r = 2 * (tid - 128);
+    const double2 s = r < rows ? gather(GRAM + r) : double2{0.0, 0.0};
+    S_lds[r] = s.x;
+    S_lds[r + 1] = s.y;
+  } else if (tid < 128 + D / 2 + D) {
+    const int r = tid - 128 - D / 2;
+    shift_lds[r] = r < rows ? static_cast<double>(pos[static_cast<int64_t>(r) * ld +
+                                                      cell_off[cell]])
+                            : 0.0;
+  }
+  __syncthreads();
+  const double n = static_cast<double>(cnt);
+  if (tile == 0 && tid < rows) {
+    const double o = origin ? origin[2 * cell + (tid & 1)] : 0.0;
+    out_mean[static_cast<int64_t>(cell) * rows + tid] = (shift_lds[tid] + S_lds[tid] / n) + o;
+  }
+  if (tid >= 128) return;
+  double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
+  int i0, j0, i1, j1;
+  decode_entry(e, RB, i0, j0);
+  decode_entry(e + 1, RB, i1, j1);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = h ? i1 : i0, j = h ? j1 : j0;
+    if (!(i < rows && j < rows && i <= j)) continue;
+    const double c = ((h ? g.y : g.x) - S_lds[i] * S_lds[j] / n) / (n - 1.0);
+    cov[i * rows + j] = c;
+    cov[j * rows + i] = c;
+  }
+}
+
 template <typename P, int RB, bool MINK>
 static int launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
                   const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
@@ -586,6 +707,10 @@ static int launch(const P *pos, int64_t ld, int T, const double *origin, const i
     hipLaunchKernelGGL((moments_kernel<P, RB, MINK, true>), dim3(static_cast<unsigned>(grid)),
                        dim3(threads), 0, s, cnt, off, MINK ? mp.cell_ref : nullptr, n_cells, pos, ld,
                        T, origin, lg_wq, tree, mean, cov, mp);
+    if (defer_root(RB, MINK, true))
+      hipLaunchKernelGGL((root_finalize_kernel<P, RB>),
+                         dim3(static_cast<unsigned>(n_cells * n_tiles(RB))), dim3(kRootThreads), 0,
+                         s, cnt, off, n_cells, grid, pos, ld, T, origin, tree.slabs[0], mean, cov);
     return CCMPC_OK;
   }
   const int64_t items = max_items(n_cells, n_bound, int64_t(1) << store_lg_chunk(RB, n_bound));

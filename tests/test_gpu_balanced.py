@@ -27,8 +27,12 @@ def _fro_rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
 
 
+# T = 28 / 40: 16x16 tiles with RB = 4 / 5, whose cells of 2..kRootFanIn items take the
+# deferred root (root_finalize_kernel) and larger ones the combine tree
 @pytest.mark.parametrize("T,dtype", [(8, torch.float64), (11, torch.float64),
-                                     (20, torch.float64), (11, torch.float32)])
+                                     (20, torch.float64), (11, torch.float32),
+                                     (28, torch.float64), (40, torch.float64),
+                                     (40, torch.float32)])
 def test_balanced_moments_match_numpy(gpu, T, dtype):
     import ccmpc.engine as eng
     cells = _cells(T, COUNTS, seed=T)
@@ -50,7 +54,7 @@ def test_balanced_moments_match_numpy(gpu, T, dtype):
         np.testing.assert_array_equal(cov[j], cov[j].T)
 
 
-@pytest.mark.parametrize("T", [8, 12])
+@pytest.mark.parametrize("T", [8, 12, 40])
 def test_balanced_equals_power_of_two_items(gpu, T):
     """The same cells through both paths: the capacity alone moves the launch into balanced
     mode (the chunk is computed from the actual counts, not from the bound)."""
