@@ -623,20 +623,32 @@ __device__ __forceinline__ void cell_items_balanced(int cell, int G, const int64
   }
 }
 
-// The deferred root (defer_root): one workgroup per (cell, 16x16 tile).  Threads 0..127 sum one
-// entry pair of the tile over the cell's item slabs, threads 128.. the row sums and the shift,
-// all loads in one round; then the tile's covariance entries (and, in tile 0, the mean) by
-// finalize_cell's expressions.  Cells of one item were finalised by the moments launch, cells
-// past kRootFanIn items by its combine tree.
-constexpr int kRootThreads = 256;
+// The deferred root (defer_root): one workgroup per (cell, 16x16 tile).  The root gather sums
+// a cell's slabs in groups of kFanIn (sum_group2) and adds the group sums in order; here each of
+// the <= kRootFanIn / kFanIn groups is a thread of its own (group q of entry pair k: thread
+// q * 128 + k for the tile's 128 pairs, then the row-sum pairs), every load of the cell in flight
+// in one round, and the group sums are added in LDS in the same order: the same bits.  Then the
+// tile's covariance entries (and, in tile 0, the mean) by finalize_cell's expressions.  Cells of
+// one item were finalised by the moments launch, cells past kRootFanIn items by its combine tree.
+constexpr int kRootGroups = kRootFanIn / kFanIn;
+static_assert(kRootGroups * kFanIn == kRootFanIn, "root = whole fan-in groups");
+template <int RB>
+struct RootGeo {
+  static constexpr int D = 16 * RB;
+  static constexpr int PAIRS = 128 + D / 2;               // tile pairs, then row-sum pairs
+  static constexpr int GATHER = kRootGroups * PAIRS;      // gather threads
+  static constexpr int THREADS = (GATHER + D + 63) / 64 * 64;  // + the shift loads
+};
 template <typename P, int RB>
-__global__ __launch_bounds__(kRootThreads) void root_finalize_kernel(
+__global__ __launch_bounds__(RootGeo<RB>::THREADS) void root_finalize_kernel(
     const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off, int n_cells, int G,
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const double *__restrict__ slabs0, double *__restrict__ out_mean,
     double *__restrict__ out_cov) {
-  constexpr int NT = n_tiles(RB), D = 16 * RB, E = slab_doubles(RB), GRAM = NT * 256;
-  static_assert(128 + D / 2 + D <= kRootThreads, "thread roles");
+  using RG = RootGeo<RB>;
+  constexpr int NT = n_tiles(RB), D = RG::D, E = slab_doubles(RB), GRAM = NT * 256;
+  constexpr int PAIRS = RG::PAIRS;
+  __shared__ double2 part[kRootGroups][PAIRS];
   __shared__ double S_lds[D];
   __shared__ double shift_lds[D];
   const int cell = blockIdx.x / NT, tile = blockIdx.x % NT, tid = threadIdx.x;
@@ -645,30 +657,34 @@ __global__ __launch_bounds__(kRootThreads) void root_finalize_kernel(
   int64_t cnt;
   cell_items_balanced(cell, G, cell_cnt, n_cells, first, nit, cnt);
   if (nit <= 1 || nit > kRootFanIn) return;  // uniform
-  const double *root = slabs0 + static_cast<int64_t>(first) * E;
-  auto gather = [&](int e) {  // gather_root's order for one entry pair
-    double2 s = sum_group2(root, min(nit, kFanIn), E, e);
-    for (int k = kFanIn; k < nit; k += kFanIn) {
-      const double2 t = sum_group2(root + static_cast<int64_t>(k) * E, min(nit - k, kFanIn), E, e);
-      s.x += t.x;
-      s.y += t.y;
-    }
-    return s;
-  };
-  const int e = tile * 256 + 2 * tid;
-  double2 g{0.0, 0.0};
-  if (tid < 128) {
-    g = gather(e);
-  } else if (tid < 128 + D / 2) {
-    const int r = 2 * (tid - 128);
-    const double2 s = r < rows ? gather(GRAM + r) : double2{0.0, 0.0};
-    S_lds[r] = s.x;
-    S_lds[r + 1] = s.y;
-  } else if (tid < 128 + D / 2 + D) {
-    const int r = tid - 128 - D / 2;
+  if (tid < RG::GATHER) {
+    const int q = tid / PAIRS, k = tid % PAIRS;
+    const int e = k < 128 ? tile * 256 + 2 * k : GRAM + 2 * (k - 128);
+    const bool live = q * kFanIn < nit && (k < 128 || 2 * (k - 128) < rows);
+    if (live)
+      part[q][k] = sum_group2(slabs0 + static_cast<int64_t>(first + q * kFanIn) * E,
+                              min(nit - q * kFanIn, kFanIn), E, e);
+  } else if (tid < RG::GATHER + D) {
+    const int r = tid - RG::GATHER;
     shift_lds[r] = r < rows ? static_cast<double>(pos[static_cast<int64_t>(r) * ld +
                                                       cell_off[cell]])
                             : 0.0;
+  }
+  __syncthreads();
+  const int ng = (nit + kFanIn - 1) / kFanIn;
+  auto total = [&](int k) {  // gather_root's order: group 0, then += group 1, 2, ...
+    double2 s = part[0][k];
+    for (int q = 1; q < ng; ++q) {
+      s.x += part[q][k].x;
+      s.y += part[q][k].y;
+    }
+    return s;
+  };
+  if (tid >= 128 && tid < PAIRS) {
+    const int r = 2 * (tid - 128);
+    const double2 s = r < rows ? total(tid) : double2{0.0, 0.0};
+    S_lds[r] = s.x;
+    S_lds[r + 1] = s.y;
   }
   __syncthreads();
   const double n = static_cast<double>(cnt);
@@ -677,14 +693,19 @@ __global__ __launch_bounds__(kRootThreads) void root_finalize_kernel(
     out_mean[static_cast<int64_t>(cell) * rows + tid] = (shift_lds[tid] + S_lds[tid] / n) + o;
   }
   if (tid >= 128) return;
-  double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
+  const int e = tile * 256 + 2 * tid;
   int i0, j0, i1, j1;
   decode_entry(e, RB, i0, j0);
   decode_entry(e + 1, RB, i1, j1);
+  const bool use0 = i0 < rows && j0 < rows && i0 <= j0;
+  const bool use1 = i1 < rows && j1 < rows && i1 <= j1;
+  if (!use0 && !use1) return;
+  const double2 g = total(tid);
+  double *cov = out_cov + static_cast<int64_t>(cell) * rows * rows;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    if (!(h ? use1 : use0)) continue;
     const int i = h ? i1 : i0, j = h ? j1 : j0;
-    if (!(i < rows && j < rows && i <= j)) continue;
     const double c = ((h ? g.y : g.x) - S_lds[i] * S_lds[j] / n) / (n - 1.0);
     cov[i * rows + j] = c;
     cov[j * rows + i] = c;
@@ -709,7 +730,7 @@ static int launch(const P *pos, int64_t ld, int T, const double *origin, const i
                        T, origin, lg_wq, tree, mean, cov, mp);
     if (defer_root(RB, MINK, true))
       hipLaunchKernelGGL((root_finalize_kernel<P, RB>),
-                         dim3(static_cast<unsigned>(n_cells * n_tiles(RB))), dim3(kRootThreads), 0,
+                         dim3(static_cast<unsigned>(n_cells * n_tiles(RB))), dim3(RootGeo<RB>::THREADS), 0,
                          s, cnt, off, n_cells, grid, pos, ld, T, origin, tree.slabs[0], mean, cov);
     return CCMPC_OK;
   }
