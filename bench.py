@@ -8,9 +8,10 @@ in HBM -> per-cell moments -> every (cell, t, tau) MVOE half-space record.  One 
 cycle, replayed as one hipGraph.  Synthetic seeded particle clouds (no Trajectron++ weights or
 CARLA exist here).
 
-Multi-GPU (torchrun, one process per GPU): every rank plans its own independent scene
-(weak scaling, no data-path collective); value = cycles completed by all ranks / max-over-ranks
-wall time.  Rank 0 prints ONE JSON line.
+Multi-GPU (one process per GPU): every rank plans its own independent scene (weak scaling, no
+data-path collective); value = cycles completed by all ranks / max-over-ranks wall time.  Rank
+0 prints ONE JSON line.  Under torchrun the ranks come from its env; `bench.py --gpus N` run
+alone starts the N ranks itself as one child torchrun (launch_ranks) before any GPU call.
 """
 import argparse
 import glob
@@ -33,7 +34,7 @@ HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 HBM_ACHIEVABLE = 6.29e12   # MI355X_MICROARCH.md: 6.29 TB/s measured (float4 copy, 79 % of spec)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
@@ -51,7 +52,12 @@ def parse():
                          "the fused ideal rollout)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip 'c4_sharded' (BASELINE configs[3] sharded over the ranks)")
-    return ap.parse_args()
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
+                    help="process-group backend for N > 1 (default nccl = RCCL; gloo only to "
+                         "rehearse several ranks on one card)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, report the world size and exit (no GPU work)")
+    return ap.parse_args(argv)
 
 
 def time_config(dev, seed, name, O, N, T, scenes, cold=True):
@@ -259,23 +265,86 @@ def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True):
     return out
 
 
+def bench_backend(args):
+    """nccl (= RCCL over xGMI) unless --backend / CCMPC_BENCH_BACKEND says gloo, which exists
+    only to rehearse the N > 1 code path with several ranks on one card (RCCL will not form a
+    communicator from two ranks on one device)."""
+    return args.backend or os.environ.get("CCMPC_BENCH_BACKEND", "nccl")
+
+
+def launcher_argv(args, argv, env):
+    """The child command that starts `--gpus N` ranks, or None when this process is already a
+    rank (torchrun set WORLD_SIZE) or N == 1.  `python -m torch.distributed.run` as a CHILD
+    process of a parent that has not touched the GPU (no exec; counting devices does not
+    initialise HIP): one process per GPU, rendezvous on 127.0.0.1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+            f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` run directly (not under torchrun): start the N ranks as one child
+    torchrun and return its exit code; rank 0 of the child prints the JSON line on the inherited
+    stdout.  None when this process should run the benchmark itself."""
+    cmd = launcher_argv(args, sys.argv[1:], os.environ)
+    if cmd is None:
+        return None
+    if bench_backend(args) == "nccl" and not args.launch_check:
+        have = torch.cuda.device_count()          # does not initialise HIP on this image
+        if have < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} needs {args.gpus} visible GPUs, found {have} "
+                             "(--backend gloo rehearses several ranks on one card)")
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["CCMPC_BENCH_SPAWNED"] = "1"
+    if args.backend:
+        env["CCMPC_BENCH_BACKEND"] = args.backend
+    return subprocess.run(cmd, env=env).returncode
+
+
 def init_dist(args):
-    """One process per GPU (torchrun env).  Backend nccl (= RCCL over xGMI); the env override
-    CCMPC_BENCH_BACKEND=gloo exists only to rehearse the N > 1 code path with several ranks on
-    one card (RCCL will not form a communicator from two ranks on one device)."""
+    """One process per GPU (torchrun env), checked against --gpus on every path."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun "
+                         f"--nproc-per-node {args.gpus}, or run bench.py --gpus N alone")
     if world > 1:
         import torch.distributed as dist
-        backend = os.environ.get("CCMPC_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
+        backend = bench_backend(args)
+        if args.launch_check:                       # launcher rehearsal: no GPU touched
+            dist.init_process_group("gloo")
+        elif backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     return world, rank, local
+
+
+def launch_check(world, rank):
+    """--launch-check: every rank reports what the launcher gave it (no GPU work); rank 0
+    prints one JSON line.  Used by the CPU test of the launcher."""
+    ranks = [rank]
+    if world > 1:
+        import torch.distributed as dist
+        got = [None] * world
+        dist.all_gather_object(got, {"rank": rank, "world": dist.get_world_size()})
+        ranks = [g["rank"] for g in got]
+        assert all(g["world"] == world for g in got)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": ranks}), flush=True)
 
 
 def barrier(world):
@@ -478,15 +547,37 @@ def episode_c1(dev, cpu_steps=2, with_cpu=True):
     return out
 
 
-def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8):
-    """The drop-in planning step at C2's shape (O = 4 OVs, np = 5000, ph = 8) through
-    MidlevelAgent.predict_and_constrain: do_prediction (the sampler tail) + make_ovehicles +
-    compute_obstacle_constraints_GMM_Minkowski_idealprediction (v8ideal/__init__.py:414-505,
-    :781-964) -- one hipGraph replay per step with the packed input upload and the record /
-    moment / L4 download inside it, then the 9-tuple on the host (constraints built lazily).
-    A fresh Philox seed per step.  Beside it: the same step through the eager drop-in calls,
-    and the oracle's make_ovehicles + Minkowski generator (with vertices / L4) on the same
-    sampler output, on one host core."""
+def pp_sampler_draws(pmf, gmm, N, T, seed, dev):
+    """Device tensors shaped as Trajectron++ hands them over (prediction.py:81-86): z ~ p(z|x)
+    (torch.multinomial: the one-hot sample's argmax, :103), every sample's own GMM parameters
+    (the latent's row + a per-sample perturbation, as an autoregressive decoder's outputs differ
+    per sample), and GMM2D.rsample's standard-normal noise."""
+    g = torch.Generator(device=dev).manual_seed(int(seed))
+    O = pmf.shape[0]
+    z = torch.multinomial(torch.as_tensor(pmf, device=dev), N, replacement=True,
+                          generator=g).to(torch.int32)
+    base = torch.as_tensor(gmm, device=dev)
+    pp = torch.stack([base[o][z[o].long()] for o in range(O)])
+    pp = pp + 0.02 * torch.randn(pp.shape, device=dev, generator=g)
+    pp[..., 4].clamp_(-0.9, 0.9)
+    eps = torch.randn((O, N, T, 2), device=dev, generator=g)
+    return pp.float().contiguous(), z, eps
+
+
+def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8, per_particle=False,
+                eager_steps=50, cpu_reps=5, label="C2 shape"):
+    """The drop-in planning step through MidlevelAgent.predict_and_constrain: do_prediction
+    (the sampler tail) + make_ovehicles + compute_obstacle_constraints_GMM_Minkowski_
+    idealprediction (v8ideal/__init__.py:414-505, :781-964) -- one hipGraph replay per step
+    with the packed input upload and the record / moment / L4 download inside it, then the
+    9-tuple on the host (constraints built lazily).  Default: C2's shape (O = 4, np = 5000,
+    ph = 8) in the synthetic per-latent sampler mode, a fresh Philox seed per step.
+    per_particle: the upstream boundary instead -- every sample's GMM parameters, z and the
+    noise as device tensors (pp_sampler_draws), copied device-to-device into the graph's
+    buffers inside each timed step.  N > 8192 takes the graph's non-fused branch (sampler, then
+    ccmpc_bucket).  Beside it: the same step through the eager drop-in calls, and the oracle's
+    make_ovehicles + Minkowski generator (with vertices / L4) on the same sampler output, on one
+    host core."""
     from ccmpc import engine, episode, ovehicle, planner
     init, pmf, gmm = episode.synthetic_gmm(O, T=ph, seed=20251015)
     minpos = np.array([150.0, -120.0])
@@ -498,10 +589,17 @@ def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8):
     ref = np.array([ego + [4.0 * (t + 1), 0.5 * (t + 1)] for t in range(ph)])
     agent = planner.MidlevelAgent(prediction_horizon=ph, device=dev)
     params = episode.Params(O, K, 0)
+    draws = pp_sampler_draws(pmf, gmm, N, ph, 7, dev) if per_particle else None
+
+    def sampler_of(seed):
+        if per_particle:
+            return dict(init_state=init, latent_pmf=pmf, gmm=draws[0], z=draws[1], eps=draws[2],
+                        N=N, seed=seed, per_particle=True)
+        return dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=seed)
 
     def graph_step(seed):
-        sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=seed)
-        return agent.predict_and_constrain(params, sampler, eps, ph, ref, minpos, pasts)
+        return agent.predict_and_constrain(params, sampler_of(seed), eps, ph, ref, minpos,
+                                           pasts)
 
     for i in range(20):
         graph_step(i)
@@ -517,7 +615,10 @@ def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8):
     eager = planner.MidlevelAgent(prediction_horizon=ph, device=dev)
 
     def eager_step(seed):
-        z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=seed, device=dev)
+        s = sampler_of(seed)
+        z, store = engine.sample_unicycle(init, pmf, s["gmm"], N, ph, seed=seed, device=dev,
+                                          z=s.get("z"), eps=s.get("eps"),
+                                          per_particle=per_particle)
         ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, device=dev)
         return eager.compute_obstacle_constraints_GMM_Minkowski_idealprediction(
             params, ovs, None, None, None, eps, None, ph, ref)
@@ -525,30 +626,38 @@ def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8):
     for i in range(5):
         eager_step(i)
     te = []
-    for i in range(50):
+    for i in range(eager_steps):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         eager_step(2000 + i)
         te.append(time.perf_counter() - t0)
     med = statistics.median(ts)
-    res = {"config": f"C2 shape drop-in step: {O} OVs x np={N} x ph={ph}, L=25 latent values, "
-                     f"K={K} kept modes; sampler -> bucketing -> Minkowski cycle -> L4 -> "
-                     "9-tuple (MidlevelAgent.predict_and_constrain)",
+    mode = ("per-particle GMM parameters + z + noise as device tensors (Trajectron++'s "
+            "boundary, prediction.py:81-86)" if per_particle
+            else "synthetic per-latent GMM, Philox z and noise")
+    res = {"config": f"{label} drop-in step: {O} OVs x np={N} x ph={ph}, L=25 latent values, "
+                     f"K={K} kept modes; {mode}; sampler -> bucketing -> Minkowski cycle -> L4 "
+                     "-> 9-tuple (MidlevelAgent.predict_and_constrain)",
            "steps": steps, "constraints_per_step": n_cons,
+           "graph_branch": "fused sampler+bucketing" if g.fused else "sampler -> ccmpc_bucket",
            "dropin_step_us_median": round(med * 1e6, 1),
            "dropin_step_us_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
            "graph_replay_us": round(t_graph * 1e6, 1),
            "eager_calls_step_us_median": round(statistics.median(te) * 1e6, 1),
-           "note": "wall clock per call on the host, inputs from host memory, outputs (records, "
+           "note": "wall clock per call on the host, host inputs from host memory (per-particle "
+                   "tensors: device-to-device copies inside the step), outputs (records, "
                    "moments, L4, statistics) on the host when it returns; graph_replay_us = "
-                   "HIP events around back-to-back replays (packed H2D + 5 kernels + packed D2H)"}
+                   "HIP events around back-to-back replays (packed H2D + kernels + packed D2H)"}
     if with_cpu:
         from oracle import ccmpc_oracle as orc
-        z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=7, device=dev)
+        s = sampler_of(7)
+        z, store = engine.sample_unicycle(init, pmf, s["gmm"], N, ph, seed=7, device=dev,
+                                          z=s.get("z"), eps=s.get("eps"),
+                                          per_particle=per_particle)
         zc = z.cpu().numpy()
         pred = np.stack([store.cell_positions(o) for o in range(O)]).astype(np.float32)
         tc = []
-        for _ in range(5):
+        for _ in range(cpu_reps):
             t0 = time.perf_counter()
             oovs = orc.make_ovehicles(pred, zc, pmf, minpos, pasts, [np.array([4.5, 2.5])] * O,
                                       ph)
@@ -655,7 +764,13 @@ def ellipsoid_parity(ovs, ref, T, h):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world, rank, local = init_dist(args)
+    if args.launch_check:
+        launch_check(world, rank)
+        return
     dev = torch.device("cuda", torch.cuda.current_device() if world > 1 else local)
     torch.cuda.set_device(dev)
 
@@ -706,6 +821,10 @@ def main():
         "value": round(value, 2),
         "unit": "cycles/s",
         "n_gpus": world,
+        "rccl_world_size": world if _backend() == "nccl" else None,
+        "dist_backend": _backend() or "none (one rank)",
+        "launcher": ("bench.py --gpus N (child torchrun)" if os.environ.get("CCMPC_BENCH_SPAWNED")
+                     else ("torchrun" if world > 1 else "single process")),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 5),
@@ -770,6 +889,11 @@ def main():
         from threadpoolctl import threadpool_limits
         with threadpool_limits(limits=1):
             out["dropin_step_c2"] = dropin_step(dev, with_cpu=not args.no_cpu)
+            out["dropin_step_c2_pp"] = dropin_step(dev, with_cpu=False, per_particle=True)
+            # C1's real particle count (tests/Hz20/params.py:377): the graph's non-fused branch
+            out["dropin_step_c1_100k"] = dropin_step(
+                dev, steps=100, with_cpu=not args.no_cpu, O=1, N=100_000, eager_steps=20,
+                cpu_reps=2, label="C1 (n_predictions = 100 000)")
             out["episode_c1"] = episode_c1(dev, with_cpu=not args.no_cpu)
             out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
     if not args.no_sweep and rank == 0:

@@ -33,6 +33,21 @@ class ScenePredictions:
         self.cell_pmf = cell_pmf
         self.init_center = init_center
         self._l4 = None
+        self._owner = None                      # (graph, generation) when over a graph's buffers
+
+    def bind_generation(self, owner):
+        """This scene lives in the buffers of `owner` (a step.MinkowskiStepGraph) as its current
+        launch left them; a later replay of the same graph overwrites them, after which every
+        read of the device store raises instead of silently returning the newer frame's data
+        (the reference's per-frame OVehicles are independent)."""
+        self._owner = (owner, owner.generation)
+
+    def check_live(self):
+        if self._owner is not None and self._owner[0].generation != self._owner[1]:
+            raise RuntimeError(
+                "stale planning-step data: this frame's particle store was overwritten by a "
+                "later step of the same shape (read vertices / pred_positions / pred_yaws "
+                "before the next predict_and_constrain, or copy them)")
 
     @property
     def O(self):
@@ -51,6 +66,7 @@ class ScenePredictions:
         """Headings / vertices / L4 over all ph steps (cached per scene)."""
         need = (self._l4 is None or (with_yaw and self._l4["yaw"] is None)
                 or (with_vertices and self._l4["vertices"] is None))
+        self.check_live()
         if need:
             self._l4 = engine.l4(self.store, self.cell_past_last(), self.cell_bbox(),
                                  with_yaw=with_yaw, with_vertices=with_vertices)
@@ -101,6 +117,7 @@ class OVehicle:
     def pred_positions(self):
         """list over modes of (N_k, T, 2) float64 world positions (host copy, cached)."""
         if self._pos is None:
+            self.scene.check_live()
             self._pos = [self.scene.store.cell_positions(c) for c in self.cells]
         return self._pos
 
@@ -108,6 +125,7 @@ class OVehicle:
     def pred_yaws(self):
         """list over modes of (N_k, T) headings (ovehicle.py:72-76), computed on the GPU."""
         if self._yaw is None:
+            self.scene.check_live()
             st = self.scene.store
             if st.counts is None:
                 st.sync_counts()
@@ -127,6 +145,22 @@ def scene_from_positions(ov_cells, pasts, bboxes=None, device="cuda", dtype=torc
     pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
     scene = ScenePredictions(store, K, [p[-1] for p in pasts], bboxes)
     return [OVehicle(scene, o, past=pasts[o]) for o in range(len(K))]
+
+
+def check_kept_modes_drawn(centre, K):
+    """A kept mode (p(z|x) > filter) that drew no particle of its own: the reference builds
+    `np.array([])` for it (v8ideal/__init__.py:493-494) and fails in from_trajectron at
+    `ps[:,0,1]` (ovehicle.py:72, IndexError) before any rare particle is assigned.  The device
+    bucketing gives that mode the centre 0 / 0 = NaN (the mean of its own particles, :80), so
+    no rare particle is ever assigned to it; the drop-in raises the reference's error instead of
+    returning that cell.  centre: per-cell init_center (host, (C, 2)), cells in (ov, k) order."""
+    bad = np.flatnonzero(np.isnan(np.asarray(centre, np.float64).reshape(-1, 2)).any(1))
+    if bad.size:
+        c = int(bad[0])
+        first = np.concatenate([[0], np.cumsum(K)])
+        o = int(np.searchsorted(first, c, side="right") - 1)
+        raise IndexError(f"too many indices for array: kept mode {c - int(first[o])} of OV {o} "
+                         "drew no particle (ovehicle.py:72 fails on its empty prediction array)")
 
 
 def make_ovehicles(predictions, z, latent_probs, minpos, pasts, bboxes=None, T=None,
@@ -155,6 +189,7 @@ def make_ovehicles(predictions, z, latent_probs, minpos, pasts, bboxes=None, T=N
     store, K, pmf, centre = engine.bucket(z_dev, store_in, latent_probs, mp,
                                           filter_pmf=filter_pmf)
     store.sync_counts()
+    check_kept_modes_drawn(centre.cpu().numpy(), K)
     pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
     bboxes = np.tile(DEFAULT_BBOX, (O, 1)) if bboxes is None else np.asarray(bboxes)
     scene = ScenePredictions(store, K, [p[-1] for p in pasts], bboxes, pmf, centre)

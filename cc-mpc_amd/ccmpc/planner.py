@@ -23,6 +23,7 @@ Differences from the reference, all at the boundary:
   * the unseeded RNG of predict_ideal (:2664, :2699) is a Philox stream keyed by
     (seed, frame, cell), so runs are reproducible.
 """
+import collections
 import functools
 import os
 
@@ -355,7 +356,11 @@ class MidlevelAgent:
         self.mpc_params = mpc.MPCParams.reference_defaults()
         self._ltv = None                   # (x_init, T_full) -> (xbar, Gamma), first step's
         self._qp = {}
-        self._graphs = {}                  # (O, N, ph, L, K) -> step.MinkowskiStepGraph
+        # (O, N, ph, L, K, per_particle, eps_in) -> step.MinkowskiStepGraph, least recently
+        # used first: a graph holds pinned packs, a device store and workspaces, and the kept
+        # modes per OV change from frame to frame in an episode, so the cache is bounded
+        self._graphs = collections.OrderedDict()
+        self.max_graphs = int(kwargs.get("max_graphs", 8))
         self._risk_memo = {}
 
     # ------------------------------------------------------------------------------------
@@ -623,13 +628,23 @@ class MidlevelAgent:
         (:414-467, the sampler tail of prediction.py:81-86), make_ovehicles (:469-505) and
         compute_obstacle_constraints_GMM_Minkowski_idealprediction (:781-964).
 
-        sampler: dict(init_state (O, 4), latent_pmf (O, L), gmm (O, L, ph, 5), N, seed) -- the
-        per-latent sampler inputs.  At Tsh == ph the whole chain is ONE hipGraph replay
-        (ccmpc.step.MinkowskiStepGraph, cached per (O, N, ph, L, K)): inputs up in one copy, five
-        kernels, outputs down in one copy, then the 9-tuple over host views (constraints built
-        lazily).  Below ph the generator runs on the saved moments' ideal rollout, after the
-        same sampler and bucketing calls.  Returns (ovehicles, 9-tuple).  The OVehicles and the
-        device records stay valid until the next graph step of the same shape."""
+        sampler: the sampler tail's inputs, in one of two forms --
+          per-latent (synthetic): dict(init_state (O, 4), latent_pmf (O, L), gmm (O, L, ph, 5),
+              N, seed): z and the noise are Philox draws on the device;
+          per-particle (Trajectron++'s boundary, prediction.py:81-86): dict(init_state,
+              latent_pmf, gmm (O, N, ph, 5) per-sample parameters, z (O, N) latent ids, eps
+              (O, N, ph, 2) or None, N, seed, per_particle=True), gmm / z / eps DEVICE tensors
+              as p_y_xz and sample_p leave them (no host round trip); seed keys the noise
+              when eps is None.
+        At Tsh == ph the whole chain is ONE hipGraph replay (ccmpc.step.MinkowskiStepGraph,
+        cached per shape and sampler mode in an LRU of `max_graphs`): inputs up in one copy (the
+        per-particle tensors by device copies into the graph's buffers), the sampler +
+        bucketing + cycle + L4 kernels, outputs down in one copy, then the 9-tuple over host
+        views (constraints built lazily).  Below ph the generator runs on the saved moments'
+        ideal rollout, after the same sampler and bucketing calls.  Returns (ovehicles,
+        9-tuple).  The 9-tuple's arrays are host copies; the OVehicles' device-backed fields
+        (pred_positions, pred_yaws, vertices) must be read before the next graph step of the
+        same shape -- after it they raise (ScenePredictions.check_live)."""
         from . import ovehicle, step
         T, ph = int(Tsh), self.prediction_horizon
         init = np.asarray(sampler["init_state"], np.float64)
@@ -637,38 +652,52 @@ class MidlevelAgent:
         O, L = pmf.shape
         N, seed = int(sampler["N"]), int(sampler["seed"])
         gmm = sampler["gmm"]
+        pp = bool(sampler.get("per_particle", False))
+        z_in, eps_in = sampler.get("z"), sampler.get("eps")
+        if pp and z_in is None:
+            raise ValueError("per-particle GMM parameters need the injected z (prediction.py:103)")
         pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
         past_last = np.array([p[-1] for p in pasts])
         bboxes = (_default_bboxes(O) if bboxes is None
                   else np.asarray(bboxes, np.float64).reshape(O, 2))
         if T != ph:
             z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=seed,
-                                              device=self.device)
+                                              device=self.device, z=z_in, eps=eps_in,
+                                              per_particle=pp)
             ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, bboxes,
                                           filter_pmf=filter_pmf, device=self.device)
             out = self.compute_obstacle_constraints_GMM_Minkowski_idealprediction(
                 params, ovs, None, None, None, eps_ura, None, T, ref_traj)
             return ovs, out
+        if not pp and (z_in is not None or eps_in is not None):
+            raise ValueError("injected z / eps go with per_particle=True at the graph step")
         K = (pmf > filter_pmf).sum(1).tolist()
         if min(K) == 0:
             raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent "
                              f"mode with p(z|x) > {filter_pmf} (ovehicle.py:96-97)")
-        key = (O, N, ph, L, tuple(K))
-        g = self._graphs.get(key)
+        key = (O, N, ph, L, tuple(K), pp, eps_in is not None)
+        g = self._graphs.pop(key, None)
         if g is None:
-            g = step.MinkowskiStepGraph(O, N, ph, L, K, device=self.device, R=self.R)
-            self._graphs[key] = g
-        g.set_inputs(seed, init, pmf, gmm, minpos, ref_traj,
+            g = step.MinkowskiStepGraph(O, N, ph, L, K, device=self.device, R=self.R,
+                                        per_particle=pp, eps_in=eps_in is not None)
+            while len(self._graphs) >= self.max_graphs:
+                self._graphs.popitem(last=False)           # least recently used
+        self._graphs[key] = g                              # most recently used
+        g.set_inputs(seed, init, pmf, None if pp else gmm, minpos, ref_traj,
                      self._cell_risk_host(np.asarray(eps_ura), K), past_last, bboxes,
                      filter_pmf=filter_pmf)
+        if pp:
+            g.set_device_inputs(gmm, z_in, eps_in)
         g.launch()
         # host objects that need no output are built while the graph runs
         st = g.store
         scene = ovehicle.ScenePredictions(st, K, past_last, bboxes)
+        scene.bind_generation(g)
         ovs = [ovehicle.OVehicle(scene, j, past=pasts[j]) for j in range(O)]
         vertices, direct = LazyVertices(scene, ph), _object_grid(O)
         g.wait()
         o = g.out.snapshot()            # every output in one host copy (outlives the replay)
+        ovehicle.check_kept_modes_drawn(o["centre"], K)
         st.counts = o["cnt"].tolist()
         st.offsets = o["off"].tolist()
         scene.cell_pmf, scene.init_center = o["pmf"], o["centre"]

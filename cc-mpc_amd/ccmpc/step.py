@@ -80,11 +80,24 @@ class MinkowskiStepGraph:
 
     O OVs with N particles each over T = ph steps; L latent values; K kept modes per OV (the
     host decides them from p(z|x), as make_ovehicles does, so the shape is known before the
-    step runs).  gmm_shape is (O, L, T, 5) per-latent parameters (the synthetic / per-latent
-    mode of the sampler)."""
+    step runs).
+
+    Two sampler modes:
+      per_particle=False  gmm (O, L, T, 5) per-latent parameters, z and the noise drawn by
+                          Philox on the device (the synthetic mode); gmm travels in the packed
+                          host inputs.
+      per_particle=True   the boundary Trajectron++ hands over on the GPU (prediction.py:81-86):
+                          every sample's own GMM parameters gmm[o][t][5][n] (p_y_xz's
+                          autoregressive decoder), the one-hot z's argmax (:103) and, with
+                          eps_in, GMM2D.rsample's standard-normal draws -- all DEVICE tensors,
+                          written into this graph's own device buffers (pp_gmm, pp_z, pp_eps)
+                          by set_device_inputs, never through the host.
+
+    ``generation`` counts launches: objects built over this graph's buffers (ScenePredictions)
+    record the generation they belong to and refuse reads after a later replay."""
 
     def __init__(self, O, N, T, L, K, device="cuda", dt=0.5, R=risk.R_COLLISION, tol=1e-8,
-                 maxiter=1000):
+                 maxiter=1000, per_particle=False, eps_in=False):
         self.device = engine.require_device(device)
         lib = _lib.load()
         self.O, self.N, self.T, self.L = int(O), int(N), int(T), int(L)
@@ -95,12 +108,24 @@ class MinkowskiStepGraph:
         self.P = P = max(T * (T - 1) // 2, 1)
         self.max_k = max(self.K)
         self.dt, self.R, self.tol, self.maxiter = float(dt), float(R), float(tol), int(maxiter)
+        self.per_particle, self.eps_in = bool(per_particle), bool(eps_in)
+        if self.eps_in and not self.per_particle:
+            raise ValueError("eps_in is part of the per-particle (Trajectron++ boundary) mode")
+        self.generation = 0
         f64, f32, i32, i64, u8 = torch.float64, torch.float32, torch.int32, torch.int64, torch.uint8
-        self.inp = Pack([("seed", (1,), i64), ("init", (O, 4), f64), ("cdf", (O, L), f64),
-                         ("gmm", (O, L, T, 5), f32), ("keep", (O, L), i32), ("nk", (O,), i32),
+        gmm_field = [] if self.per_particle else [("gmm", (O, L, T, 5), f32)]
+        self.inp = Pack([("seed", (1,), i64), ("init", (O, 4), f64), ("cdf", (O, L), f64)]
+                        + gmm_field +
+                        [("keep", (O, L), i32), ("nk", (O,), i32),
                          ("base", (O,), i32), ("minpos", (O, 2), f64), ("region", (O,), i64),
                          ("origin", (C, 2), f64), ("ref", (1, T, 2), f64), ("risk", (C, 3), f64),
                          ("past", (C, 2), f64), ("bbox", (C, 2), f64)], self.device)
+        self.pp_gmm = self.pp_z = self.pp_eps = None
+        if self.per_particle:       # device-side inputs (particle-minor, the sampler's layout)
+            self.pp_gmm = torch.zeros((O, T, 5, N), dtype=f32, device=self.device)
+            self.pp_z = torch.zeros((O, N), dtype=i32, device=self.device)
+            if self.eps_in:
+                self.pp_eps = torch.zeros((O, T, 2, N), dtype=f32, device=self.device)
         self.out = Pack([("rec", (C, P, 128), u8), ("pl", (C, T), f64), ("mean", (C, T, 2), f64),
                          ("cov", (C, 2 * T, 2 * T), f64), ("A", (C, T, 4, 2), f64),
                          ("b", (C, T, 4), f64), ("yaw_mean", (C, T), f64),
@@ -157,17 +182,22 @@ class MinkowskiStepGraph:
         i, o, st = self.inp, self.out, self.store
         O, N, T, L = self.O, self.N, self.T, self.L
         ws = self.bucket_ws
+        if self.per_particle:
+            gmm, layout, z_in, eps = (p(self.pp_gmm), _lib.GMM_PER_PARTICLE, p(self.pp_z),
+                                      p(self.pp_eps))
+        else:
+            gmm, layout, z_in, eps = p(i.d("gmm")), _lib.GMM_PER_LATENT, None, None
         if self.fused:
             return [(lib.ccmpc_sample_bucket, (
-                p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None, None,
+                p(i.d("init")), p(i.d("cdf")), L, gmm, layout, z_in, eps,
                 O, N, T, self.dt, 0, p(i.d("seed")), 0, p(i.d("keep")), p(i.d("nk")),
                 p(i.d("base")), self.max_k, p(i.d("minpos")), p(i.d("region")), p(ws),
                 ws.numel(), None, p(st.pos), st.ld, p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")),
                 p(o.d("centre")), s))]
         sm = self.samples
         return [(lib.ccmpc_sample_unicycle_ex, (
-                    p(i.d("init")), p(i.d("cdf")), L, p(i.d("gmm")), _lib.GMM_PER_LATENT, None,
-                    None, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld,
+                    p(i.d("init")), p(i.d("cdf")), L, gmm, layout, z_in,
+                    eps, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld,
                     s)),
                 (lib.ccmpc_bucket, (p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
                                     p(i.d("nk")), p(i.d("base")), self.max_k,
@@ -252,7 +282,12 @@ class MinkowskiStepGraph:
         i.h("seed")[0] = sd - (1 << 64) if sd >= (1 << 63) else sd
         i.h("init").reshape(-1)[:] = np.asarray(init_state, np.float64).reshape(-1)
         np.cumsum(pmf, axis=1, out=i.h("cdf"))
-        np.copyto(i.h("gmm").reshape(-1), np.asarray(gmm).reshape(-1), casting="same_kind")
+        if self.per_particle:
+            if gmm is not None:
+                raise ValueError("per-particle graph: pass the device parameters to "
+                                 "set_device_inputs, not set_inputs")
+        else:
+            np.copyto(i.h("gmm").reshape(-1), np.asarray(gmm).reshape(-1), casting="same_kind")
         mp = np.asarray(minpos, np.float64)
         if mp.size == 2:
             i.h("minpos")[:] = mp.reshape(1, 2)
@@ -269,6 +304,43 @@ class MinkowskiStepGraph:
                 i.h(name).reshape(-1)[:] = v.reshape(-1)
             else:
                 np.take(v.reshape(O, 2), self._ov_of_cell, axis=0, out=i.h(name))
+
+    def set_device_inputs(self, gmm, z, eps=None):
+        """The per-particle mode's device inputs for the next launch, as Trajectron++ leaves
+        them on the GPU (prediction.py:81-86): gmm (O, N, T, 5) -- or already the sampler's
+        particle-minor (O, T, 5, N) -- z (O, N) latent ids (the one-hot z's argmax, :103) and,
+        when the graph was built with eps_in, eps (O, N, T, 2) standard-normal draws (or (O, T,
+        2, N)).  Each is one device-to-device copy on the current stream into the graph's own
+        buffer, ordered before the replay; a tensor that already IS the buffer is not copied
+        (an upstream that writes pp_gmm / pp_z / pp_eps directly costs nothing here).  z is not
+        validated on the host (that would synchronise): the kernels clamp it into [0, L)."""
+        if not self.per_particle:
+            raise ValueError("set_device_inputs needs a graph built with per_particle=True")
+        O, N, T = self.O, self.N, self.T
+
+        def put(dst, src, natural, minor, perm):
+            if not torch.is_tensor(src) or src.device != self.device:
+                raise ValueError("per-particle inputs must be tensors on the graph's device")
+            if src.data_ptr() == dst.data_ptr() and tuple(src.shape) == tuple(dst.shape):
+                return
+            if tuple(src.shape) == minor:
+                dst.copy_(src)
+            elif tuple(src.shape) == natural:
+                dst.copy_(src.permute(*perm))
+            else:
+                raise ValueError(f"shape {tuple(src.shape)}: expected {natural} or {minor}")
+
+        put(self.pp_gmm, gmm, (O, N, T, 5), (O, T, 5, N), (0, 2, 3, 1))
+        if not torch.is_tensor(z) or tuple(z.shape) != (O, N) or z.device != self.device:
+            raise ValueError(f"z must be a ({O}, {N}) tensor on the graph's device")
+        if z.data_ptr() != self.pp_z.data_ptr():
+            self.pp_z.copy_(z)
+        if self.eps_in:
+            if eps is None:
+                raise ValueError("this graph was built with eps_in: eps is required")
+            put(self.pp_eps, eps, (O, N, T, 2), (O, T, 2, N), (0, 2, 3, 1))
+        elif eps is not None:
+            raise ValueError("this graph draws the noise itself (built without eps_in)")
 
     def bind(self):
         """Pre-convert every argument of the step's C-ABI calls for the current stream (the
@@ -297,6 +369,7 @@ class MinkowskiStepGraph:
     def launch(self, direct=False):
         """Enqueue one step (inputs up, the kernels, outputs down) without waiting: one graph
         replay, or (direct) the bound C-ABI calls."""
+        self.generation += 1
         if direct:
             if getattr(self, "_calls", None) is None:
                 self.bind()

@@ -642,6 +642,10 @@ struct RootGeo {
   static constexpr int PAIRS = 128 + D / 2;               // tile pairs, then row-sum pairs
   static constexpr int GATHER = kRootGroups * PAIRS;      // gather threads
   static constexpr int THREADS = (GATHER + D + 63) / 64 * 64;  // + the shift loads
+  // a CCMPC_ROOT_FANIN build knob too wide for one workgroup must fail here, not at launch
+  static_assert(THREADS <= 1024, "deferred root: kRootFanIn too wide for one workgroup");
+  static_assert(sizeof(double2) * kRootGroups * PAIRS + 2 * sizeof(double) * D <= 64 * 1024,
+                "deferred root: LDS partials exceed the static 64 KiB");
 };
 template <typename P, int RB>
 __global__ __launch_bounds__(RootGeo<RB>::THREADS) void root_finalize_kernel(

@@ -47,8 +47,14 @@ constexpr int kFWaves = kFThreads / 64;
 constexpr int kFGroups = kFusedMaxN / kFP;    // centre groups (P1 blocks) per OV at most
 constexpr int kRThreads = 256;                // P2: rare-list slots per block
 constexpr int kRWaves = kRThreads / 64;
+// per-OV header: tot[kMaxKept + 1] at h[0..], the int64 cell starts cstart[kMaxKept] at
+// h + 2 * kMaxKept
 constexpr int kHdrInts = 64;
-constexpr int kCntStride = 32;                // >= kMaxKept + 1                  // per-OV header: tot[kMaxKept + 1], cstart[kMaxKept]
+// per-group category counts: kept modes 0..K-1, then the rare count
+constexpr int kCntStride = 32;
+static_assert(kMaxKept + 1 <= 2 * kMaxKept, "tot[] must end before the cell starts");
+static_assert(4 * kMaxKept <= kHdrInts, "cell starts (int64) must fit the per-OV header");
+static_assert(kCntStride >= kMaxKept + 1, "group counts: one slot per kept mode + rare");
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
 __device__ unsigned long long g_fused_ts[3][kStepProbeWG * kStepProbeSlots];
 #define FUSED_TS(kern, k) CCMPC_STEP_TS(g_fused_ts[kern], k)

@@ -53,6 +53,59 @@ def test_episode_schedule_matches_oracle_chain(gpu):
             assert c.d == pytest.approx(r["d"], rel=1e-8)
 
 
+def test_episode_at_reference_scale(gpu):
+    """C1 at the reference's own scale: one OV, n_predictions = 100 000 particles per frame
+    (tests/Hz20/params.py:372-383, the "np5000" label) and 1e6-sample predict_ideal rollouts
+    (v8ideal/__init__.py:2640) on every shrinking step.  Frames 0 and 10 are chained against
+    the oracle (frame 0 on the sampler's particles; frame 10 on the oracle's own 1e6-sample
+    rollout of frame 0's moments with the same Philox draws); the rest of the schedule (T = 6..1,
+    then two receding affine steps) is checked by properties: every record OK, the reference's
+    record counts, each record's centre equal to the saved moments' mean at its t, and the
+    lower bounds probabilities."""
+    from ccmpc import episode
+    n_ideal, seed = 1_000_000, 11
+    rep = episode.EpisodeReplay(O=1, N=100_000, ph=8, n_ideal=n_ideal, receding_steps=2,
+                                seed=seed, device=gpu)
+    mom = None
+    for frame, T, kind in rep.schedule():
+        ovs, out = rep.step(frame, T, kind)
+        K = [ov.n_states for ov in ovs]
+        assert sum(sum(p.shape[0] for p in ov.pred_positions) for ov in ovs) == 100_000
+        cons = out[0]
+        if kind == "affine":
+            assert len(cons) == sum(K) * T and all(c.side in (-1, 1) for c in cons)
+            continue
+        P = T * (T - 1) // 2
+        assert len(cons) == sum(K) * P, (frame, T)
+        h = rep.agent.last_records.reshape(sum(K), -1)[:, :P]
+        assert np.all(h["status"] == 0)
+        mean = rep.agent._moments[frame][0]
+        mean = mean.cpu().numpy() if hasattr(mean, "cpu") else np.asarray(mean)
+        for c in range(sum(K)):
+            t_of = h[c]["t_tau"] >> 16
+            np.testing.assert_array_equal(h[c]["mean0"], mean[c, t_of, 0])
+            np.testing.assert_array_equal(h[c]["mean1"], mean[c, t_of, 1])
+            assert np.all((h[c]["lower_bound"] >= 0) & (h[c]["lower_bound"] <= 1))
+        if frame > 10:
+            continue
+        ref = rep.ref_traj(frame)
+        oracle_ovs = _oracle_ovs(ovs, rep.ph)
+        if T == rep.ph:
+            want = orc.minkowski_generator(oracle_ovs, T, rep.ph, ref, with_l4=False)
+            mom = orc.save_moments([ov.pred_positions for ov in oracle_ovs], T)
+        else:
+            ideal = orc.predict_ideal(mom, K, T, n_ideal, seed=seed * 1_000_003 + frame)
+            want = orc.minkowski_generator(oracle_ovs, T, rep.ph, ref, ideal_trajs=ideal,
+                                           with_l4=False)
+            del ideal
+        recs = want["records"]
+        assert len(recs) == len(cons)
+        for c, r in zip(cons, recs):
+            assert (c.ov, c.k, c.t, c.tau) == (r["ov"], r["k"], r["t"], r["tau"])
+            assert c.which == r["which"] and c.side == r["side"], (frame, T, c)
+            assert c.d == pytest.approx(r["d"], rel=1e-8)
+
+
 def test_episode_timing_log(gpu):
     from ccmpc import episode
     rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=100_000, receding_steps=2,
