@@ -14,6 +14,35 @@ def cells_from_fixture(g):
     return out
 
 
+REFLOOP = ["refloop_o2_t8", "refloop_o1_t12", "refloop_o3_t12", "refloop_o2_t40",
+           "refloop_shrink_t7"]
+
+
+def refloop_inputs(g):
+    """A refloop_* fixture (the reference's own generator loops, make_golden.py
+    pin_generator_glue): (K, T, ph, cells per OV, yaws per OV (the ones the reference read),
+    ideal clouds per cell or None)."""
+    T, ph = int(g["T"]), int(g["ph"])
+    K = [int(k) for k in g["K"]]
+    cells = cells_from_fixture(g)
+    yaws, out_c, out_y, j, y0 = g["yaws"], [], [], 0, 0
+    for k in K:
+        out_c.append(cells[j:j + k])
+        ys = []
+        for c in cells[j:j + k]:
+            ys.append(yaws[y0:y0 + c.shape[0]])
+            y0 += c.shape[0]
+        out_y.append(ys)
+        j += k
+    ideal = None
+    if "ideal" in g.files:
+        ideal, o = [], 0
+        for n in g["ideal_counts"]:
+            ideal.append(g["ideal"][o:o + n])
+            o += n
+    return K, T, ph, out_c, out_y, ideal
+
+
 def ovehicles_from_fixture(g):
     T = int(g["T"])
     K = [int(k) for k in g["K"]]

@@ -455,14 +455,236 @@ def pin_predict_ideal(rng):
              x0=np.array(x0s), rows=rows, traj_rows=sel, traj_mean=mean, traj_cov=cov)
 
 
+# ---- the generator loops themselves (rows a9, a10, a11, a3) ---------------------------------
+class _XY:
+    """temp_x[t][i] (v8ideal/__init__.py:2932: X[t, 0], X[t, 1]) -- a marker of the step."""
+
+    def __init__(self, t):
+        self.t = t
+
+
+class _Stack:
+    """cp.vstack([temp_x[t][0], temp_x[t][1]]): `n.T @ it` becomes the linear form n . x_t.
+    __array_ufunc__ = None makes numpy's matmul defer to __rmatmul__."""
+    __array_ufunc__ = None
+
+    def __init__(self, t):
+        self.t = t
+
+    def __rmatmul__(self, n):
+        return _Linear(self.t, np.array(n, dtype=float))
+
+
+class _Linear:
+    """n . x_t; a comparison with a right-hand side is the recorded constraint."""
+    __array_ufunc__ = None
+
+    def __init__(self, t, n):
+        self.t, self.n = t, n
+
+    def __ge__(self, rhs):
+        return (+1, self.t, self.n, complex(rhs))
+
+    def __le__(self, rhs):
+        return (-1, self.t, self.n, complex(rhs))
+
+
+def _recording_cp():
+    """The slice of cvxpy the generators touch with road-boundary constraints off: vstack of
+    two temp_x entries and a 2-norm of a constant vector (evaluated)."""
+    import types
+
+    def vstack(items):
+        assert len(items) == 2 and items[0].t == items[1].t
+        return _Stack(items[0].t)
+
+    def norm(x, p=2):
+        assert p == 2
+        return np.linalg.norm(np.asarray(x), 2)
+    return types.SimpleNamespace(vstack=vstack, norm=norm)
+
+
+def reference_generators():
+    """The reference's own compute_obstacle_constraints_GMM_Minkowski_idealprediction
+    (v8ideal/__init__.py:781-964), compute_obstacle_constraints_GMM_affine (:1378-1539) and
+    save_moments (:2575-2618), each taken from the file's syntax tree unchanged and executed in a
+    namespace of numpy / scipy / the reference makeconstraint module and a recording `cp`.
+    Outside their class body the methods' private names are not mangled, so the `self` they
+    get carries the attributes `__params`, `__prediction_horizon`, `__ego_vehicle` literally;
+    predict_ideal, __compute_vertices and __compute_overapproximations (pinned separately:
+    ideal_ref.npz, ovehicle_l4.npz) are stubs; save_moments' pickle.dump is captured."""
+    import copy
+    import logging
+    import types
+    import scipy.linalg
+    import scipy.stats
+    path = os.path.join(REF_MID, "v8ideal", "__init__.py")
+    ns = {"np": np, "scipy": scipy_mod(), "linalg": scipy.linalg, "norm": scipy.stats.norm,
+          "makeconstraint": load_reference(), "cp": _recording_cp(), "logging": logging,
+          "copy": copy, "os": os}
+    saved = {}
+
+    class _File:
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    ns_sm = dict(ns, open=lambda *a, **k: _File(),
+                 pickle=types.SimpleNamespace(dump=lambda obj, f: saved.update(moments=obj)))
+    mink = reference_function(path, "compute_obstacle_constraints_GMM_Minkowski_idealprediction",
+                              cls="MidlevelAgent", namespace=ns)
+    aff = reference_function(path, "compute_obstacle_constraints_GMM_affine",
+                             cls="MidlevelAgent", namespace=ns)
+    save_moments = reference_function(path, "save_moments", cls="MidlevelAgent",
+                                      namespace=ns_sm)
+    return mink, aff, save_moments, saved
+
+
+def _agent_self(ph, save_moments, ideal=None):
+    import types
+    me = types.SimpleNamespace(road_boundary_constraints=False)
+    setattr(me, "__params", types.SimpleNamespace(M_big=10_000, L=4))
+    setattr(me, "__prediction_horizon", ph)
+    setattr(me, "__ego_vehicle", types.SimpleNamespace(id=0))
+    setattr(me, "__compute_vertices", lambda params, ovehicles: None)
+    setattr(me, "__compute_overapproximations", lambda params, ovehicles, vertices: (None, None))
+    me.predict_ideal = lambda ovehicles, T, ego_id, params: ideal
+    me.save_moments = lambda *a: save_moments(me, *a)
+    return me
+
+
+def _grid_cells(grid, K):
+    return np.array([grid[o][k] for o in range(len(K)) for k in range(K[o])], dtype=float)
+
+
+def run_reference_generators(cells_per_ov, yaws_per_ov, T, ph, ref_traj, ideal=None,
+                             with_affine=True):
+    """Both reference generators on one planning step; returns npz-ready arrays."""
+    import types
+    mink, aff, save_moments, saved = reference_generators()
+    K = [len(c) for c in cells_per_ov]
+    O = len(K)
+    ovs = [types.SimpleNamespace(n_states=K[o], pred_positions=list(cells_per_ov[o]),
+                                 pred_yaws=list(yaws_per_ov[o])) for o in range(O)]
+    params = types.SimpleNamespace(O=O, K=np.array(K), frame=40)
+    eps_ura = np.zeros((O, max(K)))
+    for o in range(O):
+        eps_ura[o, :] = 0.05 / O                    # v8ideal/__init__.py:2920-2926
+    temp_x = [[_XY(t), _XY(t), 1] for t in range(ph)]
+    out = {}
+    for kind, fn in (("mk", mink), ("aff", aff)):
+        if kind == "aff" and not with_affine:
+            continue
+        me = _agent_self(ph, save_moments, ideal)
+        saved.clear()
+        res = fn(me, params, ovs, None, None, temp_x, eps_ura, None, T, ref_traj)
+        cons, ovc, st_mean, st_cov = res[0], res[4], res[6], res[7]
+        assert all(isinstance(c, tuple) for c in cons)
+        out[f"{kind}_side"] = np.array([c[0] for c in cons], np.int64)
+        out[f"{kind}_t"] = np.array([c[1] for c in cons], np.int64)
+        out[f"{kind}_n"] = np.array([c[2] for c in cons]).reshape(-1, 2)
+        rhs = np.array([c[3] for c in cons])
+        assert np.all(rhs.imag == 0)
+        out[f"{kind}_rhs"] = rhs.real
+        out[f"{kind}_ovconstraint"] = np.bool_(ovc)
+        out[f"{kind}_state_mean"] = np.stack([_grid_cells(g, K) for g in st_mean], 1)
+        out[f"{kind}_state_cov"] = np.stack([_grid_cells(g, K) for g in st_cov], 1)
+        if kind == "mk":
+            if T == ph:
+                out["mk_prob_lower_save"] = np.array(getattr(me, "__prob_lower_save"), float)
+            mom = saved["moments"]
+            C = sum(K)
+            xc = np.zeros((C, T, T, 2, 2))
+            c = 0
+            for o in range(O):
+                for k in range(K[o]):
+                    for t in range(T):
+                        for tau in range(t):
+                            xc[c, t, tau] = mom["cross_cov"][o][k][t][tau]
+                    c += 1
+            out["mom_mean"] = np.array([[mom["mean_p0p1"][o][k][t] for t in range(T)]
+                                        for o in range(O) for k in range(K[o])])
+            out["mom_cov"] = np.array([[mom["cov_p0p1"][o][k][t] for t in range(T)]
+                                       for o in range(O) for k in range(K[o])])
+            out["mom_xcov"] = xc
+    return out
+
+
+def _fixture_inputs(cells_per_ov, T, ph, ref_traj):
+    pasts = np.array([[c[0][0, 0, 0] - 4.0, c[0][0, 0, 1] - 1.0] for c in cells_per_ov])
+    yaws = [[orc._step_yaws(c, pasts[o], ph) for c in cells]
+            for o, cells in enumerate(cells_per_ov)]
+    counts, flat = pack_cells([c for cs in cells_per_ov for c in cs])
+    return pasts, yaws, dict(T=T, ph=ph, K=np.array([len(c) for c in cells_per_ov]),
+                             counts=counts, positions=flat, ref_traj=ref_traj, past=pasts,
+                             yaws=np.concatenate([y for ys in yaws for y in ys]))
+
+
+def pin_generator_glue(rng):
+    """The reference's own generator loops on five planning steps -> tests/golden/refloop_*.npz:
+    the two whole-cycle fixtures' inputs (cycle_o2_t8, cycle_o1_t12), a multi-OV T = 12 step, a
+    T = 40 step (780 (t, tau) pairs per cell), and one shrinking step (ph = 8, T = 7) on
+    injected ideal trajectories (the T < ph switch :885-888, eps / ph with ph != T)."""
+    def ego_ref(cells, T):
+        ego = np.array(cells[0][0][:, 0].mean(0)) + np.array([-12.0, 3.0])
+        return np.array([ego + np.array([4.0 * (t + 1), 0.5 * (t + 1)]) for t in range(T)])
+
+    steps = []
+    for name in ("cycle_o2_t8", "cycle_o1_t12"):
+        g = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+        T, K = int(g["T"]), [int(k) for k in g["K"]]
+        flat, cnt = g["positions"], g["counts"]
+        cells, c0 = [], 0
+        for n in cnt:
+            cells.append(flat[c0:c0 + n])
+            c0 += n
+        it = iter(cells)
+        steps.append(("refloop_" + name[6:], [[next(it) for _ in range(k)] for k in K], T, T,
+                      np.asarray(g["ref_traj"]), None))
+    for name, Ks, lo, hi, T in (("refloop_o3_t12", (2, 1, 3), 150, 420, 12),
+                                ("refloop_o2_t40", (1, 2), 120, 220, 40)):
+        cells = [[random_walk_cell(rng, int(rng.integers(lo, hi)), T) for _ in range(k)]
+                 for k in Ks]
+        steps.append((name, cells, T, T, ego_ref(cells, T), None))
+    # shrinking step: sampler particles over ph = 8, ideal rollouts (T = 7) of their moments
+    ph, T, Ks = 8, 7, (2, 1)
+    cells = [[random_walk_cell(rng, int(rng.integers(200, 400)), ph) for _ in range(k)]
+             for k in Ks]
+    mom = orc.save_moments(cells, ph)
+    x0s = [[mom["mean_p0p1"][o][k][0] + rng.normal(0, 0.3, 2) for k in range(Ks[o])]
+           for o in range(len(Ks))]
+    Zs = [[[rng.normal(size=(300, 2)) for _ in range(T)] for _ in range(Ks[o])]
+          for o in range(len(Ks))]
+    ideal = orc.predict_ideal(mom, list(Ks), T, 300, x0s=x0s, Zs=Zs)
+    steps.append(("refloop_shrink_t7", cells, T, ph, ego_ref(cells, ph), ideal))
+
+    for name, cells, T, ph, ref_traj, ideal_trajs in steps:
+        pasts, yaws, inputs = _fixture_inputs(cells, T, ph, ref_traj)
+        outs = run_reference_generators(cells, yaws, T, ph, ref_traj, ideal=ideal_trajs,
+                                        with_affine=ideal_trajs is None)
+        if ideal_trajs is not None:
+            inputs["ideal"] = np.concatenate([ideal_trajs[o][k] for o in range(len(cells))
+                                              for k in range(len(cells[o]))])
+            inputs["ideal_counts"] = np.array([ideal_trajs[o][k].shape[0]
+                                               for o in range(len(cells))
+                                               for k in range(len(cells[o]))])
+        np.savez(os.path.join(HERE, name + ".npz"), **inputs, **outs)
+
+
 def main_reference_glue():
     rng = np.random.default_rng(20261016)
     pin_ovehicles_and_l4(rng)
     pin_predict_ideal(rng)
+    pin_generator_glue(np.random.default_rng(20261017))
     print("reference-glue fixtures written to", HERE)
 
 
 if __name__ == "__main__":
+    if "--generators-only" in sys.argv:
+        pin_generator_glue(np.random.default_rng(20261017))
+        sys.exit(0)
     if "--glue-only" not in sys.argv:
         main()
     main_reference_glue()

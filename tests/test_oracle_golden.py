@@ -5,7 +5,7 @@ import pytest
 
 from oracle import ccmpc_oracle as orc
 
-from _cycle_inputs import ovehicles_from_fixture
+from _cycle_inputs import REFLOOP, ovehicles_from_fixture, refloop_inputs
 
 
 def rel(a, b):
@@ -93,6 +93,57 @@ def test_affine_cycle_matches_reference(golden, name):
     np.testing.assert_array_equal([r["side"] for r in recs], g["aff_side"])
     np.testing.assert_allclose([r["margin"] for r in recs], g["aff_margin"], rtol=1e-12)
     np.testing.assert_allclose([r["rhs"] for r in recs], g["aff_rhs"], rtol=1e-13)
+
+
+@pytest.mark.parametrize("name", REFLOOP)
+def test_generators_match_reference_loops(golden, name):
+    """The oracle's restated generator glue against the reference's OWN loops
+    (v8ideal/__init__.py:781-964 and :1378-1539 run by make_golden.py with a recording cp):
+    constraint order, step and side exact; n, rhs, the state statistics, prob_lower_save and
+    the saved moments (save_moments :2575-2618) to rounding -- including a T < ph step on
+    injected ideal trajectories (the Tpred = T switch, :885-888)."""
+    g = golden(name)
+    K, T, ph, cells, yaws, ideal = refloop_inputs(g)
+    ovs = [orc.OVehicle(ph, np.asarray(g["past"][o]).reshape(1, 2), np.ones(K[o]) / K[o],
+                        cells[o], yaws[o], np.zeros((K[o], 2)), np.array([4.5, 2.5]))
+           for o in range(len(K))]
+    ideal_trajs = None
+    if ideal is not None:
+        it = iter(ideal)
+        ideal_trajs = {o: {k: next(it) for k in range(K[o])} for o in range(len(K))}
+    mk = orc.minkowski_generator(ovs, T, ph, g["ref_traj"], ideal_trajs=ideal_trajs,
+                                 with_l4=False)
+    recs = mk["records"]
+    np.testing.assert_array_equal([r["t"] for r in recs], g["mk_t"])
+    np.testing.assert_array_equal([r["side"] for r in recs], g["mk_side"])
+    assert rel([r["n"] for r in recs], g["mk_n"]) < 1e-12
+    np.testing.assert_allclose([r["d"] for r in recs], g["mk_rhs"], rtol=1e-12)
+    assert bool(mk["OVconstraint"]) == bool(g["mk_ovconstraint"])
+    C = sum(K)
+    sm = np.array([[mk["ov_state_mean"][j][o][k] for j in range(3)]
+                   for o in range(len(K)) for k in range(K[o])], float)
+    sc = np.array([[mk["ov_state_cov"][j][o][k] for j in range(3)]
+                   for o in range(len(K)) for k in range(K[o])], float)
+    np.testing.assert_array_equal(sm, g["mk_state_mean"])
+    np.testing.assert_array_equal(sc, g["mk_state_cov"])
+    if T == ph:
+        np.testing.assert_allclose(np.array(mk["prob_lower_save"], float),
+                                   g["mk_prob_lower_save"], rtol=1e-9)
+    mom = mk["moments"]
+    for c, (o, k) in enumerate([(o, k) for o in range(len(K)) for k in range(K[o])]):
+        for t in range(T):
+            np.testing.assert_array_equal(mom["mean_p0p1"][o][k][t], g["mom_mean"][c, t])
+            np.testing.assert_array_equal(mom["cov_p0p1"][o][k][t], g["mom_cov"][c, t])
+            for tau in range(t):
+                np.testing.assert_array_equal(mom["cross_cov"][o][k][t][tau],
+                                              g["mom_xcov"][c, t, tau])
+    assert len(recs) == C * T * (T - 1) // 2
+    if "aff_t" in g.files:
+        af = orc.affine_generator(ovs, T, ph, g["ref_traj"], with_l4=False)["records"]
+        np.testing.assert_array_equal([r["t"] for r in af], g["aff_t"])
+        np.testing.assert_array_equal([r["side"] for r in af], g["aff_side"])
+        assert rel([r["n"] for r in af], g["aff_n"]) < 1e-13
+        np.testing.assert_allclose([r["rhs"] for r in af], g["aff_rhs"], rtol=1e-12)
 
 
 def test_predict_ideal_with_injected_draws(golden):
