@@ -362,6 +362,9 @@ class MidlevelAgent:
         self._graphs = collections.OrderedDict()
         self.max_graphs = int(kwargs.get("max_graphs", 8))
         self._risk_memo = {}
+        self._u_prev = []                  # executed controls of this shrinking episode (:3186)
+        self.last_generator_output = None
+        self.last_ctrl = None
 
     # ------------------------------------------------------------------------------------
     def _saved(self, frame):
@@ -716,6 +719,62 @@ class MidlevelAgent:
                UnionGrid(o["b"], K, ph, first),
                self._ov_in_junction(scene, mean0), direct, st_mean, st_cov, 0)
         return ovs, out
+
+    def compute_prediction_controls(self, frame, Tsh, shrinking, sampler, minpos, pasts, x_init,
+                                    goal, ref_traj, bboxes=None, apply_robust=True):
+        """__compute_prediction_controls (v8ideal/__init__.py:3163-3210) without CARLA: one
+        planning frame of the reference harness loop (tests/Hz20/__init__.py:297-359 ->
+        run_step :3226-3284) from the sampler inputs on.
+
+          do_prediction + make_ovehicles   the sampler tail and the bucketing (`sampler`: the
+                                           dict predict_and_constrain takes)
+          make_local_params                O, K, frame, x_init
+          do_highlevel_control             shrinking and apply_robust: the Minkowski generator
+                                           (:2934-2952; one graph replay at Tsh == ph), else the
+                                           GMM-affine generator (:2954-2976); then the QP
+                                           (:2850-3043) on the device records
+          U_prev / warm start              the executed control U_star.T.ravel()[:nu] appended
+                                           (:3186; reset at Tsh == ph, the first shrinking step)
+
+        Returns (speeds, angles, timeout) as the reference does: X_star's speed column and its
+        heading reflected about the x axis (utility.npu.reflect_radians_about_x_axis: -psi;
+        python-utility is absent, restated), timeout False (the QP has no time limit here).
+        Raises InSimulationException where the reference's CPLEX solve fails (:3099-3110).  The
+        frame's 9-tuple and QP result stay on the agent (last_generator_output, last_ctrl)."""
+        from . import episode, ovehicle
+        T, ph = int(Tsh), self.prediction_horizon
+        pmf = np.asarray(sampler["latent_pmf"], np.float64)
+        O = pmf.shape[0]
+        if T == ph:
+            self._u_prev = []
+        if shrinking and apply_robust:
+            K = (pmf > sampler.get("filter_pmf", 0.1)).sum(1).tolist()
+            eps_ura = np.full((O, max(K)), 0.05 / O)              # :2909-2916
+            params = episode.Params(O, K, frame)
+            params.x_init = np.asarray(x_init, np.float64)
+            ovs, out = self.predict_and_constrain(params, sampler, eps_ura, T, ref_traj, minpos,
+                                                  pasts, bboxes)
+        else:
+            pp = bool(sampler.get("per_particle", False))
+            z, store = engine.sample_unicycle(
+                sampler["init_state"], pmf, sampler["gmm"], int(sampler["N"]), ph,
+                seed=int(sampler["seed"]), device=self.device, z=sampler.get("z"),
+                eps=sampler.get("eps"), per_particle=pp)
+            ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, bboxes,
+                                          device=self.device)
+            K = [ov.n_states for ov in ovs]
+            eps_ura = np.full((O, max(K)), 0.05 / O)
+            params = episode.Params(O, K, frame)
+            params.x_init = np.asarray(x_init, np.float64)
+            out = self.compute_obstacle_constraints_GMM_affine(
+                params, ovs, None, None, None, eps_ura, None, T, ref_traj)
+        self.last_generator_output = (ovs, out)
+        up = np.concatenate(self._u_prev) if (T < ph and self._u_prev) else None
+        ctrl = self.solve_planning_qp(x_init, goal, ref_traj, T, u_prev=up)
+        self.last_ctrl = ctrl
+        self._u_prev.append(np.asarray(ctrl["u"][:2]))        # U_star.T.ravel()[:nu] (:3186)
+        X = ctrl["X_star"]
+        return X[:, 3].copy(), -X[:, 2], False
 
     def solve_planning_qp(self, x_init, goal, ref_traj, Tsh, u_prev=None, lon=3.7,
                           u_order=mpc.U_ORDER_F):

@@ -106,6 +106,40 @@ def test_episode_at_reference_scale(gpu):
             assert c.d == pytest.approx(r["d"], rel=1e-8)
 
 
+def test_compute_prediction_controls_drives_the_schedule(gpu):
+    """MidlevelAgent.compute_prediction_controls -- the CARLA-free __compute_prediction_controls
+    (v8ideal/__init__.py:3163-3210): sampler -> make_ovehicles -> the generator the schedule
+    selects -> QP -> U_prev -- driven frame by frame like the reference harness loop, equal to
+    EpisodeReplay's separate calls (eager generator + solve_planning_qp) step for step."""
+    from ccmpc import episode, planner
+    seed = 3
+    rep = episode.EpisodeReplay(O=2, N=3000, ph=8, n_ideal=20_000, receding_steps=2, seed=seed,
+                                device=gpu)
+    agent = planner.MidlevelAgent(prediction_horizon=8, n_ideal=20_000, seed=seed, device=gpu)
+    n_cmp = 0
+    for frame, T, kind in rep.schedule():
+        ovs, out = rep.step(frame, T, kind)
+        want = rep.plan(frame, T)
+        sampler = dict(init_state=rep.init, latent_pmf=rep.pmf, gmm=rep.gmm, N=rep.N,
+                       seed=rep.seed * 7919 + frame)
+        ref = rep.ref_traj(frame)
+        try:
+            speeds, angles, timeout = agent.compute_prediction_controls(
+                frame, T, kind == "minkowski", sampler, rep.minpos, rep.pasts,
+                rep.x_init(frame), ref[-1] + [4.0, 0.5], ref)
+        except planner.InSimulationException:
+            assert want is None, (frame, T)
+            break                                   # the reference's episode ends here
+        assert want is not None and timeout is False
+        np.testing.assert_array_equal(speeds, want["X_star"][:, 3])
+        np.testing.assert_array_equal(angles, -want["X_star"][:, 2])
+        g_cons, e_cons = agent.last_generator_output[1][0], out[0]
+        assert len(g_cons) == len(e_cons)
+        assert all(a.rhs == b.rhs and a.side == b.side for a, b in zip(g_cons, e_cons))
+        n_cmp += 1
+    assert n_cmp >= 3
+
+
 def test_episode_timing_log(gpu):
     from ccmpc import episode
     rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=100_000, receding_steps=2,
