@@ -494,7 +494,7 @@ def cpu_baseline(ovs, ref, T, cycles):
     return best[0], best[1], best[2], total
 
 
-def episode_c1(dev, cpu_steps=2, with_cpu=True):
+def episode_c1(dev, cpu_steps=2, with_cpu=True, N=5000):
     """BASELINE configs[0] (tests/Hz20/test_montecarlo.py v8ideal scene4_ov1_brake ph8
     np5000): one obstacle, the full planning schedule of an episode through
     MidlevelAgent -- 8 shrinking Minkowski steps (T = 8..1; T < 8 on 1e6-sample predict_ideal
@@ -502,13 +502,13 @@ def episode_c1(dev, cpu_steps=2, with_cpu=True):
     -> one fused launch -> host HalfSpace objects), synchronised.  Beside it, the oracle on the
     first `cpu_steps` planning steps with the same particles and the same Philox draws."""
     from ccmpc import episode
-    rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=1_000_000, receding_steps=4,
+    rep = episode.EpisodeReplay(O=1, N=N, ph=8, n_ideal=1_000_000, receding_steps=4,
                                 device=dev)
     rep.run()                                   # warm-up (allocations, first launches)
-    rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=1_000_000, receding_steps=4,
+    rep = episode.EpisodeReplay(O=1, N=N, ph=8, n_ideal=1_000_000, receding_steps=4,
                                 device=dev)
     log = rep.run()
-    out = {"config": "C1 schedule: 1 OV, np=5000, ph=8, n_ideal=1e6, 8 shrinking + 4 receding "
+    out = {"config": f"C1 schedule: 1 OV, np={N}, ph=8, n_ideal=1e6, 8 shrinking + 4 receding "
                      "planning steps (synthetic GMM predictions)",
            "steps": [{k: (round(v, 3) if k in ("ms", "qp_ms") else v) for k, v in st.items()}
                      for st in log],
@@ -895,6 +895,8 @@ def main():
                 dev, steps=100, with_cpu=not args.no_cpu, O=1, N=100_000, eager_steps=20,
                 cpu_reps=2, label="C1 (n_predictions = 100 000)")
             out["episode_c1"] = episode_c1(dev, with_cpu=not args.no_cpu)
+            # the reference's real particle count at the "np5000" label (params.py:377)
+            out["episode_c1_np100k"] = episode_c1(dev, with_cpu=False, N=100_000)
             out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
     if not args.no_sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)

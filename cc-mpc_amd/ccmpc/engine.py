@@ -5,6 +5,7 @@ in libccmpc.so.  All functions enqueue on torch's current stream and never synch
 whole constraint-generation cycle can be captured into a hipGraph (torch.cuda.CUDAGraph).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -37,6 +38,16 @@ def _round4(x):
     return (int(x) + 3) // 4 * 4
 
 
+# Cell offsets and ld of the stores built here, in particles: a multiple of 4 is what the
+# kernels need (16-byte vector loads); a multiple of 16 puts every f64 load group of a cell on
+# whole 128-byte lines (A/B knob, CCMPC_STORE_ALIGN).
+STORE_ALIGN = int(os.environ.get("CCMPC_STORE_ALIGN", "4"))
+
+
+def _round_to(x, a):
+    return (int(x) + a - 1) // a * a
+
+
 class ParticleStore:
     """Plane-major SoA particle clouds of several cells (see include/ccmpc.h).
 
@@ -46,16 +57,19 @@ class ParticleStore:
     """
 
     def __init__(self, T, counts, dtype=torch.float64, device="cuda", origin=None,
-                 capacity=None):
+                 capacity=None, align=None):
         self.device = require_device(device)
         self.T = int(T)
         counts = [int(c) for c in counts]
+        al = STORE_ALIGN if align is None else int(align)
+        if al < 4 or al % 4:
+            raise ValueError("store alignment must be a multiple of 4 particles")
         offs, cur = [], 0
         for c in counts:
             offs.append(cur)
-            cur = _round4(cur + max(c, 0))
+            cur = _round_to(cur + max(c, 0), al)
         self.n_bound = cur if capacity is None else max(cur, int(capacity))
-        self.ld = max(_round4(self.n_bound), 4)
+        self.ld = max(_round_to(self.n_bound, al), al)
         self.dtype = dtype
         self.pos = torch.zeros((2 * self.T, self.ld), dtype=dtype, device=self.device)
         self.counts = counts
