@@ -39,9 +39,12 @@ def _round4(x):
 
 
 # Cell offsets and ld of the stores built here, in particles: a multiple of 4 is what the
-# kernels need (16-byte vector loads); a multiple of 16 puts every f64 load group of a cell on
-# whole 128-byte lines (A/B knob, CCMPC_STORE_ALIGN).
-STORE_ALIGN = int(os.environ.get("CCMPC_STORE_ALIGN", "4"))
+# kernels need (16-byte vector loads); 32 puts every load group of a cell on whole 128-byte
+# lines (a 16-particle f64 step, a 32-particle Scheme4 / f32 step), so the waves that stream
+# neighbouring groups never share a line.  Measured against 4 (profiles/r03/ab3_store_align32.log):
+# C5 85.9 -> 81.1 us cold, the per-GPU C4 batch 37.4 -> 36.0 us cold, C2 / C3 unchanged.
+# CCMPC_STORE_ALIGN overrides it (A/B).
+STORE_ALIGN = int(os.environ.get("CCMPC_STORE_ALIGN", "32"))
 
 
 def _round_to(x, a):
@@ -52,7 +55,8 @@ class ParticleStore:
     """Plane-major SoA particle clouds of several cells (see include/ccmpc.h).
 
     pos[(2t + c), off[j] + i] = coordinate c of particle i of cell j at step t.
-    Cell offsets are 4-aligned and ld is a multiple of 4 (16-byte vector loads).
+    Cell offsets and ld are multiples of `align` particles (STORE_ALIGN = 32 by default; the
+    kernels need a multiple of 4: 16-byte vector loads).
     F64 stores hold world coordinates; F32 stores hold coordinates relative to ``origin[j]``.
     """
 

@@ -199,53 +199,12 @@ __device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &lo
 // waves (every wave within one group of the others, whatever the chunk).
 struct WaveRange {
   int64_t p0, stride, p1, ngroups;
-  int64_t outer;  // weighted dealing only: particles per round of groups
-  bool old;       // weighted dealing only: a first-dispatched wave (share SO, else SY)
 };
-
-// Weighted balanced dealing (build knob, long horizons): the two waves of a SIMD run the
-// matrix pipe unequally -- the first-dispatched (older) wave gets the issue priority and
-// finishes its round-robin share long before its partner (C5: ~24 us of a ~66 us stream), which
-// then runs alone and cannot hide its own load latency.  With CCMPC_BAL_SO : CCMPC_BAL_SY !=
-// 1 : 1, each round of 4 (SO + SY) groups gives the older waves 0..3 SO consecutive groups each
-// and the younger waves 4..7 SY each.  Static, so the reduction stays deterministic.
-#ifndef CCMPC_BAL_SO
-#define CCMPC_BAL_SO 1
-#endif
-#ifndef CCMPC_BAL_SY
-#define CCMPC_BAL_SY 1
-#endif
-template <int SO, int SY>
-__device__ __forceinline__ int64_t group_at(const WaveRange &r, int64_t gi) {
-  if constexpr (SO == 1 && SY == 1) {
-    return r.p0 + gi * r.stride;
-  } else {
-    return r.old ? r.p0 + (gi / SO) * r.outer + (gi % SO) * r.stride
-                 : r.p0 + (gi / SY) * r.outer + (gi % SY) * r.stride;
-  }
-}
-
-template <bool BAL, int SO = 1, int SY = 1>
+template <bool BAL>
 __device__ __forceinline__ WaveRange wave_range(int64_t a, int64_t b, int w, int nw, int64_t wq,
                                                 int64_t gs) {
   WaveRange r;
-  r.outer = 0;
-  r.old = false;
-  if constexpr (BAL && (SO != 1 || SY != 1)) {
-    const int half = nw / 2;
-    r.old = w < half;
-    const int share = r.old ? SO : SY;
-    const int start = r.old ? w * SO : half * SO + (w - half) * SY;
-    const int64_t R = static_cast<int64_t>(half) * (SO + SY);
-    const int64_t ng = a < b ? ceil_div(b - a, gs) : 0;
-    const int64_t full = ng / R, rem = ng - full * R;
-    const int64_t tail = rem - start;
-    r.p0 = a + static_cast<int64_t>(start) * gs;
-    r.stride = gs;
-    r.outer = R * gs;
-    r.p1 = b;
-    r.ngroups = full * share + (tail <= 0 ? 0 : (tail < share ? tail : share));
-  } else if (BAL) {
+  if (BAL) {
     r.p0 = a + static_cast<int64_t>(w) * gs;
     r.stride = nw * gs;
     r.p1 = b;
@@ -309,9 +268,7 @@ void moments_kernel(
     const int g = lane >> 4;
     const int64_t cnt = loc.cnt;
     const double pre = MINK ? prefetch_tail(mp, loc, rows) : 0.0;
-    constexpr int SO = (BAL && RB >= 3 && G::NW == 8) ? CCMPC_BAL_SO : 1;
-    constexpr int SY = (BAL && RB >= 3 && G::NW == 8) ? CCMPC_BAL_SY : 1;
-    const WaveRange wr = wave_range<BAL, SO, SY>(a, b, w, G::NW, int64_t(1) << lg_wq, 16 * S);
+    const WaveRange wr = wave_range<BAL>(a, b, w, G::NW, int64_t(1) << lg_wq, 16 * S);
     const int64_t p1 = wr.p1;
 
     double sh[RB];
@@ -339,7 +296,7 @@ void moments_kernel(
     // never multiplied) so there is no divergent join for the waitcnt pass to merge.
     // sched_barrier(0) fences keep the four phases in program order, so each MFMA group waits
     // (vmcnt) only for its own buffer while the other buffer's loads stay in flight.
-    const int64_t ngroups = wr.ngroups;
+    const int64_t ngroups = wr.ngroups, st = wr.stride;
 #if CCMPC_PRIO  // experiment: static priority for the second-dispatched half (MI355X_MICROARCH.md)
     if (G::NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(CCMPC_PRIO);
 #endif
@@ -349,25 +306,22 @@ void moments_kernel(
       // ring of DP load groups: group g lives in buf[g % DP]; DP - 1 groups are in flight
       // while one is multiplied
 #pragma unroll
-      for (int d = 0; d < DP - 1; ++d)
-        load_group<P, RB, S>(buf[d], rowp, group_at<SO, SY>(wr, d), p1, g);
+      for (int d = 0; d < DP - 1; ++d) load_group<P, RB, S>(buf[d], rowp, wr.p0 + d * st, p1, g);
       int64_t gi = 0;
       for (; gi + DP <= ngroups; gi += DP) {
 #pragma unroll
         for (int d = 0; d < DP; ++d) {
-          load_group<P, RB, S>(buf[(d + DP - 1) % DP], rowp, group_at<SO, SY>(wr, gi + d + DP - 1),
-                               p1, g);
+          load_group<P, RB, S>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1,
+                               g);
           __builtin_amdgcn_sched_barrier(0);
-          mfma_group<P, RB, S, NACC>(buf[d], sh, live, group_at<SO, SY>(wr, gi + d), p1, g, acc,
-                                     s1);
+          mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
 #pragma unroll
       for (int d = 0; d < DP - 1; ++d)  // the < DP groups left were loaded ahead
         if (gi + d < ngroups)
-          mfma_group<P, RB, S, NACC>(buf[d], sh, live, group_at<SO, SY>(wr, gi + d), p1, g, acc,
-                                     s1);
+          mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
     }
     PROBE_TS(2);
 #if CCMPC_PRIO
