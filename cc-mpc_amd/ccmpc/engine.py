@@ -285,7 +285,9 @@ def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="c
     dev = require_device(device)
     O, L, t_init, t_cdf, t_gmm, layout, t_z, t_eps = _sampler_inputs(
         init_state, latent_pmf, gmm, N, T, dev, z, eps, per_particle)
-    store = ParticleStore(T, [N] * O, dtype=torch.float32, device=dev, origin=np.zeros((O, 2)))
+    # the sampler writes OV o at o * round4(N): the kernel's own layout (align 4)
+    store = ParticleStore(T, [N] * O, dtype=torch.float32, device=dev, origin=np.zeros((O, 2)),
+                          align=4)
     out_z = torch.empty((O, N), dtype=torch.int32, device=dev)
     _lib.check(lib.ccmpc_sample_unicycle_ex(
         _p(t_init), _p(t_cdf), L, _p(t_gmm), layout, _p(t_z), _p(t_eps), O, N, T, float(dt),
@@ -454,7 +456,7 @@ def ideal_rollout(prev_mean, prev_cov, src_cell, T, n_samples, x0=None, Z=None, 
     lib = _lib.load()
     C = src_cell.shape[0]
     T_src = prev_mean.shape[1]
-    store = ParticleStore(T, [n_samples] * C, dtype=torch.float64, device=prev_mean.device,
+    store = ParticleStore(T, [n_samples] * C, dtype=torch.float64, device=prev_mean.device, align=4,
                           capacity=C * n_samples)
     status = torch.empty(C, dtype=torch.int32, device=prev_mean.device)
     _lib.check(lib.ccmpc_ideal_rollout(_p(prev_mean), _p(prev_cov), T_src, _p(src_cell), C, T,

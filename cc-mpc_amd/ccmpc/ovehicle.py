@@ -176,7 +176,7 @@ def make_ovehicles(predictions, z, latent_probs, minpos, pasts, bboxes=None, T=N
     else:
         pred = np.asarray(predictions, np.float32)
         O, N, T_, _ = pred.shape
-        store_in = engine.ParticleStore(T_, [N] * O, dtype=torch.float32, device=dev,
+        store_in = engine.ParticleStore(T_, [N] * O, dtype=torch.float32, device=dev, align=4,
                                         origin=np.zeros((O, 2)))
         host = np.zeros((2 * T_, store_in.ld), np.float32)
         for o in range(O):

@@ -154,7 +154,7 @@ class MinkowskiStepGraph:
             self.bucket_ws = torch.zeros(fused_ws, dtype=u8, device=self.device)
         else:
             self.z = torch.empty((O, N), dtype=i32, device=self.device)
-            self.samples = engine.ParticleStore(T, [N] * O, dtype=f32, device=self.device,
+            self.samples = engine.ParticleStore(T, [N] * O, dtype=f32, device=self.device, align=4,
                                                 origin=np.zeros((O, 2)))
             self.bucket_ws = torch.zeros(
                 max(lib.ccmpc_bucket_workspace_bytes(O, N, L, self.max_k), 16), dtype=u8,
