@@ -17,7 +17,7 @@
 //              write-through; the OV's last arriving block sums them in the canonical order
 //              (bucket.hpp) -> centres
 //   B2 keys    per block: key histogram (LDS int atomics, exact), published write-through; the
-//              OV's last arriving block scans them -> bin offsets (bin-major, block-minor),
+//              OV's last arriving block scans them -> per chunk of 16 blocks the bin starts,
 //              4-aligned cell offsets
 //   B3 scatter per block: stable rank inside the block (wave ballots, waves in order) -> copy
 //              the particle's 2T coordinates to its bucket slot
@@ -34,6 +34,7 @@ namespace ccmpc {
 constexpr int kBucketBlock = 256;
 constexpr int kPerThread = 1;  // one round per block: many short blocks (C2 shape: 80, not 20)
 constexpr int kSpan = kBucketBlock * kPerThread;  // particles per block, in sample order
+constexpr int kChunkRows = 16;  // blocks per chunk of the bin-offset scan
 
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
 __device__ unsigned long long g_bkt_ts[3][kStepProbeWG * kStepProbeSlots];
@@ -62,7 +63,7 @@ struct BucketArgs {
   int G;                    // groups per OV = ceil(N / 64)
   double *centre;           // [n_ov][max_k][2]
   int32_t *hist;            // [n_ov][nb][nbins]
-  int64_t *bin_off;         // [n_ov][nb][nbins]
+  int64_t *chunk_off;       // [n_ov][ceil(nb / kChunkRows)][nbins]: each chunk's bin starts
   // outputs
   float *out;
   int64_t ld_out;
@@ -237,23 +238,44 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
   BKT_TS(1, 2);
   if (!arrive_last(a.ctr + a.n_ov + o, a.nb, &flag)) return;
   BKT_TS(1, 3);
-  // the OV's scan: bin totals (blocks in order), bins in (kept mode, group) order
-  // (loads in batches of 8, all in flight together: a dependent chain of nb round trips
-  // was the kernel's whole latency)
-  auto column_sum = [&](int b, int k_end) {
-    int64_t s = 0;
-    int k = 0;
-    for (; k + 8 <= k_end; k += 8) {
-      int32_t v[8];
+  // The OV's scan, as integer sums over the published block histograms (exact: the order of the
+  // additions does not matter).  (1) per (chunk of kChunkRows blocks, bin) column sums -- every
+  // load of a task in flight together, two tasks per round, all threads -- into chunk_off and
+  // the bin totals (LDS int64 atomics); (2) bin starts and cell offsets; (3) per bin, each
+  // chunk's start in place of its sum.  bucket_scatter adds the block's offset inside its chunk
+  // (<= kChunkRows - 1 rows).  The old per-bin serial column walk over all nb blocks (twice) was
+  // a dependent chain of ~nb / 8 round trips: 63 us at N = 100 000.
+  const int nch = (a.nb + kChunkRows - 1) / kChunkRows;
+  int64_t *coff = a.chunk_off + static_cast<int64_t>(o) * nch * stride;
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) start[b] = 0;
+  __syncthreads();
+  const int tasks = nch * nbins;
+  auto chunk_sum = [&](int task) {
+    const int c = task / nbins, b = task - c * nbins;
+    const int r0 = c * kChunkRows, nr = min(kChunkRows, a.nb - r0);
+    int32_t v[kChunkRows];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ld1_sc1(rh, 4 * static_cast<int>((k + j) * stride + b));
+    for (int j = 0; j < kChunkRows; ++j)
+      v[j] = ld1_sc1(rh, 4 * static_cast<int>((r0 + (j < nr ? j : nr - 1)) * stride + b));
+    int64_t sum = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
-    }
-    for (; k < k_end; ++k) s += ld1_sc1(rh, 4 * static_cast<int>(k * stride + b));
-    return s;
+    for (int j = 0; j < kChunkRows; ++j) sum += j < nr ? v[j] : 0;
+    return sum;
   };
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) start[b] = column_sum(b, a.nb);
+  for (int t0 = threadIdx.x; t0 < tasks; t0 += 2 * blockDim.x) {
+    const int t1 = t0 + blockDim.x;
+    const int64_t s0 = chunk_sum(t0);
+    const int64_t s1 = t1 < tasks ? chunk_sum(t1) : 0;
+    coff[(t0 / nbins) * stride + t0 % nbins] = s0;
+    atomicAdd(reinterpret_cast<unsigned long long *>(&start[t0 % nbins]),
+              static_cast<unsigned long long>(s0));
+    if (t1 < tasks) {
+      coff[(t1 / nbins) * stride + t1 % nbins] = s1;
+      atomicAdd(reinterpret_cast<unsigned long long *>(&start[t1 % nbins]),
+                static_cast<unsigned long long>(s1));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's chunk sums, read below
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t cur = a.region[o];
@@ -272,19 +294,25 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
     }
   }
   __syncthreads();
-  // every block's offset in each bin: the bin's start + the counts of the blocks before it
+  // each chunk's start in every bin: the bin's start + the sums of the chunks before it
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(coff, 0, 0x7fffffff,
+                                                                       0x00020000);
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
-    int64_t s = start[b];
-    int64_t *dst = a.bin_off + static_cast<int64_t>(o) * a.nb * stride + b;
-    for (int k = 0; k < a.nb; k += 8) {
-      int32_t v[8];
+    int64_t run = start[b];
+    for (int c0 = 0; c0 < nch; c0 += 8) {
+      int64_t v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = k + j < a.nb ? ld1_sc1(rh, 4 * static_cast<int>((k + j) * stride + b)) : 0;
+      for (int j = 0; j < 8; ++j) {  // 8-byte sc1 loads: L2-served (no stale L1 line)
+        const int c = c0 + j < nch ? c0 + j : nch - 1;
+        const int off = 8 * static_cast<int>(c * stride + b);
+        const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rc, off, 0, 16);
+        const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rc, off + 4, 0, 16);
+        v[j] = static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (k + j < a.nb) dst[(k + j) * stride] = s;
-        s += v[j];
+        if (c0 + j < nch) coff[(c0 + j) * stride + b] = run;
+        run += c0 + j < nch ? v[j] : 0;
       }
     }
   }
@@ -303,7 +331,11 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
   const int K = a.n_kept[o];
   const int nbins = K * (a.L + 1);
   const int64_t stride = static_cast<int64_t>(a.max_k) * (a.L + 1);
-  const int64_t *boff = a.bin_off + (static_cast<int64_t>(o) * a.nb + blk) * stride;
+  // this block's start in every bin: its chunk's start (bucket_hist) + the histograms of the
+  // blocks before it in the chunk
+  const int nch = (a.nb + kChunkRows - 1) / kChunkRows, ch = blk / kChunkRows;
+  const int64_t *coff = a.chunk_off + (static_cast<int64_t>(o) * nch + ch) * stride;
+  const int32_t *hist0 = a.hist + static_cast<int64_t>(o) * a.nb * stride;
   const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
   // kPerThread == 1: this thread's particle, its key inputs and its 2T coordinates, every load
   // issued together with the block's tables
@@ -327,7 +359,15 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
     cen_s[j >> 1][j & 1] = a.centre[(o * a.max_k + (j >> 1)) * 2 + (j & 1)];
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
     run[b] = 0;
-    boff_s[b] = boff[b];
+    int32_t v[kChunkRows - 1];
+    const int r0 = ch * kChunkRows, nr = blk - r0;  // rows of this chunk before the block
+#pragma unroll
+    for (int j = 0; j < kChunkRows - 1; ++j)
+      v[j] = hist0[static_cast<int64_t>(r0 + (j < nr ? j : 0)) * stride + b];
+    int64_t s = coff[b];
+#pragma unroll
+    for (int j = 0; j < kChunkRows - 1; ++j) s += j < nr ? v[j] : 0;
+    boff_s[b] = s;
   }
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int r = 0; r < kPerThread; ++r) {
@@ -366,7 +406,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
 inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  size_t ctr, part, gpart, centre, hist, bin_off, total;
+  size_t ctr, part, gpart, centre, hist, chunk_off, total;
   int E1, G;
 };
 
@@ -386,8 +426,8 @@ inline WsLayout bucket_ws(int64_t n_ov, int64_t N, int64_t L, int64_t max_k) {
   o += align256(sizeof(double) * n_ov * max_k * 2);
   w.hist = o;
   o += align256(sizeof(int32_t) * n_ov * nb * max_k * (L + 1));
-  w.bin_off = o;
-  o += align256(sizeof(int64_t) * n_ov * nb * max_k * (L + 1));
+  w.chunk_off = o;
+  o += align256(sizeof(int64_t) * n_ov * ((nb + kChunkRows - 1) / kChunkRows) * max_k * (L + 1));
   w.total = o;
   return w;
 }
@@ -431,6 +471,9 @@ extern "C" int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in
   CCMPC_REQUIRE(max_k >= 1 && max_k <= kMaxKept && max_k * (n_latent + 1) <= kMaxBins,
                 "max_k out of range");
   CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536 && N >= 1 && N < (int64_t(1) << 31), "bad sizes");
+  // the per-OV histogram / chunk-offset tables are addressed with 32-bit buffer offsets
+  CCMPC_REQUIRE(8 * ((N + kSpan - 1) / kSpan) * max_k * (n_latent + 1) < (int64_t(1) << 31),
+                "N x kept modes x latents too large for one bucketing call");
   if (n_ov == 0) return CCMPC_OK;
   CCMPC_REQUIRE(z && pos_in && keep_map && n_kept && cell_base && minpos && region && pos_out &&
                     cell_off && cell_cnt && cell_pmf && init_center,
@@ -464,7 +507,7 @@ extern "C" int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in
   a.G = L.G;
   a.centre = reinterpret_cast<double *>(ws + L.centre);
   a.hist = reinterpret_cast<int32_t *>(ws + L.hist);
-  a.bin_off = reinterpret_cast<int64_t *>(ws + L.bin_off);
+  a.chunk_off = reinterpret_cast<int64_t *>(ws + L.chunk_off);
   a.out = pos_out;
   a.ld_out = ld_out;
   a.cell_off = cell_off;
