@@ -720,227 +720,6 @@ __global__ __launch_bounds__(RootGeo<RB>::THREADS) void root_finalize_kernel(
   }
 }
 
-// ---- long horizons (T > 24, moments only): LDS-staged Gram, one 16 x 16 tile per wave ------
-// At T = 40 the register-fed kernel above keeps all 15 tiles of accumulators in every wave
-// beside its load ring: 252 VGPRs, two waves per SIMD, one load group in flight per wave -- the
-// two waves of a SIMD drift ~24 us apart and the matrix pipe idles ~40 % of the stream (C5:
-// 66 us of stream for 38 us of MFMA work).  Here the workgroup's 16 waves stream each stage of
-// kLSP particles x 2T rows into LDS together (16-byte loads, kLRing stages in flight in
-// registers, shifted and masked as they are stored), and wave w < n_tiles owns Gram tile w:
-// per stage kLSP / 4 MFMAs on operands read from LDS, two accumulator chains, no cross-wave
-// combine -- each tile's slab entries come from one wave; the diagonal-tile waves also sum the
-// rows.  Same slab layout (Scheme16), so the combine tree, the deferred root and the finaliser
-// are unchanged.
-constexpr int kLW = 8;            // waves per workgroup (2 per SIMD)
-constexpr int kLSP = 64;          // particles per stage
-// LDS row stride (doubles): 66 = 4 banks mod 64 per row, so the 16 rows of a 16-lane pass of
-// a 16-byte read hit 16 distinct bank quads
-constexpr int kLStride = kLSP + 2;
-constexpr int kLRing = 3;         // stages of loads in flight (register slots)
-// Row blocks from which the moments-only launch stages in LDS (build knob; 9 = off).  Measured
-// at C5 (profiles/r03/ab4_c5_lds_staged.log): 16 waves x 1 tile 125 us, the same with 16-byte
-// LDS reads 258 us (spills at 128 VGPRs), 8 waves x 2 tiles 110 us -- against 82 us for the
-// register-fed kernel: off.
-#ifndef CCMPC_LDS_GRAM_MIN_RB
-#define CCMPC_LDS_GRAM_MIN_RB 9
-#endif
-
-template <typename P>
-struct LChunk;
-template <>
-struct LChunk<double> {
-  using V = double2;
-  static constexpr int N = 2;
-  __device__ static double at(const V &v, int e) { return e ? v.y : v.x; }
-};
-template <>
-struct LChunk<float> {
-  using V = float4;
-  static constexpr int N = 4;
-  __device__ static double at(const V &v, int e) {
-    return static_cast<double>(e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w);
-  }
-};
-
-template <int RB>
-__device__ __forceinline__ void tile_rows(int t, int &bi, int &bj) {  // decode_entry's order
-  bi = 0;
-  while (t >= RB - bi) {
-    t -= RB - bi;
-    ++bi;
-  }
-  bj = bi + t;
-}
-
-template <typename P, int RB, bool BAL>
-__global__ __launch_bounds__(kLW * 64, 2) void momentsL_kernel(
-    const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off, int n_cells,
-    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin, int lg_chunk,
-    TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov) {
-  using CK = LChunk<P>;
-  constexpr int NT = n_tiles(RB), D = 16 * RB, E = slab_doubles(RB);
-  constexpr int PPC = CK::N;                      // particles per 16-byte chunk
-  constexpr int QPR = kLSP / PPC;                 // chunks per row per stage
-  constexpr int CH = D * QPR;                     // chunks per stage
-  constexpr int NTH = kLW * 64;
-  constexpr int NC = (CH + NTH - 1) / NTH;        // chunks per thread per stage
-  constexpr bool DEFER = defer_root(RB, false, BAL);
-  constexpr int TPW = (NT + kLW - 1) / kLW;      // tiles per wave (RB = 4, 5: 2)
-  static_assert(TPW <= 2, "at most two tiles per wave");
-  __shared__ double xs[2][D * kLStride];
-  __shared__ double slab_lds[E];
-  __shared__ double shift_lds[D];
-  __shared__ double S_lds[D];
-  __shared__ double mean_lds[D];
-  __shared__ int flag;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rows = 2 * T;
-  const MinkParams none{};
-
-  auto item = [&](const ItemLoc &loc, int32_t nit, int64_t a, int64_t b) {
-    for (int r = tid; r < D; r += NTH)
-      shift_lds[r] = (r < rows && loc.cnt > 0)
-                         ? static_cast<double>(pos[static_cast<int64_t>(r) * ld + loc.off]) : 0.0;
-    const P *base = pos + loc.off;
-    // this thread's chunks of a stage (the same every stage): row, first particle column
-    int crow[NC], ccol[NC];
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int c = min(tid + j * NTH, CH - 1);  // past CH: a duplicate, never stored
-      crow[j] = c / QPR;
-      ccol[j] = (c % QPR) * PPC;
-    }
-    const int64_t qlast = b > a ? (b - 1) & ~int64_t(PPC - 1) : a;  // last whole chunk of the item
-    const int64_t nstage = b > a ? (b - a + kLSP - 1) / kLSP : 0;
-    typename CK::V regs[kLRing][NC];
-    auto issue = [&](typename CK::V (&v)[NC], int64_t s) {  // clamped: always addressable
-#pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        int64_t p = a + s * kLSP + ccol[j];
-        p = p < qlast ? p : qlast;
-        const int r = crow[j] < rows ? crow[j] : 0;
-        v[j] = *reinterpret_cast<const typename CK::V *>(base + static_cast<int64_t>(r) * ld + p);
-      }
-    };
-    auto stash = [&](const typename CK::V (&v)[NC], int64_t s, double *buf) {
-#pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        if (tid + j * NTH >= CH) continue;
-        const int64_t p0 = a + s * kLSP + ccol[j];
-        const bool live = crow[j] < rows;
-        const double sh = shift_lds[crow[j]];
-        double x[PPC];
-#pragma unroll
-        for (int e = 0; e < PPC; ++e) x[e] = (live && p0 + e < b) ? CK::at(v[j], e) - sh : 0.0;
-        double *dst = buf + crow[j] * kLStride + ccol[j];
-#pragma unroll
-        for (int e = 0; e < PPC; e += 2)
-          *reinterpret_cast<double2 *>(dst + e) = double2{x[e], x[e + 1]};
-      }
-    };
-    // the wave's tiles 2w, 2w + 1 (decode_entry order) and their operand rows.  k-step kk feeds
-    // lane (r, k) particle 16 k + kk of the stage (any assignment of a stage's particles to
-    // k-steps gives the same Gram sum): a lane's particles are contiguous, so one 16-byte LDS
-    // read brings two k-steps
-    const int r = lane & 15, k = lane >> 4;
-    int tb[2], ta[2], oa[2], ob[2];
-    bool has[2], diag[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int t = TPW * w + q;
-      has[q] = q < TPW && t < NT;
-      tile_rows<RB>(has[q] ? t : 0, ta[q], tb[q]);
-      diag[q] = ta[q] == tb[q];
-      oa[q] = (16 * ta[q] + r) * kLStride + 16 * k;
-      ob[q] = (16 * tb[q] + r) * kLStride + 16 * k;
-    }
-    d4 acc[2][2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) acc[q][0] = acc[q][1] = d4{0.0, 0.0, 0.0, 0.0};
-    double s1 = 0.0;  // the wave's diagonal tile (at most one), its rows
-    auto compute = [&](const double *buf) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (!has[q]) continue;  // uniform
-#pragma unroll 4
-        for (int kk = 0; kk < kLSP / 4; kk += 2) {
-          const double2 av = *reinterpret_cast<const double2 *>(buf + oa[q] + kk);
-          const double2 bv = diag[q] ? av : *reinterpret_cast<const double2 *>(buf + ob[q] + kk);
-          acc[q][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acc[q][0], 0, 0, 0);
-          acc[q][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, acc[q][1], 0, 0, 0);
-          if (diag[q]) s1 += av.x + av.y;
-        }
-      }
-    };
-    __syncthreads();  // shift_lds
-    // ring: stage s in LDS buffer s % 2; stages s + 1 and s + 2 in flight in registers
-#pragma unroll
-    for (int d = 0; d < kLRing; ++d) issue(regs[d], d);
-    stash(regs[0], 0, xs[0]);
-    __syncthreads();
-    for (int64_t s = 0; s < nstage; s += kLRing) {
-#pragma unroll
-      for (int d = 0; d < kLRing; ++d) {
-        if (s + d >= nstage) break;  // uniform
-        compute(xs[(s + d) & 1]);
-        if (s + d + 1 < nstage) stash(regs[(d + 1) % kLRing], s + d + 1, xs[(s + d + 1) & 1]);
-        issue(regs[d], s + d + kLRing);
-        __syncthreads();
-      }
-    }
-    // rows sums of the diagonal tile: lanes (r, k) hold particles 16 k + kk
-    s1 += __shfl_xor(s1, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    const double s1n = __shfl_down(s1, 1, 64);
-    const EpilogueLds L{slab_lds, shift_lds, S_lds, mean_lds, nullptr, nullptr, nullptr, &flag};
-    cell_epilogue<Scheme16<RB>, false, false, DEFER>(
-        [&](double *dst, bool to_lds) {
-          const __amdgpu_buffer_rsrc_t rs = slab_rsrc(dst);
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            if (!has[q]) continue;
-            const d4 v = acc[q][0] + acc[q][1];
-            const int e = (TPW * w + q) * 256 + 4 * lane;
-            if (to_lds) {
-#pragma unroll
-              for (int c = 0; c < 4; ++c) dst[e + c] = v[c];
-            } else {
-              st2_sc1(rs, 8 * e, v[0], v[1]);
-              st2_sc1(rs, 8 * (e + 2), v[2], v[3]);
-            }
-            if (diag[q] && lane < 16 && (lane & 1) == 0) {
-              const int es = NT * 256 + 16 * ta[q] + lane;
-              if (to_lds) {
-                dst[es] = s1;
-                dst[es + 1] = s1n;
-              } else {
-                st2_sc1(rs, 8 * es, s1, s1n);
-              }
-            }
-          }
-          __syncthreads();
-        },
-        loc, nit, T, tree, origin, out_mean, out_cov, none, L);
-  };
-
-  if (BAL) {
-    ItemLoc loc;
-    int64_t chunk;
-    if (!locate_balanced(blockIdx.x, gridDim.x, cell_cnt, cell_off, n_cells, loc, &chunk))
-      return;  // uniform
-    const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) * chunk;
-    item(loc, static_cast<int32_t>(loc.cnt > 0 ? ceil_div_fast(loc.cnt, chunk) : 1), i0,
-         min(i0 + chunk, loc.cnt));
-    return;
-  }
-  ItemLoc loc;
-  if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc)) return;  // uniform
-  const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
-  item(loc, items_of(loc.cnt, lg_chunk), i0, min(i0 + (int64_t(1) << lg_chunk), loc.cnt));
-}
-
 template <typename P, int RB, bool MINK>
 static int launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
                   const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
@@ -948,34 +727,6 @@ static int launch(const P *pos, int64_t ld, int T, const double *origin, const i
   constexpr int threads = Geo<RB>::NW * 64;
   const int lg_wq = store_lg_wave_quota(RB, n_bound);
   TreeLayout tree;
-  if constexpr (!MINK && RB >= CCMPC_LDS_GRAM_MIN_RB) {
-    // long horizons, moments only: the LDS-staged kernel (same items in power-of-two mode,
-    // so the same workspace; its own resident grid in balanced mode)
-    const int gridL = balanced_mode(n_bound) ? resident_grid<momentsL_kernel<P, RB, true>>(
-                                                   kLW * 64) : 0;
-    if (gridL > 0 && 2 * n_cells <= gridL) {
-      if (!tree_layout(ws, ws_bytes, balanced_max_items(threads), n_cells, slab_doubles(RB),
-                       tree))
-        return CCMPC_ERR_WORKSPACE;
-      hipLaunchKernelGGL((momentsL_kernel<P, RB, true>), dim3(static_cast<unsigned>(gridL)),
-                         dim3(kLW * 64), 0, s, cnt, off, n_cells, pos, ld, T, origin, 0, tree,
-                         mean, cov);
-      if (defer_root(RB, false, true))
-        hipLaunchKernelGGL((root_finalize_kernel<P, RB>),
-                           dim3(static_cast<unsigned>(n_cells * n_tiles(RB))),
-                           dim3(RootGeo<RB>::THREADS), 0, s, cnt, off, n_cells, gridL, pos, ld, T,
-                           origin, tree.slabs[0], mean, cov);
-      return CCMPC_OK;
-    }
-    const int lg_chunk = store_lg_chunk(RB, n_bound);
-    const int64_t items = max_items(n_cells, n_bound, int64_t(1) << lg_chunk);
-    if (!tree_layout(ws, ws_bytes, items, n_cells, slab_doubles(RB), tree))
-      return CCMPC_ERR_WORKSPACE;
-    hipLaunchKernelGGL((momentsL_kernel<P, RB, false>), dim3(static_cast<unsigned>(items)),
-                       dim3(kLW * 64), 0, s, cnt, off, n_cells, pos, ld, T, origin, lg_chunk, tree,
-                       mean, cov);
-    return CCMPC_OK;
-  }
   const int grid =
       balanced_mode(n_bound) ? resident_grid<moments_kernel<P, RB, MINK, true>>(threads) : 0;
   if (grid > 0 && 2 * n_cells <= grid) {
