@@ -17,6 +17,8 @@
 // evaluated in float64 and rounded to float32.
 #include "sampler.hpp"
 
+#include <type_traits>
+
 namespace ccmpc {
 
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
@@ -37,19 +39,26 @@ __device__ unsigned long long g_samp_ts[kStepProbeWG * kStepProbeSlots];
 // actions of the block's particles in parallel into LDS (the Philox / Box-Muller / exp work),
 // then one wave runs the Unicycle chain, one lane per particle -- the serial part is just the
 // integration.
-constexpr int kSampP = 64;       // particles per block (one wave in the chain phase)
+constexpr int kSampP = 64;       // particles per chain wave (one lane each)
 constexpr int kSlots = 8;        // waves drawing actions
 constexpr int kSampThreads = kSampP * kSlots;
+// Chain waves per block: 1 for small clouds (many short blocks spread the serial chain phase);
+// 4 for large ones (N > kSampWideN per OV): one block per 256 particles instead of 64, so a
+// 100 000-particle cloud is 391 blocks of which four waves integrate, not 1563 blocks each
+// running one chain wave while seven wait.  The per-particle arithmetic and Philox keys do not
+// depend on the block shape: the same bits either way.
+constexpr int kSampWideN = 8192;
 
-template <bool PP, bool ZIN, bool EPSIN>
+template <bool PP, bool ZIN, bool EPSIN, int NCH>
 __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
     const double *__restrict__ init_state, const double *__restrict__ latent_cdf, int n_latent,
     const float *__restrict__ gmm, const int32_t *__restrict__ z_in,
     const float *__restrict__ eps_in, int64_t N, int T, float dt, uint64_t seed_arg,
     const uint64_t *__restrict__ seed_dev, uint32_t ov_base, int32_t *__restrict__ out_z,
     float *__restrict__ out_pos, int64_t ld) {
-  __shared__ float act[2][40][kSampP];  // (dphi, a) per (t, particle); T <= 40
-  __shared__ int zs[kSampP];
+  constexpr int PB = kSampP * NCH;       // particles per block
+  extern __shared__ float act[];          // (dphi, a) per (t, particle): [2][T][PB]
+  __shared__ int zs[PB];
   __shared__ double cdf_s[64];           // this OV's latent CDF, one coalesced read
   __shared__ float gmm_s[PP ? 1 : 64 * 40 * 5 / 4];  // per-latent rows, staged when they fit
   CCMPC_STEP_TS(g_samp_ts, 0);
@@ -58,8 +67,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
   // a seed in device memory lets a captured graph draw fresh particles on every replay
   const uint64_t seed = seed_dev ? *seed_dev : seed_arg;
   const uint32_t key = ov_base + static_cast<uint32_t>(ov);  // global OV id keys the streams
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kSampP + lane;
-  const bool valid = i < N;
+  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * PB;
   if (!ZIN && threadIdx.x < n_latent)
     cdf_s[threadIdx.x] = latent_cdf[static_cast<int64_t>(ov) * n_latent + threadIdx.x];
   // the OV's per-latent parameter table (L x T x 5 floats) read once, in parallel with the CDF,
@@ -71,7 +79,9 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
       gmm_s[e] = gmm[static_cast<int64_t>(ov) * gsz + e];
   __syncthreads();
   CCMPC_STEP_TS(g_samp_ts, 1);
-  if (slot == 0 && valid) {
+  for (int q = threadIdx.x; q < PB; q += blockDim.x) {
+    const int64_t i = blk0 + q;
+    if (i >= N) continue;
     int z;
     if (ZIN) {
       z = z_in[static_cast<int64_t>(ov) * N + i];
@@ -79,18 +89,26 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
     } else {
       z = draw_latent(i, key, seed, cdf_s, n_latent);
     }
-    zs[lane] = z;
+    zs[q] = z;
     out_z[static_cast<int64_t>(ov) * N + i] = z;
   }
   __syncthreads();
   CCMPC_STEP_TS(g_samp_ts, 2);
-  if (valid)
-    for (int t = slot; t < T; t += kSlots)
-      draw_action<PP, EPSIN>(t, i, zs[lane], ov, T, n_latent, N, key, seed, gmm, gmm_s, staged,
-                             eps_in, act[0][t][lane], act[1][t][lane]);
+  // every (t, chain) pair's 64 actions: chain c = the block's particles 64 c .. 64 c + 63
+  for (int u = slot; u < T * NCH; u += kSlots) {
+    const int t = u / NCH, c = u - t * NCH;
+    const int q = c * kSampP + lane;
+    const int64_t i = blk0 + q;
+    if (i < N)
+      draw_action<PP, EPSIN>(t, i, zs[q], ov, T, n_latent, N, key, seed, gmm, gmm_s, staged,
+                             eps_in, act[t * PB + q], act[(T + t) * PB + q]);
+  }
   __syncthreads();
   CCMPC_STEP_TS(g_samp_ts, 3);
-  if (slot != 0 || !valid) return;
+  if (slot >= NCH) return;
+  const int q = slot * kSampP + lane;
+  const int64_t i = blk0 + q;
+  if (i >= N) return;
   const double *st = init_state + 4 * ov;
   float x = static_cast<float>(st[0]), y = static_cast<float>(st[1]);
   float phi = static_cast<float>(st[2]), v = static_cast<float>(st[3]);
@@ -98,7 +116,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
   sincos_rn(phi, s0, c0);
   float *o = out_pos + static_cast<int64_t>(ov) * ((N + 3) & ~int64_t(3)) + i;
   for (int t = 0; t < T; ++t) {
-    unicycle_step(x, y, phi, v, s0, c0, act[0][t][lane], act[1][t][lane], dt);
+    unicycle_step(x, y, phi, v, s0, c0, act[t * PB + q], act[(T + t) * PB + q], dt);
     o[(2 * t) * ld] = x;
     o[(2 * t + 1) * ld] = y;
   }
@@ -106,14 +124,33 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
 }
 
 template <bool PP, bool ZIN, bool EPSIN>
-static void launch_sampler(dim3 grid, hipStream_t s, const double *init_state,
+static void launch_sampler(int64_t n_ov, hipStream_t s, const double *init_state,
                            const double *latent_cdf, int n_latent, const float *gmm,
                            const int32_t *z_in, const float *eps_in, int64_t N, int T, float dt,
                            uint64_t seed, const uint64_t *seed_dev, uint32_t ov_base,
                            int32_t *out_z, float *out_pos, int64_t ld) {
-  hipLaunchKernelGGL((sample_unicycle_kernel<PP, ZIN, EPSIN>), grid, dim3(kSampThreads), 0, s,
-                     init_state, latent_cdf, n_latent, gmm, z_in, eps_in, N, T, dt, seed,
-                     seed_dev, ov_base, out_z, out_pos, ld);
+  auto go = [&](auto nch) {
+    constexpr int NCH = decltype(nch)::value, PB = kSampP * NCH;
+    const dim3 grid(static_cast<unsigned>((N + PB - 1) / PB), static_cast<unsigned>(n_ov));
+    const size_t lds = sizeof(float) * 2 * T * PB;
+    if (lds > 48 * 1024) {  // long horizons on wide blocks: allow the larger dynamic LDS once
+      static bool raised = false;
+      if (!raised) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(
+                                &sample_unicycle_kernel<PP, ZIN, EPSIN, NCH>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(sizeof(float) * 2 * 40 * PB));
+        raised = true;
+      }
+    }
+    hipLaunchKernelGGL((sample_unicycle_kernel<PP, ZIN, EPSIN, NCH>), grid, dim3(kSampThreads),
+                       lds, s, init_state, latent_cdf, n_latent, gmm, z_in, eps_in, N, T, dt,
+                       seed, seed_dev, ov_base, out_z, out_pos, ld);
+  };
+  if (N > kSampWideN)
+    go(std::integral_constant<int, 4>{});
+  else
+    go(std::integral_constant<int, 1>{});
 }
 
 }  // namespace ccmpc
@@ -155,13 +192,12 @@ extern "C" int ccmpc_sample_unicycle_ex(const double *init_state, const double *
   CCMPC_REQUIRE(init_state && gmm && out_z && out_pos, "null pointer");
   CCMPC_REQUIRE(z_in || latent_cdf, "latent_cdf is needed when z is drawn here");
   CCMPC_REQUIRE(ld >= n_ov * ((N + 3) & ~int64_t(3)), "ld too small");
-  const dim3 grid(static_cast<unsigned>((N + kSampP - 1) / kSampP), static_cast<unsigned>(n_ov));
   hipStream_t s = as_stream(stream);
   const int L = static_cast<int>(n_latent), Ti = static_cast<int>(T);
   const float fdt = static_cast<float>(dt);
   const uint32_t base = static_cast<uint32_t>(ov_base);
 #define CCMPC_SAMPLER(PP, ZIN, EPSIN)                                                        \
-  launch_sampler<PP, ZIN, EPSIN>(grid, s, init_state, latent_cdf, L, gmm, z_in, eps_in, N, Ti, \
+  launch_sampler<PP, ZIN, EPSIN>(n_ov, s, init_state, latent_cdf, L, gmm, z_in, eps_in, N, Ti, \
                                  fdt, seed, seed_dev, base, out_z, out_pos, ld)
   const int mode = (pp ? 4 : 0) | (z_in ? 2 : 0) | (eps_in ? 1 : 0);
   switch (mode) {

@@ -164,3 +164,35 @@ def test_fused_refuses_large_clouds_and_bad_args(gpu):
                                  None, None, None, 1, None, None, None, 0, None, None, 0, None,
                                  None, None, None, None)
     assert rc == -1
+
+
+@pytest.mark.parametrize("T,mode", [(8, "philox"), (40, "philox"), (8, "injected"),
+                                    (8, "per_particle")])
+def test_wide_sampler_blocks_give_the_narrow_blocks_bits(gpu, T, mode):
+    """Above 8192 particles per OV the sampler runs four chain waves per block (256 particles)
+    instead of one; particle i's draws and chain depend only on (i, OV, seed), so the first
+    8192 particles of a 20 000-particle call equal an 8192-particle call bit for bit, in every
+    input mode (Philox, injected z / eps, per-particle parameters)."""
+    from ccmpc import engine as e
+    O, L, Nw, Nn = 2, 25, 20_000, 8192
+    init, pmf, gmm = _inputs(O, L, T, 12)
+    kw = {}
+    if mode != "philox":
+        g = torch.Generator().manual_seed(5)
+        z = torch.multinomial(torch.as_tensor(pmf), Nw, replacement=True,
+                              generator=g).to(torch.int32)
+        eps = torch.randn((O, Nw, T, 2), generator=g, dtype=torch.float32)
+        kw = dict(z=z, eps=eps)
+        if mode == "per_particle":
+            pp = np.stack([gmm[o][z[o].numpy()] for o in range(O)])
+            pp[..., 1] += np.random.default_rng(3).normal(0, 0.05, pp[..., 1].shape).astype(
+                np.float32)
+            kw["per_particle"] = True
+    gw = pp if kw.get("per_particle") else gmm
+    zw, sw = e.sample_unicycle(init, pmf, gw, Nw, T, seed=77, device=gpu, **kw)
+    kn = {k: (v[:, :Nn].contiguous() if torch.is_tensor(v) else v) for k, v in kw.items()}
+    gn = pp[:, :Nn] if kw.get("per_particle") else gmm
+    zn, sn = e.sample_unicycle(init, pmf, gn, Nn, T, seed=77, device=gpu, **kn)
+    np.testing.assert_array_equal(zw.cpu().numpy()[:, :Nn], zn.cpu().numpy())
+    for o in range(O):
+        np.testing.assert_array_equal(sw.cell_positions(o)[:Nn], sn.cell_positions(o))
