@@ -269,10 +269,12 @@ inline size_t l4_split_bytes(int64_t T, int64_t n_cells, int S, size_t *o1, size
 #endif
 constexpr int64_t kL4Tail2Max = CCMPC_L4_TAIL2_MAX;
 
+constexpr int kL4MaxSplit = 64;  // workgroups per (cell, t): one wave holds their partials
+
 inline int l4_split_factor(int64_t n_cells, int64_t n_bound) {
   const int64_t per = n_cells > 0 ? (n_bound + n_cells - 1) / n_cells : 0;
   const int64_t S = (per + 1023) / 1024;  // ~1024 particles per workgroup on the average cell
-  return static_cast<int>(S < 1 ? 1 : (S > 64 ? 64 : S));
+  return static_cast<int>(S < 1 ? 1 : (S > kL4MaxSplit ? kL4MaxSplit : S));
 }
 
 // Pass 2's per-particle work over [i0, i1) of one (cell, t): the bbox corners at the particle's
@@ -366,14 +368,21 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
     st2_sc1(rm, 16, s2, 0.0);
   }
   if (!arrive_last(sp.ctr + ct, sp.S, &flag)) return;
+  // every chunk's partials loaded at once (thread k: chunk k), then summed in chunk order by one
+  // thread from LDS: deterministic, and one L2 round trip instead of S dependent ones
+  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part1 + static_cast<int64_t>(ct) * sp.S * 4);
+  __shared__ double2 pu[kL4MaxSplit], pv[kL4MaxSplit];
+  if (threadIdx.x < sp.S) {
+    pu[threadIdx.x] = ld2_sc1(rp, 32 * threadIdx.x);
+    pv[threadIdx.x] = ld2_sc1(rp, 32 * threadIdx.x + 16);
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {  // chunk order: deterministic
-    const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part1 + static_cast<int64_t>(ct) * sp.S * 4);
     double a = 0.0, b1 = 0.0, b2 = 0.0;
     for (int k = 0; k < sp.S; ++k) {
-      const double2 u = ld2_sc1(rp, 32 * k), v = ld2_sc1(rp, 32 * k + 16);
-      a += u.x;
-      b1 += u.y;
-      b2 += v.x;
+      a += pu[k].x;
+      b1 += pu[k].y;
+      b2 += pv[k].x;
     }
     const double nn = static_cast<double>(n);
     const double theta = a / nn;
@@ -435,21 +444,27 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass2_kernel(
   }
   const int nct = gridDim.x / sp.S;
   if (!arrive_last(sp.ctr + nct + ct, sp.S, &flag)) return;
-  if (threadIdx.x == 0) {
+  // the maxima over chunks (order-free): the first wave loads them all at once and reduces
+  if (threadIdx.x < 64) {
     const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part2 + static_cast<int64_t>(ct) * sp.S * 4);
     double b[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    for (int k = 0; k < sp.S; ++k) {
-      const double2 u = ld2_sc1(rp, 32 * k), v = ld2_sc1(rp, 32 * k + 16);
-      b[0] = fmax(b[0], u.x);
-      b[1] = fmax(b[1], u.y);
-      b[2] = fmax(b[2], v.x);
-      b[3] = fmax(b[3], v.y);
+    if (threadIdx.x < sp.S) {
+      const double2 u = ld2_sc1(rp, 32 * threadIdx.x), v = ld2_sc1(rp, 32 * threadIdx.x + 16);
+      b[0] = u.x;
+      b[1] = u.y;
+      b[2] = v.x;
+      b[3] = v.y;
     }
-    for (int q = 0; q < 4; ++q) {
-      out_A[static_cast<int64_t>(ct) * 8 + 2 * q] = A[q][0];
-      out_A[static_cast<int64_t>(ct) * 8 + 2 * q + 1] = A[q][1];
-      out_b[static_cast<int64_t>(ct) * 4 + q] = b[q];
-    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) b[q] = fmax(b[q], __shfl_xor(b[q], o, 64));
+    if (threadIdx.x == 0)
+      for (int q = 0; q < 4; ++q) {
+        out_A[static_cast<int64_t>(ct) * 8 + 2 * q] = A[q][0];
+        out_A[static_cast<int64_t>(ct) * 8 + 2 * q + 1] = A[q][1];
+        out_b[static_cast<int64_t>(ct) * 4 + q] = b[q];
+      }
   }
 }
 

@@ -4,7 +4,7 @@ bucketing kernels and the Minkowski cycle stamps s_memrealtime (100 MHz) at its 
 boundaries, so one replay of the captured step graph shows each kernel's span, its phases and
 the gaps between kernels.
 
-    python tools/probe_step.py [--direct] [--N 5000]
+    python tools/probe_step.py [--direct] [--N 5000] [--O 4]
 """
 import argparse
 import ctypes
@@ -33,11 +33,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--direct", action="store_true", help="bound C-ABI calls, not the graph")
     ap.add_argument("--N", type=int, default=5000)
+    ap.add_argument("--O", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     from ccmpc import engine, episode, planner
     dev = torch.device("cuda", 0)
-    O, N, ph = 4, a.N, 8
+    O, N, ph = a.O, a.N, 8
     init, pmf, gmm = episode.synthetic_gmm(O, T=ph, seed=20251015)
     minpos = np.array([150.0, -120.0])
     pasts = [np.array([[minpos[0] + init[o, 0] - 2.0, minpos[1] + init[o, 1]]]) for o in range(O)]
