@@ -14,13 +14,17 @@
 // mode and 1 + z for a rare latent.  Three short kernels:
 //   B1 stats   per block: latent counts (LDS int atomics, exact) and, per wave, the kept-mode
 //              sums of its 64 final positions (bucket.hpp's centre groups), published
-//              write-through; the OV's last arriving block sums them in the canonical order
-//              (bucket.hpp) -> centres
-//   B2 keys    per block: key histogram (LDS int atomics, exact), published write-through; the
-//              OV's last arriving block scans them -> per chunk of 16 blocks the bin starts,
-//              4-aligned cell offsets
+//              write-through -> centres
+//   B2 keys    per block: key histogram (LDS int atomics, exact), published write-through ->
+//              per chunk of 16 blocks the bin starts, 4-aligned cell offsets
 //   B3 scatter per block: stable rank inside the block (wave ballots, waves in order) -> copy
 //              the particle's 2T coordinates to its bucket slot
+// B1 and B2 meet in two hand-off levels: a chunk of kChunkRows = 16 blocks is exactly one centre
+// superblock (64 groups of 64 particles), so the chunk's last arriving block sums its superblock
+// in the canonical order (bucket.hpp) and its latent counts / bin totals, every load in flight at
+// once; the OV's last arriving chunk then combines the chunk results (one more round of loads).
+// A single OV-level arriver walking every block's partials was ~8 dependent round trips of
+// fresh data (10 us per kernel at N = 100 000, profiles/r03/s13_probe_step_c1_100k.log).
 // The last-arriver hand-off is the one of the moment reduction (gram.hpp: sc1 stores, drain,
 // agent-scope ticket, sc1 loads); its counters live at the head of the workspace, which must be
 // zero-filled once (every call leaves them zero).
@@ -56,31 +60,24 @@ struct BucketArgs {
   const double *minpos;     // [n_ov][2]
   int nb;                   // blocks per OV
   // workspace
-  int32_t *ctr;             // [2][n_ov] arrival counters (zero between calls)
-  double *part;             // [n_ov][nb][E1]: latent counts [L] (as doubles; E1 even)
-  int E1;
+  int32_t *ctr;             // [2][n_ov] OV arrival counters, then [2][n_ov][nch] chunk counters
+                            // (zero between calls)
+  int nch;                  // chunks of kChunkRows blocks per OV
+  int32_t *bcnt;            // [n_ov][nb][L]: each block's latent counts
+  int32_t *ccnt;            // [n_ov][nch][L]: each chunk's latent counts
   double *gpart;            // [n_ov][G][max_k][2]: per 64-particle group kept-mode sums
   int G;                    // groups per OV = ceil(N / 64)
+  double *csup;             // [n_ov][nch][max_k][2]: each chunk's superblock sums (bucket.hpp)
   double *centre;           // [n_ov][max_k][2]
   int32_t *hist;            // [n_ov][nb][nbins]
-  int64_t *chunk_off;       // [n_ov][ceil(nb / kChunkRows)][nbins]: each chunk's bin starts
+  int32_t *ctot;            // [n_ov][nch][nbins]: each chunk's bin totals
+  int64_t *chunk_off;       // [n_ov][nch][nbins]: each chunk's bin starts
   // outputs
   float *out;
   int64_t ld_out;
   int64_t *cell_off, *cell_cnt;
   double *cell_pmf, *init_center;
 };
-
-__device__ __forceinline__ double block_sum256(double v, double *red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  const double s = (red[0] + red[1]) + (red[2] + red[3]);
-  __syncthreads();
-  return s;
-}
 
 __device__ __forceinline__ void final_world(const BucketArgs &a, int o, int64_t i, double &x,
                                             double &y) {
@@ -89,15 +86,34 @@ __device__ __forceinline__ void final_world(const BucketArgs &a, int o, int64_t 
   y = static_cast<double>(p[(2 * (a.T - 1) + 1) * a.ld_in]) + a.minpos[2 * o + 1];
 }
 
+static_assert(kChunkRows * (kBucketBlock / kCentreGroup) == kCentreSuper,
+              "a chunk of blocks is one centre superblock");
+
+// The chunk's and OV's arrival counters (stats: which = 0, hist: which = 1).
+__device__ __forceinline__ int32_t *chunk_ctr(const BucketArgs &a, int which, int o, int ch) {
+  return a.ctr + 2 * a.n_ov + (static_cast<int64_t>(which) * a.n_ov + o) * a.nch + ch;
+}
+__device__ __forceinline__ int32_t *ov_ctr(const BucketArgs &a, int which, int o) {
+  return a.ctr + which * a.n_ov + o;
+}
+// The OV level of the hand-off: the OV's last arriving chunk goes on.  An OV of one chunk has
+// no second level (its chunk's last arriver is the OV's), but still drains its stores, which it
+// reads back below.
+__device__ __forceinline__ bool ov_last(const BucketArgs &a, int which, int o, int *flag) {
+  if (a.nch > 1) return arrive_last(ov_ctr(a, which, o), a.nch, flag);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  return true;
+}
+
 __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
   BKT_TS(0, 0);
   __shared__ int cnt[64];
-  __shared__ double red[4];
   __shared__ int flag;
   __shared__ int keep_s[64];
   __shared__ int zv_s[kMaxKept];
-  __shared__ double nk_s[kMaxKept];
-  __shared__ double2 sup_s[kMaxKept][kCentreSuper];
+  __shared__ int nk_s[kMaxKept];
+  __shared__ double2 sup_s[kMaxKept][kCentreSuper];  // a superblock's partials / chunk sums
   const int o = blockIdx.y, blk = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int K = a.n_kept[o];
@@ -114,6 +130,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
     cnt[l] = 0;
     keep_s[l] = a.keep_map[o * a.L + l];
   }
+  if (threadIdx.x < kMaxKept) nk_s[threadIdx.x] = 0;
   __syncthreads();
   BKT_TS(0, 1);
   if (zv >= 0) atomicAdd(&cnt[zv], 1);
@@ -127,73 +144,104 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
     if (lane == 0 && g < a.G) st2_sc1(rg, 16 * (g * a.max_k + k), sx, sy);
   }
   __syncthreads();
-  // latent counts, published write-through; the OV's last arriver combines them
-  double *mine = a.part + (static_cast<int64_t>(o) * a.nb + blk) * a.E1;
-  const __amdgpu_buffer_rsrc_t rm = slab_rsrc(mine);
-  for (int e = 2 * threadIdx.x; e < a.L; e += 2 * blockDim.x)
-    st2_sc1(rm, 8 * e, static_cast<double>(cnt[e]),
-            e + 1 < a.L ? static_cast<double>(cnt[e + 1]) : 0.0);
+  // latent counts, published write-through
+  const __amdgpu_buffer_rsrc_t rb = raw_rsrc(a.bcnt + static_cast<int64_t>(o) * a.nb * a.L);
+  for (int l = threadIdx.x; l < a.L; l += blockDim.x) st1_sc1(rb, 4 * (blk * a.L + l), cnt[l]);
   BKT_TS(0, 2);
-  if (!arrive_last(a.ctr + o, a.nb, &flag)) return;
+  // ---- chunk level: the chunk's last arriving block -----------------------------------------
+  const int ch = blk / kChunkRows, r0 = ch * kChunkRows, nr = min(kChunkRows, a.nb - r0);
+  if (!arrive_last(chunk_ctr(a, 0, o, ch), nr, &flag)) return;
   BKT_TS(0, 3);
+  // (1) the superblock's K x 64 group partials into LDS and (2) the chunk's latent counts, every
+  // load in flight together
+  const int g0 = ch * kCentreSuper, ng = min(kCentreSuper, a.G - g0);
+  constexpr int kPartRounds = kMaxKept * kCentreSuper / kBucketBlock;
+  double2 pv[kPartRounds];
+#pragma unroll
+  for (int r = 0; r < kPartRounds; ++r) {
+    const int t = threadIdx.x + r * kBucketBlock, k = t / kCentreSuper, q = t % kCentreSuper;
+    const int kc = k < K ? k : (K > 0 ? K - 1 : 0), qc = q < ng ? q : ng - 1;  // valid addresses
+    pv[r] = ld2_sc1(rg, 16 * ((g0 + qc) * a.max_k + kc));
+  }
+  int32_t cv[kChunkRows];
+  const bool counter = threadIdx.x < a.L;
+#pragma unroll
+  for (int j = 0; j < kChunkRows; ++j)
+    cv[j] = counter ? ld1_sc1(rb, 4 * ((r0 + (j < nr ? j : nr - 1)) * a.L + threadIdx.x)) : 0;
+#pragma unroll
+  for (int r = 0; r < kPartRounds; ++r) {
+    const int t = threadIdx.x + r * kBucketBlock, k = t / kCentreSuper, q = t % kCentreSuper;
+    if (k < K) sup_s[k][q] = pv[r];
+  }
+  int32_t csum = 0;
+#pragma unroll
+  for (int j = 0; j < kChunkRows; ++j) csum += j < nr ? cv[j] : 0;
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs = slab_rsrc(a.csup + static_cast<int64_t>(o) * a.nch * a.max_k * 2);
+  const __amdgpu_buffer_rsrc_t rc = raw_rsrc(a.ccnt + static_cast<int64_t>(o) * a.nch * a.L);
+  if (threadIdx.x < K) {  // S_ch = 0.0 + P_{64 ch} + P_{64 ch + 1} + ... (bucket.hpp)
+    double2 acc = {0.0, 0.0};
+    for (int q = 0; q < ng; ++q) {
+      acc.x += sup_s[threadIdx.x][q].x;
+      acc.y += sup_s[threadIdx.x][q].y;
+    }
+    st2_sc1(rs, 16 * (ch * a.max_k + threadIdx.x), acc.x, acc.y);
+  }
+  if (counter) st1_sc1(rc, 4 * (ch * a.L + threadIdx.x), csum);
+  BKT_TS(0, 4);
+  // ---- OV level: the OV's last arriving chunk ------------------------------------------------
+  if (!ov_last(a, 0, o, &flag)) return;
+  BKT_TS(0, 5);
   for (int l = threadIdx.x; l < a.L; l += blockDim.x) {
     const int k = keep_s[l];
     if (k >= 0) zv_s[k] = l;
   }
   __syncthreads();
-  // n_k: kept mode k's own particles (integer-exact in any order); every mode's loads together
-  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(a.part + static_cast<int64_t>(o) * a.nb * a.E1);
-  constexpr int KB = 4;
-  for (int k0 = 0; k0 < K; k0 += KB) {
-    double n[KB];
-#pragma unroll
-    for (int j = 0; j < KB; ++j) n[j] = 0.0;
-    for (int b = threadIdx.x; b < a.nb; b += blockDim.x) {
-      double2 c[KB];
-#pragma unroll
-      for (int j = 0; j < KB; ++j) {
-        const int k = k0 + j < K ? k0 + j : K - 1;  // clamped: always a valid address
-        c[j] = ld2_sc1(rp, 8 * (b * a.E1 + (zv_s[k] & ~1)));
-      }
-#pragma unroll
-      for (int j = 0; j < KB; ++j) n[j] += (zv_s[k0 + j < K ? k0 + j : K - 1] & 1) ? c[j].y : c[j].x;
-    }
-#pragma unroll
-    for (int j = 0; j < KB; ++j) {
-      const double s = block_sum256(n[j], red);
-      if (k0 + j < K && threadIdx.x == 0) nk_s[k0 + j] = s;
-    }
-  }
-  // the canonical centre sums (bucket.hpp): superblocks in parallel, then left to right
-  const int J = (a.G + kCentreSuper - 1) / kCentreSuper;
+  // n_k: kept mode k's own particles, summed over the chunks (integer-exact in any order); the
+  // chunk sums S_ch in windows of kCentreSuper chunks, added left to right (bucket.hpp)
   double2 tot = {0.0, 0.0};  // thread k's running sum of mode k
-  for (int j0 = 0; j0 < J; j0 += kCentreSuper) {
-    const int nj = min(kCentreSuper, J - j0);
-    for (int u = threadIdx.x; u < K * nj; u += blockDim.x) {
-      const int k = u / nj, j = j0 + u % nj;
-      sup_s[k][j - j0] = superblock_sum(j, a.G, [&](int gg) {
-        return ld2_sc1(rg, 16 * (gg * a.max_k + k));
-      });
+  for (int c0 = 0; c0 < a.nch; c0 += kCentreSuper) {
+    const int nc = min(kCentreSuper, a.nch - c0);
+    double2 sv[kPartRounds];
+    int32_t nv[kPartRounds];
+#pragma unroll
+    for (int r = 0; r < kPartRounds; ++r) {
+      const int t = threadIdx.x + r * kBucketBlock, k = t / kCentreSuper, q = t % kCentreSuper;
+      const int kc = k < K ? k : (K > 0 ? K - 1 : 0), qc = q < nc ? q : nc - 1;
+      sv[r] = ld2_sc1(rs, 16 * ((c0 + qc) * a.max_k + kc));
+      nv[r] = K > 0 ? ld1_sc1(rc, 4 * ((c0 + qc) * a.L + zv_s[kc])) : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kPartRounds; ++r) {
+      const int t = threadIdx.x + r * kBucketBlock, k = t / kCentreSuper, q = t % kCentreSuper;
+      if (k < K && q < nc) {
+        sup_s[k][q] = sv[r];
+        atomicAdd(&nk_s[k], nv[r]);
+      }
     }
     __syncthreads();
     if (threadIdx.x < K)
-      for (int j = 0; j < nj; ++j) {
-        tot.x += sup_s[threadIdx.x][j].x;
-        tot.y += sup_s[threadIdx.x][j].y;
+      for (int q = 0; q < nc; ++q) {
+        tot.x += sup_s[threadIdx.x][q].x;
+        tot.y += sup_s[threadIdx.x][q].y;
       }
     __syncthreads();
   }
   if (threadIdx.x < K) {
     const int k = threadIdx.x;
-    const double cx = tot.x / nk_s[k], cy = tot.y / nk_s[k];
+    const double n = static_cast<double>(nk_s[k]);
+    const double cx = tot.x / n, cy = tot.y / n;
     a.centre[(o * a.max_k + k) * 2] = cx;
     a.centre[(o * a.max_k + k) * 2 + 1] = cy;
     const int cell = a.cell_base[o] + k;
     a.init_center[2 * cell] = cx;
     a.init_center[2 * cell + 1] = cy;
   }
-  BKT_TS(0, 4);
+  BKT_TS(0, 6);
 }
+
+// Chunk bin totals the OV's last arriver keeps in LDS for the chunk starts (beyond: re-read)
+constexpr int kHistKeep = 4096;  // 16 KB: N <= ~200 000 at 78 bins
 
 __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
   BKT_TS(1, 0);
@@ -202,6 +250,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
   __shared__ int flag;
   __shared__ int keep_s[64];
   __shared__ double cen_s[kMaxKept][2];
+  __shared__ int32_t pre_s[kHistKeep];  // [chunk][bin]: the bin's count in the chunks before
   const int o = blockIdx.y, blk = blockIdx.x;
   const int K = a.n_kept[o];
   const int G = a.L + 1;
@@ -230,52 +279,51 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
     if (zs[r] >= 0) atomicAdd(&h[key_staged(zs[r], xs[r], ys[r], keep_s, cen_s, K, a.L)], 1);
   __syncthreads();
   const int64_t stride = static_cast<int64_t>(a.max_k) * G;
-  int32_t *hist0 = a.hist + static_cast<int64_t>(o) * a.nb * stride;
-  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hist0, 0, 0x7fffffff,
-                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rh = raw_rsrc(a.hist + static_cast<int64_t>(o) * a.nb * stride);
   for (int b = threadIdx.x; b < nbins; b += blockDim.x)
     st1_sc1(rh, 4 * static_cast<int>(blk * stride + b), h[b]);
   BKT_TS(1, 2);
-  if (!arrive_last(a.ctr + a.n_ov + o, a.nb, &flag)) return;
+  // ---- chunk level: the chunk's bin totals (every row's load in flight together) ------------
+  const int ch = blk / kChunkRows, r0 = ch * kChunkRows, nr = min(kChunkRows, a.nb - r0);
+  if (!arrive_last(chunk_ctr(a, 1, o, ch), nr, &flag)) return;
   BKT_TS(1, 3);
-  // The OV's scan, as integer sums over the published block histograms (exact: the order of the
-  // additions does not matter).  (1) per (chunk of kChunkRows blocks, bin) column sums -- every
-  // load of a task in flight together, two tasks per round, all threads -- into chunk_off and
-  // the bin totals (LDS int64 atomics); (2) bin starts and cell offsets; (3) per bin, each
-  // chunk's start in place of its sum.  bucket_scatter adds the block's offset inside its chunk
-  // (<= kChunkRows - 1 rows).  The old per-bin serial column walk over all nb blocks (twice) was
-  // a dependent chain of ~nb / 8 round trips: 63 us at N = 100 000.
-  const int nch = (a.nb + kChunkRows - 1) / kChunkRows;
-  int64_t *coff = a.chunk_off + static_cast<int64_t>(o) * nch * stride;
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) start[b] = 0;
-  __syncthreads();
-  const int tasks = nch * nbins;
-  auto chunk_sum = [&](int task) {
-    const int c = task / nbins, b = task - c * nbins;
-    const int r0 = c * kChunkRows, nr = min(kChunkRows, a.nb - r0);
+  const __amdgpu_buffer_rsrc_t rt = raw_rsrc(a.ctot + static_cast<int64_t>(o) * a.nch * stride);
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
     int32_t v[kChunkRows];
 #pragma unroll
     for (int j = 0; j < kChunkRows; ++j)
       v[j] = ld1_sc1(rh, 4 * static_cast<int>((r0 + (j < nr ? j : nr - 1)) * stride + b));
-    int64_t sum = 0;
+    int32_t sum = 0;
 #pragma unroll
     for (int j = 0; j < kChunkRows; ++j) sum += j < nr ? v[j] : 0;
-    return sum;
-  };
-  for (int t0 = threadIdx.x; t0 < tasks; t0 += 2 * blockDim.x) {
-    const int t1 = t0 + blockDim.x;
-    const int64_t s0 = chunk_sum(t0);
-    const int64_t s1 = t1 < tasks ? chunk_sum(t1) : 0;
-    coff[(t0 / nbins) * stride + t0 % nbins] = s0;
-    atomicAdd(reinterpret_cast<unsigned long long *>(&start[t0 % nbins]),
-              static_cast<unsigned long long>(s0));
-    if (t1 < tasks) {
-      coff[(t1 / nbins) * stride + t1 % nbins] = s1;
-      atomicAdd(reinterpret_cast<unsigned long long *>(&start[t1 % nbins]),
-                static_cast<unsigned long long>(s1));
-    }
+    st1_sc1(rt, 4 * static_cast<int>(ch * stride + b), sum);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's chunk sums, read below
+  BKT_TS(1, 4);
+  // ---- OV level: bin totals, cell offsets, every chunk's start in every bin -----------------
+  if (!ov_last(a, 1, o, &flag)) return;
+  BKT_TS(1, 5);
+  // pass 1 (thread per bin): running counts over the chunks, 32 loads in flight
+  const bool keep = static_cast<int64_t>(a.nch) * nbins <= kHistKeep;
+  constexpr int kBatch = 32;
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+    int64_t run = 0;
+    for (int c0 = 0; c0 < a.nch; c0 += kBatch) {
+      int32_t v[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int c = c0 + j < a.nch ? c0 + j : a.nch - 1;
+        v[j] = ld1_sc1(rt, 4 * static_cast<int>(c * stride + b));
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        if (c0 + j < a.nch) {
+          if (keep) pre_s[(c0 + j) * nbins + b] = static_cast<int32_t>(run);
+          run += v[j];
+        }
+      }
+    }
+    start[b] = run;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t cur = a.region[o];
@@ -294,29 +342,34 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_hist(BucketArgs a) {
     }
   }
   __syncthreads();
-  // each chunk's start in every bin: the bin's start + the sums of the chunks before it
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(coff, 0, 0x7fffffff,
-                                                                       0x00020000);
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
-    int64_t run = start[b];
-    for (int c0 = 0; c0 < nch; c0 += 8) {
-      int64_t v[8];
+  // pass 2: each chunk's start in every bin (plain stores: read by the next launch)
+  int64_t *coff = a.chunk_off + static_cast<int64_t>(o) * a.nch * stride;
+  if (keep) {
+    for (int t = threadIdx.x; t < a.nch * nbins; t += blockDim.x) {
+      const int c = t / nbins, b = t - c * nbins;
+      coff[c * stride + b] = start[b] + pre_s[t];
+    }
+  } else {
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+      int64_t run = start[b];
+      for (int c0 = 0; c0 < a.nch; c0 += kBatch) {
+        int32_t v[kBatch];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {  // 8-byte sc1 loads: L2-served (no stale L1 line)
-        const int c = c0 + j < nch ? c0 + j : nch - 1;
-        const int off = 8 * static_cast<int>(c * stride + b);
-        const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rc, off, 0, 16);
-        const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rc, off + 4, 0, 16);
-        v[j] = static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
-      }
+        for (int j = 0; j < kBatch; ++j) {
+          const int c = c0 + j < a.nch ? c0 + j : a.nch - 1;
+          v[j] = ld1_sc1(rt, 4 * static_cast<int>(c * stride + b));
+        }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (c0 + j < nch) coff[(c0 + j) * stride + b] = run;
-        run += c0 + j < nch ? v[j] : 0;
+        for (int j = 0; j < kBatch; ++j) {
+          if (c0 + j < a.nch) {
+            coff[(c0 + j) * stride + b] = run;
+            run += v[j];
+          }
+        }
       }
     }
   }
-  BKT_TS(1, 4);
+  BKT_TS(1, 6);
 }
 
 __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
@@ -333,8 +386,8 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
   const int64_t stride = static_cast<int64_t>(a.max_k) * (a.L + 1);
   // this block's start in every bin: its chunk's start (bucket_hist) + the histograms of the
   // blocks before it in the chunk
-  const int nch = (a.nb + kChunkRows - 1) / kChunkRows, ch = blk / kChunkRows;
-  const int64_t *coff = a.chunk_off + (static_cast<int64_t>(o) * nch + ch) * stride;
+  const int ch = blk / kChunkRows;
+  const int64_t *coff = a.chunk_off + (static_cast<int64_t>(o) * a.nch + ch) * stride;
   const int32_t *hist0 = a.hist + static_cast<int64_t>(o) * a.nb * stride;
   const int64_t i0 = static_cast<int64_t>(blk) * kSpan;
   // kPerThread == 1: this thread's particle, its key inputs and its 2T coordinates, every load
@@ -406,28 +459,34 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_scatter(BucketArgs a) {
 inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  size_t ctr, part, gpart, centre, hist, chunk_off, total;
-  int E1, G;
+  size_t ctr, bcnt, ccnt, gpart, csup, centre, hist, ctot, chunk_off, total;
+  int G, nch;
 };
 
 inline WsLayout bucket_ws(int64_t n_ov, int64_t N, int64_t L, int64_t max_k) {
-  const int64_t nb = (N + kSpan - 1) / kSpan;
+  const int64_t nb = (N + kSpan - 1) / kSpan, nch = (nb + kChunkRows - 1) / kChunkRows;
   WsLayout w;
-  w.E1 = static_cast<int>((L + 1) & ~int64_t(1));
   w.G = static_cast<int>((N + kCentreGroup - 1) / kCentreGroup);
+  w.nch = static_cast<int>(nch);
   size_t o = 0;
   w.ctr = o;  // arrival counters first: the zero-filled head of the workspace
-  o += align256(sizeof(int32_t) * 2 * n_ov);
-  w.part = o;
-  o += align256(sizeof(double) * n_ov * nb * w.E1);
+  o += align256(sizeof(int32_t) * 2 * n_ov * (1 + nch));
+  w.bcnt = o;
+  o += align256(sizeof(int32_t) * n_ov * nb * L);
+  w.ccnt = o;
+  o += align256(sizeof(int32_t) * n_ov * nch * L);
   w.gpart = o;
   o += align256(sizeof(double) * n_ov * w.G * max_k * 2);
+  w.csup = o;
+  o += align256(sizeof(double) * n_ov * nch * max_k * 2);
   w.centre = o;
   o += align256(sizeof(double) * n_ov * max_k * 2);
   w.hist = o;
   o += align256(sizeof(int32_t) * n_ov * nb * max_k * (L + 1));
+  w.ctot = o;
+  o += align256(sizeof(int32_t) * n_ov * nch * max_k * (L + 1));
   w.chunk_off = o;
-  o += align256(sizeof(int64_t) * n_ov * ((nb + kChunkRows - 1) / kChunkRows) * max_k * (L + 1));
+  o += align256(sizeof(int64_t) * n_ov * nch * max_k * (L + 1));
   w.total = o;
   return w;
 }
@@ -437,8 +496,9 @@ inline WsLayout bucket_ws(int64_t n_ov, int64_t N, int64_t L, int64_t max_k) {
 using namespace ccmpc;
 
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
-// which: 0 stats (slots 0 start, 1 loaded, 2 published, 3 last arriver, 4 done), 1 hist (same),
-// 2 scatter (0 start, 1 loaded, 2 done)  (tools/probe_step.py)
+// which: 0 stats (slots 0 start, 1 loaded, 2 published, 3 chunk's last arriver, 4 chunk
+// published, 5 OV's last arriver, 6 done), 1 hist (same), 2 scatter (0 start, 1 loaded, 2 done)
+// (tools/probe_step.py)
 extern "C" int ccmpc_probe_bucket_timestamps(void *host, int which, int reset) {
   if (which < 0 || which > 2) return -1;
   const size_t bytes = sizeof(g_bkt_ts[0]);
@@ -501,12 +561,15 @@ extern "C" int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in
   a.minpos = minpos;
   a.nb = static_cast<int>((N + kSpan - 1) / kSpan);
   a.ctr = reinterpret_cast<int32_t *>(ws + L.ctr);
-  a.part = reinterpret_cast<double *>(ws + L.part);
-  a.E1 = L.E1;
+  a.nch = L.nch;
+  a.bcnt = reinterpret_cast<int32_t *>(ws + L.bcnt);
+  a.ccnt = reinterpret_cast<int32_t *>(ws + L.ccnt);
   a.gpart = reinterpret_cast<double *>(ws + L.gpart);
   a.G = L.G;
+  a.csup = reinterpret_cast<double *>(ws + L.csup);
   a.centre = reinterpret_cast<double *>(ws + L.centre);
   a.hist = reinterpret_cast<int32_t *>(ws + L.hist);
+  a.ctot = reinterpret_cast<int32_t *>(ws + L.ctot);
   a.chunk_off = reinterpret_cast<int64_t *>(ws + L.chunk_off);
   a.out = pos_out;
   a.ld_out = ld_out;

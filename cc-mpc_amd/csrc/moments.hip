@@ -42,7 +42,7 @@ __device__ unsigned long long g_probe_ts[kProbeMaxWG * kProbeSlots];
   do {                                                                                         \
     if (threadIdx.x == 0 && blockIdx.x < kProbeMaxWG)                                          \
       g_probe_ts[blockIdx.x * kProbeSlots + (k)] = __builtin_amdgcn_s_memrealtime();           \
-    if ((k) == 0 && threadIdx.x == 0 && blockIdx.x < kProbeMaxWG)                              \
+    if ((k) == 0 && !(CCMPC_PROBE & 16) && threadIdx.x == 0 && blockIdx.x < kProbeMaxWG)       \
       g_probe_ts[blockIdx.x * kProbeSlots + 7] =                                               \
           (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg(0xF814)) << 32) |         \
           __builtin_amdgcn_s_getreg(0xF804); /* XCC_ID : HW_ID, slot 7 */                       \
@@ -50,6 +50,18 @@ __device__ unsigned long long g_probe_ts[kProbeMaxWG * kProbeSlots];
 #else
 #define PROBE_TS(k) \
   do {              \
+  } while (0)
+#endif
+// CCMPC_PROBE & 16 (with 4): slot 7 = the root gather's end instead of the hardware ids
+#if (CCMPC_PROBE & 4) && (CCMPC_PROBE & 16)
+#define PROBE_GATHERED()                                                                       \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kProbeMaxWG)                                          \
+      g_probe_ts[blockIdx.x * kProbeSlots + 7] = __builtin_amdgcn_s_memrealtime();             \
+  } while (0)
+#else
+#define PROBE_GATHERED() \
+  do {                   \
   } while (0)
 #endif
 
@@ -184,6 +196,7 @@ __device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &lo
     PROBE_TS(4);
     if (!last) return;
     gather_root<E>(root, root_n, L.slab);
+    PROBE_GATHERED();
   }
   finalize_cell<Sch>([&](int e) { return double2{L.slab[e], L.slab[e + 1]}; }, loc.cnt, T,
                      L.shift, L.S, o0, o1, mean, cov, L.mean, COV_IN_LDS ? L.cov : nullptr);

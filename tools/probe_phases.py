@@ -45,7 +45,7 @@ def one(name, what, dev, lib, back_to_back=1):
     ts = ts[live]
     t0 = ts[:, 0].min()
     rel = np.where(ts > 0, ts - t0, -1)
-    end = rel.max()
+    end = rel[:, :7].max()
     fin = rel[:, 5] >= 0
     print(f"== {name} {what} (last of {back_to_back} back-to-back): {live.sum()} WGs, "
           f"kernel span {end / 100:.2f} us")
@@ -56,6 +56,10 @@ def one(name, what, dev, lib, back_to_back=1):
     print("  combine    ", stats(rel[:, 3] - rel[:, 2]))
     print("  climb(non) ", stats((rel[:, 4] - rel[:, 3])[~fin]))
     print("  climb(last)", stats((rel[:, 4] - rel[:, 3])[fin]))
+    if os.environ.get("PROBE16"):  # PROBE=20 build: slot 7 = the root gather's end
+        g = fin & (rel[:, 7] >= 0)
+        print("  gather     ", stats((rel[:, 7] - rel[:, 4])[g]))
+        print("  finalize   ", stats((rel[:, 5] - rel[:, 7])[g]))
     print("  finalise   ", stats((rel[:, 5] - rel[:, 4])[fin]))
     print("  fin at     ", stats(rel[fin, 5]))
     if what == "cycle":

@@ -74,9 +74,9 @@ def main():
               ("rares", table(lib.ccmpc_probe_fused_timestamps, 2, 0),
                ["loaded", "centres", "keyed", "bins", "ranked", "copied"]),
               ("b.stats", table(lib.ccmpc_probe_bucket_timestamps, 0, 0),
-               ["loaded", "published", "last", "done"]),
+               ["loaded", "published", "chunk last", "chunk done", "last", "done"]),
               ("b.hist", table(lib.ccmpc_probe_bucket_timestamps, 1, 0),
-               ["loaded", "published", "last", "done"]),
+               ["loaded", "published", "chunk last", "chunk done", "last", "done"]),
               ("b.scatter", table(lib.ccmpc_probe_bucket_timestamps, 2, 0),
                ["loaded", "done"]),
               ("cycle", table(lib.ccmpc_probe_timestamps, 0, wg=8192), None)]
