@@ -29,9 +29,20 @@ __device__ unsigned long long g_l4_ts[kL4ProbeMaxWG * kL4ProbeSlots];
     if (threadIdx.x == 0 && blockIdx.x < kL4ProbeMaxWG)                                        \
       g_l4_ts[blockIdx.x * kL4ProbeSlots + (k)] = __builtin_amdgcn_s_memrealtime();            \
   } while (0)
+// the split kernels (pass = 0, 1): 0 start, 1 located, 2 particle loop done, 3 reduced and
+// published, 4 last arriver, 5 done (tools/probe_step.py)
+__device__ unsigned long long g_l4s_ts[2][kL4ProbeMaxWG * kL4ProbeSlots];
+#define L4S_TS(pass, k)                                                                        \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kL4ProbeMaxWG)                                        \
+      g_l4s_ts[pass][blockIdx.x * kL4ProbeSlots + (k)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
 #else
 #define L4_TS(k) \
   do {           \
+  } while (0)
+#define L4S_TS(pass, k) \
+  do {                  \
   } while (0)
 #endif
 
@@ -271,9 +282,20 @@ constexpr int64_t kL4Tail2Max = CCMPC_L4_TAIL2_MAX;
 
 constexpr int kL4MaxSplit = 64;  // workgroups per (cell, t): one wave holds their partials
 
+// Particles per workgroup on the average cell (build knob): 2048 halves the 784 workgroups of
+// a 100k cloud at 1024, whose dispatch alone spread over 7-12 us (profiles/r03/l4_split:
+// 100k drop-in graph 113 -> 104 us, C2 shape unchanged; 4096 costs the C2 shape 5 us).
+#ifndef CCMPC_L4_SPLIT_CHUNK
+#define CCMPC_L4_SPLIT_CHUNK 2048
+#endif
+#ifndef CCMPC_L4_SPLIT_THREADS  // threads per split workgroup (build knob)
+#define CCMPC_L4_SPLIT_THREADS kL4Threads
+#endif
+constexpr int kL4SplitThreads = CCMPC_L4_SPLIT_THREADS;
+
 inline int l4_split_factor(int64_t n_cells, int64_t n_bound) {
   const int64_t per = n_cells > 0 ? (n_bound + n_cells - 1) / n_cells : 0;
-  const int64_t S = (per + 1023) / 1024;  // ~1024 particles per workgroup on the average cell
+  const int64_t S = (per + CCMPC_L4_SPLIT_CHUNK - 1) / CCMPC_L4_SPLIT_CHUNK;
   return static_cast<int>(S < 1 ? 1 : (S > kL4MaxSplit ? kL4MaxSplit : S));
 }
 
@@ -327,7 +349,7 @@ __device__ __forceinline__ void support_rows(double theta, double (&A)[4][2]) {
 }
 
 template <typename P, bool TAIL2>
-__global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
+__global__ __launch_bounds__(kL4SplitThreads) void l4_pass1_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
     const double *__restrict__ past_last, const double *__restrict__ bbox, L4Split sp,
@@ -336,6 +358,7 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
   __shared__ double red[16];
   __shared__ double theta_s;
   __shared__ int flag;
+  L4S_TS(0, 0);
   const int ct = blockIdx.x / sp.S, part = blockIdx.x % sp.S;
   const int cell = ct / T, t = ct % T;
   const int64_t off = cell_off[cell], n = cell_cnt[cell];
@@ -345,6 +368,7 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
   const int64_t chunk = (n + sp.S - 1) / sp.S;
   const int64_t i0 = part * chunk, i1 = min(n, i0 + chunk);
   const double shift = (t == 0 && n > 0) ? heading(base, ld, 0, 0, o0, o1, px, py) : 0.0;
+  L4S_TS(0, 1);
   double s = 0.0, s1 = 0.0, s2 = 0.0;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const double y = heading(base, ld, t, i, o0, o1, px, py);
@@ -356,6 +380,7 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
     }
     if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + off + i] = y;
   }
+  L4S_TS(0, 2);
   s = block_sum(s, red);
   if (t == 0) {
     s1 = block_sum(s1, red);
@@ -367,7 +392,9 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
     st2_sc1(rm, 0, s, s1);
     st2_sc1(rm, 16, s2, 0.0);
   }
+  L4S_TS(0, 3);
   if (!arrive_last(sp.ctr + ct, sp.S, &flag)) return;
+  L4S_TS(0, 4);
   // every chunk's partials loaded at once (thread k: chunk k), then summed in chunk order by one
   // thread from LDS: deterministic, and one L2 round trip instead of S dependent ones
   const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part1 + static_cast<int64_t>(ct) * sp.S * 4);
@@ -391,6 +418,7 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
     out_yaw_mean[ct] = theta;
     if (t == 0) out_yaw0_var[cell] = (b2 - b1 * b1 / nn) / (nn - 1.0);
   }
+  L4S_TS(0, 5);
   if (!TAIL2) return;
   // small cells: the (cell, t)'s last arriver runs pass 2 over the whole cell itself (no second
   // launch, no second hand-off; the maxima are order-free, so b is the two-pass b bit for bit)
@@ -412,13 +440,14 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass1_kernel(
 }
 
 template <typename P>
-__global__ __launch_bounds__(kL4Threads) void l4_pass2_kernel(
+__global__ __launch_bounds__(kL4SplitThreads) void l4_pass2_kernel(
     const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
     const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
     const double *__restrict__ past_last, const double *__restrict__ bbox, L4Split sp,
     double *__restrict__ out_A, double *__restrict__ out_b, double *__restrict__ out_vertices) {
   __shared__ double red[16];
   __shared__ int flag;
+  L4S_TS(1, 0);
   const int ct = blockIdx.x / sp.S, part = blockIdx.x % sp.S;
   const int cell = ct / T, t = ct % T;
   const int64_t off = cell_off[cell], n = cell_cnt[cell];
@@ -431,8 +460,10 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass2_kernel(
   const double theta = sp.theta[ct];  // written by pass 1 (an earlier launch)
   double A[4][2];
   support_rows(theta, A);
+  L4S_TS(1, 1);
   double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   corner_maxima(base, ld, t, i0, i1, off, o0, o1, px, py, lon, lat, A, mx, out_vertices);
+  L4S_TS(1, 2);
   double bm[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) bm[q] = block_max(mx[q], red);
@@ -442,8 +473,10 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass2_kernel(
     st2_sc1(rm, 0, bm[0], bm[1]);
     st2_sc1(rm, 16, bm[2], bm[3]);
   }
+  L4S_TS(1, 3);
   const int nct = gridDim.x / sp.S;
   if (!arrive_last(sp.ctr + nct + ct, sp.S, &flag)) return;
+  L4S_TS(1, 4);
   // the maxima over chunks (order-free): the first wave loads them all at once and reduces
   if (threadIdx.x < 64) {
     const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part2 + static_cast<int64_t>(ct) * sp.S * 4);
@@ -466,6 +499,7 @@ __global__ __launch_bounds__(kL4Threads) void l4_pass2_kernel(
         out_b[static_cast<int64_t>(ct) * 4 + q] = b[q];
       }
   }
+  L4S_TS(1, 5);
 }
 
 }  // namespace ccmpc
@@ -480,6 +514,17 @@ extern "C" int ccmpc_probe_l4_timestamps(void *host, int reset) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_l4_ts), zeros, bytes) == hipSuccess ? 0 : -1;
   }
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_l4_ts), bytes) == hipSuccess ? 0 : -1;
+}
+extern "C" int ccmpc_probe_l4_split_timestamps(void *host, int which, int reset) {
+  if (which < 0 || which > 1) return -1;
+  const size_t bytes = sizeof(g_l4s_ts[0]);
+  if (reset) {
+    static unsigned long long zeros[kL4ProbeMaxWG * kL4ProbeSlots];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_l4s_ts), zeros, bytes, which * bytes) == hipSuccess
+               ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_l4s_ts), bytes, which * bytes) == hipSuccess
+             ? 0 : -1;
 }
 #endif
 
@@ -552,15 +597,15 @@ extern "C" int ccmpc_l4_split(const void *positions, int dtype, int64_t ld, int6
     using P = decltype(tag);
     const P *p = static_cast<const P *>(positions);
     if (tail2) {
-      hipLaunchKernelGGL((l4_pass1_kernel<P, true>), grid, dim3(kL4Threads), 0, s, p, ld, Ti,
+      hipLaunchKernelGGL((l4_pass1_kernel<P, true>), grid, dim3(kL4SplitThreads), 0, s, p, ld, Ti,
                          origin, cell_off, cell_cnt, past_last, bbox, sp, out_yaw_mean,
                          out_yaw0_var, out_yaw, out_A, out_b);
       return;
     }
-    hipLaunchKernelGGL((l4_pass1_kernel<P, false>), grid, dim3(kL4Threads), 0, s, p, ld, Ti,
+    hipLaunchKernelGGL((l4_pass1_kernel<P, false>), grid, dim3(kL4SplitThreads), 0, s, p, ld, Ti,
                        origin, cell_off, cell_cnt, past_last, bbox, sp, out_yaw_mean,
                        out_yaw0_var, out_yaw, out_A, out_b);
-    hipLaunchKernelGGL((l4_pass2_kernel<P>), grid, dim3(kL4Threads), 0, s, p, ld, Ti, origin,
+    hipLaunchKernelGGL((l4_pass2_kernel<P>), grid, dim3(kL4SplitThreads), 0, s, p, ld, Ti, origin,
                        cell_off, cell_cnt, past_last, bbox, sp, out_A, out_b, out_vertices);
   };
   if (dtype == CCMPC_F64)

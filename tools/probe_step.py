@@ -52,7 +52,8 @@ def main():
     g = next(iter(agent._graphs.values()))
     lib = engine._lib.load()
     for name, nargs in (("ccmpc_probe_sampler_timestamps", 2), ("ccmpc_probe_fused_timestamps", 3),
-                        ("ccmpc_probe_bucket_timestamps", 3), ("ccmpc_probe_timestamps", 2)):
+                        ("ccmpc_probe_bucket_timestamps", 3), ("ccmpc_probe_timestamps", 2),
+                        ("ccmpc_probe_l4_split_timestamps", 3)):
         f = getattr(lib, name)
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * (nargs - 1)
@@ -63,6 +64,8 @@ def main():
         for w in range(3):
             assert lib.ccmpc_probe_bucket_timestamps(None, w, 1) == 0
         assert lib.ccmpc_probe_timestamps(None, 1) == 0
+        for w in range(2):
+            assert lib.ccmpc_probe_l4_split_timestamps(None, w, 1) == 0
         torch.cuda.synchronize()
         g.launch(direct=a.direct)
         g.wait()
@@ -79,7 +82,11 @@ def main():
                ["loaded", "published", "chunk last", "chunk done", "last", "done"]),
               ("b.scatter", table(lib.ccmpc_probe_bucket_timestamps, 2, 0),
                ["loaded", "done"]),
-              ("cycle", table(lib.ccmpc_probe_timestamps, 0, wg=8192), None)]
+              ("cycle", table(lib.ccmpc_probe_timestamps, 0, wg=8192), None),
+              ("l4.pass1", table(lib.ccmpc_probe_l4_split_timestamps, 0, 0),
+               ["located", "loop", "published", "last", "done"]),
+              ("l4.pass2", table(lib.ccmpc_probe_l4_split_timestamps, 1, 0),
+               ["located", "loop", "published", "last", "done"])]
         ks = [k for k in ks if len(k[1])]
         t0 = ks[0][1][:, 0].min()
         print(f"--- replay {rep} ({'direct' if a.direct else 'graph'}), N={N}, times in us "
