@@ -42,6 +42,7 @@ def one(name, what, dev, lib, back_to_back=1):
     assert lib.ccmpc_probe_timestamps(buf.ctypes.data_as(ctypes.c_void_p), 0) == 0
     ts = buf.reshape(MAXWG, SLOTS).astype(np.int64)
     live = ts[:, 0] > 0
+    wg = np.flatnonzero(live)
     ts = ts[live]
     t0 = ts[:, 0].min()
     rel = np.where(ts > 0, ts - t0, -1)
@@ -67,6 +68,10 @@ def one(name, what, dev, lib, back_to_back=1):
         order = np.argsort(rel[:, 0])
         print("  slowest starters:", [int(b) for b in order[-10:]])
     print("  end at     ", stats(np.maximum(rel[:, 4], rel[:, 6])))
+    if os.environ.get("BY_XCD"):  # dispatch places workgroup i on XCD i % 8
+        for x in range(8):
+            m = (wg % 8) == x
+            print(f"  xcd {x}: start {stats(rel[m, 0])} | loop dur {stats((rel[:, 2] - rel[:, 1])[m])}")
 
 
 def main():
