@@ -87,6 +87,34 @@ constexpr int kDepth4 = CCMPC_DEPTH4;
 #endif
 constexpr int kDepth4Bal = CCMPC_DEPTH4_BAL;
 
+// Progress priority (balanced mode): issue is arbitrated by priority, then age
+// (MI355X_MICROARCH.md, two waves per SIMD), so of two co-resident workgroups the older one
+// streams ahead and finishes its item at ~14 us while its partner needs ~19 (C4/8, every CU,
+// profiles/r03/s29_c4_pairs.txt) and then cannot fill the CU alone.  With the priority
+// falling by one per quarter of the wave's groups done, whichever wave is behind outranks the
+// one ahead, so the two stay within a quarter of each other.  Arithmetic unchanged: the bits
+// are the same.
+#ifndef CCMPC_PROGRESS_PRIO
+#define CCMPC_PROGRESS_PRIO 0
+#endif
+__device__ __forceinline__ void progress_prio(int64_t done, int64_t total) {
+#if CCMPC_PROGRESS_PRIO
+  const int q = __builtin_amdgcn_readfirstlane(
+      static_cast<int>(total > 0 ? (4 * done) / total : 4));  // wave-uniform: a scalar branch
+  if (q <= 0)
+    __builtin_amdgcn_s_setprio(3);
+  else if (q == 1)
+    __builtin_amdgcn_s_setprio(2);
+  else if (q == 2)
+    __builtin_amdgcn_s_setprio(1);
+  else
+    __builtin_amdgcn_s_setprio(0);
+#else
+  (void)done;
+  (void)total;
+#endif
+}
+
 // Loads are pure loads, branch-free: every lane always issues its 16-byte loads, the address
 // clamped to the wave's last aligned quad (addressable because cell offsets and ld are
 // multiples of 4).  Masking (out-of-range particles, dead rows) happens in mfma_group, so a
@@ -322,6 +350,7 @@ void moments_kernel(
       for (int d = 0; d < DP - 1; ++d) load_group<P, RB, S>(buf[d], rowp, wr.p0 + d * st, p1, g);
       int64_t gi = 0;
       for (; gi + DP <= ngroups; gi += DP) {
+        if (BAL) progress_prio(gi, ngroups);
 #pragma unroll
         for (int d = 0; d < DP; ++d) {
           load_group<P, RB, S>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1,
@@ -337,7 +366,7 @@ void moments_kernel(
           mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
     }
     PROBE_TS(2);
-#if CCMPC_PRIO
+#if CCMPC_PRIO || CCMPC_PROGRESS_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
 
@@ -551,6 +580,7 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
       for (int d = 0; d < DP - 1; ++d) load_group4<P, NB>(buf[d], rowp, wr.p0 + d * st, p1, ml);
       int64_t gi = 0;
       for (; gi + DP <= ngroups; gi += DP) {
+        if (BAL) progress_prio(gi, ngroups);
 #pragma unroll
         for (int d = 0; d < DP; ++d) {
           load_group4<P, NB>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1, ml);
@@ -565,6 +595,9 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
           mfma_group4<P, NB>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, m, paddr, acc, s1);
     }
     PROBE_TS(2);
+#if CCMPC_PROGRESS_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
 
     if (MINK && threadIdx.x < rows + 3) ref_lds[threadIdx.x] = pre;  // read after barriers below
 #pragma unroll
