@@ -303,8 +303,9 @@ int ccmpc_sample_unicycle_ex(const double *init_state, const double *latent_cdf,
  *       cell_off/cell_cnt [n_cells], cell_pmf = N_k / N, init_center [n_cells][2] (world)
  * Rare particles go to the kept mode whose centre (mean final position) is nearest, first
  * index on ties (scipy.spatial.distance_matrix + np.argmin).  Deterministic.
- * Workspace: ccmpc_bucket_workspace_bytes; its head holds per-OV arrival counters, so
- * zero-fill it once (every call leaves them zero).  Three launches.
+ * Workspace: ccmpc_bucket_workspace_bytes; its head holds the per-OV and per-chunk (16 blocks
+ * of 256 particles) arrival counters, so zero-fill it once (every call leaves them zero).
+ * Three launches.
  * ------------------------------------------------------------------------------------- */
 size_t ccmpc_bucket_workspace_bytes(int64_t n_ov, int64_t N, int64_t n_latent, int64_t max_k);
 int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T, int64_t n_ov,
