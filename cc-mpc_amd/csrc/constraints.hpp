@@ -277,8 +277,9 @@ __device__ void minkowski_pair(const double *C, const double *mu, const double *
 // T(T-1)/2 doubles.  The record of a pair is a serial chain (two MVOE fixed points, then the
 // tangent) on one lane; its lower bound does not depend on that chain, so with >= 2 waves the
 // lower bounds run on the upper half of the group -- other waves, i.e. truly concurrently --
-// and write their record field themselves.  Includes the barrier needed before the per-t
-// minimum.
+// and write their record field themselves.  Up to 128 pairs that lower-bound wave also takes
+// the per-t minimum (no workgroup barrier: callers must not rely on one after this call); past
+// that, the barrier needed before the per-t minimum is included.
 __device__ void minkowski_cell(const double *C, const double *mu, int T, int cell,
                                const double *ref, double chi_r, double chi_p, double gamma,
                                const MinkParams &mp, double *lb_s, int tid, int nthreads) {
@@ -290,6 +291,36 @@ __device__ void minkowski_cell(const double *C, const double *mu, int T, int cel
   // (a record's chain is the tail's critical path, so fewer rounds of chains win: T = 40's 780
   // pairs on 512 threads take 2 rounds instead of 4)
   const int half = (nthreads >= 128 && P <= nthreads / 2) ? nthreads / 2 : 0;
+  if (half && P <= 2 * 64) {
+    // One lower-bound wave (threads [half, half + 64), up to two pairs per lane) also takes the
+    // per-t minimum from its own LDS writes, so nobody waits on a workgroup barrier: the record
+    // waves end with their chains (the barrier and the minimum after it used to follow the
+    // longest chain).  fmin ignores NaN as the reference's min(prob_lower, x) does, in any order.
+    if (tid < half) {
+      if (tid < P) {
+        int t, tau;
+        pair_of(tid, t, tau);
+        minkowski_pair(C, mu, ref, rows, t, tau, chi_r, chi_p, mp.R, mp.tol, mp.maxiter, rec + tid);
+      }
+      return;
+    }
+    const int lane = tid - half;
+    if (lane >= 64) return;
+    for (int p = lane; p < P; p += 64) {
+      int t, tau;
+      pair_of(p, t, tau);
+      const double lb = pair_lower_bound(pair_moments(C, rows, t, tau), gamma);
+      lb_s[p] = lb;
+      rec[p].lower_bound = lb;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes, in order
+    if (lane < T) {
+      double v = 1.0;
+      for (int tau = 0; tau < lane; ++tau) v = fmin(v, lb_s[lane * (lane - 1) / 2 + tau]);
+      mp.out_prob_lower[static_cast<int64_t>(cell) * T + lane] = v;
+    }
+    return;
+  }
   const bool lb_side = half && tid >= half;
   const int base = lb_side ? tid - half : tid, stride = half ? half : nthreads;
   for (int p = base; p < P; p += stride) {

@@ -202,6 +202,61 @@ __device__ __forceinline__ double wave_sum_dpp_f64(double v) {
   return (lane_val(15) + lane_val(31)) + (lane_val(47) + lane_val(63));
 }
 
+// ceil(n / c) for integer-valued 0 <= n < 2^53 and 0 < c, given rc ~ 1/c: one product, then
+// two exact corrections (k c and (k - 1) c are exact: both < 2^53).
+__device__ __forceinline__ double ceil_div_f64(double n, double c, double rc) {
+  double k = ceil(n * rc);
+  k = (k - 1.0) * c >= n ? k - 1.0 : k;
+  k = k * c < n ? k + 1.0 : k;
+  return k;
+}
+
+// The balanced chunk.  hi = (floor(total / ((G - n_cells) A)) + 1) A always fits (items =
+// sum_c max(1, ceil(n_c / hi)) <= G), but it pays the worst case of every cell's rounding: the
+// C4 per-GPU batch (67 cells, G = 512) got 1440-particle items where 1250 is the even share,
+// so the CUs holding two full items streamed 15% more than the average.  With the counts of
+// cells lane and 64 + lane in registers (n_cells <= 128), a bisection over multiples of A in
+// [total / G, hi] finds the SMALLEST fitting chunk: a few uniform steps of one product, two
+// corrections and a DPP wave sum each (CCMPC_BAL_SEARCH; the r02 search with a 64-bit
+// division per cell and step cost ~3 us).  Every caller with the same counts gets the same
+// chunk, so root_finalize_kernel re-derives the dealing exactly.  Measured
+// (profiles/r03/s41_bal_search_tail_ab.log, two alternating passes): the C4 per-GPU batch's
+// moments launch 27.7 / 27.8 us with the search against 27.7 / 27.9 without, C5 73.5 / 74.9
+// against 73.7 / 73.0 -- the shorter items buy nothing (the warm stream is bound by the chip's
+// rate from the Infinity Cache, not by the CUs holding two full items), so it stays off.
+#ifndef CCMPC_BAL_SEARCH
+#define CCMPC_BAL_SEARCH 0
+#endif
+__device__ __forceinline__ int64_t balanced_chunk(double td, int G, int n_cells, int64_t n0,
+                                                  int64_t n1) {
+  const int64_t A = kChunkAlign;
+  int64_t hi = static_cast<int64_t>(td / (static_cast<double>(G - n_cells) * A)) + 1;  // x A
+#if CCMPC_BAL_SEARCH
+  if (n_cells <= 128) {  // uniform
+    const int lane = threadIdx.x & 63;
+    const bool in0 = lane < n_cells, in1 = lane + 64 < n_cells;
+    const double d0 = static_cast<double>(n0), d1 = static_cast<double>(n1);
+    int64_t lo = static_cast<int64_t>(ceil(td / (static_cast<double>(G) * A)));
+    if (lo < 1) lo = 1;
+    while (lo < hi) {  // uniform: every quantity below the branch is wave-wide
+      const int64_t mid = (lo + hi) >> 1;
+      const double c = static_cast<double>(mid * A), rc = 1.0 / c;
+      double k = 0.0;
+      if (in0) k += n0 > 0 ? ceil_div_f64(d0, c, rc) : 1.0;
+      if (in1) k += n1 > 0 ? ceil_div_f64(d1, c, rc) : 1.0;
+      if (wave_sum_dpp_f64(k) <= static_cast<double>(G))
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
+  }
+#else
+  (void)n0;
+  (void)n1;
+#endif
+  return hi * A;
+}
+
 // Item id -> (cell, chunk index, ...) as locate_item, with the balanced chunk (returned in
 // *chunk_out).
 __device__ __forceinline__ bool locate_balanced(int32_t item, int G,
@@ -223,10 +278,8 @@ __device__ __forceinline__ bool locate_balanced(int32_t item, int G,
   double part = 0.0;  // exact: counts and their sum < 2^53
   for (int base = 0; base < n_cells; base += 64) part += static_cast<double>(count_at(base));
   const double td = wave_sum_dpp_f64(part);
-  const int64_t A = kChunkAlign;
-  // in units of A, +1 against the rounding of the division (the host keeps 2 n_cells <= G)
-  const int64_t chunk =
-      (static_cast<int64_t>(td / (static_cast<double>(G - n_cells) * A)) + 1) * A;
+  // the host keeps 2 n_cells <= G
+  const int64_t chunk = balanced_chunk(td, G, n_cells, n0, n1);
   *chunk_out = chunk;
   int32_t before = 0;
   for (int base = 0; base < n_cells; base += 64) {

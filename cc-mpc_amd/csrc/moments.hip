@@ -644,9 +644,8 @@ __device__ __forceinline__ void cell_items_balanced(int cell, int G, const int64
   for (int base = 0; base < n_cells; base += 64)
     part += base + lane < n_cells ? static_cast<double>(cnt[base + lane]) : 0.0;
   const double td = wave_sum_dpp_f64(part);
-  const int64_t A = kChunkAlign;
-  const int64_t chunk =
-      (static_cast<int64_t>(td / (static_cast<double>(G - n_cells) * A)) + 1) * A;
+  const int64_t n0 = lane < n_cells ? cnt[lane] : 0, n1 = lane + 64 < n_cells ? cnt[lane + 64] : 0;
+  const int64_t chunk = balanced_chunk(td, G, n_cells, n0, n1);
   int32_t before = 0;
   first = 0;
   nit = 0;
