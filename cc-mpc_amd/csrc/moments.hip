@@ -81,6 +81,15 @@ constexpr int kDepth = CCMPC_DEPTH;
 #ifndef CCMPC_PRIO
 #define CCMPC_PRIO 0
 #endif
+// Particles per lane per sub-step at RB >= 4 (T > 24): 4 or 2 (LaneVec).  W = 2 with a 4-deep
+// ring keeps 15 KB per wave in flight instead of 10 KB at the same 252 VGPRs: C5 moments 75.6 /
+// 77.1 us against 77.3 / 74.4 (a 3-deep ring 76.6 / 75.4; 5-deep spills, 91 us;
+// profiles/r03/s44_c5_pair_loads_depth_ab.log) -- bytes in flight do not bound C5's stream, so 4.
+#ifndef CCMPC_W_BIG
+#define CCMPC_W_BIG 4
+#endif
+constexpr int kWBig = CCMPC_W_BIG;
+static_assert(kWBig == 2 || kWBig == 4, "CCMPC_W_BIG must be 2 or 4");
 constexpr int kDepth4 = CCMPC_DEPTH4;
 #ifndef CCMPC_DEPTH4_BAL  // the Scheme4 ring in balanced mode (one item per resident workgroup):
 #define CCMPC_DEPTH4_BAL 3  // C4 per-GPU batch 33.9 -> 32.5 us warm, 38.7 -> 37.0 cold (ab14)
@@ -116,46 +125,86 @@ __device__ __forceinline__ void progress_prio(int64_t done, int64_t total) {
 }
 
 // Loads are pure loads, branch-free: every lane always issues its 16-byte loads, the address
-// clamped to the wave's last aligned quad (addressable because cell offsets and ld are
+// clamped to the wave's last aligned W-particle run (addressable because cell offsets and ld are
 // multiples of 4).  Masking (out-of-range particles, dead rows) happens in mfma_group, so a
 // group's loads have no consumer until its MFMAs run.  A guarded scalar fallback here turned
 // the loop into branches, and the waitcnt pass then drained vmcnt(0) before every MFMA group --
 // waiting on the NEXT group's loads too, which serialised the double buffer.
-template <typename P, int RB, int S>
-__device__ __forceinline__ void load_group(Quad<P> (&v)[S][RB], const P *const (&rowp)[RB],
-                                           int64_t gbase, int64_t p1, int g) {
-  const int64_t qlast = (p1 - 1) & ~int64_t(3);
+//
+// W = particles per lane per sub-step: 4 (Quad: two 16-byte f64 loads, a row's 16 particles of
+// a sub-step = one 128-byte line) or 2 (Pair: one 16-byte f64 load, 8 particles per sub-step);
+// the narrower form halves the registers of a load group, so the same budget keeps twice the
+// groups in flight (CCMPC_W_BIG, long horizons).
+template <typename P>
+struct Pair;
+template <>
+struct Pair<double> {
+  double2 v;
+  __device__ __forceinline__ double operator[](int j) const { return j ? v.y : v.x; }
+};
+template <>
+struct Pair<float> {
+  float2 v;
+  __device__ __forceinline__ double operator[](int j) const {
+    return static_cast<double>(j ? v.y : v.x);
+  }
+};
+__device__ __forceinline__ void load_pair(const double *__restrict__ p, Pair<double> &q) {
+  q.v = *reinterpret_cast<const double2 *>(p);
+}
+__device__ __forceinline__ void load_pair(const float *__restrict__ p, Pair<float> &q) {
+  q.v = *reinterpret_cast<const float2 *>(p);
+}
+
+template <typename P, int W>
+struct LaneVec;
+template <typename P>
+struct LaneVec<P, 4> {
+  using type = Quad<P>;
+  __device__ static void load(const P *p, type &q) { load_quad(p, q); }
+};
+template <typename P>
+struct LaneVec<P, 2> {
+  using type = Pair<P>;
+  __device__ static void load(const P *p, type &q) { load_pair(p, q); }
+};
+
+template <typename P, int RB, int S, int W>
+__device__ __forceinline__ void load_group(typename LaneVec<P, W>::type (&v)[S][RB],
+                                           const P *const (&rowp)[RB], int64_t gbase, int64_t p1,
+                                           int g) {
+  const int64_t qlast = (p1 - 1) & ~int64_t(W - 1);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    const int64_t q = gbase + 16 * s + 4 * g;
+    const int64_t q = gbase + 4 * W * s + W * g;
     const int64_t qc = q < qlast ? q : qlast;
 #pragma unroll
     for (int b = 0; b < RB; ++b) {
-#if CCMPC_PROBE & 2  // diagnostic build only: every lane re-reads one cached quad
-      load_quad(rowp[b] + (qc & 3), v[s][b]);
+#if CCMPC_PROBE & 2  // diagnostic build only: every lane re-reads one cached run
+      LaneVec<P, W>::load(rowp[b] + (qc & (W - 1)), v[s][b]);
 #else
-      load_quad(rowp[b] + qc, v[s][b]);
+      LaneVec<P, W>::load(rowp[b] + qc, v[s][b]);
 #endif
     }
   }
 }
 
-template <typename P, int RB, int S, int NACC>
-__device__ __forceinline__ void mfma_group(const Quad<P> (&raw)[S][RB], const double (&sh)[RB],
-                                           const bool (&live)[RB], int64_t gbase, int64_t p1,
-                                           int g, d4 (&acc)[NACC][n_tiles(RB)],
-                                           double (&s1)[RB]) {
+template <typename P, int RB, int S, int NACC, int W>
+__device__ __forceinline__ void mfma_group(const typename LaneVec<P, W>::type (&raw)[S][RB],
+                                           const double (&sh)[RB], const bool (&live)[RB],
+                                           int64_t gbase, int64_t p1, int g,
+                                           d4 (&acc)[NACC][n_tiles(RB)], double (&s1)[RB]) {
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    const int64_t q = gbase + 16 * s + 4 * g;
-    double v[RB][4];
+    const int64_t q = gbase + 4 * W * s + W * g;
+    double v[RB][W];
 #pragma unroll
     for (int b = 0; b < RB; ++b)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)  // shifted; out-of-range slots and dead rows become 0
+      for (int j = 0; j < W; ++j)  // shifted; out-of-range slots and dead rows become 0
         v[b][j] = (live[b] && q + j < p1) ? raw[s][b][j] - sh[b] : 0.0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < W; ++j) {
       const int a = (NACC == 2) ? (j & 1) : 0;
       int t = 0;
 #pragma unroll
@@ -171,7 +220,8 @@ __device__ __forceinline__ void mfma_group(const Quad<P> (&raw)[S][RB], const do
         }
     }
 #pragma unroll
-    for (int b = 0; b < RB; ++b) s1[b] += (v[b][0] + v[b][1]) + (v[b][2] + v[b][3]);
+    for (int b = 0; b < RB; ++b)
+      s1[b] += W == 4 ? (v[b][0] + v[b][1]) + (v[b][2 % W] + v[b][3 % W]) : v[b][0] + v[b][1];
   }
 }
 
@@ -282,6 +332,7 @@ void moments_kernel(
   constexpr int NACC = G::NACC;
   constexpr int D = 16 * RB;
   constexpr int S = G::S;
+  constexpr int W = RB >= 4 ? kWBig : 4;  // particles per lane per sub-step (LaneVec)
   constexpr int E = slab_doubles(RB);
   // the fused tail reads the covariance from LDS; it lives in the cross-wave exchange buffer,
   // which is free once the item is combined (so T = 40 keeps its 80 x 80 covariance on chip too)
@@ -309,7 +360,7 @@ void moments_kernel(
     const int g = lane >> 4;
     const int64_t cnt = loc.cnt;
     const double pre = MINK ? prefetch_tail(mp, loc, rows) : 0.0;
-    const WaveRange wr = wave_range<BAL>(a, b, w, G::NW, int64_t(1) << lg_wq, 16 * S);
+    const WaveRange wr = wave_range<BAL>(a, b, w, G::NW, int64_t(1) << lg_wq, 4 * W * S);
     const int64_t p1 = wr.p1;
 
     double sh[RB];
@@ -342,28 +393,28 @@ void moments_kernel(
     if (G::NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(CCMPC_PRIO);
 #endif
     constexpr int DP = RB >= 3 ? CCMPC_DEPTH_BIG : kDepth;
-    Quad<P> buf[DP][S][RB];
+    typename LaneVec<P, W>::type buf[DP][S][RB];
     if (ngroups > 0) {
       // ring of DP load groups: group g lives in buf[g % DP]; DP - 1 groups are in flight
       // while one is multiplied
 #pragma unroll
-      for (int d = 0; d < DP - 1; ++d) load_group<P, RB, S>(buf[d], rowp, wr.p0 + d * st, p1, g);
+      for (int d = 0; d < DP - 1; ++d) load_group<P, RB, S, W>(buf[d], rowp, wr.p0 + d * st, p1, g);
       int64_t gi = 0;
       for (; gi + DP <= ngroups; gi += DP) {
         if (BAL) progress_prio(gi, ngroups);
 #pragma unroll
         for (int d = 0; d < DP; ++d) {
-          load_group<P, RB, S>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1,
+          load_group<P, RB, S, W>(buf[(d + DP - 1) % DP], rowp, wr.p0 + (gi + d + DP - 1) * st, p1,
                                g);
           __builtin_amdgcn_sched_barrier(0);
-          mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
+          mfma_group<P, RB, S, NACC, W>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
 #pragma unroll
       for (int d = 0; d < DP - 1; ++d)  // the < DP groups left were loaded ahead
         if (gi + d < ngroups)
-          mfma_group<P, RB, S, NACC>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
+          mfma_group<P, RB, S, NACC, W>(buf[d], sh, live, wr.p0 + (gi + d) * st, p1, g, acc, s1);
     }
     PROBE_TS(2);
 #if CCMPC_PRIO || CCMPC_PROGRESS_PRIO
@@ -413,27 +464,6 @@ void moments_kernel(
 // the instruction's A[b][i][k] lane i + 4b + 16k, so ONE register per block is both the A
 // and the B operand of every block pair (I, J), as for the 16x16 tiles.  A group is 32
 // particles per wave.
-template <typename P>
-struct Pair;
-template <>
-struct Pair<double> {
-  double2 v;
-  __device__ __forceinline__ double operator[](int j) const { return j ? v.y : v.x; }
-};
-template <>
-struct Pair<float> {
-  float2 v;
-  __device__ __forceinline__ double operator[](int j) const {
-    return static_cast<double>(j ? v.y : v.x);
-  }
-};
-__device__ __forceinline__ void load_pair(const double *__restrict__ p, Pair<double> &q) {
-  q.v = *reinterpret_cast<const double2 *>(p);
-}
-__device__ __forceinline__ void load_pair(const float *__restrict__ p, Pair<float> &q) {
-  q.v = *reinterpret_cast<const float2 *>(p);
-}
-
 template <typename P, int NB>
 __device__ __forceinline__ void load_group4(Pair<P> (&v)[NB], const P *const (&rowp)[NB],
                                             int64_t gbase, int64_t p1, int m) {
