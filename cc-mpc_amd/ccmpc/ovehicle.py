@@ -154,7 +154,11 @@ def check_kept_modes_drawn(centre, K):
     bucketing gives that mode the centre 0 / 0 = NaN (the mean of its own particles, :80), so
     no rare particle is ever assigned to it; the drop-in raises the reference's error instead of
     returning that cell.  centre: per-cell init_center (host, (C, 2)), cells in (ov, k) order."""
-    bad = np.flatnonzero(np.isnan(np.asarray(centre, np.float64).reshape(-1, 2)).any(1))
+    centre = np.asarray(centre, np.float64)
+    s = float(centre.sum())       # finite centres sum to a finite value; one NaN makes it NaN
+    if s == s:
+        return
+    bad = np.flatnonzero(np.isnan(centre.reshape(-1, 2)).any(1))
     if bad.size:
         c = int(bad[0])
         first = np.concatenate([[0], np.cumsum(K)])

@@ -127,8 +127,8 @@ class HalfSpaceList:
         self._cell_of = cell_of
         self._P = self._h.shape[1]
         st = self._h["status"].reshape(-1)
-        bad = np.flatnonzero(st != 0)
-        if bad.size:
+        bad = np.flatnonzero(st) if st.any() else ()
+        if len(bad):
             c, p = divmod(int(bad[0]), self._P)
             r = self._h[c, p]
             o, k = cell_of[c]
@@ -443,8 +443,8 @@ class MidlevelAgent:
 
     def _ov_in_junction(self, scene, mean0):
         """OVconstraint (:831-851): the Town03 scene-4 T-intersection test, last mode wins."""
-        m = mean0[_last_cells(tuple(scene.K))]                      # each OV's last mode
-        return bool(np.any(~((m[:, 0] >= 190) | (m[:, 1] <= -80))))
+        m = mean0[_last_cells(tuple(scene.K))].tolist()             # each OV's last mode
+        return any(not (x >= 190 or y <= -80) for x, y in m)
 
     def _src_cells(self, prev_K, K):
         """data_idx fallback (:2648-2656): mode k reads saved mode k, or the last saved slot."""

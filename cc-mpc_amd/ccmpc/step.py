@@ -273,7 +273,7 @@ class MinkowskiStepGraph:
         pmf = np.asarray(latent_pmf, np.float64).reshape(O, L)
         kept = pmf > filter_pmf
         kc = np.cumsum(kept, axis=1)
-        if not np.array_equal(kc[:, -1], self._K_arr):
+        if not (kc[:, -1] == self._K_arr).all():
             raise ValueError(f"kept modes per OV {kc[:, -1].tolist()}; this graph was built "
                              f"for {self.K}")
         np.subtract(kc, 1, out=i.h("keep"), casting="unsafe")
