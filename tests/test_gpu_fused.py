@@ -34,6 +34,28 @@ def test_fused_cycle_bitwise_equals_two_calls(gpu, golden, name):
     assert len(h) == T * (T - 1) // 2 * store.n_cells
 
 
+@pytest.mark.parametrize("T", [16, 20])
+def test_fused_tail_both_lower_bound_paths(gpu, T):
+    """The fused tail's two lower-bound layouts against the unfused rows launch, bit for bit:
+    T = 16 (120 pairs on a 256-thread workgroup: one lower-bound wave, two pairs on most lanes,
+    the per-t minimum from that wave's own LDS writes, no workgroup barrier) and T = 20 (190
+    pairs on 512 threads: every thread takes whole pairs, then the barrier and the minimum)."""
+    from ccmpc import cycle, synthetic
+    ovs, ref, _ = synthetic.scene(5, O=3, N=4000, T=T)
+    store = eng().ParticleStore.from_cells([c for o in ovs for c in o], device=gpu)
+    cyc = cycle.MinkowskiCycle(store, [len(o) for o in ovs], ref)
+    cyc.run_unfused()
+    a = (cyc.mean.clone(), cyc.cov.clone(), cyc.rec.clone(), cyc.prob_lower.clone())
+    cyc.rec.zero_()
+    cyc.prob_lower.zero_()
+    cyc.run()
+    assert torch.equal(a[0], cyc.mean) and torch.equal(a[1], cyc.cov)
+    assert torch.equal(a[2], cyc.rec) and torch.equal(a[3], cyc.prob_lower)
+    assert np.all(cyc.records()["status"] == 0)
+    pl = cyc.prob_lower.cpu().numpy()
+    assert np.all(pl[:, 0] == 1.0) and np.all((pl >= 0.0) & (pl <= 1.0))
+
+
 def test_graph_replay_is_stable(gpu):
     from ccmpc import cycle, synthetic
     ovs, ref, _ = synthetic.scene(3, O=4, N=5000, T=8)
