@@ -425,8 +425,8 @@ __host__ __device__ constexpr int combine_tiles_per_round(int rb) {
   return n_tiles(rb) < 5 ? n_tiles(rb) : 5;
 }
 __host__ __device__ constexpr int combine_xch_doubles(int rb, int nw) {
-  return nw * combine_tiles_per_round(rb) * 256 > 16 * nw ? nw * combine_tiles_per_round(rb) * 256
-                                                          : 16 * nw;
+  // the tile rounds' park area, then the row sums' (parked with the first round)
+  return nw * combine_tiles_per_round(rb) * 256 + 16 * rb * nw;
 }
 
 // Combine the NW waves' accumulators in a fixed order (wave 0 + 1 + ... + NW-1) and write the
@@ -434,7 +434,8 @@ __host__ __device__ constexpr int combine_xch_doubles(int rb, int nw) {
 // (to_lds = true).  Rounds of up to combine_tiles_per_round tiles: every wave parks its tiles
 // in `xch` (combine_xch_doubles(RB, NW) doubles), then EVERY thread sums entry pairs over the
 // waves and stores them -- the sum and the stores are spread over the whole workgroup (with
-// wave 0 alone doing them tile by tile, T = 40's 15 tiles took 28 us).  Every thread of the
+// wave 0 alone doing them tile by tile, T = 40's 15 tiles took 28 us); the row sums are parked
+// and summed with the first round (two barriers instead of two more per row block).  Every thread of the
 // workgroup must call it.
 template <int RB, int NACC, int NW>
 __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)],
@@ -442,8 +443,18 @@ __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)]
                                               bool to_lds) {
   constexpr int NT = n_tiles(RB);
   constexpr int TB = combine_tiles_per_round(RB);
+  constexpr int XR = NW * TB * 256;  // the row sums' park area: [w][RB * 16]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(dst);
+  // the row sums ride the first round: their lane reduction, park and (fixed-order) wave sum
+  // share its two barriers instead of two more per row block
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    double x = s1[b];
+    x += __shfl_xor(x, 16, 64);
+    x += __shfl_xor(x, 32, 64);
+    if (lane < 16) xch[XR + (w * RB + b) * 16 + lane] = x;
+  }
 #pragma unroll
   for (int t0 = 0; t0 < NT; t0 += TB) {
     // park: xch[((w TB + tb) 4 + k) 64 + lane] = this wave's register k of tile t0 + tb
@@ -476,28 +487,25 @@ __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)]
         st2_sc1(rs, 8 * ge, a, b);
       }
     }
-    __syncthreads();
-  }
+    if (t0 == 0) {
+      // row-sum pair (2 i, 2 i + 1) of row block b: wave 0's value, then + waves 1, 2, ...
+      const int i = static_cast<int>(blockDim.x) - 1 - static_cast<int>(threadIdx.x);
+      if (i < 8 * RB) {
+        const int b = i >> 3, r = 2 * (i & 7);
+        const double *x = xch + XR + b * 16 + r;
+        double v0 = x[0], v1 = x[1];
 #pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    double x = s1[b];
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
-    if (lane < 16) xch[w * 16 + lane] = x;
-    __syncthreads();
-    if (w == 0 && lane < 8) {
-      double v0 = xch[2 * lane], v1 = xch[2 * lane + 1];
-#pragma unroll
-      for (int o = 1; o < NW; ++o) {
-        v0 += xch[o * 16 + 2 * lane];
-        v1 += xch[o * 16 + 2 * lane + 1];
-      }
-      const int e = NT * 256 + b * 16 + 2 * lane;
-      if (to_lds) {
-        dst[e] = v0;
-        dst[e + 1] = v1;
-      } else {
-        st2_sc1(rs, 8 * e, v0, v1);
+        for (int o = 1; o < NW; ++o) {
+          v0 += x[o * RB * 16];
+          v1 += x[o * RB * 16 + 1];
+        }
+        const int e = NT * 256 + b * 16 + r;
+        if (to_lds) {
+          dst[e] = v0;
+          dst[e + 1] = v1;
+        } else {
+          st2_sc1(rs, 8 * e, v0, v1);
+        }
       }
     }
     __syncthreads();
