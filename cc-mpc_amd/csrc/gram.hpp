@@ -811,21 +811,27 @@ __device__ __forceinline__ void gather_root(const double *__restrict__ root, int
 template <typename Sch, typename Reader>
 __device__ void finalize_cell(Reader rd, int64_t cnt, int T, const double *shift_lds,
                               double *S_lds, double o0, double o1, double *__restrict__ mean,
-                              double *__restrict__ cov, double *mean_lds, double *cov_lds) {
+                              double *__restrict__ cov, double *mean_lds, double *cov_lds,
+                              const double *S_in = nullptr) {
   constexpr int GRAM = Sch::GRAM;
   constexpr int D = Sch::D;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int rows = 2 * T;
   const double n = static_cast<double>(cnt);
-  // rd(e) returns the summed entry pair (e, e+1), e even
-  for (int r = 2 * tid; r < D; r += 2 * nth) {
-    const double2 s = r < rows ? rd(GRAM + r) : double2{0.0, 0.0};
-    S_lds[r] = s.x;
-    S_lds[r + 1] = s.y;
+  // rd(e) returns the summed entry pair (e, e+1), e even.  S_in: the summed row sums already in
+  // LDS (a slab there, entries GRAM.. after the caller's barrier) -- no copy, no barrier
+  const double *S = S_in;
+  if (!S) {
+    for (int r = 2 * tid; r < D; r += 2 * nth) {
+      const double2 s = r < rows ? rd(GRAM + r) : double2{0.0, 0.0};
+      S_lds[r] = s.x;
+      S_lds[r + 1] = s.y;
+    }
+    __syncthreads();
+    S = S_lds;
   }
-  __syncthreads();
   for (int r = tid; r < rows; r += nth) {
-    const double m = (shift_lds[r] + S_lds[r] / n) + ((r & 1) ? o1 : o0);
+    const double m = (shift_lds[r] + S[r] / n) + ((r & 1) ? o1 : o0);
     mean[r] = m;
     if (mean_lds) mean_lds[r] = m;
   }
@@ -841,7 +847,7 @@ __device__ void finalize_cell(Reader rd, int64_t cnt, int T, const double *shift
     for (int h = 0; h < 2; ++h) {
       if (!(h ? use1 : use0)) continue;
       const int i = h ? i1 : i0, j = h ? j1 : j0;
-      const double c = ((h ? g.y : g.x) - S_lds[i] * S_lds[j] / n) / (n - 1.0);
+      const double c = ((h ? g.y : g.x) - S[i] * S[j] / n) / (n - 1.0);
       cov[i * rows + j] = c;
       cov[j * rows + i] = c;
       if (cov_lds) {

@@ -277,7 +277,8 @@ __device__ __forceinline__ void cell_epilogue(Publish publish, const ItemLoc &lo
     PROBE_GATHERED();
   }
   finalize_cell<Sch>([&](int e) { return double2{L.slab[e], L.slab[e + 1]}; }, loc.cnt, T,
-                     L.shift, L.S, o0, o1, mean, cov, L.mean, COV_IN_LDS ? L.cov : nullptr);
+                     L.shift, L.S, o0, o1, mean, cov, L.mean, COV_IN_LDS ? L.cov : nullptr,
+                     L.slab + Sch::GRAM);
   PROBE_TS(5);
   if (MINK)
     minkowski_cell(COV_IN_LDS ? L.cov : cov, L.mean, T, cell, L.ref, L.ref[rows],
