@@ -112,6 +112,29 @@ struct ItemLoc {
   int64_t cnt, off;
 };
 
+// Wave-wide inclusive prefix sum of an int32 by DPP row shifts (rows of 16 lanes) and three
+// readlanes of the row totals: register moves instead of __shfl_up's six dependent
+// ds_bpermute round trips (~0.35 us of every launch's locate).  All 64 lanes must be active.
+__device__ __forceinline__ int32_t wave_incl_scan_i32(int32_t x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  const int32_t r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31),
+                r2 = __builtin_amdgcn_readlane(x, 47);
+  const int row = (threadIdx.x & 63) >> 4;
+  return x + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+}
+// Lane l's value (l wave-uniform): a scalar readlane instead of a ds_bpermute round trip.
+__device__ __forceinline__ int32_t lane_i32(int32_t v, int l) {
+  return __builtin_amdgcn_readlane(v, l);
+}
+__device__ __forceinline__ int64_t lane_i64(int64_t v, int l) {
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(v), l));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(v >> 32), l));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
 // Item id -> (cell, chunk index, the cell's first item, count, offset, reference selector):
 // one wave-parallel prefix scan of the cells' item counts in 32-bit arithmetic (items < 2^31:
 // the grid is sized by them), so everything an item needs arrives with one memory round trip.
@@ -129,22 +152,17 @@ __device__ __forceinline__ bool locate_item(int32_t item, const int64_t *__restr
     const int64_t o = (c < n_cells) ? off[c] : 0;
     const int32_t rs = (cell_ref && c < n_cells) ? cell_ref[c] : 0;  // same round trip
     const int32_t mine = (c < n_cells) ? items_of(n, lg_chunk) : 0;
-    int32_t incl = mine;
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-      const int32_t y = __shfl_up(incl, s, 64);
-      if (lane >= s) incl += y;
-    }
-    const int32_t total = __shfl(incl, 63, 64);
+    const int32_t incl = wave_incl_scan_i32(mine);
+    const int32_t total = lane_i32(incl, 63);
     if (item < before + total) {
       const unsigned long long m = __ballot(before + incl > item);
       const int l = __ffsll(static_cast<long long>(m)) - 1;
       loc.cell = base + l;
-      loc.first = before + __shfl(incl - mine, l, 64);
+      loc.first = before + lane_i32(incl - mine, l);
       loc.chunk_idx = item - loc.first;
-      loc.cnt = __shfl(n, l, 64);
-      loc.off = __shfl(o, l, 64);
-      loc.ref_sel = __shfl(rs, l, 64);
+      loc.cnt = lane_i64(n, l);
+      loc.off = lane_i64(o, l);
+      loc.ref_sel = lane_i32(rs, l);
       return true;
     }
     before += total;
@@ -289,6 +307,9 @@ __device__ __forceinline__ bool locate_balanced(int32_t item, int G,
     const int64_t o = base == 0 ? o0 : base == 64 ? o1 : (in ? off[c] : 0);
     const int32_t rs = base == 0 ? rs0 : base == 64 ? rs1 : ((cell_ref && in) ? cell_ref[c] : 0);
     const int32_t mine = in ? static_cast<int32_t>(n > 0 ? ceil_div_fast(n, chunk) : 1) : 0;
+    // __shfl_up / __shfl here, not wave_incl_scan_i32 / lane_*: the DPP form frees ~8 VGPRs,
+    // which lets a third T = 12 balanced Scheme4 workgroup onto each CU, and that layout was
+    // measured slower (C4 per-GPU batch 32.1 -> 34.7 us, profiles/r03/s52_dpp_locate_ab.log)
     int32_t incl = mine;
 #pragma unroll
     for (int s = 1; s < 64; s <<= 1) {
@@ -425,8 +446,8 @@ __host__ __device__ constexpr int combine_tiles_per_round(int rb) {
   return n_tiles(rb) < 5 ? n_tiles(rb) : 5;
 }
 __host__ __device__ constexpr int combine_xch_doubles(int rb, int nw) {
-  // the tile rounds' park area, then the row sums' (parked with the first round)
-  return nw * combine_tiles_per_round(rb) * 256 + 16 * rb * nw;
+  // the tile rounds' park area, then the row sums' (every lane's, parked with the first round)
+  return nw * combine_tiles_per_round(rb) * 256 + 64 * rb * nw;
 }
 
 // Combine the NW waves' accumulators in a fixed order (wave 0 + 1 + ... + NW-1) and write the
@@ -446,15 +467,12 @@ __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)]
   constexpr int XR = NW * TB * 256;  // the row sums' park area: [w][RB * 16]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const __amdgpu_buffer_rsrc_t rs = slab_rsrc(dst);
-  // the row sums ride the first round: their lane reduction, park and (fixed-order) wave sum
-  // share its two barriers instead of two more per row block
+  // the row sums ride the first round: every lane parks its partial (lane r + 16 g: row r of
+  // particle group g) and the summing thread adds the four groups as the xor-16 / xor-32 lane
+  // butterfly did, ((g0 + g1) + (g2 + g3)), then the waves in order -- the same bits without
+  // two dependent cross-lane round trips per row block before the barrier
 #pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    double x = s1[b];
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
-    if (lane < 16) xch[XR + (w * RB + b) * 16 + lane] = x;
-  }
+  for (int b = 0; b < RB; ++b) xch[XR + (w * RB + b) * 64 + lane] = s1[b];
 #pragma unroll
   for (int t0 = 0; t0 < NT; t0 += TB) {
     // park: xch[((w TB + tb) 4 + k) 64 + lane] = this wave's register k of tile t0 + tb
@@ -492,12 +510,15 @@ __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)]
       const int i = static_cast<int>(blockDim.x) - 1 - static_cast<int>(threadIdx.x);
       if (i < 8 * RB) {
         const int b = i >> 3, r = 2 * (i & 7);
-        const double *x = xch + XR + b * 16 + r;
-        double v0 = x[0], v1 = x[1];
+        auto rowsum = [&](int o, int rr) {  // wave o's row rr: ((g0 + g1) + (g2 + g3))
+          const double *x = xch + XR + (o * RB + b) * 64 + rr;
+          return (x[0] + x[16]) + (x[32] + x[48]);
+        };
+        double v0 = rowsum(0, r), v1 = rowsum(0, r + 1);
 #pragma unroll
         for (int o = 1; o < NW; ++o) {
-          v0 += x[o * RB * 16];
-          v1 += x[o * RB * 16 + 1];
+          v0 += rowsum(o, r);
+          v1 += rowsum(o, r + 1);
         }
         const int e = NT * 256 + b * 16 + r;
         if (to_lds) {

@@ -686,20 +686,15 @@ __device__ __forceinline__ void cell_items_balanced(int cell, int G, const int64
     const int64_t nn = c < n_cells ? cnt[c] : 0;
     const int32_t mine =
         c < n_cells ? static_cast<int32_t>(nn > 0 ? ceil_div_fast(nn, chunk) : 1) : 0;
-    int32_t incl = mine;
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-      const int32_t y = __shfl_up(incl, s, 64);
-      if (lane >= s) incl += y;
-    }
+    const int32_t incl = wave_incl_scan_i32(mine);
     if (cell < base + 64) {
       const int l = cell - base;
-      first = before + __shfl(incl - mine, l, 64);
-      nit = __shfl(mine, l, 64);
-      n = __shfl(nn, l, 64);
+      first = before + lane_i32(incl - mine, l);
+      nit = lane_i32(mine, l);
+      n = lane_i64(nn, l);
       return;
     }
-    before += __shfl(incl, 63, 64);
+    before += lane_i32(incl, 63);
   }
 }
 
