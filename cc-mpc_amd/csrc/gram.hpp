@@ -130,9 +130,10 @@ __device__ __forceinline__ int32_t lane_i32(int32_t v, int l) {
   return __builtin_amdgcn_readlane(v, l);
 }
 __device__ __forceinline__ int64_t lane_i64(int64_t v, int l) {
-  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(v), l));
-  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(v >> 32), l));
-  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  const int32_t lo = __builtin_amdgcn_readlane(static_cast<int32_t>(v), l);
+  const int32_t hi = __builtin_amdgcn_readlane(static_cast<int32_t>(v >> 32), l);
+  return static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) |
+                              static_cast<uint32_t>(lo));
 }
 
 // Item id -> (cell, chunk index, the cell's first item, count, offset, reference selector):
@@ -456,8 +457,8 @@ __host__ __device__ constexpr int combine_xch_doubles(int rb, int nw) {
 // in `xch` (combine_xch_doubles(RB, NW) doubles), then EVERY thread sums entry pairs over the
 // waves and stores them -- the sum and the stores are spread over the whole workgroup (with
 // wave 0 alone doing them tile by tile, T = 40's 15 tiles took 28 us); the row sums are parked
-// and summed with the first round (two barriers instead of two more per row block).  Every thread of the
-// workgroup must call it.
+// and summed with the first round (two barriers instead of two more per row block).  Every
+// thread of the workgroup must call it.
 template <int RB, int NACC, int NW>
 __device__ __forceinline__ void combine_waves(const d4 (&acc)[NACC][n_tiles(RB)],
                                               const double (&s1)[RB], double *xch, double *dst,
