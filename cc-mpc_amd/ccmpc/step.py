@@ -276,8 +276,9 @@ class MinkowskiStepGraph:
         if not (kc[:, -1] == self._K_arr).all():
             raise ValueError(f"kept modes per OV {kc[:, -1].tolist()}; this graph was built "
                              f"for {self.K}")
-        np.subtract(kc, 1, out=i.h("keep"), casting="unsafe")
-        i.h("keep")[~kept] = -1
+        keep = i.h("keep")               # kept: its rank among the kept latents; else -1
+        np.multiply(kc, kept, out=keep, casting="unsafe")
+        keep -= 1
         sd = int(seed) & (2**64 - 1)
         i.h("seed")[0] = sd - (1 << 64) if sd >= (1 << 63) else sd
         i.h("init").reshape(-1)[:] = np.asarray(init_state, np.float64).reshape(-1)
