@@ -55,6 +55,10 @@ def parse(argv=None):
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
                     help="process-group backend for N > 1 (default nccl = RCCL; gloo only to "
                          "rehearse several ranks on one card)")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="form the process group (nccl = RCCL) even at N = 1, so the one "
+                         "exchange (c4_sharded's record all-gather) runs through RCCL on a "
+                         "single card")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, report the world size and exit (no GPU work)")
     return ap.parse_args(argv)
@@ -144,7 +148,7 @@ def c4_sharded(dev, seed, world, rank, steps=20, warmup=3, cfg=None, return_reco
     cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], np.array(refs), scene_K=K)
     launch = cyc.bind().launch
     gather = None
-    if world > 1:
+    if world > 1 or _backend() is not None:     # a process group (also world 1: --dist-always)
         import torch.distributed as dist
         gloo = dist.get_backend() == "gloo"
         counts = cdist.record_counts(store.n_cells, "cpu" if gloo else dev)
@@ -183,7 +187,7 @@ def c4_sharded(dev, seed, world, rank, steps=20, warmup=3, cfg=None, return_reco
         "step_us": round(elapsed * 1e6, 2), "scenes_per_s": round(c["scenes"] / elapsed, 1),
         "constraints_per_step": int(n_rec),
         "constraints_per_s": round(n_rec / elapsed, 1),
-        "record_gather": ("none (N=1)" if world == 1 else
+        "record_gather": ("none (N=1)" if gather is None else
                           ("RCCL" if _backend() == "nccl" else _backend())
                           + " all_gather of every rank's records, inside the step"),
         "rank0": {"particles": n_part, "cells": store.n_cells, "alg_bytes_per_launch": alg,
@@ -317,9 +321,14 @@ def init_dist(args):
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torchrun "
                          f"--nproc-per-node {args.gpus}, or run bench.py --gpus N alone")
-    if world > 1:
+    if world > 1 or getattr(args, "dist_always", False):
         import torch.distributed as dist
         backend = bench_backend(args)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.launch_check:                       # launcher rehearsal: no GPU touched
             dist.init_process_group("gloo")
         elif backend == "nccl":
@@ -348,7 +357,7 @@ def launch_check(world, rank):
 
 
 def barrier(world):
-    if world > 1:
+    if world > 1 or _backend() is not None:
         import torch.distributed as dist
         dist.barrier()
 
@@ -902,7 +911,7 @@ def main():
         out["roofline_sweep"] = sweep(dev, args.seed)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if _backend() is not None:
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -325,24 +325,121 @@ def _mean_tangent_from_arrays(d):
             _cells_grid(d["mnt_cov"], K, T), 0, const_idx)
 
 
+def _flip_y_state(actor):
+    """carlautil's location / rotation / speed with flip_y=True (python-utility is absent,
+    restated): [x, -y, -yaw (rad), |v_xy|] -- make_local_params' x_init from the simulator
+    (v8ideal/__init__.py:520-531, get_current_velocity :507-512)."""
+    loc, rot, vel = actor.get_location(), actor.get_transform().rotation, actor.get_velocity()
+    return np.array([loc.x, -loc.y, -np.deg2rad(rot.yaw), np.sqrt(vel.x ** 2 + vel.y ** 2)])
+
+
+class PlanFollower:
+    """Stand-in for the low-level VehiclePIDController (lowlevel/v1_1.py) the agent hands its
+    plan to (:3255-3257, :3277-3279): set_plan(speeds, angles, step_period) keeps the plan,
+    step() returns the control for the current frame as {target_speed, target_angle} (the
+    planned speed / heading of the plan step the frame falls in).  The PID loop and CARLA's
+    VehicleControl are outside the path."""
+
+    def __init__(self):
+        self.speeds = self.angles = None
+        self.period, self.k = 1, 0
+
+    def set_plan(self, speeds, angles, step_period):
+        self.speeds, self.angles = np.asarray(speeds), np.asarray(angles)
+        self.period, self.k = max(int(step_period), 1), 0
+
+    def step(self):
+        if self.speeds is None or len(self.speeds) == 0:
+            return None
+        i = min(self.k // self.period, len(self.speeds) - 1)
+        self.k += 1
+        return {"target_speed": float(self.speeds[i]), "target_angle": float(self.angles[i])}
+
+
 class MidlevelAgent:
-    """Constraint-generation surface of v8ideal.MidlevelAgent (v8ideal/__init__.py:202-235).
+    """v8ideal.MidlevelAgent (v8ideal/__init__.py:202-235) with the reference's constructor:
+    MidlevelAgent(ego_vehicle, map_reader, other_vehicle_ids, eval_stg, scene_builder_cls=...,
+    scene_config=..., n_burn_interval=4, n_predictions=100, prediction_horizon=8,
+    control_horizon=6, step_horizon=1, ..., **kwargs) -- the harness splats its scenario /
+    control / debug dicts into it (tests/Hz20/__init__.py:183-193), unknown keys land in
+    **kwargs as they do there (:234).
 
-    Only the arguments the chance-constraint path reads are kept; the CARLA/Trajectron/QP
-    arguments of the reference constructor are accepted and ignored (**kwargs, as :234)."""
+    The simulator-side arguments are duck-typed: ego_vehicle / map_reader / the scene builder
+    / eval_stg need only the attributes ccmpc.standins documents (a real carla.Vehicle has
+    them).  Without them the agent is the constraint-generation surface alone (every test
+    that calls the generators directly builds it as MidlevelAgent(prediction_horizon=...)).
 
-    def __init__(self, prediction_horizon=8, control_horizon=None, n_predictions=100,
-                 ego_vehicle_id=0, n_ideal=1_000_000, record_interval=10, seed=0,
-                 road_boundary_constraints=False, device="cuda", data_dir=None, **kwargs):
+    Keyword extras of this implementation: n_ideal (predict_ideal's sample count, :2640),
+    seed (the Philox streams that replace the reference's unseeded RNGs), device, data_dir
+    (load_data from .npz files), reference_trajectory (load_refT's route, instead of the
+    pickle at out/data/referenceTrajectory/T/refT), max_graphs (the step-graph cache size),
+    record_interval / ego_vehicle_id when there is no scene_config / ego_vehicle."""
+
+    def __init__(self, ego_vehicle=None, map_reader=None, other_vehicle_ids=(), eval_stg=None,
+                 scene_builder_cls=None, scene_config=None, n_burn_interval=4,
+                 n_predictions=100, prediction_horizon=8, control_horizon=None, step_horizon=1,
+                 road_boundary_constraints=False, angle_boundary_constraints=False,
+                 log_cplex=True, log_agent=False, plot_simulation=False, plot_boundary=False,
+                 plot_scenario=False, plot_vertices=False, plot_overapprox=False,
+                 get_computeTime=True, turn_choices=(), max_distance=100, *,
+                 n_ideal=1_000_000, seed=0, device="cuda", data_dir=None, **kwargs):
         self.device = engine.require_device(device)
         self.prediction_horizon = int(prediction_horizon)
-        self.control_horizon = int(control_horizon or prediction_horizon)
+        # the reference's default is 6 (:215); clipped so a short-horizon agent built for the
+        # generators alone stays valid under the reference's assert (:236)
+        self.control_horizon = int(control_horizon if control_horizon is not None
+                                   else min(6, self.prediction_horizon))
+        if self.control_horizon > self.prediction_horizon:
+            raise AssertionError("control_horizon <= prediction_horizon (:236)")
         self.n_predictions = int(n_predictions)
+        self.n_burn_interval = int(n_burn_interval)
+        self.step_horizon = int(step_horizon)
         self.n_ideal = int(n_ideal)
-        self.record_interval = int(record_interval)
-        self.ego_vehicle_id = ego_vehicle_id
+        self.scene_config = scene_config
+        self.record_interval = int(scene_config.record_interval if scene_config is not None
+                                   else kwargs.get("record_interval", 10))
+        self._ego = ego_vehicle
+        self.ego_vehicle_id = (ego_vehicle.id if ego_vehicle is not None
+                               else kwargs.get("ego_vehicle_id", 0))
         self.seed = int(seed)
         self.road_boundary_constraints = road_boundary_constraints
+        self.angle_boundary_constraints = angle_boundary_constraints
+        self.log_cplex, self.log_agent = log_cplex, log_agent
+        self.get_computeTime = get_computeTime
+        self.plot_simulation = False           # plotting is outside the path (:305-310)
+        self._map_reader, self._eval_stg = map_reader, eval_stg
+        self._scene_builder_cls, self._scene_builder = scene_builder_cls, None
+        self._first_frame = None
+        self._other_vehicles = {}
+        world = ego_vehicle.get_world() if ego_vehicle is not None else None
+        if world is not None:
+            ids = list(other_vehicle_ids)
+            self._other_vehicles = dict(zip(ids, world.get_actors(ids)))     # :267-272
+        # __steptime (:275-278): record_interval x the simulator's fixed step
+        self.steptime = (self.record_interval * world.get_settings().fixed_delta_seconds
+                         if world is not None else 0.5)
+        self._sensor_listening = False
+        self._lidar_feeds = collections.OrderedDict()
+        self._local_planner = kwargs.get("local_planner") or PlanFollower()
+        self._X_warm = None                    # __X_warmstarting (:290)
+        self._U_warm = None                    # __U_warmstarting (:288)
+        self.offline_index = 0
+        self.refT = None
+        self._ref_route = (None if kwargs.get("reference_trajectory") is None
+                           else np.asarray(kwargs["reference_trajectory"], np.float64))
+        self._road_boundary = None
+        self._goal = None
+        self._max_distance = float(max_distance)
+        self._turn_choices = list(turn_choices)
+        if ego_vehicle is not None:            # __make_global_params (:82-120), bbox / steer
+            ext = ego_vehicle.bounding_box.extent
+            self.ego_lon, self.ego_lat = 2.0 * ext.x, 2.0 * ext.y
+            steer = ego_vehicle.get_physics_control().wheels[0].max_steer_angle
+            self.mpc_params_steer = float(steer)
+        else:
+            self.ego_lon, self.ego_lat, self.mpc_params_steer = 3.7, 1.79, 70.0
+        if map_reader is not None and ego_vehicle is not None:
+            self._setup_road_boundary_conditions(self._turn_choices, self._max_distance)
         self.R = risk.R_COLLISION
         self._moments = {}                 # frame -> (mean [C,T,2], cov [C,2T,2T], K, T)
         self._mean_tangent = {}            # frame -> affine_scale meanNtangent (save_data)
@@ -353,7 +450,7 @@ class MidlevelAgent:
         self.prob_lower_save = None
         self.last_records = None
         self._last_rec = None              # (device records, kind, T) of the last generator
-        self.mpc_params = mpc.MPCParams.reference_defaults()
+        self.mpc_params = mpc.MPCParams.reference_defaults(self.mpc_params_steer)
         self._ltv = None                   # (x_init, T_full) -> (xbar, Gamma), first step's
         self._qp = {}
         # (O, N, ph, L, K, per_particle, eps_in) -> step.MinkowskiStepGraph, least recently
@@ -361,10 +458,216 @@ class MidlevelAgent:
         # modes per OV change from frame to frame in an episode, so the cache is bounded
         self._graphs = collections.OrderedDict()
         self.max_graphs = int(kwargs.get("max_graphs", 8))
+        if self.max_graphs < 1:
+            raise ValueError(f"max_graphs must be >= 1, got {self.max_graphs}")
         self._risk_memo = {}
         self._u_prev = []                  # executed controls of this shrinking episode (:3186)
         self.last_generator_output = None
         self.last_ctrl = None
+
+    # ------------------------------------------------------------------------------------
+    # The harness-facing surface (tests/Hz20/__init__.py:183-359): construction, sensor and
+    # goal accessors, run_step with the reference's frame gating, and the private
+    # __compute_prediction_controls chain do_prediction -> make_ovehicles ->
+    # make_local_params -> do_highlevel_control on the device path.
+
+    def _setup_road_boundary_conditions(self, turn_choices, max_distance):
+        """:170-200: the route's RoadBoundaryConstraint; its last point is the initial goal."""
+        self._road_boundary = self._map_reader.road_boundary_constraints_from_actor(
+            self._ego, max_distance, choices=turn_choices, flip_y=True)
+        x, y = np.asarray(self._road_boundary.points)[-1]
+        self._goal = {"x": float(x), "y": float(y), "is_relative": False}
+
+    def start_sensor(self):
+        """:359-363.  The semantic-lidar feed only shapes Trajectron++'s map input, which is
+        outside the path: the stand-in just marks the sensor listening."""
+        self._sensor_listening = True
+
+    def stop_sensor(self):
+        self._sensor_listening = False
+
+    @property
+    def sensor_is_listening(self):
+        return self._sensor_listening
+
+    def destroy(self):
+        """:407-412 (no CARLA resources are held; graphs and workspaces are released)."""
+        self._sensor_listening = False
+        self._graphs.clear()
+
+    def get_goal(self):
+        """:344-345: a copy, as an attribute dict (harness code writes goal.x / goal.y)."""
+        from .standins import AttrDict
+        return AttrDict(dict(self._goal)) if self._goal is not None else None
+
+    def set_goal(self, x=None, y=None, distance=None, is_relative=True, **kwargs):
+        """:350-357."""
+        if x is not None and y is not None:
+            self._goal = {"x": x, "y": y, "is_relative": is_relative}
+        elif distance is not None:
+            px, py = self._road_boundary.get_point_from_start(distance)
+            self._goal = {"x": float(px), "y": float(py), "is_relative": False}
+        else:
+            raise NotImplementedError("Unknown method of setting motion planner goal.")
+
+    def get_vehicle_state(self, flip_x=False, flip_y=False):
+        """:331-341: the last planning step's x_init once one ran, else the simulator's state
+        (flip_y as carlautil does)."""
+        x = getattr(self, "x_init", None)
+        if x is not None:
+            return x
+        if self._ego is None:
+            raise AttributeError("no ego vehicle and no planning step yet")
+        st = _flip_y_state(self._ego)
+        if not flip_y:
+            st = st * np.array([1.0, -1.0, -1.0, 1.0])
+        return st
+
+    def get_final_state(self):
+        return self.planned_finalstate
+
+    def do_first_step(self, frame):
+        """:3212-3224."""
+        self._first_frame = frame
+        self._scene_builder = self._scene_builder_cls(
+            self, self._map_reader, self._ego, self._other_vehicles, self._lidar_feeds,
+            "test", self._first_frame, scene_config=self.scene_config, debug=False)
+
+    def run_step(self, frame, offline_index=0, Tsh=6, shrinking=False, control=None):
+        """:3226-3284.  Captures the scene every frame; plans when (frame - first_frame) is a
+        multiple of record_interval, past n_burn_interval planning periods and on the
+        step_horizon grid; hands the plan to the low-level follower; applies `control` (or the
+        follower's) to the ego.  Returns the QP time-out flag; raises InSimulationException
+        where the reference's CPLEX solve fails."""
+        self.offline_index = offline_index
+        if self._first_frame is None:
+            self.do_first_step(frame)
+        self._scene_builder.capture_trajectory(frame)
+        timeout = False
+        if (frame - self._first_frame) % self.record_interval == 0:
+            frame_id = int((frame - self._first_frame) / self.record_interval)
+            if frame_id < self.n_burn_interval:
+                pass                                   # burn: collect data only (:3250-3252)
+            elif (frame_id - self.n_burn_interval) % self.step_horizon == 0:
+                speeds, angles, timeout = self.__compute_prediction_controls(frame, Tsh,
+                                                                             shrinking)
+                self._local_planner.set_plan(speeds, angles, self.record_interval)
+        if not control:
+            control = self._local_planner.step()
+        if self._ego is not None and hasattr(self._ego, "apply_control"):
+            self._ego.apply_control(control)
+        return timeout
+
+    def do_prediction(self, frame):
+        """:414-467: the frame's scene from the scene builder, then generate_vehicle_latents
+        (prediction.py:19-105).  Trajectron++'s encoder and GRU decoder run in eval_stg; what
+        reaches this path is the sampler tail's input (per-OV latent pmf, initial state, GMM
+        parameters, and for Trajectron++'s own boundary the per-sample parameters, z and noise
+        as device tensors).  The rollout itself (GMM2D.rsample + Unicycle) runs inside the
+        planning step on the GPU, so `boundary` stands where the reference's `predictions` /
+        `z` arrays stand."""
+        scene = self._scene_builder.get_scene()
+        timestep = int((frame - self._first_frame) / self.record_interval)
+        b = self._eval_stg.sample_boundary(scene, timestep, self.n_predictions,
+                                           self.prediction_horizon)
+        return {"scene": scene, "timestep": timestep, "nodes": list(b["nodes"]),
+                "boundary": b, "latent_probs": np.asarray(b["latent_probs"], np.float64),
+                "past_dict": {timestep: scene.past(timestep, max_h=10)}}
+
+    def _ov_inputs(self, pred):
+        """make_ovehicles (:469-505) up to the bucketing: the non-ego nodes' rows of the sampler
+        boundary, minpos = (x_min, y_min), pasts (+ minpos) and bboxes of the OV actors."""
+        nodes, b, ts = pred["nodes"], pred["boundary"], pred["timestep"]
+        sel = [i for i, n in enumerate(nodes) if n.id != "ego"]
+        scene = pred["scene"]
+        minpos = np.array([scene.x_min, scene.y_min])
+        pasts = [pred["past_dict"][ts][nodes[i]] + minpos for i in sel]
+        bboxes = []
+        for i in sel:
+            a = self._other_vehicles.get(int(nodes[i].id))
+            ext = a.bounding_box.extent if a is not None else None
+            bboxes.append([2.0 * ext.x, 2.0 * ext.y] if ext is not None else [4.5, 2.5])
+        idx = np.asarray(sel)
+
+        def rows(x):
+            if x is None:
+                return None
+            if torch.is_tensor(x):
+                return x if len(sel) == x.shape[0] else x[torch.as_tensor(idx, device=x.device)].contiguous()
+            return np.asarray(x)[idx]
+
+        sampler = {"init_state": rows(b["init_state"]), "latent_pmf": rows(b["latent_probs"]),
+                   "gmm": rows(b["gmm"]), "N": int(b["N"]), "seed": int(b["seed"])}
+        if b.get("per_particle"):
+            sampler.update(per_particle=True, z=rows(b["z"]), eps=rows(b.get("eps")))
+        if "filter_pmf" in b:
+            sampler["filter_pmf"] = b["filter_pmf"]
+        return sampler, minpos, pasts, np.asarray(bboxes, np.float64)
+
+    def make_local_params(self, frame, Tsh):
+        """:514-568 (the ego part): x_init is the previous plan's first state when there is
+        one (:526-532, the reference's warm start), else the simulator's; the LTV model is
+        built by the QP (solve_planning_qp) at Tsh == ph and kept below it (:2842-2871)."""
+        if self._X_warm is not None:
+            x_init = np.asarray(self._X_warm[0], np.float64)
+        else:
+            x_init = _flip_y_state(self._ego)
+        self.x_init = x_init
+        return x_init
+
+    def load_refT(self, offline_idx, Tsh, x_init):
+        """:2768-2787 on the route given as reference_trajectory=: the route point nearest
+        x_init, or the next one when the nearest lies behind the third nearest (the
+        reference's "closest ahead point"), and Tsh points from there."""
+        ref = self._ref_route
+        if ref is None:
+            raise FileNotFoundError("no reference trajectory (reference_trajectory=) for "
+                                    "load_refT (the reference reads out/data/"
+                                    "referenceTrajectory/T/refT)")
+        norm2 = np.linalg.norm(ref[:, :2] - np.asarray(x_init, np.float64)[:2], axis=1)
+        s = np.argsort(norm2)
+        if s[0] < s[2]:
+            index_min = s[0]
+        elif s[0] > s[2]:
+            index_min = s[1]
+        self.refT = ref[index_min:index_min + Tsh]
+        if len(self.refT) < Tsh:
+            raise IndexError(f"reference trajectory ends {Tsh - len(self.refT)} steps short of "
+                             "the horizon (the reference's objective indexes past it)")
+        return self.refT
+
+    def compute_segs_polytopes_and_goal(self, x_init, Tsh):
+        """:590-608: the route goal one horizon of speed-limited travel ahead of x_init."""
+        v_lim = min(self._ego.get_speed_limit() * 0.28, self.mpc_params.max_v)
+        distance = v_lim * self.steptime * Tsh + 1
+        segments = self._road_boundary.collect_segs_polytopes_and_goal(
+            np.asarray(x_init)[:2], distance)
+        return segments, np.asarray(segments.goal, np.float64)
+
+    def __compute_prediction_controls(self, frame, Tsh, shrinking):
+        """:3163-3210 on the device path: prediction boundary -> (make_ovehicles + generator +
+        QP in compute_prediction_controls) -> warm start (:3187-3193) -> speeds / angles."""
+        pred = self.do_prediction(frame)
+        sampler, minpos, pasts, bboxes = self._ov_inputs(pred)
+        x_init = self.make_local_params(frame, Tsh)
+        # do_highlevel_control (:2814, :2840): refT, then the route goal
+        ref = self.load_refT(int(self.offline_index / 10) + 1, Tsh, x_init)
+        _, goal = self.compute_segs_polytopes_and_goal(x_init, Tsh)
+        speeds, angles, timeout = self.compute_prediction_controls(
+            frame, Tsh, shrinking, sampler, minpos, pasts, x_init, goal, ref, bboxes)
+        self.control_horizon_last = Tsh        # __control_horizon = Tsh (:3170)
+        c = self.last_ctrl
+        self._U_warm, self._X_warm = c["U_star"], c["X_star"]
+        self.planned_finalstate = c["X_star"][-1]
+        log = getattr(self, "_step_log", None)
+        if log is not None:                    # the harness replay's per-step record
+            log.append({"frame": frame, "T": int(Tsh), "shrinking": bool(shrinking),
+                        "sampler": sampler, "minpos": minpos, "pasts": pasts,
+                        "bboxes": bboxes, "x_init": x_init.copy(), "goal": goal,
+                        "ref": np.array(ref), "records": np.array(self.last_records),
+                        "speeds": speeds, "angles": angles, "U_star": c["U_star"],
+                        "X_star": c["X_star"], "u": c["u"]})
+        return speeds, angles, timeout
 
     # ------------------------------------------------------------------------------------
     def _saved(self, frame):
@@ -497,7 +800,7 @@ class MidlevelAgent:
             m_scene, c_scene = mean, cov
         # save_moments (:960): the moments of exactly the particles this step reduced
         self._moments[params.frame] = (mean, cov, list(K), T)
-        h = engine.halfspaces(rec)
+        h = engine.halfspaces(rec)[:, :T * (T - 1) // 2]     # T = 1 keeps one unused slot
         self.last_records = h
         self._last_rec = (rec, mpc.REC_HALFSPACE, T)
         constraints = self._records_to_halfspaces(h, scene, T)
@@ -745,15 +1048,16 @@ class MidlevelAgent:
         T, ph = int(Tsh), self.prediction_horizon
         pmf = np.asarray(sampler["latent_pmf"], np.float64)
         O = pmf.shape[0]
+        fp = float(sampler.get("filter_pmf", 0.1))     # one value for K, the graph and buckets
         if T == ph:
             self._u_prev = []
         if shrinking and apply_robust:
-            K = (pmf > sampler.get("filter_pmf", 0.1)).sum(1).tolist()
+            K = (pmf > fp).sum(1).tolist()
             eps_ura = np.full((O, max(K)), 0.05 / O)              # :2909-2916
             params = episode.Params(O, K, frame)
             params.x_init = np.asarray(x_init, np.float64)
             ovs, out = self.predict_and_constrain(params, sampler, eps_ura, T, ref_traj, minpos,
-                                                  pasts, bboxes)
+                                                  pasts, bboxes, filter_pmf=fp)
         else:
             pp = bool(sampler.get("per_particle", False))
             z, store = engine.sample_unicycle(
@@ -761,7 +1065,7 @@ class MidlevelAgent:
                 seed=int(sampler["seed"]), device=self.device, z=sampler.get("z"),
                 eps=sampler.get("eps"), per_particle=pp)
             ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, bboxes,
-                                          device=self.device)
+                                          filter_pmf=fp, device=self.device)
             K = [ov.n_states for ov in ovs]
             eps_ura = np.full((O, max(K)), 0.05 / O)
             params = episode.Params(O, K, frame)
@@ -770,7 +1074,7 @@ class MidlevelAgent:
                 params, ovs, None, None, None, eps_ura, None, T, ref_traj)
         self.last_generator_output = (ovs, out)
         up = np.concatenate(self._u_prev) if (T < ph and self._u_prev) else None
-        ctrl = self.solve_planning_qp(x_init, goal, ref_traj, T, u_prev=up)
+        ctrl = self.solve_planning_qp(x_init, goal, ref_traj, T, u_prev=up, lon=self.ego_lon)
         self.last_ctrl = ctrl
         self._u_prev.append(np.asarray(ctrl["u"][:2]))        # U_star.T.ravel()[:nu] (:3186)
         X = ctrl["X_star"]
@@ -792,7 +1096,8 @@ class MidlevelAgent:
             raise ValueError(f"records are for T = {T}, not Tsh = {Tsh}")
         ph = self.prediction_horizon
         if T == ph or self._ltv is None:
-            self._ltv = mpc.ltv(np.asarray(x_init, np.float64)[None], ph, Ts=0.5, lon=lon)
+            self._ltv = mpc.ltv(np.asarray(x_init, np.float64)[None], ph, Ts=self.steptime,
+                                lon=lon)
         xbar, gamma = self._ltv
         key = (rec.shape[0], T, kind, u_order)
         qp = self._qp.get(key)

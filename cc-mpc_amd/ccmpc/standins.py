@@ -1,0 +1,348 @@
+"""Stand-ins for the simulator and the learned predictor around the planner's outer surface.
+
+The reference harness (tests/Hz20/__init__.py:37-447) drives v8ideal.MidlevelAgent with
+CARLA actors, a MapQuerier, a TrajectronPlusPlusSceneBuilder and a trained Trajectron++.
+None of them exist here (no simulator, un-vendored Trajectron++ submodule, no weights), so
+these classes supply exactly the attributes the agent reads, with CARLA's own names where
+the agent reads CARLA objects:
+
+  StubWorld / StubVehicle     carla.World / carla.Vehicle: tick(), get_settings()
+                              .fixed_delta_seconds, get_actors(ids), get_location(),
+                              get_transform().rotation, get_velocity(), bounding_box.extent,
+                              get_physics_control().wheels[0].max_steer_angle,
+                              get_speed_limit(), apply_control(), id
+  OnlineConfig                collect/generate/scene/__init__.py OnlineConfig (record_interval)
+  PolylineRoadBoundary        RoadBoundaryConstraint's goal rule (collect/generate/map/
+                              road.py:621-677) over a polyline route; no road polytopes (the
+                              road-boundary MILP variant is out of scope)
+  StubMapReader               MapQuerier.road_boundary_constraints_from_actor
+                              (collect/generate/map/__init__.py:392)
+  ReplaySceneBuilder          TrajectronPlusPlusSceneBuilder's capture_trajectory / get_scene
+                              over constant-velocity OV tracks (positions relative to the
+                              scene's (x_min, y_min), as Trajectron++ scenes are)
+  SyntheticTrajectron         eval_stg: hands the sampler tail the inputs p_y_xz produces
+                              (prediction.py:70-86) -- per-OV latent pmf, the unicycle
+                              initial state and either per-(latent, step) GMM2D parameters
+                              (z and noise drawn on the GPU from a Philox stream keyed by
+                              the timestep) or per-sample GMM parameters + z + noise as device
+                              tensors, Trajectron++'s own boundary
+
+Everything is seeded and deterministic.  None of this is on the compute path: it is the
+replay's input side (SURVEY.md 8d's synthetic generator), like ccmpc.synthetic.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import episode
+
+
+class AttrDict(dict):
+    """utility.AttrDict (python-utility, absent): a dict with attribute access."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k) from None
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+class _Vec:
+    def __init__(self, x=0.0, y=0.0, z=0.0):
+        self.x, self.y, self.z = float(x), float(y), float(z)
+
+
+class _Rot:
+    def __init__(self, pitch=0.0, yaw=0.0, roll=0.0):
+        self.pitch, self.yaw, self.roll = float(pitch), float(yaw), float(roll)
+
+
+class _Transform:
+    def __init__(self, location, rotation):
+        self.location, self.rotation = location, rotation
+
+
+class OnlineConfig:
+    """collect/generate/scene OnlineConfig: the planner reads record_interval (frames per
+    planning step) from it."""
+
+    def __init__(self, record_interval=10, node_type=None):
+        self.record_interval = int(record_interval)
+        self.node_type = node_type
+
+
+class StubVehicle:
+    """A carla.Vehicle with the attributes the agent reads.  Positions are CARLA's (left-handed,
+    y down the map); the agent flips y as carlautil does (flip_y=True).  apply_control records
+    the last control; tick() moves the vehicle by the control's target speed / angle (a
+    kinematic stand-in for the PID follower and the physics)."""
+
+    def __init__(self, world, actor_id, x, y, yaw_deg=0.0, speed=0.0, lon=3.7, lat=1.79,
+                 max_steer_deg=70.0, speed_limit_kmh=30.0):
+        self.world, self.id = world, int(actor_id)
+        self._loc = _Vec(x, y, 0.0)
+        self._rot = _Rot(0.0, yaw_deg, 0.0)
+        self._speed = float(speed)
+        self.bounding_box = AttrDict(extent=_Vec(lon / 2.0, lat / 2.0, 0.75))
+        self._max_steer = float(max_steer_deg)
+        self._speed_limit = float(speed_limit_kmh)
+        self.controls = []
+
+    def get_world(self):
+        return self.world
+
+    def get_location(self):
+        return _Vec(self._loc.x, self._loc.y, self._loc.z)
+
+    def get_transform(self):
+        return _Transform(self.get_location(), _Rot(self._rot.pitch, self._rot.yaw, self._rot.roll))
+
+    def get_velocity(self):
+        h = math.radians(self._rot.yaw)
+        return _Vec(self._speed * math.cos(h), self._speed * math.sin(h), 0.0)
+
+    def get_physics_control(self):
+        return AttrDict(wheels=[AttrDict(max_steer_angle=self._max_steer)])
+
+    def get_speed_limit(self):
+        return self._speed_limit
+
+    def apply_control(self, control):
+        self.controls.append(control)
+
+    def _advance(self, dt):
+        c = self.controls[-1] if self.controls else None
+        if isinstance(c, dict) and "target_speed" in c:
+            self._speed = float(c["target_speed"])
+            # the agent already reflected the plan's heading back into CARLA's frame (:3208)
+            self._rot.yaw = math.degrees(float(c["target_angle"]))
+        h = math.radians(self._rot.yaw)
+        self._loc.x += self._speed * math.cos(h) * dt
+        self._loc.y += self._speed * math.sin(h) * dt
+
+    def destroy(self):
+        pass
+
+
+class StubWorld:
+    """carla.World in synchronous mode: tick() advances the frame counter (and the vehicles)."""
+
+    def __init__(self, first_frame=1000, fixed_delta_seconds=0.05):
+        self.frame = int(first_frame)
+        self._settings = AttrDict(fixed_delta_seconds=float(fixed_delta_seconds),
+                                  synchronous_mode=True)
+        self.actors = {}
+
+    def add(self, vehicle):
+        self.actors[vehicle.id] = vehicle
+        return vehicle
+
+    def get_settings(self):
+        return self._settings
+
+    def get_actors(self, ids):
+        return [self.actors[int(i)] for i in ids]
+
+    def tick(self):
+        for a in self.actors.values():
+            a._advance(self._settings.fixed_delta_seconds)
+        self.frame += 1
+        return self.frame
+
+
+class PolylineRoadBoundary:
+    """RoadBoundaryConstraint over a polyline route (points in the planner's flipped frame):
+    collect_segs_polytopes_and_goal's goal rule (road.py:663-666: the route point nearest the
+    position, then the first point at or past min(its distance + distance, path length)), and
+    get_point_from_start (:621-637, linear instead of the cubic spline between points)."""
+
+    def __init__(self, points):
+        self.points = np.asarray(points, np.float64).reshape(-1, 2)
+        seg = np.linalg.norm(np.diff(self.points, axis=0), axis=1)
+        self.distances = np.concatenate([[0.0], np.cumsum(seg)])
+
+    @property
+    def path_length(self):
+        return float(self.distances[-1])
+
+    def get_point_from_start(self, distance):
+        d = self.distances
+        if not 0.0 <= distance <= d[-1]:
+            return self.points[-1]
+        return np.array([np.interp(distance, d, self.points[:, 0]),
+                         np.interp(distance, d, self.points[:, 1])])
+
+    def collect_segs_polytopes_and_goal(self, position, distance):
+        beg_idx = int(np.argmin(np.linalg.norm(self.points - np.asarray(position)[:2], axis=1)))
+        end_dist = min(self.distances[beg_idx] + distance, self.path_length)
+        # distance_to_point is indexed by the right-closed intervals (d[j-1], d[j]] -> point j
+        j = max(int(np.searchsorted(self.distances, end_dist, side="left")), 1)
+        return AttrDict(polytopes=[], polytope_ids=[], mask=np.zeros(0, bool),
+                        goal=self.points[j].copy())
+
+
+class StubMapReader:
+    """MapQuerier.road_boundary_constraints_from_actor (map/__init__.py:392) returning a
+    PolylineRoadBoundary along the given route."""
+
+    def __init__(self, route_points):
+        self.route_points = np.asarray(route_points, np.float64)
+
+    def road_boundary_constraints_from_actor(self, actor, max_distance, choices=(), flip_y=True):
+        return PolylineRoadBoundary(self.route_points)
+
+
+def straight_route(start, heading, length=200.0, step=2.0):
+    """A straight route from `start` (flipped frame) along `heading` (radians)."""
+    s = np.arange(0.0, length + step, step)
+    return np.stack([start[0] + s * math.cos(heading), start[1] + s * math.sin(heading)], 1)
+
+
+class _Node:
+    def __init__(self, node_id):
+        self.id = node_id
+
+    def __repr__(self):
+        return f"VEHICLE/{self.id}"
+
+
+class ReplayScene:
+    """The Trajectron++ scene of one planning frame: x_min / y_min (the offset its positions are
+    relative to), dt, nodes, and each node's history (prediction_output_to_trajectories'
+    past_dict, max_h steps, relative positions)."""
+
+    def __init__(self, x_min, y_min, dt, nodes, tracks, timestep):
+        self.x_min, self.y_min, self.dt = x_min, y_min, dt
+        self.nodes = nodes
+        self._tracks, self.timestep = tracks, timestep
+
+    def past(self, timestep, max_h=10):
+        out = {}
+        for n in self.nodes:
+            tr = self._tracks[n.id]
+            lo = max(0, timestep - max_h)
+            out[n] = np.asarray(tr[lo:timestep + 1], np.float64)
+        return out
+
+    def state(self, node, timestep):
+        """Unicycle state [x, y, heading, speed] (relative) of `node` at `timestep`."""
+        return self._tracks[node.id + "/state"][timestep]
+
+
+class ReplaySceneBuilder:
+    """TrajectronPlusPlusSceneBuilder (collect/generate/scene/v3_2/trajectron_scene.py) with the
+    constructor the agent calls (v8ideal/__init__.py:3212-3224): capture_trajectory(frame)
+    records every OV's position each record_interval frames; get_scene() returns the frame's
+    ReplayScene.  OVs move at constant velocity from the world's actors' current states."""
+
+    def __init__(self, agent, map_reader, ego_vehicle, other_vehicles, lidar_feeds, scene_name,
+                 first_frame, scene_config=None, debug=False, minpos=(150.0, -120.0)):
+        self.ego, self.other_vehicles = ego_vehicle, other_vehicles
+        self.first_frame = int(first_frame)
+        self.record_interval = scene_config.record_interval if scene_config else 10
+        self.dt = self.record_interval * ego_vehicle.get_world().get_settings().fixed_delta_seconds
+        self.minpos = np.asarray(minpos, np.float64)
+        self.nodes = [_Node("ego")] + [_Node(str(i)) for i in other_vehicles]
+        self.tracks = {n.id: [] for n in self.nodes}
+        for n in self.nodes:
+            self.tracks[n.id + "/state"] = []
+        self.timestep = -1
+
+    def _actor(self, node):
+        return self.ego if node.id == "ego" else self.other_vehicles[int(node.id)]
+
+    def capture_trajectory(self, frame):
+        if (frame - self.first_frame) % self.record_interval:
+            return
+        self.timestep = (frame - self.first_frame) // self.record_interval
+        for n in self.nodes:
+            a = self._actor(n)
+            loc, rot, vel = a.get_location(), a.get_transform().rotation, a.get_velocity()
+            rel = np.array([loc.x, -loc.y]) - self.minpos            # flip_y, scene-relative
+            self.tracks[n.id].append(rel)
+            self.tracks[n.id + "/state"].append(
+                np.array([rel[0], rel[1], -math.radians(rot.yaw), math.hypot(vel.x, vel.y)]))
+
+    def get_scene(self):
+        return ReplayScene(self.minpos[0], self.minpos[1], self.dt, self.nodes, self.tracks,
+                           self.timestep)
+
+
+class SyntheticTrajectron:
+    """eval_stg stand-in.  sample_boundary(scene, timestep, num_samples, ph) returns what the
+    sampler tail receives from Trajectron++ (prediction.py:70-86) for every node of the scene
+    (the ego included, as generate_vehicle_latents returns it; make_ovehicles skips it):
+
+      nodes, init_state (n, 4) [x, y, heading, speed] relative to the scene, latent_probs (n, L)
+      per_particle=False: gmm (n, L, ph, 5) per-(latent, step) GMM2D parameters, seed (the
+          sampler draws z and the noise on the GPU from it)
+      per_particle=True:  gmm (n, N, ph, 5), z (n, N) latent ids, eps (n, N, ph, 2) -- device
+          tensors, drawn with torch on the device as p_y_xz leaves them
+
+    The per-latent parameters are ccmpc.episode.synthetic_gmm's, fixed per node; the draws are
+    keyed by (seed, timestep), so a frame's predictions are reproducible."""
+
+    def __init__(self, L=25, ph=8, seed=0, per_particle=False, with_eps=True, device="cuda"):
+        self.L, self.ph, self.seed = int(L), int(ph), int(seed)
+        self.per_particle, self.with_eps = bool(per_particle), bool(with_eps)
+        self.device = device
+        self._gmm = {}
+
+    def _node_params(self, i):
+        if i not in self._gmm:
+            _, pmf, gmm = episode.synthetic_gmm(1, L=self.L, T=self.ph,
+                                                seed=20251015 + 97 * self.seed + i)
+            self._gmm[i] = (pmf[0], gmm[0])
+        return self._gmm[i]
+
+    def sample_boundary(self, scene, timestep, num_samples, ph):
+        assert ph == self.ph
+        nodes = list(scene.nodes)
+        n = len(nodes)
+        init = np.stack([scene.state(nd, timestep) for nd in nodes])
+        pmf = np.stack([self._node_params(i)[0] for i in range(n)])
+        gmm = np.stack([self._node_params(i)[1] for i in range(n)])
+        seed = (self.seed * 7919 + int(timestep)) & 0x7FFFFFFF
+        out = AttrDict(nodes=nodes, init_state=init, latent_probs=pmf, N=int(num_samples),
+                       seed=seed, per_particle=self.per_particle)
+        if not self.per_particle:
+            out.gmm = gmm
+            return out
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        pmf_t = torch.as_tensor(pmf, device=self.device)
+        z = torch.multinomial(pmf_t, int(num_samples), replacement=True, generator=g)
+        base = torch.as_tensor(gmm, dtype=torch.float32, device=self.device)    # (n, L, ph, 5)
+        pp = torch.gather(base, 1, z[:, :, None, None].expand(n, int(num_samples), ph, 5))
+        # the GRU decoder conditions every sample on its own history: per-sample jitter
+        pp = pp + 0.02 * torch.randn(pp.shape, generator=g, device=self.device,
+                                     dtype=torch.float32)
+        out.gmm, out.z = pp.contiguous(), z.to(torch.int32).contiguous()
+        out.eps = (torch.randn((n, int(num_samples), ph, 2), generator=g, device=self.device,
+                               dtype=torch.float32) if self.with_eps else None)
+        return out
+
+
+def town03_scene(world=None, n_ov=1, ego_xy=(140.0, 81.0), ego_yaw_deg=0.0, ego_speed=6.0,
+                 ov_gap=25.0, ov_speed=4.0, ov_lateral=0.0, first_frame=1000):
+    """A stand-in for the Town03 scene-4 setup of the Monte-Carlo test (tests/Hz20/params.py's
+    MONTECARLO_scene4_*): the ego on a straight road (CARLA frame); n_ov OVs driving parallel
+    to it, OV j ov_gap + 8 j metres ahead and ov_lateral metres to the side (alternating
+    sides); and the route the map reader follows.  Returns (world, ego, ov_ids, map_reader)."""
+    world = world or StubWorld(first_frame=first_frame)
+    ego = world.add(StubVehicle(world, 1, ego_xy[0], ego_xy[1], ego_yaw_deg, ego_speed))
+    ids = []
+    h = math.radians(ego_yaw_deg)
+    for j in range(n_ov):
+        lat = ov_lateral * (1.0 if j % 2 == 0 else -1.0)
+        x = ego_xy[0] + (ov_gap + 8.0 * j) * math.cos(h) - lat * math.sin(h)
+        y = ego_xy[1] + (ov_gap + 8.0 * j) * math.sin(h) + lat * math.cos(h)
+        ov = world.add(StubVehicle(world, 100 + j, x, y, ego_yaw_deg, ov_speed))
+        ids.append(ov.id)
+    start = np.array([ego_xy[0], -ego_xy[1]])
+    route = straight_route(start, -math.radians(ego_yaw_deg))
+    return world, ego, ids, StubMapReader(route)

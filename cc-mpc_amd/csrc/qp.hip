@@ -1121,12 +1121,17 @@ inline QpPlan qp_plan(int T, int64_t R) {
 }
 
 template <bool ROWS_LDS, int NM>
-void launch_qp(dim3 grid, dim3 block, size_t lds, hipStream_t s, const QpArgs &a) {
-  static const bool attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kQpLdsBytes)) == hipSuccess;
-  (void)attr;
+hipError_t launch_qp(dim3 grid, dim3 block, size_t lds, hipStream_t s, const QpArgs &a) {
+  // the dynamic-LDS limit is a per-device attribute: set it on every launch (cheap), so a
+  // process that drives several devices raises it on each, and report a failure as such
+  if (lds > 48 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kQpLdsBytes));
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM>), grid, block, lds, s, a);
+  return hipSuccess;
 }
 
 }  // namespace ccmpc
@@ -1225,12 +1230,18 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   const int nm = n <= 16 ? 16 : 0;
   const dim3 grid(static_cast<unsigned>(n_scenes)), block(kQpThreads);
   hipStream_t s = as_stream(stream);
+  hipError_t attr;
   if (in_lds) {
-    if (nm == 16) launch_qp<true, 16>(grid, block, lds, s, a);
-    else launch_qp<true, 0>(grid, block, lds, s, a);
+    attr = nm == 16 ? launch_qp<true, 16>(grid, block, lds, s, a)
+                    : launch_qp<true, 0>(grid, block, lds, s, a);
   } else {
-    if (nm == 16) launch_qp<false, 16>(grid, block, lds, s, a);
-    else launch_qp<false, 0>(grid, block, lds, s, a);
+    attr = nm == 16 ? launch_qp<false, 16>(grid, block, lds, s, a)
+                    : launch_qp<false, 0>(grid, block, lds, s, a);
+  }
+  if (attr != hipSuccess) {
+    set_error(std::string(__func__) + ": hipFuncSetAttribute(MaxDynamicSharedMemorySize) "
+              "failed: " + hipGetErrorString(attr));
+    return CCMPC_ERR_LAUNCH;
   }
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;

@@ -124,33 +124,31 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
 }
 
 template <bool PP, bool ZIN, bool EPSIN>
-static void launch_sampler(int64_t n_ov, hipStream_t s, const double *init_state,
-                           const double *latent_cdf, int n_latent, const float *gmm,
-                           const int32_t *z_in, const float *eps_in, int64_t N, int T, float dt,
-                           uint64_t seed, const uint64_t *seed_dev, uint32_t ov_base,
-                           int32_t *out_z, float *out_pos, int64_t ld) {
-  auto go = [&](auto nch) {
+static hipError_t launch_sampler(int64_t n_ov, hipStream_t s, const double *init_state,
+                                 const double *latent_cdf, int n_latent, const float *gmm,
+                                 const int32_t *z_in, const float *eps_in, int64_t N, int T,
+                                 float dt, uint64_t seed, const uint64_t *seed_dev,
+                                 uint32_t ov_base, int32_t *out_z, float *out_pos, int64_t ld) {
+  auto go = [&](auto nch) -> hipError_t {
     constexpr int NCH = decltype(nch)::value, PB = kSampP * NCH;
     const dim3 grid(static_cast<unsigned>((N + PB - 1) / PB), static_cast<unsigned>(n_ov));
     const size_t lds = sizeof(float) * 2 * T * PB;
-    if (lds > 48 * 1024) {  // long horizons on wide blocks: allow the larger dynamic LDS once
-      static bool raised = false;
-      if (!raised) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(
-                                &sample_unicycle_kernel<PP, ZIN, EPSIN, NCH>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(sizeof(float) * 2 * 40 * PB));
-        raised = true;
-      }
+    if (lds > 48 * 1024) {
+      // long horizons on wide blocks: allow the larger dynamic LDS.  The attribute is per
+      // device, and cheap to set, so it is set on every such launch (the current device may
+      // change between calls) and a failure is reported here rather than as a launch error
+      const hipError_t e = hipFuncSetAttribute(
+          reinterpret_cast<const void *>(&sample_unicycle_kernel<PP, ZIN, EPSIN, NCH>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL((sample_unicycle_kernel<PP, ZIN, EPSIN, NCH>), grid, dim3(kSampThreads),
                        lds, s, init_state, latent_cdf, n_latent, gmm, z_in, eps_in, N, T, dt,
                        seed, seed_dev, ov_base, out_z, out_pos, ld);
+    return hipSuccess;
   };
-  if (N > kSampWideN)
-    go(std::integral_constant<int, 4>{});
-  else
-    go(std::integral_constant<int, 1>{});
+  if (N > kSampWideN) return go(std::integral_constant<int, 4>{});
+  return go(std::integral_constant<int, 1>{});
 }
 
 }  // namespace ccmpc
@@ -196,9 +194,10 @@ extern "C" int ccmpc_sample_unicycle_ex(const double *init_state, const double *
   const int L = static_cast<int>(n_latent), Ti = static_cast<int>(T);
   const float fdt = static_cast<float>(dt);
   const uint32_t base = static_cast<uint32_t>(ov_base);
+  hipError_t attr = hipSuccess;
 #define CCMPC_SAMPLER(PP, ZIN, EPSIN)                                                        \
-  launch_sampler<PP, ZIN, EPSIN>(n_ov, s, init_state, latent_cdf, L, gmm, z_in, eps_in, N, Ti, \
-                                 fdt, seed, seed_dev, base, out_z, out_pos, ld)
+  attr = launch_sampler<PP, ZIN, EPSIN>(n_ov, s, init_state, latent_cdf, L, gmm, z_in, eps_in, \
+                                        N, Ti, fdt, seed, seed_dev, base, out_z, out_pos, ld)
   const int mode = (pp ? 4 : 0) | (z_in ? 2 : 0) | (eps_in ? 1 : 0);
   switch (mode) {
     case 0: CCMPC_SAMPLER(false, false, false); break;
@@ -209,6 +208,11 @@ extern "C" int ccmpc_sample_unicycle_ex(const double *init_state, const double *
     default: CCMPC_SAMPLER(true, true, true); break;
   }
 #undef CCMPC_SAMPLER
+  if (attr != hipSuccess) {
+    set_error(std::string(__func__) + ": hipFuncSetAttribute(MaxDynamicSharedMemorySize) "
+              "failed: " + hipGetErrorString(attr));
+    return CCMPC_ERR_LAUNCH;
+  }
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

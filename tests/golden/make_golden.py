@@ -33,8 +33,33 @@ REF_MC = "/root/reference/collect/in_simulation/midlevel/v8ideal/makeconstraint.
 
 REF_MID = "/root/reference/collect/in_simulation/midlevel"
 
+# The reference files whose code this script executes, pinned by content: regenerating the
+# fixtures from a changed (untrusted) file fails before anything in it runs.
+REF_SHA256 = {
+    "v8ideal/__init__.py": "779778706a79bea299910e094563eb22a806d35e1614749b74bff54c6e91e807",
+    "v8ideal/makeconstraint.py": "36f6fa8528041c6757a1f94f671ae8bcb49ec3fcae36595b063cb03e30e7d910",
+    "ovehicle.py": "903dc28df8c0a79f70fabeb15e195005027f889f99478fb0ea3111330f162bb2",
+    "util.py": "6f6cccf4de49c17f229b171180b2c0a9589791b10554ed955a310b1d4280016f",
+}
+
+
+def check_reference_file(path):
+    import hashlib
+    rel = os.path.relpath(path, REF_MID)
+    want = REF_SHA256.get(rel)
+    got = hashlib.sha256(open(path, "rb").read()).hexdigest()
+    if want is None or got != want:
+        raise RuntimeError(f"{path}: sha256 {got} is not the pinned {want}; refusing to execute")
+
+
+# What the executed method bodies may touch of `os`: path joining only (save_moments /
+# predict_ideal build their pickle paths with it, :2613, :2627); no filesystem or process calls.
+SAFE_OS = __import__("types").SimpleNamespace(
+    path=__import__("types").SimpleNamespace(join=os.path.join))
+
 
 def load_reference():
+    check_reference_file(REF_MC)
     spec = importlib.util.spec_from_file_location("ref_makeconstraint", REF_MC)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
@@ -47,6 +72,7 @@ def reference_function(path, name, cls=None, namespace=None):
     source is taken from the file's syntax tree unchanged (decorators dropped, so a classmethod
     takes its class as a plain first argument) and executed in `namespace`."""
     import ast
+    check_reference_file(path)
     tree = ast.parse(open(path).read(), filename=path)
     body = tree.body
     if cls is not None:
@@ -436,7 +462,7 @@ def pin_predict_ideal(rng):
     np_proxy = types.ModuleType("numpy_injected")
     np_proxy.__dict__.update({k: getattr(np, k) for k in dir(np) if not k.startswith("__")})
     np_proxy.random = fake_random
-    ns = {"np": np_proxy, "os": os, "logging": logging, "open": lambda *a, **k: _FakeFile(),
+    ns = {"np": np_proxy, "os": SAFE_OS, "logging": logging, "open": lambda *a, **k: _FakeFile(),
           "pickle": types.SimpleNamespace(load=lambda f: mom)}
     predict_ideal = reference_function(os.path.join(REF_MID, "v8ideal", "__init__.py"),
                                        "predict_ideal", cls="MidlevelAgent", namespace=ns)
@@ -521,7 +547,7 @@ def reference_generators():
     path = os.path.join(REF_MID, "v8ideal", "__init__.py")
     ns = {"np": np, "scipy": scipy_mod(), "linalg": scipy.linalg, "norm": scipy.stats.norm,
           "makeconstraint": load_reference(), "cp": _recording_cp(), "logging": logging,
-          "copy": copy, "os": os}
+          "copy": copy, "os": SAFE_OS}
     saved = {}
 
     class _File:
