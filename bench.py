@@ -620,6 +620,7 @@ def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8, per_particle=F
     n_cons = len(out[0])
     g = next(iter(agent._graphs.values()))
     t_graph = time_graph_replay(g, dev)
+    t_graph_l4 = time_graph_replay(g, dev, with_l4=True)
 
     eager = planner.MidlevelAgent(prediction_horizon=ph, device=dev)
 
@@ -652,11 +653,15 @@ def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8, per_particle=F
            "dropin_step_us_median": round(med * 1e6, 1),
            "dropin_step_us_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
            "graph_replay_us": round(t_graph * 1e6, 1),
+           "graph_replay_with_l4_us": round(t_graph_l4 * 1e6, 1),
            "eager_calls_step_us_median": round(statistics.median(te) * 1e6, 1),
            "note": "wall clock per call on the host, host inputs from host memory (per-particle "
                    "tensors: device-to-device copies inside the step), outputs (records, "
-                   "moments, L4, statistics) on the host when it returns; graph_replay_us = "
-                   "HIP events around back-to-back replays (packed H2D + kernels + packed D2H)"}
+                   "moments, statistics) on the host when it returns, the L4 outputs read on "
+                   "access from a second graph on a side stream; graph_replay_us = HIP events "
+                   "around back-to-back replays of the record path (packed H2D + sampler + "
+                   "bucketing + cycle + packed D2H), graph_replay_with_l4_us the same with the "
+                   "L4 graph after each"}
     if with_cpu:
         from oracle import ccmpc_oracle as orc
         s = sampler_of(7)
@@ -681,15 +686,30 @@ def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8, per_particle=F
     return res
 
 
-def time_graph_replay(g, dev, n=200):
-    """HIP-event time per replay of a captured step graph, back to back."""
+def time_graph_replay(g, dev, n=200, with_l4=False):
+    """HIP-event time per replay of a captured step's record-path graph (A), back to back; with
+    with_l4, per step of A then the L4 graph (B) on the side stream, as launch() orders them
+    (the next A waits for B: it rewrites the store B reads)."""
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(10):
+    main = torch.cuda.current_stream(dev)
+
+    def one():
+        if with_l4:
+            main.wait_stream(g.side)
         g.graph.replay()
+        if with_l4:
+            g.side.wait_stream(main)
+            with torch.cuda.stream(g.side):
+                g.graph_l4.replay()
+
+    for _ in range(10):
+        one()
     torch.cuda.synchronize(dev)
     ev0.record()
     for _ in range(n):
-        g.graph.replay()
+        one()
+    if with_l4:
+        main.wait_stream(g.side)
     ev1.record()
     ev1.synchronize()
     return ev0.elapsed_time(ev1) * 1e-3 / n

@@ -70,6 +70,9 @@ SIGNATURES = {
     "ccmpc_ideal_minkowski_cycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P, _U64,
                                                    _P, _P, _SZ, _P, _P, _P, _D, _D, _I32, _P,
                                                    _P, _P, _P, _P, _P]),
+    "ccmpc_ideal_minkowski_cycle_ex": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _P,
+                                                      _U64, _P, _P, _P, _SZ, _P, _P, _P, _D, _D,
+                                                      _I32, _P, _P, _P, _P, _P, _P]),
     "ccmpc_sample_unicycle": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _D, _U64, _I64,
                                              _P, _P, _I64, _P]),
     "ccmpc_sample_unicycle_ex": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P, _P, _I64, _I64, _I64,

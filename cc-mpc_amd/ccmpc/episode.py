@@ -11,8 +11,9 @@ chance constraints:
 
 The CARLA world and the learned Trajectron++ encoder/decoder are outside this path; the replay
 feeds the GPU sampler synthetic per-OV GMM action parameters (SURVEY.md 8d generator) and times
-each planning step end to end (sampler -> bucketing -> one fused launch -> host HalfSpace
-objects -> the QP on the device records, do_highlevel_control :2850-3110).  The ego is not
+each planning step end to end (one step-graph replay: sampler -> bucketing -> the generator's
+fused launch, then the host HalfSpace objects -> the QP on the device records,
+do_highlevel_control :2850-3110).  The ego is not
 simulated: each step plans from a synthetic state on the reference trajectory, and the
 shrinking steps pass the first control of every earlier step as the executed controls
 (U_prev, :3186).  An infeasible QP is logged (the reference raises InSimulationException and
@@ -108,25 +109,42 @@ class EpisodeReplay:
         steps += [(10 * (self.ph + r), self.ph, "affine") for r in range(self.receding_steps)]
         return steps
 
-    def step(self, frame, T, kind):
-        ovs = self.predict(frame)
-        K = [ov.n_states for ov in ovs]
+    def sampler(self, frame):
+        """The frame's sampler-boundary inputs (seed keyed by the frame)."""
+        return dict(init_state=self.init, latent_pmf=self.pmf, gmm=self.gmm, N=self.N,
+                    seed=self.seed * 7919 + frame)
+
+    def step(self, frame, T, kind, eager=False):
+        """One planning step: do_prediction + make_ovehicles + the schedule's generator as a
+        step-graph replay (MidlevelAgent.predict_and_constrain / _affine), or (eager) the
+        separate calls -- the GPU sampler, the bucketing, then the generator method on the
+        OVehicles -- which give the same bits."""
+        if eager:
+            ovs = self.predict(frame)
+            K = [ov.n_states for ov in ovs]
+        else:
+            K = (self.pmf > 0.1).sum(1).tolist()
         eps = np.zeros((self.O, max(K)))
         eps[:, :] = 0.05 / self.O                    # eps_ura (v8ideal/__init__.py:2920-2926)
         params = Params(self.O, K, frame)
+        ref = self.ref_traj(frame)
+        if not eager:
+            fn = (self.agent.predict_and_constrain if kind == "minkowski"
+                  else self.agent.predict_and_constrain_affine)
+            return fn(params, self.sampler(frame), eps, T, ref, self.minpos, self.pasts)
         gen = (self.agent.compute_obstacle_constraints_GMM_Minkowski_idealprediction
                if kind == "minkowski" else self.agent.compute_obstacle_constraints_GMM_affine)
-        out = gen(params, ovs, None, None, None, eps, None, T, self.ref_traj(frame))
+        out = gen(params, ovs, None, None, None, eps, None, T, ref)
         return ovs, out
 
-    def run(self, sync=True):
+    def run(self, sync=True, eager=False):
         """Runs the whole schedule; returns one record per planning step."""
         log = []
         for frame, T, kind in self.schedule():
             if sync:
                 torch.cuda.synchronize(self.device)
             t0 = time.perf_counter()
-            ovs, out = self.step(frame, T, kind)
+            ovs, out = self.step(frame, T, kind, eager=eager)
             if sync:
                 torch.cuda.synchronize(self.device)
             t1 = time.perf_counter()

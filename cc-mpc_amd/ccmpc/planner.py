@@ -35,6 +35,9 @@ from . import engine, mpc, risk
 from .ovehicle import OVehicle, ScenePredictions
 
 
+_STEP_DEBUG = os.environ.get("CCMPC_STEP_DEBUG", "0") == "1"
+
+
 class InSimulationException(Exception):
     """collect/exception.py:11: the planner's failure (an infeasible QP, :3099-3110)."""
 
@@ -211,6 +214,36 @@ class UnionGrid:
                         return grid._arr[grid._first[ov] + k, t]
                 return _O()
         return _K()
+
+
+class _LazyL4:
+    """One step graph launch's L4 outputs (graph B), fetched on first use."""
+
+    def __init__(self, graph, generation):
+        self._g, self._gen, self._v = graph, generation, None
+
+    def get(self):
+        if self._v is None:
+            self._v = self._g.l4_outputs(self._gen)
+        return self._v
+
+
+class _LazyCol:
+    """A field (or one column of it) of a _LazyL4, indexed like the array it resolves to."""
+
+    def __init__(self, l4, name, col):
+        self._l4, self._name, self._col = l4, name, col
+
+    def _arr(self):
+        a = self._l4.get()[self._name]
+        return a if self._col is None else a[:, self._col]
+
+    def __getitem__(self, idx):
+        return self._arr()[idx]
+
+    def __array__(self, dtype=None, copy=None):
+        a = self._arr()
+        return a if dtype is None else a.astype(dtype)
 
 
 def _match_modes(mean_loaded, x_init, cur_means, n_states, M_big):
@@ -751,17 +784,7 @@ class MidlevelAgent:
 
     def _src_cells(self, prev_K, K):
         """data_idx fallback (:2648-2656): mode k reads saved mode k, or the last saved slot."""
-        maxK_prev = max(prev_K)
-        src, c0 = [], 0
-        starts = np.concatenate([[0], np.cumsum(prev_K)[:-1]])
-        for o, k_o in enumerate(K):
-            for k in range(k_o):
-                d = k if k < maxK_prev else max(maxK_prev - 1, 0)
-                if d >= prev_K[o]:
-                    raise ValueError(f"saved moments of OV {o} have no mode {d} (the reference "
-                                     "reads None there and fails)")
-                src.append(int(starts[o] + d))
-        return torch.as_tensor(np.asarray(src, np.int32), device=self.device)
+        return torch.as_tensor(self._src_cells_host(prev_K, K), device=self.device)
 
     def _records_to_halfspaces(self, h, scene, T):
         return HalfSpaceList(h, scene.cell_of, T * (T - 1) // 2)
@@ -930,9 +953,9 @@ class MidlevelAgent:
     def predict_and_constrain(self, params, sampler, eps_ura, Tsh, ref_traj, minpos, pasts,
                               bboxes=None, filter_pmf=0.1):
         """One planning frame's prediction + Minkowski constraint generation, as
-        do_highlevel_control runs them (v8ideal/__init__.py:2934-2976): do_prediction
-        (:414-467, the sampler tail of prediction.py:81-86), make_ovehicles (:469-505) and
-        compute_obstacle_constraints_GMM_Minkowski_idealprediction (:781-964).
+        do_highlevel_control runs them on the shrinking horizon (v8ideal/__init__.py:2934-2952):
+        do_prediction (:414-467, the sampler tail of prediction.py:81-86), make_ovehicles
+        (:469-505) and compute_obstacle_constraints_GMM_Minkowski_idealprediction (:781-964).
 
         sampler: the sampler tail's inputs, in one of two forms --
           per-latent (synthetic): dict(init_state (O, 4), latent_pmf (O, L), gmm (O, L, ph, 5),
@@ -942,17 +965,70 @@ class MidlevelAgent:
               (O, N, ph, 2) or None, N, seed, per_particle=True), gmm / z / eps DEVICE tensors
               as p_y_xz and sample_p leave them (no host round trip); seed keys the noise
               when eps is None.
-        At Tsh == ph the whole chain is ONE hipGraph replay (ccmpc.step.MinkowskiStepGraph,
-        cached per shape and sampler mode in an LRU of `max_graphs`): inputs up in one copy (the
-        per-particle tensors by device copies into the graph's buffers), the sampler +
-        bucketing + cycle + L4 kernels, outputs down in one copy, then the 9-tuple over host
-        views (constraints built lazily).  Below ph the generator runs on the saved moments'
-        ideal rollout, after the same sampler and bucketing calls.  Returns (ovehicles,
-        9-tuple).  The 9-tuple's arrays are host copies; the OVehicles' device-backed fields
-        (pred_positions, pred_yaws, vertices) must be read before the next graph step of the
-        same shape -- after it they raise (ScenePredictions.check_live)."""
-        from . import ovehicle, step
+        Every step is a hipGraph replay (ccmpc.step.StepGraph, cached per shape and sampler
+        mode in an LRU of `max_graphs`): inputs up in one copy (the per-particle tensors by
+        device copies into the graph's buffers), the sampler + bucketing + generator kernels,
+        the records / moments down in one copy, then the 9-tuple over host views (constraints
+        built lazily).  At Tsh == ph the generator is the one-launch Minkowski cycle; below ph
+        the 1e6-sample ideal rollout of the saved moments (predict_ideal, :2620-2711) fused with
+        its moments and half-spaces, beside the sampled scene's moments (the t = 0 statistics).
+        The L4 outputs (vertices / A_union / b_union, the heading statistics) come from a
+        second graph on a side stream and are read on access.  Returns (ovehicles, 9-tuple);
+        the OVehicles' device-backed fields (pred_positions, pred_yaws, vertices) must be read
+        before the next step of the same shape -- after it they raise
+        (ScenePredictions.check_live)."""
         T, ph = int(Tsh), self.prediction_horizon
+        kind = "minkowski" if T == ph else "ideal"
+        ovs, g, o, scene, K = self._graph_step(kind, params, sampler, eps_ura, T, ref_traj,
+                                               minpos, pasts, bboxes, filter_pmf)
+        h = o["rec"].reshape(-1).view(engine._lib.HALFSPACE_DTYPE).reshape(g.C, g.P)
+        if kind == "ideal":
+            st = o["status"]
+            if st.any():
+                raise np.linalg.LinAlgError(f"predict_ideal: conditional covariance not PD in "
+                                            f"cells {np.nonzero(st)[0].tolist()}")
+            self._moments[params.frame] = (o["imean"], o["icov"], list(K), T)   # :960
+        else:
+            self._moments[params.frame] = (o["mean"], o["cov"], list(K), T)     # :960
+            self.prob_lower_save = list(o["pl"][-1])          # last cell wins (:947, :961)
+        P = T * (T - 1) // 2
+        constraints = HalfSpaceList(h, scene.cell_of, P)
+        self.last_records = h[:, :P]
+        self._last_rec = (g.out.d("rec"), mpc.REC_HALFSPACE, T)
+        return ovs, self._step_tuple(g, o, scene, K, 0, constraints=constraints)
+
+    def predict_and_constrain_affine(self, params, sampler, eps_ura, Tsh, ref_traj, minpos,
+                                     pasts, bboxes=None, filter_pmf=0.1):
+        """The receding-horizon frame (do_highlevel_control :2954-2976): do_prediction +
+        make_ovehicles + compute_obstacle_constraints_GMM_affine (:1378-1539) as one graph
+        replay (sampler -> bucketing -> moments -> GMM-affine), the L4 graph beside it.
+        Arguments and result as predict_and_constrain."""
+        T = int(Tsh)
+        if T != self.prediction_horizon:
+            raise ValueError("the affine generator runs on the prediction horizon's particles")
+        ovs, g, o, scene, K = self._graph_step("affine", params, sampler, eps_ura, T, ref_traj,
+                                               minpos, pasts, bboxes, filter_pmf)
+        h = o["rec"].reshape(-1).view(engine._lib.AFFINE_DTYPE).reshape(g.C, T)
+        self.last_records = h
+        self._last_rec = (g.out.d("rec"), mpc.REC_AFFINE, T)
+        st = h["status"]
+        if st.any():
+            c, t = divmod(int(np.flatnonzero(st.reshape(-1))[0]), T)
+            ov, k = scene.cell_of[c]
+            raise engine._lib.record_error(h[c, t]["status"],
+                                           f"affine constraint (ov={ov}, k={k}, t={t})")
+        cons = [HalfSpace(ov, k, t, -1, np.array([r["n0"], r["n1"]]), float(r["d"]),
+                          float(r["rhs"]), int(r["side"]), int(r["which"]), float(r["margin"]))
+                for c, (ov, k) in enumerate(scene.cell_of) for t, r in enumerate(h[c])]
+        out = self._step_tuple(g, o, scene, K, 0, constraints=cons, ov_constraint=False)
+        return ovs, out
+
+    def _graph_step(self, kind, params, sampler, eps_ura, T, ref_traj, minpos, pasts, bboxes,
+                    filter_pmf):
+        """Inputs -> the cached StepGraph of this shape -> replay -> wait -> one snapshot of the
+        record-path outputs.  Returns (ovehicles, graph, outputs, scene, K)."""
+        from . import ovehicle, step
+        ph = self.prediction_horizon
         init = np.asarray(sampler["init_state"], np.float64)
         pmf = np.asarray(sampler["latent_pmf"], np.float64)
         O, L = pmf.shape
@@ -962,66 +1038,94 @@ class MidlevelAgent:
         z_in, eps_in = sampler.get("z"), sampler.get("eps")
         if pp and z_in is None:
             raise ValueError("per-particle GMM parameters need the injected z (prediction.py:103)")
+        if not pp and (z_in is not None or eps_in is not None):
+            raise ValueError("injected z / eps go with per_particle=True at the graph step")
         pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
         past_last = np.array([p[-1] for p in pasts])
         bboxes = (_default_bboxes(O) if bboxes is None
                   else np.asarray(bboxes, np.float64).reshape(O, 2))
-        if T != ph:
-            z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=seed,
-                                              device=self.device, z=z_in, eps=eps_in,
-                                              per_particle=pp)
-            ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, bboxes,
-                                          filter_pmf=filter_pmf, device=self.device)
-            out = self.compute_obstacle_constraints_GMM_Minkowski_idealprediction(
-                params, ovs, None, None, None, eps_ura, None, T, ref_traj)
-            return ovs, out
-        if not pp and (z_in is not None or eps_in is not None):
-            raise ValueError("injected z / eps go with per_particle=True at the graph step")
         K = (pmf > filter_pmf).sum(1).tolist()
         if min(K) == 0:
             raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent "
                              f"mode with p(z|x) > {filter_pmf} (ovehicle.py:96-97)")
-        key = (O, N, ph, L, tuple(K), pp, eps_in is not None)
+        prev = None
+        extra = {}
+        if kind == "ideal":
+            prev = self._moments.get(params.frame - self.record_interval)
+            if prev is None:
+                raise KeyError(f"no moments saved for frame {params.frame - self.record_interval}"
+                               " (the reference fails to load its pickle here)")
+            extra = dict(prev_K=tuple(prev[2]), T_src=int(prev[3]), n_ideal=self.n_ideal)
+        key = (kind, O, N, ph, T, L, tuple(K), pp, eps_in is not None) + tuple(
+            sorted(extra.items()))
         g = self._graphs.pop(key, None)
         if g is None:
-            g = step.MinkowskiStepGraph(O, N, ph, L, K, device=self.device, R=self.R,
-                                        per_particle=pp, eps_in=eps_in is not None)
-            while len(self._graphs) >= self.max_graphs:
+            g = step.StepGraph(O, N, ph, L, K, device=self.device, R=self.R, per_particle=pp,
+                               eps_in=eps_in is not None, kind=kind, T=T, **extra)
+            while self._graphs and len(self._graphs) >= self.max_graphs:
                 self._graphs.popitem(last=False)           # least recently used
         self._graphs[key] = g                              # most recently used
         g.set_inputs(seed, init, pmf, None if pp else gmm, minpos, ref_traj,
                      self._cell_risk_host(np.asarray(eps_ura), K), past_last, bboxes,
                      filter_pmf=filter_pmf)
+        if kind == "ideal":
+            src = self._src_cells_host(prev[2], K)
+            g.set_ideal_inputs(prev[0], prev[1], src,
+                               (self.seed * 1_000_003 + int(params.frame)) & (2**63 - 1))
         if pp:
             g.set_device_inputs(gmm, z_in, eps_in)
+        if _STEP_DEBUG:
+            print(f"[ccmpc step] frame {params.frame} kind {kind} T {T} K {K} key {key} "
+                  f"graphs {len(self._graphs)} gen {g.generation}", flush=True)
         g.launch()
         # host objects that need no output are built while the graph runs
         st = g.store
         scene = ovehicle.ScenePredictions(st, K, past_last, bboxes)
         scene.bind_generation(g)
         ovs = [ovehicle.OVehicle(scene, j, past=pasts[j]) for j in range(O)]
-        vertices, direct = LazyVertices(scene, ph), _object_grid(O)
         g.wait()
-        o = g.out.snapshot()            # every output in one host copy (outlives the replay)
+        o = g.out.snapshot()            # the record path's outputs in one host copy
         ovehicle.check_kept_modes_drawn(o["centre"], K)
         st.counts = o["cnt"].tolist()
         st.offsets = o["off"].tolist()
         scene.cell_pmf, scene.init_center = o["pmf"], o["centre"]
-        h = o["rec"].reshape(-1).view(engine._lib.HALFSPACE_DTYPE).reshape(g.C, g.P)
-        constraints = HalfSpaceList(h, scene.cell_of, T * (T - 1) // 2)
-        self.last_records = h
-        self._last_rec = (g.out.d("rec"), mpc.REC_HALFSPACE, T)
-        mean, cov = o["mean"], o["cov"]
-        self._moments[params.frame] = (mean, cov, list(K), T)     # save_moments (:960)
-        self.prob_lower_save = list(o["pl"][-1])                  # last cell wins (:947, :961)
-        mean0, cov0 = mean[:, 0, :], cov[:, 0:2, 0:2]
-        st_mean, st_cov = self._state_stats(scene, mean0, cov0,
-                                            (o["yaw_mean"][:, 0], o["yaw0_var"]))
+        return ovs, g, o, scene, K
+
+    def _step_tuple(self, g, o, scene, K, mean_tangent, constraints=None, ov_constraint=None):
+        """The generator's 9-tuple over one step's outputs; vertices, A_union / b_union and the
+        heading part of the state statistics read graph B's L4 outputs on access."""
+        ph = self.prediction_horizon
+        if constraints is None:
+            constraints = HalfSpaceList(o["rec"].reshape(-1).view(engine._lib.HALFSPACE_DTYPE)
+                                        .reshape(g.C, g.P), scene.cell_of, g.T * (g.T - 1) // 2)
+        gen = g.generation
+        l4 = _LazyL4(g, gen)
+        mean0, cov0 = o["mean"][:, 0, :], o["cov"][:, 0:2, 0:2]
         first = _first_cells(tuple(K))
-        out = (constraints, vertices, UnionGrid(o["A"], K, ph, first),
-               UnionGrid(o["b"], K, ph, first),
-               self._ov_in_junction(scene, mean0), direct, st_mean, st_cov, 0)
-        return ovs, out
+        K = list(K)
+        st_mean = (CellGrid(mean0[:, 0], K, first), CellGrid(mean0[:, 1], K, first),
+                   CellGrid(_LazyCol(l4, "yaw_mean", 0), K, first))
+        st_cov = (CellGrid(cov0[:, 0, 0], K, first), CellGrid(cov0[:, 1, 1], K, first),
+                  CellGrid(_LazyCol(l4, "yaw0_var", None), K, first))
+        occ = self._ov_in_junction(scene, mean0) if ov_constraint is None else ov_constraint
+        return (constraints, LazyVertices(scene, ph), UnionGrid(_LazyCol(l4, "A", None), K, ph,
+                                                                first),
+                UnionGrid(_LazyCol(l4, "b", None), K, ph, first), occ, _object_grid(scene.O),
+                st_mean, st_cov, mean_tangent)
+
+    def _src_cells_host(self, prev_K, K):
+        """_src_cells as a host int32 array."""
+        maxK_prev = max(prev_K)
+        starts = np.concatenate([[0], np.cumsum(prev_K)[:-1]])
+        src = []
+        for o, k_o in enumerate(K):
+            for k in range(k_o):
+                d = k if k < maxK_prev else max(maxK_prev - 1, 0)
+                if d >= prev_K[o]:
+                    raise ValueError(f"saved moments of OV {o} have no mode {d} (the reference "
+                                     "reads None there and fails)")
+                src.append(int(starts[o] + d))
+        return np.asarray(src, np.int32)
 
     def compute_prediction_controls(self, frame, Tsh, shrinking, sampler, minpos, pasts, x_init,
                                     goal, ref_traj, bboxes=None, apply_robust=True):
@@ -1044,7 +1148,7 @@ class MidlevelAgent:
         python-utility is absent, restated), timeout False (the QP has no time limit here).
         Raises InSimulationException where the reference's CPLEX solve fails (:3099-3110).  The
         frame's 9-tuple and QP result stay on the agent (last_generator_output, last_ctrl)."""
-        from . import episode, ovehicle
+        from . import episode
         T, ph = int(Tsh), self.prediction_horizon
         pmf = np.asarray(sampler["latent_pmf"], np.float64)
         O = pmf.shape[0]
@@ -1059,19 +1163,12 @@ class MidlevelAgent:
             ovs, out = self.predict_and_constrain(params, sampler, eps_ura, T, ref_traj, minpos,
                                                   pasts, bboxes, filter_pmf=fp)
         else:
-            pp = bool(sampler.get("per_particle", False))
-            z, store = engine.sample_unicycle(
-                sampler["init_state"], pmf, sampler["gmm"], int(sampler["N"]), ph,
-                seed=int(sampler["seed"]), device=self.device, z=sampler.get("z"),
-                eps=sampler.get("eps"), per_particle=pp)
-            ovs = ovehicle.make_ovehicles(store, z, pmf, minpos, pasts, bboxes,
-                                          filter_pmf=fp, device=self.device)
-            K = [ov.n_states for ov in ovs]
+            K = (pmf > fp).sum(1).tolist()
             eps_ura = np.full((O, max(K)), 0.05 / O)
             params = episode.Params(O, K, frame)
             params.x_init = np.asarray(x_init, np.float64)
-            out = self.compute_obstacle_constraints_GMM_affine(
-                params, ovs, None, None, None, eps_ura, None, T, ref_traj)
+            ovs, out = self.predict_and_constrain_affine(params, sampler, eps_ura, T, ref_traj,
+                                                         minpos, pasts, bboxes, filter_pmf=fp)
         self.last_generator_output = (ovs, out)
         up = np.concatenate(self._u_prev) if (T < ph and self._u_prev) else None
         ctrl = self.solve_planning_qp(x_init, goal, ref_traj, T, u_prev=up, lon=self.ego_lon)

@@ -1,26 +1,33 @@
-"""One planning step of v8ideal's prediction + constraint path as ONE hipGraph replay.
+"""One planning step of v8ideal's prediction + constraint path as hipGraph replays.
 
-Per planning frame the reference runs (v8ideal/__init__.py:2934-2976 -> :414-505, :781-964):
+Per planning frame the reference runs (v8ideal/__init__.py:2934-2976 -> :414-505, :781-964,
+:1378-1539):
 
     do_prediction       Trajectron++ sample (prediction.py:81-86)
     make_ovehicles      bucketing by latent mode (:469-505, ovehicle.py:24-117)
-    generator           compute_obstacle_constraints_GMM_Minkowski_idealprediction at Tsh == ph
-                        (moments -> MVOE half-spaces, vertices / L4, t = 0 state statistics)
+    generator           compute_obstacle_constraints_GMM_Minkowski_idealprediction (shrinking,
+                        robust) or compute_obstacle_constraints_GMM_affine (receding): the
+                        half-spaces, vertices / L4 and the t = 0 state statistics
 
-For a fixed shape (OVs, particles, horizon, latent count and kept modes per OV) the whole chain
-is five kernels that need nothing from the host between them: the sampler, the bucketing, the
-one-launch Minkowski cycle and the L4 kernel read the bucketed cell counts on the device.  So
-``MinkowskiStepGraph`` captures
+For a fixed shape (OVs, particles, horizon, latent count, kept modes per OV and, below ph, the
+saved moments' cells) every stage is a kernel that needs nothing from the host between them:
+the sampler, the bucketing, the moment / half-space kernels and the L4 kernel read the bucketed
+cell counts on the device.  ``StepGraph`` captures, per kind,
 
-    packed H2D of the step's host inputs  ->  sampler  ->  bucketing  ->  { cycle | L4 }
-    ->  packed D2H of every output the 9-tuple needs
+    minkowski (T == ph)  copy-in -> sampler -> bucketing -> Minkowski cycle -> copy-out
+    ideal     (T <  ph)  copy-in -> { ideal rollout + moments + half-spaces on the saved
+                         moments (predict_ideal, :824-825) | sampler -> bucketing -> the scene's
+                         moments (the t = 0 statistics, :864-875) } -> copy-out
+    affine    (T == ph)  copy-in -> sampler -> bucketing -> moments -> GMM-affine -> copy-out
 
-(the cycle and the L4 kernel are parallel branches of the graph: both only read the bucketed
-store)
+as graph A, and the L4 outer approximation (vertices / A_union / b_union and the heading
+statistics, :627-736) as graph B, replayed on a side stream after A.  The host waits for A
+only: the records, moments and counts come back without waiting on L4, whose outputs (only
+returned by the generator, never fed to the QP, :951-952) are read lazily.
 
-into one graph.  A step is: write the inputs into pinned memory, replay, wait for the stream,
-read the outputs through zero-copy NumPy views.  The Philox seed travels in the packed inputs
-(ccmpc_sample_unicycle_ex's seed_dev), so every replay draws a fresh particle set.
+A step is: write the inputs into pinned memory, replay, wait, read the outputs through NumPy
+views of one snapshot.  The Philox seeds travel in the packed inputs (ccmpc_sample_unicycle_ex
+and ccmpc_ideal_minkowski_cycle_ex read them on the device), so every replay draws afresh.
 
 Outputs live in the graph's buffers until the next replay of the same graph; what the caller
 keeps across steps (the saved moments) is copied out.
@@ -75,15 +82,17 @@ class Pack:
         return {name: nd(shape, dt, raw, off) for name, shape, dt, off in self._views}
 
 
-class MinkowskiStepGraph:
-    """Sampler -> bucketing -> Minkowski cycle -> L4 for a fixed shape, as one hipGraph.
+class StepGraph:
+    """Sampler -> bucketing -> the step's generator kernels (graph A) and L4 (graph B) for one
+    shape.
 
-    O OVs with N particles each over T = ph steps; L latent values; K kept modes per OV (the
-    host decides them from p(z|x), as make_ovehicles does, so the shape is known before the
-    step runs).
+    O OVs with N particles each over ph steps; L latent values; K kept modes per OV (the host
+    decides them from p(z|x), as make_ovehicles does, so the shape is known before the step
+    runs).  kind: "minkowski" (T == ph), "ideal" (T < ph, on the saved moments of prev_K cells
+    over T_src steps, n_ideal rollout samples per cell) or "affine" (T == ph).
 
     Two sampler modes:
-      per_particle=False  gmm (O, L, T, 5) per-latent parameters, z and the noise drawn by
+      per_particle=False  gmm (O, L, ph, 5) per-latent parameters, z and the noise drawn by
                           Philox on the device (the synthetic mode); gmm travels in the packed
                           host inputs.
       per_particle=True   the boundary Trajectron++ hands over on the GPU (prediction.py:81-86):
@@ -96,11 +105,18 @@ class MinkowskiStepGraph:
     ``generation`` counts launches: objects built over this graph's buffers (ScenePredictions)
     record the generation they belong to and refuse reads after a later replay."""
 
-    def __init__(self, O, N, T, L, K, device="cuda", dt=0.5, R=risk.R_COLLISION, tol=1e-8,
-                 maxiter=1000, per_particle=False, eps_in=False):
+    def __init__(self, O, N, ph, L, K, device="cuda", dt=0.5, R=risk.R_COLLISION, tol=1e-8,
+                 maxiter=1000, per_particle=False, eps_in=False, kind="minkowski", T=None,
+                 prev_K=None, T_src=None, n_ideal=1_000_000):
         self.device = engine.require_device(device)
         lib = _lib.load()
-        self.O, self.N, self.T, self.L = int(O), int(N), int(T), int(L)
+        if kind not in ("minkowski", "ideal", "affine"):
+            raise ValueError(f"unknown step kind {kind!r}")
+        self.kind = kind
+        self.O, self.N, self.ph, self.L = int(O), int(N), int(ph), int(L)
+        self.T = T = int(T if T is not None else ph)
+        if (kind == "ideal") != (T < self.ph) or not 1 <= T <= self.ph:
+            raise ValueError(f"kind {kind!r} with T = {T}, ph = {self.ph}")
         self.K = [int(k) for k in K]
         if len(self.K) != self.O or min(self.K) < 1:
             raise ValueError("K must give >= 1 kept mode for each OV")
@@ -113,28 +129,47 @@ class MinkowskiStepGraph:
             raise ValueError("eps_in is part of the per-particle (Trajectron++ boundary) mode")
         self.generation = 0
         f64, f32, i32, i64, u8 = torch.float64, torch.float32, torch.int32, torch.int64, torch.uint8
-        gmm_field = [] if self.per_particle else [("gmm", (O, L, T, 5), f32)]
-        self.inp = Pack([("seed", (1,), i64), ("init", (O, 4), f64), ("cdf", (O, L), f64)]
-                        + gmm_field +
-                        [("keep", (O, L), i32), ("nk", (O,), i32),
-                         ("base", (O,), i32), ("minpos", (O, 2), f64), ("region", (O,), i64),
-                         ("origin", (C, 2), f64), ("ref", (1, T, 2), f64), ("risk", (C, 3), f64),
-                         ("past", (C, 2), f64), ("bbox", (C, 2), f64)], self.device)
+        ph_, L_ = self.ph, self.L
+        gmm_field = [] if self.per_particle else [("gmm", (O, L_, ph_, 5), f32)]
+        fields = ([("seed", (1,), i64), ("init", (O, 4), f64), ("cdf", (O, L_), f64)] + gmm_field +
+                  [("keep", (O, L_), i32), ("nk", (O,), i32), ("base", (O,), i32),
+                   ("minpos", (O, 2), f64), ("region", (O,), i64), ("origin", (C, 2), f64),
+                   ("ref", (1, T, 2), f64), ("past", (C, 2), f64), ("bbox", (C, 2), f64)])
+        fields += [("gamma", (C,), f64)] if kind == "affine" else [("risk", (C, 3), f64)]
+        if kind == "ideal":
+            self.prev_K = [int(k) for k in prev_K]
+            self.T_src = int(T_src if T_src is not None else T + 1)
+            if not T < self.T_src <= 40:
+                raise ValueError(f"saved moments over T_src = {self.T_src} steps cannot roll "
+                                 f"out T = {T}")
+            self.n_ideal = int(n_ideal)
+            Cp, Ts = sum(self.prev_K), self.T_src
+            fields += [("iseed", (1,), i64), ("src", (C,), i32), ("pmean", (Cp, Ts, 2), f64),
+                       ("pcov", (Cp, 2 * Ts, 2 * Ts), f64)]
+        self.inp = Pack(fields, self.device)
         self.pp_gmm = self.pp_z = self.pp_eps = None
         if self.per_particle:       # device-side inputs (particle-minor, the sampler's layout)
-            self.pp_gmm = torch.zeros((O, T, 5, N), dtype=f32, device=self.device)
+            self.pp_gmm = torch.zeros((O, ph_, 5, N), dtype=f32, device=self.device)
             self.pp_z = torch.zeros((O, N), dtype=i32, device=self.device)
             if self.eps_in:
-                self.pp_eps = torch.zeros((O, T, 2, N), dtype=f32, device=self.device)
-        self.out = Pack([("rec", (C, P, 128), u8), ("pl", (C, T), f64), ("mean", (C, T, 2), f64),
-                         ("cov", (C, 2 * T, 2 * T), f64), ("A", (C, T, 4, 2), f64),
-                         ("b", (C, T, 4), f64), ("yaw_mean", (C, T), f64),
-                         ("yaw0_var", (C,), f64), ("cnt", (C,), i64), ("off", (C,), i64),
-                         ("pmf", (C,), f64), ("centre", (C, 2), f64)], self.device)
-        # small clouds: sampler + bucketing in three short launches (ccmpc_sample_bucket), whose cells need
-        # K (N + 4) slots per OV; else the sampler's sample-order store + ccmpc_bucket
-        fused_ws = lib.ccmpc_sample_bucket_workspace_bytes(O, N, T, self.max_k) \
-            if self.max_k * (L + 1) <= 512 else 0
+                self.pp_eps = torch.zeros((O, ph_, 2, N), dtype=f32, device=self.device)
+        out = [("cnt", (C,), i64), ("off", (C,), i64), ("pmf", (C,), f64),
+               ("centre", (C, 2), f64), ("mean", (C, ph_, 2), f64),
+               ("cov", (C, 2 * ph_, 2 * ph_), f64)]
+        if kind == "affine":
+            out += [("rec", (C, T, 128), u8)]
+        else:
+            out += [("rec", (C, P, 128), u8), ("pl", (C, T), f64)]
+        if kind == "ideal":
+            out += [("imean", (C, T, 2), f64), ("icov", (C, 2 * T, 2 * T), f64),
+                    ("status", (C,), i32)]
+        self.out = Pack(out, self.device)
+        self.out_l4 = Pack([("A", (C, ph_, 4, 2), f64), ("b", (C, ph_, 4), f64),
+                            ("yaw_mean", (C, ph_), f64), ("yaw0_var", (C,), f64)], self.device)
+        # small clouds: sampler + bucketing in three short launches (ccmpc_sample_bucket), whose
+        # cells need K (N + 4) slots per OV; else the sampler's sample-order store + ccmpc_bucket
+        fused_ws = lib.ccmpc_sample_bucket_workspace_bytes(O, N, ph_, self.max_k) \
+            if self.max_k * (L_ + 1) <= 512 else 0
         self.fused = fused_ws > 0
         region, cur, n_bound = [], 0, 0
         for o in range(O):
@@ -143,7 +178,7 @@ class MinkowskiStepGraph:
                                         else N + 4 * self.K[o]))
             n_bound = engine._round4(n_bound + N + 4 * self.K[o])
         self.region = np.asarray(region, np.int64)
-        st = engine.ParticleStore(T, [0] * C, dtype=f32, device=self.device,
+        st = engine.ParticleStore(ph_, [0] * C, dtype=f32, device=self.device,
                                   origin=np.zeros((C, 2)), capacity=cur)
         st.cell_off, st.cell_cnt, st.origin = self.out.d("off"), self.out.d("cnt"), \
             self.inp.d("origin")
@@ -154,33 +189,40 @@ class MinkowskiStepGraph:
             self.bucket_ws = torch.zeros(fused_ws, dtype=u8, device=self.device)
         else:
             self.z = torch.empty((O, N), dtype=i32, device=self.device)
-            self.samples = engine.ParticleStore(T, [N] * O, dtype=f32, device=self.device, align=4,
-                                                origin=np.zeros((O, 2)))
+            self.samples = engine.ParticleStore(ph_, [N] * O, dtype=f32, device=self.device,
+                                                align=4, origin=np.zeros((O, 2)))
             self.bucket_ws = torch.zeros(
-                max(lib.ccmpc_bucket_workspace_bytes(O, N, L, self.max_k), 16), dtype=u8,
+                max(lib.ccmpc_bucket_workspace_bytes(O, N, L_, self.max_k), 16), dtype=u8,
                 device=self.device)
         self.ws = engine.Workspace(self.device)
-        self.ws.get(lib.ccmpc_moments_workspace_bytes(T, C, st.n_bound))
+        self.ws.get(lib.ccmpc_moments_workspace_bytes(ph_, C, st.n_bound))
+        if kind == "ideal":         # its own: the rollout runs beside the scene's moments
+            self.ideal_ws = engine.Workspace(self.device)
+            self.ideal_ws.get(lib.ccmpc_ideal_moments_workspace_bytes(T, C, self.n_ideal))
+            self.aux = torch.cuda.Stream(device=self.device)
+            self._ev_fork = torch.cuda.Event()
+            self._ev_join = torch.cuda.Event()
+            # the rollout as a branch beside the sampling, or (CCMPC_STEP_IDEAL_FORK=0) first on
+            # the one stream
+            self.ideal_fork = os.environ.get("CCMPC_STEP_IDEAL_FORK", "1") == "1"
         self.l4_ws = engine.Workspace(self.device)      # its own: layouts differ
-        self.l4_ws.get(lib.ccmpc_l4_workspace_bytes(T, C, st.n_bound))
+        self.l4_ws.get(lib.ccmpc_l4_workspace_bytes(ph_, C, st.n_bound))
         self.side = torch.cuda.Stream(device=self.device)
-        # the cycle and the L4 kernel as parallel graph branches, or (CCMPC_STEP_LINEAR=1) one
-        # after the other on one stream
-        self.branch = os.environ.get("CCMPC_STEP_LINEAR", "0") != "1"
-        self.cycle_first = os.environ.get("CCMPC_STEP_CYCLE_FIRST", "0") == "1"
         # the packed copies as copy kernels that read / write the pinned pack directly, or
         # (CCMPC_STEP_COPY_KERNEL=0) as memcpy nodes (a runtime blit of ~4.8 us each): the
         # kernels take ~8 us off a step (profiles/r02/v33_step_copy_kernel.txt)
         self.copy_kernel = os.environ.get("CCMPC_STEP_COPY_KERNEL", "1") == "1"
-        self.graph = None
+        self.graph = self.graph_l4 = None
         self._static_set = False
+        self._l4_cur = None                 # snapshot of the current generation's L4 outputs
+        self._l4_prev = None                # (generation, snapshot) of the one before
 
     # ---------------------------------------------------------------------------------------
     def _sample_calls(self, s):
         """The sampling + bucketing stage's C-ABI calls: [(fn, args)]."""
         lib, p = _lib.load(), engine._p
         i, o, st = self.inp, self.out, self.store
-        O, N, T, L = self.O, self.N, self.T, self.L
+        O, N, T, L = self.O, self.N, self.ph, self.L
         ws = self.bucket_ws
         if self.per_particle:
             gmm, layout, z_in, eps = (p(self.pp_gmm), _lib.GMM_PER_PARTICLE, p(self.pp_z),
@@ -206,53 +248,86 @@ class MinkowskiStepGraph:
                                     p(o.d("pmf")), p(o.d("centre")), s))]
 
     def _enqueue(self):
+        """Graph A on the current stream."""
         lib, p, s = _lib.load(), engine._p, engine._stream()
         i, o, st = self.inp, self.out, self.store
-        T, C = self.T, self.C
+        T, C, ph = self.T, self.C, self.ph
         chk = engine._lib.check
         copy = lib.ccmpc_copy_kernel_async if self.copy_kernel else lib.ccmpc_copy_async
         chk(copy(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
+        main = torch.cuda.current_stream(self.device)
+        if self.kind == "ideal":
+            # the rollout needs only the saved moments: a branch beside the sampling.  The fork
+            # / join events are the graph's own, alive as long as it is: an event recorded into
+            # a capture and destroyed before the graph (what wait_stream's temporary does) left
+            # a dangling reference that crashed the replay once the memory was reused
+            if self.ideal_fork:
+                self._ev_fork.record(main)
+                self.aux.wait_event(self._ev_fork)
+            with torch.cuda.stream(self.aux if self.ideal_fork else main):
+                iws = self.ideal_ws.buf
+                chk(lib.ccmpc_ideal_minkowski_cycle_ex(
+                    p(i.d("pmean")), p(i.d("pcov")), self.T_src, p(i.d("src")), C, T,
+                    self.n_ideal, None, 0, p(i.d("iseed")), None, p(iws), iws.numel(),
+                    p(i.d("ref")), None, p(i.d("risk")), self.R, self.tol, self.maxiter,
+                    p(o.d("imean")), p(o.d("icov")), p(o.d("status")), p(o.d("rec")),
+                    p(o.d("pl")), engine._stream()), "ccmpc_ideal_minkowski_cycle_ex")
         for fn, args in self._sample_calls(s):
             chk(fn(*args), fn.__name__)
-        # the cycle and the L4 kernel only read the bucketed store: two graph branches (the
-        # fork is taken after the sampling; which branch is captured first is a knob)
-        main = torch.cuda.current_stream(self.device)
-        side = self.side if self.branch else main
-        side.wait_stream(main)
-
-        def l4():
-            with torch.cuda.stream(side):
-                lws = self.l4_ws.buf
-                chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, T, p(st.origin),
-                                       p(o.d("off")), p(o.d("cnt")), C, st.n_bound,
-                                       p(i.d("past")), p(i.d("bbox")), p(lws), lws.numel(),
-                                       p(o.d("A")), p(o.d("b")), p(o.d("yaw_mean")),
-                                       p(o.d("yaw0_var")), None, None, engine._stream()),
-                    "ccmpc_l4_split")
-
-        def cycle():
-            mws = self.ws.buf
+        mws = self.ws.buf
+        if self.kind == "minkowski":
             chk(lib.ccmpc_minkowski_cycle(
-                p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
+                p(st.pos), engine.F32, st.ld, ph, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
                 st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
                 self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")),
                 p(o.d("pl")), s), "ccmpc_minkowski_cycle")
-
-        for stage in ((cycle, l4) if self.cycle_first else (l4, cycle)):
-            stage()
-        main.wait_stream(side)
+        else:
+            chk(lib.ccmpc_moments(p(st.pos), engine.F32, st.ld, ph, p(st.origin), p(o.d("off")),
+                                  p(o.d("cnt")), C, st.n_bound, p(mws), mws.numel(),
+                                  p(o.d("mean")), p(o.d("cov")), s), "ccmpc_moments")
+            if self.kind == "affine":
+                chk(lib.ccmpc_affine(p(o.d("mean")), p(o.d("cov")), T, C, p(i.d("ref")), None,
+                                     p(i.d("gamma")), self.R, p(o.d("rec")), s), "ccmpc_affine")
+            elif self.ideal_fork:
+                self._ev_join.record(self.aux)
+                main.wait_event(self._ev_join)
         chk(copy(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
 
+    def _enqueue_l4(self):
+        """Graph B on the current stream: L4 over the bucketed store, then its copy-out."""
+        lib, p, s = _lib.load(), engine._p, engine._stream()
+        i, o, q, st = self.inp, self.out, self.out_l4, self.store
+        copy = lib.ccmpc_copy_kernel_async if self.copy_kernel else lib.ccmpc_copy_async
+        lws = self.l4_ws.buf
+        chk = engine._lib.check
+        chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, self.ph, p(st.origin),
+                               p(o.d("off")), p(o.d("cnt")), self.C, st.n_bound,
+                               p(i.d("past")), p(i.d("bbox")), p(lws), lws.numel(),
+                               p(q.d("A")), p(q.d("b")), p(q.d("yaw_mean")),
+                               p(q.d("yaw0_var")), None, None, s), "ccmpc_l4_split")
+        chk(copy(p(q.host), p(q.dev), q.nbytes, s), "ccmpc_copy_async")
+
     def capture(self):
-        """Record the step into a hipGraph (after one eager run that warms every kernel)."""
+        """Record graphs A and B (after one eager run of each that warms every kernel).
+
+        torch hands out streams from a small pool, so this graph's capture / aux / side
+        streams can be another graph's streams, which may still hold that graph's last L4
+        replay: the device is drained first, so no stream joins a capture with work pending
+        (a fork into a stream with pending uncaptured work corrupted the captured graph:
+        segfaults in the first replay once the pool had wrapped)."""
+        torch.cuda.synchronize(self.device)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             self._enqueue()
-        s.synchronize()
+            self._enqueue_l4()
+        torch.cuda.synchronize(self.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=s):
             self._enqueue()
+        self.graph_l4 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_l4, stream=s):
+            self._enqueue_l4()
         torch.cuda.synchronize(self.device)
         return self
 
@@ -261,7 +336,8 @@ class MinkowskiStepGraph:
                    past_last, bbox, filter_pmf=0.1):
         """Write one step's host inputs into the pinned input pack (no device work; every field
         written in place, no temporaries).  The kept modes implied by latent_pmf must match the
-        graph's K.  past_last / bbox: per cell (C, 2) or per OV (O, 2)."""
+        graph's K.  past_last / bbox: per cell (C, 2) or per OV (O, 2).  cell_risk: (C, 3)
+        (chi2_r, chi2_p, Gamma) per cell; the affine kind reads its Gamma column."""
         i, O, L, C = self.inp, self.O, self.L, self.C
         if not self._static_set:       # shape-fixed fields and helpers: once
             i.h("nk")[:] = self.K
@@ -279,8 +355,7 @@ class MinkowskiStepGraph:
         keep = i.h("keep")               # kept: its rank among the kept latents; else -1
         np.multiply(kc, kept, out=keep, casting="unsafe")
         keep -= 1
-        sd = int(seed) & (2**64 - 1)
-        i.h("seed")[0] = sd - (1 << 64) if sd >= (1 << 63) else sd
+        i.h("seed")[0] = _as_i64(seed)
         i.h("init").reshape(-1)[:] = np.asarray(init_state, np.float64).reshape(-1)
         np.cumsum(pmf, axis=1, out=i.h("cdf"))
         if self.per_particle:
@@ -298,13 +373,33 @@ class MinkowskiStepGraph:
             i.h("minpos")[:] = mp
             np.take(mp, self._ov_of_cell, axis=0, out=i.h("origin"))
         i.h("ref").reshape(-1)[:] = np.asarray(ref_traj, np.float64)[:self.T].reshape(-1)
-        i.h("risk").reshape(-1)[:] = np.asarray(cell_risk, np.float64).reshape(3 * C)
+        cr = np.asarray(cell_risk, np.float64).reshape(C, 3)
+        if self.kind == "affine":
+            i.h("gamma")[:] = cr[:, 2]
+        else:
+            i.h("risk")[:] = cr
         for name, v in (("past", past_last), ("bbox", bbox)):
             v = np.asarray(v, np.float64)
             if v.size == 2 * C:
                 i.h(name).reshape(-1)[:] = v.reshape(-1)
             else:
                 np.take(v.reshape(O, 2), self._ov_of_cell, axis=0, out=i.h(name))
+
+    def set_ideal_inputs(self, prev_mean, prev_cov, src_cell, seed):
+        """The shrinking step's saved moments (the previous frame's mean [Cp, T_src, 2] and cov
+        [Cp, 2 T_src, 2 T_src], host arrays or device tensors), each current cell's source cell
+        (the data_idx fallback, :2648-2656) and the rollout's Philox seed."""
+        if self.kind != "ideal":
+            raise ValueError("set_ideal_inputs belongs to the shrinking (ideal) step")
+        i = self.inp
+        for name, v in (("pmean", prev_mean), ("pcov", prev_cov)):
+            v = v.cpu().numpy() if torch.is_tensor(v) else np.asarray(v, np.float64)
+            if v.shape != i.h(name).shape:
+                raise ValueError(f"{name}: shape {v.shape}, this graph holds {i.h(name).shape}")
+            i.h(name)[...] = v
+        src = src_cell.cpu().numpy() if torch.is_tensor(src_cell) else np.asarray(src_cell)
+        i.h("src")[:] = src.reshape(-1)
+        i.h("iseed")[0] = _as_i64(seed)
 
     def set_device_inputs(self, gmm, z, eps=None):
         """The per-particle mode's device inputs for the next launch, as Trajectron++ leaves
@@ -317,7 +412,7 @@ class MinkowskiStepGraph:
         validated on the host (that would synchronise): the kernels clamp it into [0, L)."""
         if not self.per_particle:
             raise ValueError("set_device_inputs needs a graph built with per_particle=True")
-        O, N, T = self.O, self.N, self.T
+        O, N, T = self.O, self.N, self.ph
 
         def put(dst, src, natural, minor, perm):
             if not torch.is_tensor(src) or src.device != self.device:
@@ -343,48 +438,32 @@ class MinkowskiStepGraph:
         elif eps is not None:
             raise ValueError("this graph draws the noise itself (built without eps_in)")
 
-    def bind(self):
-        """Pre-convert every argument of the step's C-ABI calls for the current stream (the
-        direct-launch alternative to the graph: one foreign call per stage, the cycle and L4
-        back to back on one stream)."""
-        lib, p, s = _lib.load(), engine._p, engine._stream()
-        i, o, st = self.inp, self.out, self.store
-        T, C = self.T, self.C
-        mws = self.ws.buf
-        self._calls = [(lib.ccmpc_copy_async, (p(i.dev), p(i.host), i.nbytes, s))] + \
-            self._sample_calls(s) + [
-            (lib.ccmpc_minkowski_cycle, (
-                p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")), p(o.d("cnt")), C,
-                st.n_bound, p(mws), mws.numel(), p(i.d("ref")), None, p(i.d("risk")), self.R,
-                self.tol, self.maxiter, p(o.d("mean")), p(o.d("cov")), p(o.d("rec")),
-                p(o.d("pl")), s)),
-            (lib.ccmpc_l4_split, (p(st.pos), engine.F32, st.ld, T, p(st.origin), p(o.d("off")),
-                                  p(o.d("cnt")), C, st.n_bound, p(i.d("past")), p(i.d("bbox")),
-                                  p(self.l4_ws.buf), self.l4_ws.buf.numel(), p(o.d("A")),
-                                  p(o.d("b")), p(o.d("yaw_mean")), p(o.d("yaw0_var")), None,
-                                  None, s)),
-            (lib.ccmpc_copy_async, (p(o.host), p(o.dev), o.nbytes, s)),
-        ]
-        return self
-
     def launch(self, direct=False):
-        """Enqueue one step (inputs up, the kernels, outputs down) without waiting: one graph
-        replay, or (direct) the bound C-ABI calls."""
+        """Enqueue one step without waiting: graph A on the current stream, then graph B (L4)
+        on the side stream once A is done.  direct: the same C-ABI calls enqueued eagerly
+        instead of the graph replays."""
+        # the previous generation's L4 outputs stay readable until the replay after this one
+        if self.generation > 0:
+            self._l4_prev = (self.generation, self.l4_outputs(self.generation))
+        self._l4_cur = None
         self.generation += 1
+        main = torch.cuda.current_stream(self.device)
+        main.wait_stream(self.side)      # the last L4 has read the store this replay rewrites
         if direct:
-            if getattr(self, "_calls", None) is None:
-                self.bind()
-            for fn, args in self._calls:
-                rc = fn(*args)
-                if rc != 0:
-                    _lib.check(rc, fn.__name__)
-            return
-        if self.graph is None:
-            self.capture()
-        self.graph.replay()
+            self._enqueue()
+        else:
+            if self.graph is None:
+                self.capture()
+            self.graph.replay()
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            if direct:
+                self._enqueue_l4()
+            else:
+                self.graph_l4.replay()
 
     def wait(self):
-        """Return when the launched step's output pack is on the host."""
+        """Return when the launched step's output pack (graph A) is on the host."""
         torch.cuda.current_stream(self.device).synchronize()
 
     def replay(self):
@@ -392,5 +471,36 @@ class MinkowskiStepGraph:
         self.launch()
         self.wait()
 
+    def l4_outputs(self, generation=None):
+        """{A, b, yaw_mean, yaw0_var} host arrays of launch `generation` (default: the latest),
+        waiting for its L4 graph; the generation before the latest stays readable, older ones
+        raise (their buffers were overwritten)."""
+        gen = self.generation if generation is None else generation
+        if gen == self.generation:
+            if self._l4_cur is None:
+                self.side.synchronize()
+                self._l4_cur = self.out_l4.snapshot()
+            return self._l4_cur
+        if self._l4_prev is not None and self._l4_prev[0] == gen:
+            return self._l4_prev[1]
+        raise RuntimeError(f"stale planning-step data: the L4 outputs of launch {gen} were "
+                           f"overwritten (this graph is at launch {self.generation})")
+
     def records(self):
-        return self.out.h("rec").reshape(-1).view(_lib.HALFSPACE_DTYPE).reshape(self.C, self.P)
+        return self.out.h("rec").reshape(-1).view(
+            _lib.AFFINE_DTYPE if self.kind == "affine" else _lib.HALFSPACE_DTYPE).reshape(
+            self.C, -1)
+
+
+def _as_i64(seed):
+    sd = int(seed) & (2**64 - 1)
+    return sd - (1 << 64) if sd >= (1 << 63) else sd
+
+
+class MinkowskiStepGraph(StepGraph):
+    """The full-horizon (T == ph) Minkowski step: StepGraph(kind="minkowski")."""
+
+    def __init__(self, O, N, T, L, K, device="cuda", dt=0.5, R=risk.R_COLLISION, tol=1e-8,
+                 maxiter=1000, per_particle=False, eps_in=False):
+        super().__init__(O, N, T, L, K, device=device, dt=dt, R=R, tol=tol, maxiter=maxiter,
+                         per_particle=per_particle, eps_in=eps_in, kind="minkowski")

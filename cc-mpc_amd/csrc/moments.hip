@@ -202,7 +202,13 @@ __device__ __forceinline__ void mfma_group(const typename LaneVec<P, W>::type (&
     for (int b = 0; b < RB; ++b)
 #pragma unroll
       for (int j = 0; j < W; ++j)  // shifted; out-of-range slots and dead rows become 0
+#if CCMPC_PROBE & 32  // diagnostic build only: no masks (wrong at partial groups; timing bound)
+        v[b][j] = raw[s][b][j] - sh[b];
+#elif CCMPC_PROBE & 64  // diagnostic build only: neither masks nor the shift
+        v[b][j] = raw[s][b][j];
+#else
         v[b][j] = (live[b] && q + j < p1) ? raw[s][b][j] - sh[b] : 0.0;
+#endif
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const int a = (NACC == 2) ? (j & 1) : 0;
@@ -531,7 +537,13 @@ __device__ __forceinline__ void mfma_group4(const Pair<P> (&loaded)[NB], const d
     double v[NB];  // sub-step j: shifted; out-of-range slots and dead rows become 0
 #pragma unroll
     for (int I = 0; I < NB; ++I) {
+#if CCMPC_PROBE & 32
+      v[I] = raw[I][j] - sh[I];
+#elif CCMPC_PROBE & 64
+      v[I] = raw[I][j];
+#else
       v[I] = (live[I] && q + j < p1) ? raw[I][j] - sh[I] : 0.0;
+#endif
       s1[I] += v[I];
     }
     int p = 0;

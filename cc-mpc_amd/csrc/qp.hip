@@ -18,6 +18,7 @@
 // bitwise reproducible.  Cholesky and both triangular solves run on wave 0 (lane = row),
 // wave-synchronous, with no workgroup barrier per column.
 #include "ccmpc_common.hpp"
+#include <cstdlib>
 
 namespace ccmpc {
 
@@ -172,11 +173,14 @@ __device__ __forceinline__ double wave_min(double v) {
   return v;
 }
 
-// Block reductions of up to 2 values (every thread gets the result); two barriers.
+// Block reductions of up to 2 values (every thread gets the result); two barriers.  NW = 1
+// (one wave per scene): the wave reduction alone, no LDS and no barrier.
+template <int NW>
 __device__ __forceinline__ void block_max2(double &a, double &b, double *red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   a = wave_max(a);
   b = wave_max(b);
+  if (NW == 1) return;
   if (lane == 0) {
     red[2 * w] = a;
     red[2 * w + 1] = b;
@@ -184,34 +188,39 @@ __device__ __forceinline__ void block_max2(double &a, double &b, double *red) {
   __syncthreads();
   a = red[0];
   b = red[1];
-  for (int k = 1; k < kQpWaves; ++k) {
+  for (int k = 1; k < NW; ++k) {
     a = fmax(a, red[2 * k]);
     b = fmax(b, red[2 * k + 1]);
   }
   __syncthreads();
 }
+template <int NW>
 __device__ __forceinline__ double block_sum(double a, double *red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   a = wave_sum(a);
+  if (NW == 1) return a;
   if (lane == 0) red[w] = a;
   __syncthreads();
   a = red[0];
-  for (int k = 1; k < kQpWaves; ++k) a += red[k];
+  for (int k = 1; k < NW; ++k) a += red[k];
   __syncthreads();
   return a;
 }
+template <int NW>
 __device__ __forceinline__ double block_min(double a, double *red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   a = wave_min(a);
+  if (NW == 1) return a;
   if (lane == 0) red[w] = a;
   __syncthreads();
   a = red[0];
-  for (int k = 1; k < kQpWaves; ++k) a = fmin(a, red[k]);
+  for (int k = 1; k < NW; ++k) a = fmin(a, red[k]);
   __syncthreads();
   return a;
 }
 
 // Block argmax (largest value, smallest index on ties); every thread gets the result.
+template <int NW>
 __device__ __forceinline__ void block_argmax(double &v, double &idx, double *red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -222,6 +231,7 @@ __device__ __forceinline__ void block_argmax(double &v, double &idx, double *red
       idx = oi;
     }
   }
+  if (NW == 1) return;
   if (lane == 0) {
     red[2 * w] = v;
     red[2 * w + 1] = idx;
@@ -229,7 +239,7 @@ __device__ __forceinline__ void block_argmax(double &v, double &idx, double *red
   __syncthreads();
   v = red[0];
   idx = red[1];
-  for (int k = 1; k < kQpWaves; ++k) {
+  for (int k = 1; k < NW; ++k) {
     if (red[2 * k] > v || (red[2 * k] == v && red[2 * k + 1] < idx)) {
       v = red[2 * k];
       idx = red[2 * k + 1];
@@ -251,6 +261,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The workgroup's barrier; with one wave per scene, the wave-level ordering above (a wave runs
+// its LDS instructions in order, so every lane then sees every other lane's writes)
+template <int NW>
+__device__ __forceinline__ void qp_sync() {
+  if (NW == 1)
+    wave_sync();
+  else
+    __syncthreads();
 }
 
 // Wave-level dense Cholesky and triangular solves (called by one whole wave; lane = row, two
@@ -445,8 +465,12 @@ __device__ __forceinline__ double hctrl_mul(const double *z, int i, int T, int o
   return acc;
 }
 
-template <bool ROWS_LDS, int NM>
-__global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
+// NW waves per scene: 4 (the general form), or 1 for n = 2T <= 16 (the reference's ph = 8):
+// every barrier is then a wave-level ordering and every reduction a wave butterfly, which
+// takes the ~30 workgroup barriers per IPM iteration off the chain.
+template <bool ROWS_LDS, int NM, int NW>
+__global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
+  constexpr int NTH = 64 * NW;
   extern __shared__ double lds[];
   const int64_t sc = blockIdx.x;
   if (sc >= A.S) return;
@@ -496,11 +520,11 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
   auto grow = [&](int k) { return 4 * (Tp + k / 3) + (k % 3 == 2 ? 3 : k % 3); };
 
   // ---- setup -------------------------------------------------------------------------------
-  for (int e = tid; e < T3 * n; e += kQpThreads) {
+  for (int e = tid; e < T3 * n; e += NTH) {
     const int k = e / n, j = e % n;
     Gs[e] = Gam[static_cast<int64_t>(grow(k)) * ncol + 2 * Tp + j];
   }
-  for (int k = tid; k < T3; k += kQpThreads) {
+  for (int k = tid; k < T3; k += NTH) {
     // constant part of the state: x_bar + Gamma_p u_prev - Gamma_f u_bar (:2877-2891)
     const int r = grow(k);
     const double *gr = Gam + static_cast<int64_t>(r) * ncol;
@@ -512,7 +536,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     c3[k] = c;
     y[k] = 0.0;
   }
-  for (int j = tid; j < n; j += kQpThreads) {
+  for (int j = tid; j < n; j += NTH) {
     // min_u / max_u = vstack((full(T, a), full(T, delta))).T.ravel() (:2874-2875): the bounds
     // interleave (accel, steer) per step like Gamma's columns, whatever U's reshape order
     const int c = j & 1;
@@ -520,8 +544,8 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     lb[j] = c == 0 ? p.min_a : -p.max_delta;
     z[j] = 0.0;
   }
-  __syncthreads();
-  for (int k = tid; k < T3; k += kQpThreads) {
+  qp_sync<NW>();
+  for (int k = tid; k < T3; k += NTH) {
     // objective's linear term in output space: 2 (w_ref (c - ref_t) + [t = T-1] w_final (c - g))
     const int t = k / 3, a = k % 3;
     double v = 0.0;
@@ -535,7 +559,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
   // obstacle rows: a . (y_xy + c_xy) <= b  ->  a . y_xy <= b' = b - a . c_xy
   int skipped = 0;
   double hmax = 0.0;
-  for (int64_t r = tid; r < R; r += kQpThreads) {
+  for (int64_t r = tid; r < R; r += NTH) {
     const int64_t cell = r / P;
     const int pp = static_cast<int>(r - cell * P);
     const unsigned char *rec = A.rec + (c0 * P + r) * 128;
@@ -569,10 +593,10 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     rw.t[r] = static_cast<double>(obst_step(r));
     hmax = fmax(hmax, fabs(b));
   }
-  __syncthreads();
+  qp_sync<NW>();
   // f = Gs^T qf (for the scaling of the dual residual)
   double fmax_ = 0.0;
-  for (int j = tid; j < n; j += kQpThreads) {
+  for (int j = tid; j < n; j += NTH) {
     double v = 0.0;
     for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * qf[k];
     fmax_ = fmax(fmax_, fabs(v));
@@ -614,13 +638,13 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
   auto row_gd = [&](int64_t r, const double *ydd, const double *dzz) -> double {
     return row_lin(r, ydd, dzz);
   };
-  for (int64_t r = tid; r < mrows; r += kQpThreads) {
+  for (int64_t r = tid; r < mrows; r += NTH) {
     const double g = row_g(r, y, z);
     rw.s[r] = fmax(-g, 1.0);
     rw.l[r] = 1.0;
     if (r < nbox + nv) hmax = fmax(hmax, fabs(g));  // bounds' right-hand sides (z = y = 0)
   }
-  block_max2(hmax, fmax_, red);
+  block_max2<NW>(hmax, fmax_, red);
   const double tol_p = A.tol * (1.0 + hmax), tol_d = A.tol * (1.0 + fmax_);
 
   // Per-step sums over a step's obstacle rows, in a fixed order (wave per step, lane-strided,
@@ -650,12 +674,12 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     QP_MARK(0);
     // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
     double rpmax = 0.0, sl = 0.0;
-    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+    for (int64_t r = tid; r < mrows; r += NTH) {
       const double rp = row_g(r, y, z) + rw.s[r];
       rpmax = fmax(rpmax, fabs(rp));
       sl += rw.s[r] * rw.l[r];
     }
-    for (int t = w; t < T; t += kQpWaves) {
+    for (int t = w; t < T; t += NW) {
       double la0 = 0.0, la1 = 0.0, w00 = 0.0, w01 = 0.0, w11 = 0.0;
       const int64_t cnt = step_count(t);
       for (int64_t i = lane; i < cnt; i += 64) {
@@ -685,17 +709,17 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
         bw[4 * t + 3] = rw.l[rv] / rw.s[rv] + rw.l[rv + 1] / rw.s[rv + 1];
       }
     }
-    __syncthreads();
+    qp_sync<NW>();
     QP_MARK(1);
     // ---- I2: dual residual, normal matrix ---------------------------------------------------
     double rdmax = 0.0;
-    for (int j = tid; j < n; j += kQpThreads) {
+    for (int j = tid; j < n; j += NTH) {
       double v = hctrl_mul(z, j, T, order, p) + rw.l[2 * j] - rw.l[2 * j + 1];
       for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * q[k];
       rd[j] = v;
       rdmax = fmax(rdmax, fabs(v));
     }
-    for (int e = tid; e < n * n; e += kQpThreads) {
+    for (int e = tid; e < n * n; e += NTH) {
       const int i = e / n, j = e % n;
       if (j > i) continue;
       double v = hctrl(i, j, T, order, p);
@@ -710,8 +734,8 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       }
       M[i * ldm + j] = v;
     }
-    block_max2(rpmax, rdmax, red);
-    mu = block_sum(sl, red) / static_cast<double>(mrows);
+    block_max2<NW>(rpmax, rdmax, red);
+    mu = block_sum<NW>(sl, red) / static_cast<double>(mrows);
 #ifdef CCMPC_QP_TRACE
     const double tr_rp = rpmax, tr_rd = rdmax;
     if (it == 0 && tid == 0 && sc == 0)
@@ -761,7 +785,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       }
       if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
     }
-    __syncthreads();
+    qp_sync<NW>();
     if (red[8 * kQpWaves - 1] != 0.0) {  // weights overflowed: the iteration broke down;
       status = CCMPC_QP_MAXITER;           // only a verified polish can still answer
       break;
@@ -781,16 +805,16 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       }
     };
     auto gs_times_dz = [&]() {
-      for (int k = tid; k < T3; k += kQpThreads) {
+      for (int k = tid; k < T3; k += NTH) {
         double v = 0.0;
         for (int j = 0; j < n; ++j) v += Gs[k * n + j] * dz[j];
         yd[k] = v;
       }
-      __syncthreads();
+      qp_sync<NW>();
     };
     // rhs = -r_d - G^T u with u_r given per row; q (output space) and dz (rhs) staged in LDS
     auto build_rhs = [&](auto urow) {
-      for (int t = w; t < T; t += kQpWaves) {
+      for (int t = w; t < T; t += NW) {
         double u0 = 0.0, u1 = 0.0;
         const int64_t cnt = step_count(t);
         for (int64_t i = lane; i < cnt; i += 64) {
@@ -808,15 +832,15 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
           q[3 * t + 2] = urow(rv) - urow(rv + 1);
         }
       }
-      __syncthreads();
-      for (int j = tid; j < n; j += kQpThreads) {
+      qp_sync<NW>();
+      for (int j = tid; j < n; j += NTH) {
         double v = -rd[j] - (urow(2 * j) - urow(2 * j + 1));
         for (int k = 0; k < T3; ++k) v -= Gs[k * n + j] * q[k];
         dz[j] = v;
       }
-      __syncthreads();
+      qp_sync<NW>();
       chol_solve(dz);
-      __syncthreads();
+      qp_sync<NW>();
       gs_times_dz();
     };
     QP_MARK(3);
@@ -827,7 +851,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     });
     QP_MARK(4);
     double amax = 1.0;
-    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+    for (int64_t r = tid; r < mrows; r += NTH) {
       const double s = rw.s[r], l = rw.l[r];
       const double rp = row_g(r, y, z) + s, gd = row_gd(r, yd, dz);
       const double ds = -rp - gd, dl = l / s * (gd + rp) - l;
@@ -836,11 +860,11 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       if (ds < 0.0) amax = fmin(amax, -s / ds);
       if (dl < 0.0) amax = fmin(amax, -l / dl);
     }
-    const double aaff = block_min(amax, red);
+    const double aaff = block_min<NW>(amax, red);
     double slaff = 0.0;
-    for (int64_t r = tid; r < mrows; r += kQpThreads)
+    for (int64_t r = tid; r < mrows; r += NTH)
       slaff += (rw.s[r] + aaff * rw.ds[r]) * (rw.l[r] + aaff * rw.dl[r]);
-    const double muaff = block_sum(slaff, red) / static_cast<double>(mrows);
+    const double muaff = block_sum<NW>(slaff, red) / static_cast<double>(mrows);
     const double sr = muaff / mu, sigma = sr * sr * sr;
     QP_MARK(5);
     // ---- corrector: r_c = s l + ds_aff dl_aff - sigma mu;  u = w r_p - r_c / s ----------
@@ -853,7 +877,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
     });
     QP_MARK(6);
     amax = 1e300;
-    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+    for (int64_t r = tid; r < mrows; r += NTH) {
       const double s = rw.s[r], l = rw.l[r];
       const double rp = row_g(r, y, z) + s, gd = row_gd(r, yd, dz);
       const double rc = rc_of(r);
@@ -863,15 +887,15 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       if (ds < 0.0) amax = fmin(amax, -s / ds);
       if (dl < 0.0) amax = fmin(amax, -l / dl);
     }
-    const double alpha = fmin(1.0, 0.995 * block_min(amax, red));
+    const double alpha = fmin(1.0, 0.995 * block_min<NW>(amax, red));
 
-    for (int j = tid; j < n; j += kQpThreads) z[j] += alpha * dz[j];
-    for (int k = tid; k < T3; k += kQpThreads) y[k] += alpha * yd[k];
-    for (int64_t r = tid; r < mrows; r += kQpThreads) {
+    for (int j = tid; j < n; j += NTH) z[j] += alpha * dz[j];
+    for (int k = tid; k < T3; k += NTH) y[k] += alpha * yd[k];
+    for (int64_t r = tid; r < mrows; r += NTH) {
       rw.s[r] += alpha * rw.ds[r];
       rw.l[r] += alpha * rw.dl[r];
     }
-    __syncthreads();
+    qp_sync<NW>();
 #ifdef CCMPC_QP_TRACE
     QP_MARK(7);
     if (tid == 0 && sc == 0)
@@ -896,7 +920,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
            *sdinv = lds + lay.pdinv;
     double *fu = lds + lay.f, *y0 = rh, *rs = e2, *lam = q, *zp = dz, *yp = yd;
     // H (no barrier terms) into M; f in control space
-    for (int e = tid; e < n * n; e += kQpThreads) {
+    for (int e = tid; e < n * n; e += NTH) {
       const int i = e / n, j = e % n;
       if (j > i) continue;
       double v = hctrl(i, j, T, order, p);
@@ -907,27 +931,27 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       }
       M[i * ldm + j] = v;
     }
-    for (int j = tid; j < n; j += kQpThreads) {
+    for (int j = tid; j < n; j += NTH) {
       double v = 0.0;
       for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * qf[k];
       fu[j] = v;
     }
     // active rows, compacted in row order (ballot + prefix: deterministic)
     int na = 0;
-    for (int64_t base = 0; base < mrows; base += kQpThreads) {
+    for (int64_t base = 0; base < mrows; base += NTH) {
       const int64_t r = base + tid;
       const bool on = r < mrows && rw.s[r] < rw.l[r];
       const uint64_t mask = __ballot(on);
       if (lane == 0) red[w] = static_cast<double>(__popcll(mask));
-      __syncthreads();
+      qp_sync<NW>();
       int off = na;
       for (int k = 0; k < w; ++k) off += static_cast<int>(red[k]);
       int tot = na;
-      for (int k = 0; k < kQpWaves; ++k) tot += static_cast<int>(red[k]);
+      for (int k = 0; k < NW; ++k) tot += static_cast<int>(red[k]);
       const int pos = off + __popcll(mask & ((uint64_t(1) << lane) - 1));
       if (on && pos < n) act[pos] = static_cast<double>(r);
       na = tot;
-      __syncthreads();
+      qp_sync<NW>();
     }
     // factor H once; y0 = -L^{-1} f
     if (w == 0) {
@@ -940,14 +964,14 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       wave_store2(y0, n, b);
       if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
     }
-    __syncthreads();
+    qp_sync<NW>();
     const bool h_ok = red[8 * kQpWaves - 1] == 0.0;
     if (!h_ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
     // up to 4 rounds of active-set correction, as the oracle's polish does: drop rows whose
     // multiplier comes out negative, else add the most violated row
     for (int round = 0; h_ok && round < 4 && na <= n; ++round) {
       // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
-      for (int a = w; a < na; a += kQpWaves) {
+      for (int a = w; a < na; a += NW) {
         const int64_t r = static_cast<int64_t>(act[a]);
         double b[2];
 #pragma unroll
@@ -978,15 +1002,15 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
         d = wave_sum(d);
         if (lane == 0) rs[a] = d + row_const(r);
       }
-      __syncthreads();
-      for (int e = tid; e < na * na; e += kQpThreads) {
+      qp_sync<NW>();
+      for (int e = tid; e < na * na; e += NTH) {
         const int i = e / na, j = e % na;
         if (j > i) continue;
         double v = 0.0;
         for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
         Sm[i * ldm + j] = v;
       }
-      __syncthreads();
+      qp_sync<NW>();
       if (w == 0) {
         const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
         double b[2];
@@ -998,30 +1022,30 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
         }
         if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
       }
-      __syncthreads();
+      qp_sync<NW>();
       if (red[8 * kQpWaves - 1] != 0.0) break;  // dependent active rows
       // z = L^{-T}(y0 - W^T lambda)
-      for (int j = tid; j < n; j += kQpThreads) {
+      for (int j = tid; j < n; j += NTH) {
         double v = y0[j];
         for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
         zp[j] = v;
       }
-      __syncthreads();
+      qp_sync<NW>();
       if (w == 0) {
         double b[2];
         wave_load2(zp, n, b);
         wave_backward(M, n, ldm, dinv, b);
         wave_store2(zp, n, b);
       }
-      __syncthreads();
-      for (int k = tid; k < T3; k += kQpThreads) {
+      qp_sync<NW>();
+      for (int k = tid; k < T3; k += NTH) {
         double v = 0.0;
         for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
         yp[k] = v;
       }
-      __syncthreads();
+      qp_sync<NW>();
       double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
-      for (int64_t r = tid; r < mrows; r += kQpThreads) {
+      for (int64_t r = tid; r < mrows; r += NTH) {
         const double g = row_g(r, yp, zp);
         if (!isfinite(g)) bad = 1.0;
         if (g > viol) {
@@ -1029,17 +1053,17 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
           vrow = static_cast<double>(r);
         }
       }
-      for (int a = tid; a < na; a += kQpThreads) {
+      for (int a = tid; a < na; a += NTH) {
         if (!isfinite(lam[a])) bad = 1.0;
         lneg = fmax(lneg, -lam[a]);
       }
-      block_argmax(viol, vrow, red);
-      block_max2(lneg, bad, red);
+      block_argmax<NW>(viol, vrow, red);
+      block_max2<NW>(lneg, bad, red);
       if (bad != 0.0) break;
       if (viol <= tol_p && lneg <= tol_d) {
-        for (int j = tid; j < n; j += kQpThreads) z[j] = zp[j];
+        for (int j = tid; j < n; j += NTH) z[j] = zp[j];
         status = 0;
-        __syncthreads();
+        qp_sync<NW>();
         break;
       }
       // next active set (thread 0; na <= n entries)
@@ -1055,16 +1079,16 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
         }
         red[8 * kQpWaves - 2] = static_cast<double>(m2);
       }
-      __syncthreads();
+      qp_sync<NW>();
       na = static_cast<int>(red[8 * kQpWaves - 2]);
-      __syncthreads();
+      qp_sync<NW>();
     }
   }
 
   // ---- outputs: u, X = Gamma_f u + const (all four state rows), the objective value ----------
-  for (int j = tid; j < n; j += kQpThreads) A.out_u[sc * n + j] = z[j];
+  for (int j = tid; j < n; j += NTH) A.out_u[sc * n + j] = z[j];
   double part = 0.0;
-  for (int r = tid; r < 4 * T; r += kQpThreads) {
+  for (int r = tid; r < 4 * T; r += NTH) {
     const int gr = 4 * Tp + r;
     const double *g = Gam + static_cast<int64_t>(gr) * ncol;
     double x = xb[gr];
@@ -1083,7 +1107,7 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
       }
     }
   }
-  for (int t = tid; t < T; t += kQpThreads) {
+  for (int t = tid; t < T; t += NTH) {
     const double a0 = z[u_index(t, 0, T, order)], a1 = z[u_index(t, 1, T, order)];
     part += a0 * (p.w_accel * a0 + p.w_joint * a1) + a1 * (p.w_joint * a0 + p.w_turning * a1);
     if (t >= 1) {
@@ -1093,10 +1117,10 @@ __global__ __launch_bounds__(kQpThreads) void mpc_qp_kernel(QpArgs A) {
               d1 * (p.w_ch_joint * d0 + p.w_ch_turning * d1);
     }
   }
-  const double cost = block_sum(part, red);
+  const double cost = block_sum<NW>(part, red);
   double sk = skipped;
   double dummy = 0.0;
-  block_max2(sk, dummy, red);
+  block_max2<NW>(sk, dummy, red);
   if (tid == 0) {
     A.out_cost[sc] = cost;
     A.out_status[sc] = status | (sk > 0.0 ? CCMPC_QP_SKIPPED_ROWS : 0);
@@ -1120,17 +1144,18 @@ inline QpPlan qp_plan(int T, int64_t R) {
   return {false, false};
 }
 
-template <bool ROWS_LDS, int NM>
-hipError_t launch_qp(dim3 grid, dim3 block, size_t lds, hipStream_t s, const QpArgs &a) {
+template <bool ROWS_LDS, int NM, int NW>
+hipError_t launch_qp(dim3 grid, size_t lds, hipStream_t s, const QpArgs &a) {
+  const dim3 block(64 * NW);
   // the dynamic-LDS limit is a per-device attribute: set it on every launch (cheap), so a
   // process that drives several devices raises it on each, and report a failure as such
   if (lds > 48 * 1024) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM>),
+        reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM, NW>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kQpLdsBytes));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM, NW>), grid, block, lds, s, a);
   return hipSuccess;
 }
 
@@ -1228,15 +1253,24 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   const int n = 2 * Ti;
   // register-resident factor up to n = 16 (T <= 8, the reference's ph); larger n spills
   const int nm = n <= 16 ? 16 : 0;
-  const dim3 grid(static_cast<unsigned>(n_scenes)), block(kQpThreads);
+  // one wave per scene with the register factor (n <= 16), unless CCMPC_QP_WAVES=4 asks for the
+  // four-wave form (A/B)
+  static const int waves_env = [] {
+    const char *e = getenv("CCMPC_QP_WAVES");
+    return e ? atoi(e) : 1;
+  }();
+  const bool one_wave = nm == 16 && waves_env == 1;
+  const dim3 grid(static_cast<unsigned>(n_scenes));
   hipStream_t s = as_stream(stream);
   hipError_t attr;
   if (in_lds) {
-    attr = nm == 16 ? launch_qp<true, 16>(grid, block, lds, s, a)
-                    : launch_qp<true, 0>(grid, block, lds, s, a);
+    attr = one_wave ? launch_qp<true, 16, 1>(grid, lds, s, a)
+                    : (nm == 16 ? launch_qp<true, 16, 4>(grid, lds, s, a)
+                                : launch_qp<true, 0, 4>(grid, lds, s, a));
   } else {
-    attr = nm == 16 ? launch_qp<false, 16>(grid, block, lds, s, a)
-                    : launch_qp<false, 0>(grid, block, lds, s, a);
+    attr = one_wave ? launch_qp<false, 16, 1>(grid, lds, s, a)
+                    : (nm == 16 ? launch_qp<false, 16, 4>(grid, lds, s, a)
+                                : launch_qp<false, 0, 4>(grid, lds, s, a));
   }
   if (attr != hipSuccess) {
     set_error(std::string(__func__) + ": hipFuncSetAttribute(MaxDynamicSharedMemorySize) "

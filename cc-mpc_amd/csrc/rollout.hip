@@ -151,9 +151,11 @@ template <int RB, bool MINK>
 __global__ __launch_bounds__(256) void ideal_gram_kernel(
     const double *__restrict__ prev_mean, const double *__restrict__ prev_cov, int T_src,
     const int32_t *__restrict__ src_cell, int T, int64_t n, int64_t chunk, int64_t items_per_cell,
-    const double *__restrict__ x0, uint64_t seed, const int32_t *__restrict__ rng_cell,
-    TreeLayout tree, double *__restrict__ out_mean, double *__restrict__ out_cov,
-    int32_t *__restrict__ out_status, MinkParams mp) {
+    const double *__restrict__ x0, uint64_t seed_arg, const uint64_t *__restrict__ seed_dev,
+    const int32_t *__restrict__ rng_cell, TreeLayout tree, double *__restrict__ out_mean,
+    double *__restrict__ out_cov, int32_t *__restrict__ out_status, MinkParams mp) {
+  // seed_dev: the Philox seed from device memory (a graph replays with a fresh seed per frame)
+  const uint64_t seed = seed_dev ? *seed_dev : seed_arg;
   constexpr int NT = n_tiles(RB);
   constexpr int D = 16 * RB;
   constexpr int E = slab_doubles(RB);
@@ -281,7 +283,8 @@ inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
 template <int RB, bool MINK>
 static int launch_ideal_gram(const double *pm, const double *pc, int T_src, const int32_t *src,
                              int n_cells, int T, int64_t n, const double *x0, uint64_t seed,
-                             const int32_t *rng, void *ws, size_t ws_bytes, double *out_mean,
+                             const uint64_t *seed_dev, const int32_t *rng, void *ws,
+                             size_t ws_bytes, double *out_mean,
                              double *out_cov, int32_t *status, const MinkParams &mp,
                              hipStream_t s) {
   const int64_t chunk = ideal_chunk(n_cells, n);
@@ -291,21 +294,22 @@ static int launch_ideal_gram(const double *pm, const double *pc, int T_src, cons
     return CCMPC_ERR_WORKSPACE;
   hipLaunchKernelGGL((ideal_gram_kernel<RB, MINK>), dim3(static_cast<unsigned>(ipc * n_cells)),
                      dim3(64 * ideal_waves(RB)), 0, s, pm, pc, T_src, src, T, n, chunk, ipc, x0,
-                     seed, rng, tree, out_mean, out_cov, status, mp);
+                     seed, seed_dev, rng, tree, out_mean, out_cov, status, mp);
   return CCMPC_OK;
 }
 
 template <bool MINK>
 static int run_ideal(const double *prev_mean, const double *prev_cov, int64_t T_src,
                      const int32_t *src_cell, int64_t n_cells, int64_t T, int64_t n_samples,
-                     const double *x0, uint64_t seed, const int32_t *rng_cell, void *workspace,
-                     size_t ws_bytes, double *out_mean, double *out_cov, int32_t *out_status,
+                     const double *x0, uint64_t seed, const uint64_t *seed_dev,
+                     const int32_t *rng_cell, void *workspace, size_t ws_bytes,
+                     double *out_mean, double *out_cov, int32_t *out_status,
                      const MinkParams &mp, ccmpc_stream_t stream) {
   hipStream_t s = as_stream(stream);
   const int nc = static_cast<int>(n_cells), Ti = static_cast<int>(T), Ts = static_cast<int>(T_src);
 #define IDEAL_ARGS                                                                            \
-  prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, rng_cell, workspace, ws_bytes, \
-      out_mean, out_cov, out_status, mp, s
+  prev_mean, prev_cov, Ts, src_cell, nc, Ti, n_samples, x0, seed, seed_dev, rng_cell, workspace, \
+      ws_bytes, out_mean, out_cov, out_status, mp, s
   int rc;
   switch (row_blocks(T)) {
     case 1: rc = launch_ideal_gram<1, MINK>(IDEAL_ARGS); break;
@@ -381,8 +385,24 @@ extern "C" int ccmpc_ideal_moments(const double *prev_mean, const double *prev_c
   CHECK_IDEAL_ARGS();
   const MinkParams none{};
   return run_ideal<false>(prev_mean, prev_cov, T_src, src_cell, n_cells, T, n_samples, x0, seed,
-                          rng_cell, workspace, workspace_bytes, out_mean, out_cov, out_status, none,
-                          stream);
+                          nullptr, rng_cell, workspace, workspace_bytes, out_mean, out_cov,
+                          out_status, none, stream);
+}
+
+extern "C" int ccmpc_ideal_minkowski_cycle_ex(
+    const double *prev_mean, const double *prev_cov, int64_t T_src, const int32_t *src_cell,
+    int64_t n_cells, int64_t T, int64_t n_samples, const double *x0, uint64_t seed,
+    const uint64_t *seed_dev, const int32_t *rng_cell, void *workspace, size_t workspace_bytes,
+    const double *ref_traj, const int32_t *cell_ref, const double *cell_risk, double R,
+    double tol, int32_t maxiter, double *out_mean, double *out_cov, int32_t *out_status,
+    ccmpc_halfspace *out_rec, double *out_prob_lower, ccmpc_stream_t stream) {
+  CHECK_IDEAL_ARGS();
+  CCMPC_REQUIRE(ref_traj && cell_risk && out_rec && out_prob_lower, "null pointer");
+  CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
+  const MinkParams mp{ref_traj, cell_ref, cell_risk, R, tol, maxiter, out_rec, out_prob_lower};
+  return run_ideal<true>(prev_mean, prev_cov, T_src, src_cell, n_cells, T, n_samples, x0, seed,
+                         seed_dev, rng_cell, workspace, workspace_bytes, out_mean, out_cov,
+                         out_status, mp, stream);
 }
 
 extern "C" int ccmpc_ideal_minkowski_cycle(
@@ -392,11 +412,9 @@ extern "C" int ccmpc_ideal_minkowski_cycle(
     const int32_t *cell_ref, const double *cell_risk, double R, double tol, int32_t maxiter,
     double *out_mean, double *out_cov, int32_t *out_status, ccmpc_halfspace *out_rec,
     double *out_prob_lower, ccmpc_stream_t stream) {
-  CHECK_IDEAL_ARGS();
-  CCMPC_REQUIRE(ref_traj && cell_risk && out_rec && out_prob_lower, "null pointer");
-  CCMPC_REQUIRE(maxiter >= 1, "maxiter must be >= 1");
-  const MinkParams mp{ref_traj, cell_ref, cell_risk, R, tol, maxiter, out_rec, out_prob_lower};
-  return run_ideal<true>(prev_mean, prev_cov, T_src, src_cell, n_cells, T, n_samples, x0, seed,
-                         rng_cell, workspace, workspace_bytes, out_mean, out_cov, out_status, mp,
-                         stream);
+  return ccmpc_ideal_minkowski_cycle_ex(prev_mean, prev_cov, T_src, src_cell, n_cells, T,
+                                        n_samples, x0, seed, nullptr, rng_cell, workspace,
+                                        workspace_bytes, ref_traj, cell_ref, cell_risk, R, tol,
+                                        maxiter, out_mean, out_cov, out_status, out_rec,
+                                        out_prob_lower, stream);
 }

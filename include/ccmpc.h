@@ -242,6 +242,20 @@ int ccmpc_ideal_minkowski_cycle(const double *prev_mean, const double *prev_cov,
                                 ccmpc_halfspace *out_rec, double *out_prob_lower,
                                 ccmpc_stream_t stream);
 
+/* As ccmpc_ideal_minkowski_cycle; seed_dev (nullable) points at the Philox seed in device
+ * memory and overrides `seed`, so a captured graph draws a fresh rollout per replay (the
+ * planning-step graphs of ccmpc/step.py write it with the step's packed inputs). */
+int ccmpc_ideal_minkowski_cycle_ex(const double *prev_mean, const double *prev_cov,
+                                   int64_t T_src, const int32_t *src_cell, int64_t n_cells,
+                                   int64_t T, int64_t n_samples, const double *x0, uint64_t seed,
+                                   const uint64_t *seed_dev, const int32_t *rng_cell,
+                                   void *workspace, size_t workspace_bytes,
+                                   const double *ref_traj, const int32_t *cell_ref,
+                                   const double *cell_risk, double R, double tol, int32_t maxiter,
+                                   double *out_mean, double *out_cov, int32_t *out_status,
+                                   ccmpc_halfspace *out_rec, double *out_prob_lower,
+                                   ccmpc_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * GMM-latent particle sampler (Trajectron++ predict tail behind prediction.py:81-86):
  * z ~ Categorical(p(z|x)) by inverse CDF, per step a = mu + L eps (GMM2D.rsample, one

@@ -255,7 +255,7 @@ def test_graph_cache_is_bounded(gpu):
                                                PH, _ref(0), minpos, pasts)
         assert [ov.n_states for ov in ovs] == list(Ks)
         assert len(agent._graphs) <= 2
-    assert list(agent._graphs)[-1][4] == (1, 1)
+    assert list(agent._graphs.values())[-1].K == [1, 1]
 
 
 def test_kept_mode_without_draws_fails_like_the_reference(gpu):
