@@ -58,6 +58,11 @@ SIGNATURES = {
     "ccmpc_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "ccmpc_copy_async": (ctypes.c_int, [_P, _P, _SZ, _P]),
     "ccmpc_copy_kernel_async": (ctypes.c_int, [_P, _P, _SZ, _P]),
+    "ccmpc_graph_capture_begin": (ctypes.c_int, [_P]),
+    "ccmpc_graph_capture_end": (ctypes.c_int, [_P, _P]),
+    "ccmpc_graph_launch": (ctypes.c_int, [_P, _P]),
+    "ccmpc_signal_host": (ctypes.c_int, [_P, _P, _P]),
+    "ccmpc_graph_destroy": (ctypes.c_int, [_P]),
     "ccmpc_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "ccmpc_moments": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64, _I64, _P,
                                      _SZ, _P, _P, _P]),

@@ -71,6 +71,7 @@ class MonteCarloScenario:
         return out
 
     def episode(self, episode_idx=0):
+        self.steps = []
         stats = standins.AttrDict(success=False, infeasibility=False, steps=0, plan_steps=0,
                                   timeOver=False, initiallyFeasible=False)
         world, ego, ov_ids, map_reader = self.make_world()

@@ -35,9 +35,6 @@ from . import engine, mpc, risk
 from .ovehicle import OVehicle, ScenePredictions
 
 
-_STEP_DEBUG = os.environ.get("CCMPC_STEP_DEBUG", "0") == "1"
-
-
 class InSimulationException(Exception):
     """collect/exception.py:11: the planner's failure (an infeasible QP, :3099-3110)."""
 
@@ -486,11 +483,13 @@ class MidlevelAgent:
         self.mpc_params = mpc.MPCParams.reference_defaults(self.mpc_params_steer)
         self._ltv = None                   # (x_init, T_full) -> (xbar, Gamma), first step's
         self._qp = {}
-        # (O, N, ph, L, K, per_particle, eps_in) -> step.MinkowskiStepGraph, least recently
-        # used first: a graph holds pinned packs, a device store and workspaces, and the kept
-        # modes per OV change from frame to frame in an episode, so the cache is bounded
+        # step-graph key -> step.StepGraph, least recently used first: a graph holds pinned
+        # packs, a device store and workspaces, and the kept modes per OV change from frame to
+        # frame in an episode, so the cache is bounded.  One episode's schedule alone needs
+        # ph + 1 shapes (T = ph Minkowski, T = ph-1 .. 1 shrinking, the receding affine step):
+        # a bound below that recaptures a graph on every step (LRU over a cyclic schedule)
         self._graphs = collections.OrderedDict()
-        self.max_graphs = int(kwargs.get("max_graphs", 8))
+        self.max_graphs = int(kwargs.get("max_graphs", 2 * int(prediction_horizon) + 4))
         if self.max_graphs < 1:
             raise ValueError(f"max_graphs must be >= 1, got {self.max_graphs}")
         self._risk_memo = {}
@@ -524,8 +523,12 @@ class MidlevelAgent:
         return self._sensor_listening
 
     def destroy(self):
-        """:407-412 (no CARLA resources are held; graphs and workspaces are released)."""
+        """:407-412 (no CARLA resources are held).  The step graphs go to the process's pool
+        (step.pool_give), where the next agent of the same shapes takes them captured."""
+        from . import step
         self._sensor_listening = False
+        for key, g in self._graphs.items():
+            step.pool_give(self.device, key + (self.R,), g)
         self._graphs.clear()
 
     def get_goal(self):
@@ -1060,6 +1063,8 @@ class MidlevelAgent:
             sorted(extra.items()))
         g = self._graphs.pop(key, None)
         if g is None:
+            g = step.pool_take(self.device, key + (self.R,))
+        if g is None:
             g = step.StepGraph(O, N, ph, L, K, device=self.device, R=self.R, per_particle=pp,
                                eps_in=eps_in is not None, kind=kind, T=T, **extra)
             while self._graphs and len(self._graphs) >= self.max_graphs:
@@ -1074,9 +1079,6 @@ class MidlevelAgent:
                                (self.seed * 1_000_003 + int(params.frame)) & (2**63 - 1))
         if pp:
             g.set_device_inputs(gmm, z_in, eps_in)
-        if _STEP_DEBUG:
-            print(f"[ccmpc step] frame {params.frame} kind {kind} T {T} K {K} key {key} "
-                  f"graphs {len(self._graphs)} gen {g.generation}", flush=True)
         g.launch()
         # host objects that need no output are built while the graph runs
         st = g.store
@@ -1207,6 +1209,9 @@ class MidlevelAgent:
         goal_t = torch.as_tensor(np.asarray(goal, np.float64).reshape(1, 2), device=dev)
         up = None
         if T < ph:
+            if u_prev is None:
+                raise ValueError(f"Tsh = {T} < ph = {ph} needs u_prev, the controls executed "
+                                 "since the first shrinking step (:3186)")
             up = torch.as_tensor(np.asarray(u_prev, np.float64).reshape(1, 2 * (ph - T)),
                                  device=dev)
         u, X, cost, status, _ = qp.solve(gamma, xbar, goal_t, ref, rec, u_prev=up)

@@ -20,19 +20,30 @@ cell counts on the device.  ``StepGraph`` captures, per kind,
                          moments (the t = 0 statistics, :864-875) } -> copy-out
     affine    (T == ph)  copy-in -> sampler -> bucketing -> moments -> GMM-affine -> copy-out
 
-as graph A, and the L4 outer approximation (vertices / A_union / b_union and the heading
-statistics, :627-736) as graph B, replayed on a side stream after A.  The host waits for A
-only: the records, moments and counts come back without waiting on L4, whose outputs (only
-returned by the generator, never fed to the QP, :951-952) are read lazily.
+with the L4 outer approximation (vertices / A_union / b_union and the heading statistics,
+:627-736) as a second branch of the same graph, forked off once the store is bucketed:
 
-A step is: write the inputs into pinned memory, replay, wait, read the outputs through NumPy
-views of one snapshot.  The Philox seeds travel in the packed inputs (ccmpc_sample_unicycle_ex
+    ... bucketing -+-> generator -> copy-out -> signal A
+                   +-> L4 -> L4 copy-out -> signal B       (side stream, joined at the end)
+
+The host does not synchronise the stream: each branch ends with ccmpc_signal_host, which writes
+the step's generation number into a pinned word after everything the branch wrote, and the
+host polls that word.  So the records, moments and counts are read as soon as their copy-out
+lands, while L4 (only returned by the generator, never fed to the QP, :951-952) is still
+running; its outputs are read lazily, on access.  Two graphs alternate by the generation's
+parity, each with its own L4 output buffers, so the previous step's L4 stays readable while the
+next step runs.
+
+A step is: write the inputs into pinned memory, launch one graph, poll, read the outputs
+through NumPy views of one snapshot.  The Philox seeds travel in the packed inputs (ccmpc_sample_unicycle_ex
 and ccmpc_ideal_minkowski_cycle_ex read them on the device), so every replay draws afresh.
 
 Outputs live in the graph's buffers until the next replay of the same graph; what the caller
 keeps across steps (the saved moments) is copied out.
 """
+import collections
 import os
+import time
 
 import numpy as np
 import torch
@@ -82,9 +93,47 @@ class Pack:
         return {name: nd(shape, dt, raw, off) for name, shape, dt, off in self._views}
 
 
+class HipGraph:
+    """An executable graph captured through ccmpc_graph_capture_* (the library's calls and the
+    fork / join event pairs only), replayed on the current stream; destroyed with the object,
+    after the device has drained (its last replay may still run)."""
+
+    def __init__(self, device, fn, stream):
+        """Capture fn() on `stream`."""
+        import ctypes
+        lib = _lib.load()
+        self.device, self.exec = device, None
+        with torch.cuda.stream(stream):
+            s = engine._stream()
+            _lib.check(lib.ccmpc_graph_capture_begin(s), "ccmpc_graph_capture_begin")
+            ex = ctypes.c_void_p()
+            try:
+                fn()
+            finally:
+                rc = lib.ccmpc_graph_capture_end(s, ctypes.byref(ex))
+            _lib.check(rc, "ccmpc_graph_capture_end")
+        self.exec = ex.value
+        self._launch = lib.ccmpc_graph_launch
+
+    def replay(self, stream=None):
+        """Launch on `stream` (a raw stream handle; default: torch's current stream)."""
+        rc = self._launch(self.exec, engine._stream() if stream is None else stream)
+        if rc != 0:
+            _lib.check(rc, "ccmpc_graph_launch")
+
+    def __del__(self):
+        if self.exec:
+            try:
+                torch.cuda.synchronize(self.device)
+                _lib.load().ccmpc_graph_destroy(self.exec)
+            except Exception:       # interpreter shutdown: the process releases it
+                pass
+            self.exec = None
+
+
 class StepGraph:
-    """Sampler -> bucketing -> the step's generator kernels (graph A) and L4 (graph B) for one
-    shape.
+    """Sampler -> bucketing -> the step's generator kernels and, as a parallel branch, L4, for
+    one shape.
 
     O OVs with N particles each over ph steps; L latent values; K kept modes per OV (the host
     decides them from p(z|x), as make_ovehicles does, so the shape is known before the step
@@ -131,7 +180,8 @@ class StepGraph:
         f64, f32, i32, i64, u8 = torch.float64, torch.float32, torch.int32, torch.int64, torch.uint8
         ph_, L_ = self.ph, self.L
         gmm_field = [] if self.per_particle else [("gmm", (O, L_, ph_, 5), f32)]
-        fields = ([("seed", (1,), i64), ("init", (O, 4), f64), ("cdf", (O, L_), f64)] + gmm_field +
+        fields = ([("gen", (2,), i64), ("seed", (1,), i64), ("init", (O, 4), f64),
+                   ("cdf", (O, L_), f64)] + gmm_field +
                   [("keep", (O, L_), i32), ("nk", (O,), i32), ("base", (O,), i32),
                    ("minpos", (O, 2), f64), ("region", (O,), i64), ("origin", (C, 2), f64),
                    ("ref", (1, T, 2), f64), ("past", (C, 2), f64), ("bbox", (C, 2), f64)])
@@ -164,8 +214,13 @@ class StepGraph:
             out += [("imean", (C, T, 2), f64), ("icov", (C, 2 * T, 2 * T), f64),
                     ("status", (C,), i32)]
         self.out = Pack(out, self.device)
-        self.out_l4 = Pack([("A", (C, ph_, 4, 2), f64), ("b", (C, ph_, 4), f64),
-                            ("yaw_mean", (C, ph_), f64), ("yaw0_var", (C,), f64)], self.device)
+        # one L4 output pack per generation parity (the two graphs alternate)
+        self.out_l4s = [Pack([("A", (C, ph_, 4, 2), f64), ("b", (C, ph_, 4), f64),
+                              ("yaw_mean", (C, ph_), f64), ("yaw0_var", (C,), f64)], self.device)
+                        for _ in range(2)]
+        # pinned signal words: [0] the record path's generation, [2 + 2 p] parity p's L4
+        self.flags = torch.zeros(8, dtype=i64, pin_memory=True)
+        self._flags = self.flags.numpy()
         # small clouds: sampler + bucketing in three short launches (ccmpc_sample_bucket), whose
         # cells need K (N + 4) slots per OV; else the sampler's sample-order store + ccmpc_bucket
         fused_ws = lib.ccmpc_sample_bucket_workspace_bytes(O, N, ph_, self.max_k) \
@@ -196,12 +251,15 @@ class StepGraph:
                 device=self.device)
         self.ws = engine.Workspace(self.device)
         self.ws.get(lib.ccmpc_moments_workspace_bytes(ph_, C, st.n_bound))
+        # fork / join events per parity graph, alive as long as the graphs are: an event
+        # recorded into a capture and destroyed before the graph (what wait_stream's temporary
+        # does) left a dangling reference that crashed the replay once the memory was reused
+        self._ev = [{k: torch.cuda.Event() for k in ("fork", "join", "l4f", "l4j")}
+                    for _ in range(2)]
         if kind == "ideal":         # its own: the rollout runs beside the scene's moments
             self.ideal_ws = engine.Workspace(self.device)
             self.ideal_ws.get(lib.ccmpc_ideal_moments_workspace_bytes(T, C, self.n_ideal))
             self.aux = torch.cuda.Stream(device=self.device)
-            self._ev_fork = torch.cuda.Event()
-            self._ev_join = torch.cuda.Event()
             # the rollout as a branch beside the sampling, or (CCMPC_STEP_IDEAL_FORK=0) first on
             # the one stream
             self.ideal_fork = os.environ.get("CCMPC_STEP_IDEAL_FORK", "1") == "1"
@@ -212,10 +270,16 @@ class StepGraph:
         # (CCMPC_STEP_COPY_KERNEL=0) as memcpy nodes (a runtime blit of ~4.8 us each): the
         # kernels take ~8 us off a step (profiles/r02/v33_step_copy_kernel.txt)
         self.copy_kernel = os.environ.get("CCMPC_STEP_COPY_KERNEL", "1") == "1"
-        self.graph = self.graph_l4 = None
+        self.graphs = None                  # [parity 0, parity 1]
+        # launches before this one run eagerly (the same calls, no capture): a shape used once
+        # -- each shrinking horizon of an episode on a fresh agent -- never pays the capture
+        # and instantiation (two graphs, ~2-3 ms), a shape that recurs is graphed from its
+        # second launch on
+        self.capture_at = int(os.environ.get("CCMPC_STEP_CAPTURE_AT", "2"))
+        # the library's own capture (HipGraph), or (CCMPC_STEP_TORCH_GRAPH=1) torch.cuda.CUDAGraph
+        self.torch_graph = os.environ.get("CCMPC_STEP_TORCH_GRAPH", "0") == "1"
         self._static_set = False
-        self._l4_cur = None                 # snapshot of the current generation's L4 outputs
-        self._l4_prev = None                # (generation, snapshot) of the one before
+        self._l4_snap = {}                  # generation -> snapshot of its L4 outputs
 
     # ---------------------------------------------------------------------------------------
     def _sample_calls(self, s):
@@ -247,23 +311,21 @@ class StepGraph:
                                     p(st.pos), st.ld, p(o.d("off")), p(o.d("cnt")),
                                     p(o.d("pmf")), p(o.d("centre")), s))]
 
-    def _enqueue(self):
-        """Graph A on the current stream."""
+    def _enqueue(self, parity=0):
+        """One step on the current stream (the graph of `parity`, or its eager form)."""
         lib, p, s = _lib.load(), engine._p, engine._stream()
         i, o, st = self.inp, self.out, self.store
         T, C, ph = self.T, self.C, self.ph
+        ev = self._ev[parity]
         chk = engine._lib.check
         copy = lib.ccmpc_copy_kernel_async if self.copy_kernel else lib.ccmpc_copy_async
         chk(copy(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
         main = torch.cuda.current_stream(self.device)
         if self.kind == "ideal":
-            # the rollout needs only the saved moments: a branch beside the sampling.  The fork
-            # / join events are the graph's own, alive as long as it is: an event recorded into
-            # a capture and destroyed before the graph (what wait_stream's temporary does) left
-            # a dangling reference that crashed the replay once the memory was reused
+            # the rollout needs only the saved moments: a branch beside the sampling
             if self.ideal_fork:
-                self._ev_fork.record(main)
-                self.aux.wait_event(self._ev_fork)
+                ev["fork"].record(main)
+                self.aux.wait_event(ev["fork"])
             with torch.cuda.stream(self.aux if self.ideal_fork else main):
                 iws = self.ideal_ws.buf
                 chk(lib.ccmpc_ideal_minkowski_cycle_ex(
@@ -274,6 +336,11 @@ class StepGraph:
                     p(o.d("pl")), engine._stream()), "ccmpc_ideal_minkowski_cycle_ex")
         for fn, args in self._sample_calls(s):
             chk(fn(*args), fn.__name__)
+        # L4 only reads the bucketed store: a branch beside the generator
+        ev["l4f"].record(main)
+        self.side.wait_event(ev["l4f"])
+        with torch.cuda.stream(self.side):
+            self._enqueue_l4(parity)
         mws = self.ws.buf
         if self.kind == "minkowski":
             chk(lib.ccmpc_minkowski_cycle(
@@ -289,14 +356,18 @@ class StepGraph:
                 chk(lib.ccmpc_affine(p(o.d("mean")), p(o.d("cov")), T, C, p(i.d("ref")), None,
                                      p(i.d("gamma")), self.R, p(o.d("rec")), s), "ccmpc_affine")
             elif self.ideal_fork:
-                self._ev_join.record(self.aux)
-                main.wait_event(self._ev_join)
+                ev["join"].record(self.aux)
+                main.wait_event(ev["join"])
         chk(copy(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
+        chk(lib.ccmpc_signal_host(p(self.flags), p(i.d("gen")), s), "ccmpc_signal_host")
+        ev["l4j"].record(self.side)
+        main.wait_event(ev["l4j"])
 
-    def _enqueue_l4(self):
-        """Graph B on the current stream: L4 over the bucketed store, then its copy-out."""
+    def _enqueue_l4(self, parity):
+        """The L4 branch on the current stream: L4 over the bucketed store, its copy-out into
+        the parity's pack, its signal."""
         lib, p, s = _lib.load(), engine._p, engine._stream()
-        i, o, q, st = self.inp, self.out, self.out_l4, self.store
+        i, o, q, st = self.inp, self.out, self.out_l4s[parity], self.store
         copy = lib.ccmpc_copy_kernel_async if self.copy_kernel else lib.ccmpc_copy_async
         lws = self.l4_ws.buf
         chk = engine._lib.check
@@ -306,9 +377,11 @@ class StepGraph:
                                p(q.d("A")), p(q.d("b")), p(q.d("yaw_mean")),
                                p(q.d("yaw0_var")), None, None, s), "ccmpc_l4_split")
         chk(copy(p(q.host), p(q.dev), q.nbytes, s), "ccmpc_copy_async")
+        chk(lib.ccmpc_signal_host(p(self.flags[2 + 2 * parity:]), p(i.d("gen")), s),
+            "ccmpc_signal_host")
 
     def capture(self):
-        """Record graphs A and B (after one eager run of each that warms every kernel).
+        """Record the two parity graphs (after one eager run that warms every kernel).
 
         torch hands out streams from a small pool, so this graph's capture / aux / side
         streams can be another graph's streams, which may still hold that graph's last L4
@@ -319,15 +392,18 @@ class StepGraph:
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            self._enqueue()
-            self._enqueue_l4()
+            self._enqueue(0)
         torch.cuda.synchronize(self.device)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=s):
-            self._enqueue()
-        self.graph_l4 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_l4, stream=s):
-            self._enqueue_l4()
+        graphs = []
+        for par in range(2):
+            if self.torch_graph:    # A/B: torch's graph object around the same capture
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    self._enqueue(par)
+            else:
+                g = HipGraph(self.device, lambda par=par: self._enqueue(par), s)
+            graphs.append(g)
+        self.graphs = graphs
         torch.cuda.synchronize(self.device)
         return self
 
@@ -439,32 +515,46 @@ class StepGraph:
             raise ValueError("this graph draws the noise itself (built without eps_in)")
 
     def launch(self, direct=False):
-        """Enqueue one step without waiting: graph A on the current stream, then graph B (L4)
-        on the side stream once A is done.  direct: the same C-ABI calls enqueued eagerly
-        instead of the graph replays."""
-        # the previous generation's L4 outputs stay readable until the replay after this one
-        if self.generation > 0:
-            self._l4_prev = (self.generation, self.l4_outputs(self.generation))
-        self._l4_cur = None
+        """Enqueue one step on the current stream without waiting (the graph of this
+        generation's parity).  direct: the same C-ABI calls enqueued eagerly instead."""
         self.generation += 1
-        main = torch.cuda.current_stream(self.device)
-        main.wait_stream(self.side)      # the last L4 has read the store this replay rewrites
-        if direct:
-            self._enqueue()
+        gen = self.generation
+        self.inp.h("gen")[0] = gen      # read by this step's copy-in, then by its two signals
+        if direct or (self.graphs is None and gen < self.capture_at):
+            self._enqueue(gen & 1)
+            return
+        if self.graphs is None:
+            self.capture()
+        g = self.graphs[gen & 1]
+        if self.torch_graph:
+            g.replay()
         else:
-            if self.graph is None:
-                self.capture()
-            self.graph.replay()
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
-            if direct:
-                self._enqueue_l4()
-            else:
-                self.graph_l4.replay()
+            g.replay(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _poll(self, slot, gen, what):
+        """Spin until the pinned signal word `slot` reaches `gen`.  A word that does not arrive
+        within 5 s (a faulted kernel never signals) synchronises the device, which raises the
+        error, or else reports the missing signal."""
+        f = self._flags
+        if f[slot] >= gen:
+            return
+        deadline, n = None, 0
+        while f[slot] < gen:
+            n += 1
+            if n & 0x3FF == 0:
+                now = time.perf_counter()
+                if deadline is None:
+                    deadline = now + 5.0
+                elif now > deadline:
+                    torch.cuda.synchronize(self.device)
+                    if f[slot] < gen:
+                        raise RuntimeError(f"planning step {gen}: the {what} signal never came "
+                                           f"(word {slot} = {int(f[slot])})")
 
     def wait(self):
-        """Return when the launched step's output pack (graph A) is on the host."""
-        torch.cuda.current_stream(self.device).synchronize()
+        """Return when the launched step's output pack (records, moments, counts) is on the
+        host; the L4 branch may still run."""
+        self._poll(0, self.generation, "record path")
 
     def replay(self):
         """One step; returns when the output pack is on the host."""
@@ -473,23 +563,59 @@ class StepGraph:
 
     def l4_outputs(self, generation=None):
         """{A, b, yaw_mean, yaw0_var} host arrays of launch `generation` (default: the latest),
-        waiting for its L4 graph; the generation before the latest stays readable, older ones
-        raise (their buffers were overwritten)."""
+        waiting for its L4 branch; the latest two generations are readable (their parity packs
+        are intact), older ones only if read before (snapshots), else they raise."""
         gen = self.generation if generation is None else generation
-        if gen == self.generation:
-            if self._l4_cur is None:
-                self.side.synchronize()
-                self._l4_cur = self.out_l4.snapshot()
-            return self._l4_cur
-        if self._l4_prev is not None and self._l4_prev[0] == gen:
-            return self._l4_prev[1]
-        raise RuntimeError(f"stale planning-step data: the L4 outputs of launch {gen} were "
-                           f"overwritten (this graph is at launch {self.generation})")
+        snap = self._l4_snap.get(gen)
+        if snap is not None:
+            return snap
+        if gen < 1 or gen < self.generation - 1 or gen > self.generation:
+            raise RuntimeError(f"stale planning-step data: the L4 outputs of launch {gen} were "
+                               f"overwritten (this graph is at launch {self.generation})")
+        self._poll(2 + 2 * (gen & 1), gen, "L4")
+        snap = self.out_l4s[gen & 1].snapshot()
+        self._l4_snap = {k: v for k, v in self._l4_snap.items() if k >= self.generation - 1}
+        self._l4_snap[gen] = snap
+        return snap
 
     def records(self):
         return self.out.h("rec").reshape(-1).view(
             _lib.AFFINE_DTYPE if self.kind == "affine" else _lib.HALFSPACE_DTYPE).reshape(
             self.C, -1)
+
+
+# Step graphs released by agents that were destroyed (MidlevelAgent.destroy), by (device,
+# key): the reference harness builds a fresh agent per episode and destroys the last one
+# (tests/Hz20/__init__.py:383-399), so the next agent takes the same shapes' graphs -- already
+# captured -- instead of building them again.  A graph belongs to one agent at a time; its
+# generation counter keeps counting, so objects the old agent handed out still refuse reads
+# after the new owner's first replay.  Bounded: the least recently released go first.
+_POOL = collections.OrderedDict()
+POOL_MAX = 64
+
+
+def pool_take(device, key):
+    """A released graph of this shape, or None."""
+    k = (str(device), key)
+    lst = _POOL.get(k)
+    if not lst:
+        return None
+    g = lst.pop()
+    if not lst:
+        del _POOL[k]
+    return g
+
+
+def pool_give(device, key, g):
+    """Release a graph its agent no longer uses."""
+    k = (str(device), key)
+    _POOL.setdefault(k, []).append(g)
+    _POOL.move_to_end(k)
+    while sum(len(v) for v in _POOL.values()) > POOL_MAX:
+        k0 = next(iter(_POOL))
+        _POOL[k0].pop(0)
+        if not _POOL[k0]:
+            del _POOL[k0]
 
 
 def _as_i64(seed):

@@ -66,3 +66,75 @@ extern "C" int ccmpc_copy_kernel_async(void *dst, const void *src, size_t bytes,
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }
+
+// One 8-byte value from device memory to a pinned host word, made visible to the host after
+// everything this stream wrote before it: a system-scope release (which writes back the L2, so
+// an earlier kernel's writes to host memory land first), then a system-scope store.  The host
+// polls the word instead of synchronising the stream (ccmpc/step.py: a step's records are on
+// the host as soon as their copy-out is, while the L4 branch of the same graph still runs).
+__global__ __launch_bounds__(64) void signal_host_kernel(int64_t *dst, const int64_t *src) {
+  if (threadIdx.x != 0) return;
+  const int64_t v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope (the default)
+  __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int ccmpc_signal_host(int64_t *host_word, const int64_t *value, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(host_word && value, "null pointer");
+  CCMPC_REQUIRE(ccmpc::aligned(host_word, 8) && ccmpc::aligned(value, 8),
+                "pointers must be 8-byte aligned");
+  hipLaunchKernelGGL(signal_host_kernel, dim3(1), dim3(64), 0, ccmpc::as_stream(stream),
+                     host_word, value);
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}
+
+// Stream capture into an executable graph, replay and release (ccmpc/step.py's planning-step
+// graphs capture only this library's calls and event record / wait pairs, so they need no
+// framework graph object).  Relaxed capture mode: calls of other threads are not affected.
+extern "C" int ccmpc_graph_capture_begin(ccmpc_stream_t stream) {
+  const hipError_t e = hipStreamBeginCapture(ccmpc::as_stream(stream), hipStreamCaptureModeRelaxed);
+  if (e != hipSuccess) {
+    ccmpc::set_error(std::string("ccmpc_graph_capture_begin: ") + hipGetErrorString(e));
+    return CCMPC_ERR_LAUNCH;
+  }
+  return CCMPC_OK;
+}
+
+extern "C" int ccmpc_graph_capture_end(ccmpc_stream_t stream, void **out_exec) {
+  CCMPC_REQUIRE(out_exec, "null pointer");
+  *out_exec = nullptr;
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(ccmpc::as_stream(stream), &g);
+  if (e == hipSuccess) {
+    hipGraphExec_t x = nullptr;
+    e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e == hipSuccess) *out_exec = x;
+  }
+  if (e != hipSuccess) {
+    ccmpc::set_error(std::string("ccmpc_graph_capture_end: ") + hipGetErrorString(e));
+    return CCMPC_ERR_LAUNCH;
+  }
+  return CCMPC_OK;
+}
+
+extern "C" int ccmpc_graph_launch(void *exec, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(exec, "null graph");
+  const hipError_t e = hipGraphLaunch(static_cast<hipGraphExec_t>(exec), ccmpc::as_stream(stream));
+  if (e != hipSuccess) {
+    ccmpc::set_error(std::string("ccmpc_graph_launch: ") + hipGetErrorString(e));
+    return CCMPC_ERR_LAUNCH;
+  }
+  return CCMPC_OK;
+}
+
+extern "C" int ccmpc_graph_destroy(void *exec) {
+  if (!exec) return CCMPC_OK;
+  const hipError_t e = hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec));
+  if (e != hipSuccess) {
+    ccmpc::set_error(std::string("ccmpc_graph_destroy: ") + hipGetErrorString(e));
+    return CCMPC_ERR_LAUNCH;
+  }
+  return CCMPC_OK;
+}

@@ -32,6 +32,7 @@ constexpr int kQpThreads = 256;
 constexpr int kQpWaves = kQpThreads / 64;
 constexpr int kQpMaxT = 40;
 constexpr size_t kQpLdsBytes = 160 * 1024;
+constexpr int kQpRowDoubles = 10;  // doubles per constraint row in the row store (Rows)
 
 // ---- the LTV model ---------------------------------------------------------------------------
 // About u = 0 the bicycle model's nominal trajectory is straight at constant speed
@@ -106,7 +107,7 @@ struct QpArgs {
 // Sizes (doubles) of the LDS image; shared by host (launch sizing) and device (carving).
 struct QpLayout {
   int n, T3, ldm;
-  int gs, m, c3, y, yd, qf, q, bw, f, z, dz, rd, rh, e2, lb, ub, dinv, red;
+  int gs, m, hc, c3, y, yd, qf, q, bw, f, z, dz, rd, rh, e2, lb, ub, dinv, red;
   int pw, ps, pact, pdinv;  // the polish step's W = L^{-1} G_A^T, S = W^T W, active rows
   int rows, total;
   __host__ __device__ QpLayout(int T, int64_t R, bool rows_lds, bool polish) {
@@ -116,15 +117,16 @@ struct QpLayout {
     int o = 0;
     gs = o; o += T3 * n;
     m = o; o += n * ldm;
+    hc = o; o += n * n;  // H_ctrl (constant over the iterations)
     c3 = o; o += T3;
     y = o; o += T3;
+    z = o; o += n;   // right behind y: the rows index [y | z] as one vector
     yd = o; o += T3;
+    dz = o; o += n;  // likewise behind yd
     qf = o; o += T3;
     q = o; o += T3;
     bw = o; o += 4 * T;
     f = o; o += n;
-    z = o; o += n;
-    dz = o; o += n;
     rd = o; o += n;
     rh = o; o += n;
     e2 = o; o += n;
@@ -141,7 +143,7 @@ struct QpLayout {
     }
     rows = o;
     const int64_t mrows = 2 * n + 2 * T + R;
-    if (rows_lds) o += static_cast<int>(4 * mrows + 4 * R);
+    if (rows_lds) o += static_cast<int>(kQpRowDoubles * mrows);
     total = o;
   }
 };
@@ -150,27 +152,72 @@ __host__ __device__ inline int64_t qp_rows_per_cell(int T, int kind) {
   return kind == CCMPC_REC_KIND_HALFSPACE ? int64_t(T) * (T - 1) / 2 : T;
 }
 
-// row store: s, l, ds, dl over all m rows (box 2n, speed 2T, obstacle R), then the obstacle
-// rows' a0, a1, b' (b' = b - a . c_xy, the constant part of the state moved to the right) and
-// step t (as a double; a lookup instead of re-deriving it from the row index)
+// row store over all m rows (box 2n, speed 2T, obstacle R): s, l, ds, dl, then every row in
+// one form, g_r(v) = c0 v[i0] + c1 v[i1] + cst over v = [y (T3) | z (n)] (the layout keeps z
+// right behind y, and dz behind yd), so evaluating a row is two loads and two FMAs with no
+// branch on the row's kind.  Box row 2j (+1): c0 = +1 (-1) on z_j, cst = -ub_j (lb_j); speed
+// row 2t (+1): +1 (-1) on v_t, cst = c_v - max_v (-c_v); obstacle row: c = a, i = (3t, 3t+1),
+// cst = -b' (b' = b - a . c_xy, the constant part of the state moved to the right).
 struct Rows {
-  double *s, *l, *ds, *dl, *a0, *a1, *b, *t;
+  double *s, *l, *ds, *dl, *c0, *c1, *cst;
+  int32_t *ix;      // (i0, i1) per row
+  double *rp, *is;  // this iteration's primal residual g + s and 1 / s (set in I1)
 };
 
+// Lane moves inside a row of 16 (DPP; f64 as two 32-bit halves).  `old` is what a lane keeps
+// if its source is out of range -- never the case for the controls used here, with the whole
+// wave active (every caller reduces in wave-uniform control flow).
+template <int CTRL>
+__device__ __forceinline__ double qp_dpp(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo =
+      __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(u), CTRL, 0xf, 0xf, false);
+  const uint32_t hi =
+      __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+constexpr int kDppQuad1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppQuad2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // lane i of 8 <- lane 7-i: the other quad
+constexpr int kDppMirror = 0x140;      // lane i of 16 <- lane 15-i: the other half-row
+
+__device__ __forceinline__ double lane_bcast(double v, int src) {  // src wave-uniform
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), src);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), src);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// Sum over each group of 4 / 8 consecutive lanes (every lane of the group gets it)
+__device__ __forceinline__ double sum4(double v) {
+  v += qp_dpp<kDppQuad1>(v);
+  return v + qp_dpp<kDppQuad2>(v);
+}
+__device__ __forceinline__ double sum8(double v) {
+  v = sum4(v);
+  return v + qp_dpp<kDppHalfMirror>(v);
+}
+
+// Whole-wave reductions: four DPP steps reduce each row of 16, then the four row results are
+// combined in a fixed order from lanes 0, 16, 32, 48 (uniform result, no LDS round trips)
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = sum8(v);
+  v += qp_dpp<kDppMirror>(v);
+  return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
 }
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmax(v, qp_dpp<kDppQuad1>(v));
+  v = fmax(v, qp_dpp<kDppQuad2>(v));
+  v = fmax(v, qp_dpp<kDppHalfMirror>(v));
+  v = fmax(v, qp_dpp<kDppMirror>(v));
+  return fmax(fmax(lane_bcast(v, 0), lane_bcast(v, 16)), fmax(lane_bcast(v, 32), lane_bcast(v, 48)));
 }
 __device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmin(v, qp_dpp<kDppQuad1>(v));
+  v = fmin(v, qp_dpp<kDppQuad2>(v));
+  v = fmin(v, qp_dpp<kDppHalfMirror>(v));
+  v = fmin(v, qp_dpp<kDppMirror>(v));
+  return fmin(fmin(lane_bcast(v, 0), lane_bcast(v, 16)), fmin(lane_bcast(v, 32), lane_bcast(v, 48)));
 }
 
 // Block reductions of up to 2 values (every thread gets the result); two barriers.  NW = 1
@@ -248,12 +295,6 @@ __device__ __forceinline__ void block_argmax(double &v, double &idx, double *red
   __syncthreads();
 }
 
-__device__ __forceinline__ double lane_bcast(double v, int src) {  // src wave-uniform
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), src);
-  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), src);
-  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
-}
 
 // wave-level ordering of LDS traffic between the lanes of wave 0 (one wave executes its LDS
 // instructions in order; this keeps the compiler from moving them across the step)
@@ -357,9 +398,11 @@ __device__ __forceinline__ void wave_store2(double *x, int N, const double b[2])
 // IPM factors and solves twice per iteration, and with L in registers a column step is a
 // readlane and an FMA instead of a dependent LDS round trip.  a[k] = L[lane][k] (row form),
 // dl = 1 / L[lane][lane]; the L^T solve reads L's rows from LDS (independent of the chain, so
-// the unrolled loads issue ahead of it).
-template <int NM>
-__device__ __forceinline__ bool reg_cholesky(double (&a)[NM], int n, double &dl) {
+// the unrolled loads issue ahead of it).  The matrix is padded to NM x NM with the identity
+// (rows and columns >= n; the right-hand side 0 there), so every step runs unconditionally:
+// straight-line code, no per-column branch on a runtime n.
+template <int NM, bool SKIP = true>
+__device__ __forceinline__ bool reg_cholesky(double (&a)[NM], double &dl) {
   const int lane = threadIdx.x & 63;
   bool fail = false;
   double diag0 = 0.0;  // the lane's original diagonal (for the pivot-skip threshold)
@@ -368,11 +411,14 @@ __device__ __forceinline__ bool reg_cholesky(double (&a)[NM], int n, double &dl)
     if (k == lane) diag0 = a[k];
 #pragma unroll
   for (int j = 0; j < NM; ++j) {
-    if (j < n) {
+    {
       double d = lane_bcast(a[j], j);
       const double ajj = lane_bcast(diag0, j);
       fail = fail || !isfinite(d) || !isfinite(ajj);
-      if (!(d > 1e-30 * ajj)) d = 1e128;
+      if (!(d > 1e-30 * ajj)) {  // pivot skip (the IPM), or a failure (SKIP = false)
+        fail = fail || !SKIP;
+        d = 1e128;
+      }
       // sqrt and 1/sqrt from the hardware rsqrt + one Goldschmidt step (~1 ulp; the IPM's
       // factor needs no IEEE rounding, the polish recomputes the answer from H exactly)
       const double y = __builtin_amdgcn_rsq(d);
@@ -387,35 +433,50 @@ __device__ __forceinline__ bool reg_cholesky(double (&a)[NM], int n, double &dl)
       // trailing update without an exec-mask branch: rows above k pick up values in their
       // (never read) upper triangle; lij = 0 for rows < j keeps their finished rows intact
 #pragma unroll
-      for (int k = j + 1; k < NM; ++k) {
-        if (k < n) a[k] = fma(-lij, lane_bcast(lij, k), a[k]);
-      }
+      for (int k = j + 1; k < NM; ++k) a[k] = fma(-lij, lane_bcast(lij, k), a[k]);
     }
   }
   return fail;
 }
 
+// lt[j] = L[j][lane], the L^T solve's column (from L's lower triangle in LDS, row stride ld)
+template <int NM>
+__device__ __forceinline__ void reg_load_lt(const double *L, int ld, int n, double (&lt)[NM]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < NM; ++j) {  // every lane loads (in-bounds index), then selects
+    const double v = L[(j < n ? j : 0) * ld + (lane < j ? lane : 0)];
+    lt[j] = (lane < j && j < n) ? v : 0.0;
+  }
+}
+template <int NM>  // b <- L^{-1} b (b on lane = row)
+__device__ __forceinline__ double reg_forward(const double (&a)[NM], double dl, double b) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < NM; ++j) {
+    const double yj = lane_bcast(b, j) * lane_bcast(dl, j);
+    const double upd = fma(-a[j], yj, b);
+    b = lane == j ? yj : (lane > j ? upd : b);
+  }
+  return b;
+}
+template <int NM>  // b <- L^{-T} b
+__device__ __forceinline__ double reg_backward(const double (&lt)[NM], double dl, double b) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = NM - 1; j >= 0; --j) {
+    const double xj = lane_bcast(b, j) * lane_bcast(dl, j);
+    const double upd = fma(-lt[j], xj, b);
+    b = lane == j ? xj : (lane < j ? upd : b);
+  }
+  return b;
+}
 template <int NM>
 __device__ __forceinline__ double reg_solve(const double (&a)[NM], const double *L, int ld,
                                             double dl, int n, double b) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int j = 0; j < NM; ++j) {  // L y = b
-    if (j < n) {
-      const double yj = lane_bcast(b, j) * lane_bcast(dl, j);
-      const double upd = fma(-a[j], yj, b);
-      b = lane == j ? yj : (lane > j ? upd : b);
-    }
-  }
-#pragma unroll
-  for (int j = NM - 1; j >= 0; --j) {  // L^T x = y
-    if (j < n) {
-      const double xj = lane_bcast(b, j) * lane_bcast(dl, j);
-      const double upd = fma(-L[j * ld + (lane < j ? lane : 0)], xj, b);
-      b = lane == j ? xj : (lane < j ? upd : b);
-    }
-  }
-  return b;
+  double lt[NM];  // read ahead of the chain
+  reg_load_lt(L, ld, n, lt);
+  return reg_backward(lt, dl, reg_forward(a, dl, b));
 }
 
 // control index of U_t component c: cp.reshape(u, (T, 2)) is column-major by default
@@ -474,6 +535,9 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   extern __shared__ double lds[];
   const int64_t sc = blockIdx.x;
   if (sc >= A.S) return;
+#ifdef CCMPC_QP_TRACE
+  const uint64_t tk0 = wall_clock64();
+#endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int T = A.T, Tf = A.Tf, Tp = Tf - T;
   const int64_t c0 = A.scene_cell[sc], ncell = A.scene_cell[sc + 1] - c0;
@@ -483,7 +547,8 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   const int n = lay.n, T3 = lay.T3, ldm = lay.ldm;
   const int nbox = 2 * n, nv = 2 * T;
   const int64_t mrows = nbox + nv + R;
-  double *Gs = lds + lay.gs, *M = lds + lay.m, *c3 = lds + lay.c3, *y = lds + lay.y,
+  double *Gs = lds + lay.gs, *M = lds + lay.m, *Hc = lds + lay.hc, *c3 = lds + lay.c3,
+         *y = lds + lay.y,
          *yd = lds + lay.yd, *qf = lds + lay.qf, *q = lds + lay.q, *bw = lds + lay.bw,
          *z = lds + lay.z, *dz = lds + lay.dz, *rd = lds + lay.rd, *rh = lds + lay.rh,
          *e2 = lds + lay.e2, *lb = lds + lay.lb,
@@ -493,10 +558,20 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     rbase = lds + lay.rows;
   } else {
     const int64_t mcap = 2 * n + 2 * T + A.max_cells * P;
-    rbase = A.ws + sc * (4 * mcap + 4 * A.max_cells * P);
+    rbase = A.ws + sc * kQpRowDoubles * mcap;
   }
-  const Rows rw{rbase, rbase + mrows, rbase + 2 * mrows, rbase + 3 * mrows, rbase + 4 * mrows,
-                rbase + 4 * mrows + R, rbase + 4 * mrows + 2 * R, rbase + 4 * mrows + 3 * R};
+  const Rows rw{rbase,
+                rbase + mrows,
+                rbase + 2 * mrows,
+                rbase + 3 * mrows,
+                rbase + 4 * mrows,
+                rbase + 5 * mrows,
+                rbase + 6 * mrows,
+                reinterpret_cast<int32_t *>(rbase + 7 * mrows),
+                rbase + 8 * mrows,
+                rbase + 9 * mrows};
+  // the obstacle rows' a0, a1 (indexed by obstacle row o = r - nbox - nv)
+  const double *oa0 = rw.c0 + nbox + nv, *oa1 = rw.c1 + nbox + nv;
   // step t of obstacle row o (records of a cell in (t, tau) order, or one per t for affine)
   auto obst_step = [&](int64_t o) -> int {
     const int64_t cell = o / P;
@@ -544,6 +619,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     lb[j] = c == 0 ? p.min_a : -p.max_delta;
     z[j] = 0.0;
   }
+  for (int e = tid; e < n * n; e += NTH) Hc[e] = hctrl(e / n, e % n, T, order, p);
   qp_sync<NW>();
   for (int k = tid; k < T3; k += NTH) {
     // objective's linear term in output space: 2 (w_ref (c - ref_t) + [t = T-1] w_final (c - g))
@@ -587,11 +663,33 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     } else {
       skipped = 1;
     }
-    rw.a0[r] = a0;
-    rw.a1[r] = a1;
-    rw.b[r] = b;
-    rw.t[r] = static_cast<double>(obst_step(r));
+    const int64_t ro = nbox + nv + r;
+    const int ts = obst_step(r);
+    rw.c0[ro] = a0;
+    rw.c1[ro] = a1;
+    rw.cst[ro] = -b;
+    rw.ix[2 * ro] = 3 * ts;
+    rw.ix[2 * ro + 1] = 3 * ts + 1;
     hmax = fmax(hmax, fabs(b));
+  }
+  for (int r = tid; r < nbox + nv; r += NTH) {  // box and speed rows
+    const bool lo = r & 1;
+    int i0;
+    double cst;
+    if (r < nbox) {
+      const int j = r >> 1;
+      i0 = T3 + j;
+      cst = lo ? lb[j] : -ub[j];
+    } else {
+      const int t = (r - nbox) >> 1;
+      i0 = 3 * t + 2;
+      cst = lo ? -c3[3 * t + 2] : c3[3 * t + 2] - p.max_v;
+    }
+    rw.c0[r] = lo ? -1.0 : 1.0;
+    rw.c1[r] = 0.0;
+    rw.cst[r] = cst;
+    rw.ix[2 * r] = i0;
+    rw.ix[2 * r + 1] = i0;
   }
   qp_sync<NW>();
   // f = Gs^T qf (for the scaling of the dual residual)
@@ -604,30 +702,13 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // initial point: z = 0 (inside the control box), s = max(-g(0), 1), lambda = 1
   // g(z) = row_lin(r, Gs z, z) + row_const(r): the linear part in the state's output rows
   // yy = Gs z (or in z itself for the control bounds), constants folded into b' and the bounds
+  // (zz is yy + T3 in every caller: the pairs (y, z), (yd, dz) sit back to back)
   auto row_lin = [&](int64_t r, const double *yy, const double *zz) -> double {
-    if (r < nbox) {
-      const int j = static_cast<int>(r >> 1);
-      return (r & 1) ? -zz[j] : zz[j];
-    }
-    if (r < nbox + nv) {
-      const int t = static_cast<int>((r - nbox) >> 1);
-      return ((r - nbox) & 1) ? -yy[3 * t + 2] : yy[3 * t + 2];
-    }
-    const int64_t o = r - nbox - nv;
-    const int t = static_cast<int>(rw.t[o]);
-    return rw.a0[o] * yy[3 * t] + rw.a1[o] * yy[3 * t + 1];
+    (void)zz;
+    const int2 ix = reinterpret_cast<const int2 *>(rw.ix)[r];
+    return rw.c0[r] * yy[ix.x] + rw.c1[r] * yy[ix.y];
   };
-  auto row_const = [&](int64_t r) -> double {
-    if (r < nbox) {
-      const int j = static_cast<int>(r >> 1);
-      return (r & 1) ? lb[j] : -ub[j];
-    }
-    if (r < nbox + nv) {
-      const int t = static_cast<int>((r - nbox) >> 1);
-      return ((r - nbox) & 1) ? -c3[3 * t + 2] : c3[3 * t + 2] - p.max_v;
-    }
-    return -rw.b[r - nbox - nv];
-  };
+  auto row_const = [&](int64_t r) -> double { return rw.cst[r]; };
   auto row_g = [&](int64_t r, const double *yy, const double *zz) -> double {
     return row_lin(r, yy, zz) + row_const(r);
   };
@@ -650,23 +731,49 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // Per-step sums over a step's obstacle rows, in a fixed order (wave per step, lane-strided,
   // butterfly reduction).  Step t's rows of cell c are the run [start_t, start_t + cnt_t) of
   // the cell's records.  `val(r, t)` returns 2 (or 3) contributions of row r.
-  auto step_rows = [&](int t, int64_t idx) -> int64_t {
+  // visit step t's obstacle rows idx = first, first + S, ... (< ncell t, or ncell) in that order,
+  // fn(o) with o = cell P + t (t - 1) / 2 + j for idx = cell t + j (half-spaces; o = idx P + t
+  // for affine records): (cell, j) advances by (S / t, S % t) per visit, no division per row
+  struct StepIt {
+    int cell0, j0, qS, rS;  // first / t, first % t, S / t, S % t
+  };
+  auto step_it = [&](int t, int first, int S) -> StepIt {
+    if (A.rec_kind != CCMPC_REC_KIND_HALFSPACE || t < 1) return {0, 0, 0, 0};
+    return {first / t, first % t, S / t, S % t};
+  };
+  auto for_step_it = [&](int t, int first, int S, const StepIt &si, auto &&fn) {
     if (A.rec_kind == CCMPC_REC_KIND_HALFSPACE) {
-      const int cnt = t;
-      const int64_t cell = idx / cnt;
-      return cell * P + t * (t - 1) / 2 + (idx - cell * cnt);
+      if (t < 1) return;
+      const int64_t cnt = ncell * t, base_t = t * (t - 1) / 2;
+      int64_t cell = si.cell0;
+      int j = si.j0;
+      const int qS = si.qS, rS = si.rS;
+      for (int64_t i = first; i < cnt; i += S) {
+        fn(cell * P + base_t + j);
+        cell += qS;
+        j += rS;
+        if (j >= t) {
+          j -= t;
+          ++cell;
+        }
+      }
+    } else {
+      for (int64_t i = first; i < ncell; i += S) fn(i * P + t);
     }
-    return idx * P + t;
   };
-  auto step_count = [&](int t) -> int64_t {
-    return A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? ncell * t : ncell;
+  auto for_step = [&](int t, int first, int S, auto &&fn) {
+    for_step_it(t, first, S, step_it(t, first, S), fn);
   };
+  // one wave: lane (t, sub) = (lane >> 3, lane & 7) visits step t's rows sub, sub + 8, ...
+  // (the same every iteration: the integer divisions happen once)
+  const StepIt lane_it = NW == 1 ? step_it(lane >> 3, lane & 7, 8) : StepIt{0, 0, 0, 0};
 
   int status = 0, it = 0;
   double mu = 0.0, mu0 = 0.0;
   bool infeasible = false;
 #ifdef CCMPC_QP_TRACE
   uint64_t tmark[8] = {};
+  const uint64_t tk1 = wall_clock64();
 #endif
   constexpr int NR = NM > 0 ? NM : 1;
   double La[NR], Ldl = 0.0;  // wave 0: L of the current M (register path, NM > 0)
@@ -675,23 +782,50 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
     double rpmax = 0.0, sl = 0.0;
     for (int64_t r = tid; r < mrows; r += NTH) {
-      const double rp = row_g(r, y, z) + rw.s[r];
+      const double s = rw.s[r];
+      const double rp = row_g(r, y, z) + s;
+      rw.rp[r] = rp;
+      rw.is[r] = 1.0 / s;
       rpmax = fmax(rpmax, fabs(rp));
-      sl += rw.s[r] * rw.l[r];
+      sl += s * rw.l[r];
     }
-    for (int t = w; t < T; t += NW) {
-      double la0 = 0.0, la1 = 0.0, w00 = 0.0, w01 = 0.0, w11 = 0.0;
-      const int64_t cnt = step_count(t);
-      for (int64_t i = lane; i < cnt; i += 64) {
-        const int64_t o = step_rows(t, i);
-        const int64_t r = nbox + nv + o;
-        const double a0 = rw.a0[o], a1 = rw.a1[o], lam = rw.l[r], wr = lam / rw.s[r];
-        la0 += lam * a0;
-        la1 += lam * a1;
-        w00 += wr * a0 * a0;
-        w01 += wr * a0 * a1;
-        w11 += wr * a1 * a1;
+    qp_sync<NW>();
+    // step sums of one row: lambda a and the weights' (lambda / s) a a^T
+    double la0, la1, w00, w01, w11;
+    auto step_acc = [&](int64_t o) {
+      const int64_t r = nbox + nv + o;
+      const double a0 = oa0[o], a1 = oa1[o], lam = rw.l[r], wr = lam * rw.is[r];
+      la0 = fma(lam, a0, la0);
+      la1 = fma(lam, a1, la1);
+      const double wa0 = wr * a0;
+      w00 = fma(wa0, a0, w00);
+      w01 = fma(wa0, a1, w01);
+      w11 = fma(wr * a1, a1, w11);
+    };
+    if constexpr (NW == 1) {
+      // one wave, T <= 8: lanes (t, sub) = (lane >> 3, lane & 7), every step's sums at once
+      const int t = lane >> 3, sub = lane & 7;
+      la0 = la1 = w00 = w01 = w11 = 0.0;
+      if (t < T) for_step_it(t, sub, 8, lane_it, step_acc);
+      la0 = sum8(la0);
+      la1 = sum8(la1);
+      w00 = sum8(w00);
+      w01 = sum8(w01);
+      w11 = sum8(w11);
+      if (sub == 0 && t < T) {
+        const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+        const int64_t rv = nbox + 2 * t;
+        q[3 * t] = wp * y[3 * t] + qf[3 * t] + la0;
+        q[3 * t + 1] = wp * y[3 * t + 1] + qf[3 * t + 1] + la1;
+        q[3 * t + 2] = rw.l[rv] - rw.l[rv + 1];
+        bw[4 * t] = wp + w00;
+        bw[4 * t + 1] = w01;
+        bw[4 * t + 2] = wp + w11;
+        bw[4 * t + 3] = rw.l[rv] * rw.is[rv] + rw.l[rv + 1] * rw.is[rv + 1];
       }
+    } else for (int t = w; t < T; t += NW) {
+      la0 = la1 = w00 = w01 = w11 = 0.0;
+      for_step(t, lane, 64, step_acc);
       la0 = wave_sum(la0);
       la1 = wave_sum(la1);
       w00 = wave_sum(w00);
@@ -706,13 +840,66 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         bw[4 * t] = wp + w00;
         bw[4 * t + 1] = w01;
         bw[4 * t + 2] = wp + w11;
-        bw[4 * t + 3] = rw.l[rv] / rw.s[rv] + rw.l[rv + 1] / rw.s[rv + 1];
+        bw[4 * t + 3] = rw.l[rv] * rw.is[rv] + rw.l[rv + 1] * rw.is[rv + 1];
       }
     }
     qp_sync<NW>();
     QP_MARK(1);
     // ---- I2: dual residual, normal matrix ---------------------------------------------------
     double rdmax = 0.0;
+    if constexpr (NW == 1) {
+      // lanes (j, kq) = (lane >> 2, lane & 3): a quad per control, each lane a quarter of the
+      // T3 <= 24 output rows, summed by DPP; every load in-bounds, out-of-range terms selected
+      // away, so the unrolled loads all issue ahead of the FMA chain
+      const int j = lane >> 2, kq = lane & 3, jj = j < n ? j : 0;
+      double v = 0.0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int k = kq + 4 * i, kk = k < T3 ? k : 0;
+        const double g = Gs[kk * n + jj], qk = q[kk];
+        v = k < T3 ? fma(g, qk, v) : v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // + H_ctrl z
+        const int k = kq + 4 * i, kk = k < n ? k : 0;
+        const double h = Hc[jj * n + kk], zk = z[kk];
+        v = k < n ? fma(h, zk, v) : v;
+      }
+      v = sum4(v) + (rw.l[2 * jj] - rw.l[2 * jj + 1]);
+      if (kq == 0 && j < n) rd[j] = v;
+      rdmax = j < n ? fabs(v) : 0.0;
+      // M = H_ctrl + D_box + sum_t Gs_t^T B_t Gs_t: lane column jm = lane & 15 (its weighted
+      // Gs columns in registers), rows im = (lane >> 4) + 4 m
+      const int jm = lane & 15, jc = jm < n ? jm : 0;
+      double wx[8], wy[8], wv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int tt = t < T ? t : 0;
+        const double xj = Gs[(3 * tt) * n + jc], yj = Gs[(3 * tt + 1) * n + jc],
+                     vj = Gs[(3 * tt + 2) * n + jc];
+        const double b0 = bw[4 * tt], b1 = bw[4 * tt + 1], b2 = bw[4 * tt + 2],
+                     b3 = bw[4 * tt + 3];
+        wx[t] = t < T ? fma(b0, xj, b1 * yj) : 0.0;
+        wy[t] = t < T ? fma(b1, xj, b2 * yj) : 0.0;
+        wv[t] = t < T ? b3 * vj : 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int im = (lane >> 4) + 4 * m;
+        const bool on = im < n && jm <= im;
+        const int ic = on ? im : 0;
+        double v2 = Hc[ic * n + jc];
+        if (ic == jc) v2 += rw.l[2 * ic] * rw.is[2 * ic] + rw.l[2 * ic + 1] * rw.is[2 * ic + 1];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int tt = t < T ? t : 0;
+          const double xi = Gs[(3 * tt) * n + ic], yi = Gs[(3 * tt + 1) * n + ic],
+                       vi = Gs[(3 * tt + 2) * n + ic];
+          v2 = fma(xi, wx[t], fma(yi, wy[t], fma(vi, wv[t], v2)));
+        }
+        if (on) M[im * ldm + jm] = v2;
+      }
+    } else {
     for (int j = tid; j < n; j += NTH) {
       double v = hctrl_mul(z, j, T, order, p) + rw.l[2 * j] - rw.l[2 * j + 1];
       for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * q[k];
@@ -723,7 +910,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       const int i = e / n, j = e % n;
       if (j > i) continue;
       double v = hctrl(i, j, T, order, p);
-      if (i == j) v += rw.l[2 * i] / rw.s[2 * i] + rw.l[2 * i + 1] / rw.s[2 * i + 1];
+      if (i == j) v += rw.l[2 * i] * rw.is[2 * i] + rw.l[2 * i + 1] * rw.is[2 * i + 1];
       for (int t = 0; t < T; ++t) {
         const double xi = Gs[(3 * t) * n + i], yi = Gs[(3 * t + 1) * n + i],
                      vi = Gs[(3 * t + 2) * n + i];
@@ -733,6 +920,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
              bw[4 * t + 2] * yj) + bw[4 * t + 3] * vi * vj;
       }
       M[i * ldm + j] = v;
+    }
     }
     block_max2<NW>(rpmax, rdmax, red);
     mu = block_sum<NW>(sl, red) / static_cast<double>(mrows);
@@ -768,13 +956,16 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     // them.  Such a pivot is replaced by a huge one (the pivot-skip modified Cholesky of
     // interior point codes): that direction's component of dz becomes 0, which is what the
     // huge weight enforces anyway.
+    bool chol_fail = false;  // wave-uniform (NW == 1: the only wave)
     if (w == 0) {
       bool fail;
       if constexpr (NM > 0) {
 #pragma unroll
-        for (int k = 0; k < NR; ++k)
-          La[k] = (k < n && lane < n && k <= lane) ? M[lane * ldm + k] : 0.0;
-        fail = reg_cholesky(La, n, Ldl);
+        for (int k = 0; k < NR; ++k) {
+          const double v = M[(lane < n ? lane : 0) * ldm + (k < n ? k : 0)];
+          La[k] = (lane < n && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
+        }
+        fail = reg_cholesky(La, Ldl);
         // L overwrites M's lower triangle (read by the L^T solves)
 #pragma unroll
         for (int k = 0; k < NR; ++k)
@@ -783,10 +974,16 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       } else {
         fail = wave_cholesky(M, n, ldm, dinv, true);
       }
-      if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+      if (NW == 1)
+        chol_fail = fail;
+      else if (lane == 0)
+        red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
     }
-    qp_sync<NW>();
-    if (red[8 * kQpWaves - 1] != 0.0) {  // weights overflowed: the iteration broke down;
+    if constexpr (NW > 1) {
+      qp_sync<NW>();
+      chol_fail = red[8 * kQpWaves - 1] != 0.0;
+    }
+    if (chol_fail) {  // weights overflowed: the iteration broke down;
       status = CCMPC_QP_MAXITER;           // only a verified polish can still answer
       break;
     }
@@ -796,6 +993,14 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       if constexpr (NM > 0) {
         const double b = reg_solve(La, M, ldm, Ldl, n, lane < n ? x[lane] : 0.0);
         if (lane < n) x[lane] = b;
+        if constexpr (NW == 1) {  // yd = Gs dz, dz read back by readlane (0 beyond n)
+          const int kk = lane < T3 ? lane : 0;
+          double v = 0.0;
+#pragma unroll
+          for (int j = 0; j < NM; ++j) v = fma(Gs[kk * n + (j < n ? j : 0)], lane_bcast(b, j), v);
+          if (lane < T3) yd[lane] = v;
+          wave_sync();
+        }
       } else {
         double b[2];
         wave_load2(x, n, b);
@@ -805,6 +1010,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       }
     };
     auto gs_times_dz = [&]() {
+      if constexpr (NW == 1) return;  // done inside chol_solve from the registers
       for (int k = tid; k < T3; k += NTH) {
         double v = 0.0;
         for (int j = 0; j < n; ++j) v += Gs[k * n + j] * dz[j];
@@ -814,15 +1020,27 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     };
     // rhs = -r_d - G^T u with u_r given per row; q (output space) and dz (rhs) staged in LDS
     auto build_rhs = [&](auto urow) {
-      for (int t = w; t < T; t += NW) {
-        double u0 = 0.0, u1 = 0.0;
-        const int64_t cnt = step_count(t);
-        for (int64_t i = lane; i < cnt; i += 64) {
-          const int64_t o = step_rows(t, i);
-          const double u = urow(nbox + nv + o);
-          u0 += u * rw.a0[o];
-          u1 += u * rw.a1[o];
+      double u0, u1;
+      auto acc = [&](int64_t o) {
+        const double u = urow(nbox + nv + o);
+        u0 = fma(u, oa0[o], u0);
+        u1 = fma(u, oa1[o], u1);
+      };
+      if constexpr (NW == 1) {   // as I1: lanes (t, sub), every step at once
+        const int t = lane >> 3, sub = lane & 7;
+        u0 = u1 = 0.0;
+        if (t < T) for_step_it(t, sub, 8, lane_it, acc);
+        u0 = sum8(u0);
+        u1 = sum8(u1);
+        if (sub == 0 && t < T) {
+          const int64_t rv = nbox + 2 * t;
+          q[3 * t] = u0;
+          q[3 * t + 1] = u1;
+          q[3 * t + 2] = urow(rv) - urow(rv + 1);
         }
+      } else for (int t = w; t < T; t += NW) {
+        u0 = u1 = 0.0;
+        for_step(t, lane, 64, acc);
         u0 = wave_sum(u0);
         u1 = wave_sum(u1);
         if (lane == 0) {
@@ -833,10 +1051,23 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         }
       }
       qp_sync<NW>();
-      for (int j = tid; j < n; j += NTH) {
-        double v = -rd[j] - (urow(2 * j) - urow(2 * j + 1));
-        for (int k = 0; k < T3; ++k) v -= Gs[k * n + j] * q[k];
-        dz[j] = v;
+      if constexpr (NW == 1) {  // quad per control, as rd
+        const int j = lane >> 2, kq = lane & 3, jj = j < n ? j : 0;
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const int k = kq + 4 * i, kk = k < T3 ? k : 0;
+          const double g = Gs[kk * n + jj], qk = q[kk];
+          v = k < T3 ? fma(g, qk, v) : v;
+        }
+        v = (-rd[jj] - (urow(2 * jj) - urow(2 * jj + 1))) - sum4(v);
+        if (kq == 0 && j < n) dz[j] = v;
+      } else {
+        for (int j = tid; j < n; j += NTH) {
+          double v = -rd[j] - (urow(2 * j) - urow(2 * j + 1));
+          for (int k = 0; k < T3; ++k) v -= Gs[k * n + j] * q[k];
+          dz[j] = v;
+        }
       }
       qp_sync<NW>();
       chol_solve(dz);
@@ -846,21 +1077,30 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     QP_MARK(3);
     // ---- predictor (affine scaling): r_c = s l  ->  u = w r_p - l ---------------------------
     build_rhs([&](int64_t r) {
-      const double rp = row_g(r, y, z) + rw.s[r];
-      return rw.l[r] / rw.s[r] * rp - rw.l[r];
+      const double l = rw.l[r];
+      return l * rw.is[r] * rw.rp[r] - l;
     });
     QP_MARK(4);
-    double amax = 1.0;
+    // the largest step keeping s, lambda >= 0: min over rows of -s / ds (ds < 0) and -l / dl
+    // (dl < 0), kept as a fraction num / den (both > 0; compared by cross-multiplication) so
+    // each lane divides once
+    double anum = 1.0, aden = 1.0;
+    auto ratio_min = [&](double num, double den) {  // candidate num / den, den > 0
+      if (num * aden < anum * den) {
+        anum = num;
+        aden = den;
+      }
+    };
     for (int64_t r = tid; r < mrows; r += NTH) {
-      const double s = rw.s[r], l = rw.l[r];
-      const double rp = row_g(r, y, z) + s, gd = row_gd(r, yd, dz);
-      const double ds = -rp - gd, dl = l / s * (gd + rp) - l;
+      const double s = rw.s[r], l = rw.l[r], rp = rw.rp[r];
+      const double gd = row_gd(r, yd, dz);
+      const double ds = -rp - gd, dl = l * rw.is[r] * (gd + rp) - l;
       rw.ds[r] = ds;
       rw.dl[r] = dl;
-      if (ds < 0.0) amax = fmin(amax, -s / ds);
-      if (dl < 0.0) amax = fmin(amax, -l / dl);
+      if (ds < 0.0) ratio_min(s, -ds);
+      if (dl < 0.0) ratio_min(l, -dl);
     }
-    const double aaff = block_min<NW>(amax, red);
+    const double aaff = block_min<NW>(anum / aden, red);
     double slaff = 0.0;
     for (int64_t r = tid; r < mrows; r += NTH)
       slaff += (rw.s[r] + aaff * rw.ds[r]) * (rw.l[r] + aaff * rw.dl[r]);
@@ -872,22 +1112,22 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       return rw.s[r] * rw.l[r] + rw.ds[r] * rw.dl[r] - sigma * mu;
     };
     build_rhs([&](int64_t r) {
-      const double rp = row_g(r, y, z) + rw.s[r];
-      return rw.l[r] / rw.s[r] * rp - rc_of(r) / rw.s[r];
+      return (rw.l[r] * rw.rp[r] - rc_of(r)) * rw.is[r];
     });
     QP_MARK(6);
-    amax = 1e300;
+    anum = 1e300;
+    aden = 1.0;
     for (int64_t r = tid; r < mrows; r += NTH) {
-      const double s = rw.s[r], l = rw.l[r];
-      const double rp = row_g(r, y, z) + s, gd = row_gd(r, yd, dz);
+      const double s = rw.s[r], l = rw.l[r], rp = rw.rp[r];
+      const double gd = row_gd(r, yd, dz);
       const double rc = rc_of(r);
-      const double ds = -rp - gd, dl = (-rc - l * ds) / s;
+      const double ds = -rp - gd, dl = (-rc - l * ds) * rw.is[r];
       rw.ds[r] = ds;  // every read of this row's ds_aff / dl_aff happened above in this thread
       rw.dl[r] = dl;
-      if (ds < 0.0) amax = fmin(amax, -s / ds);
-      if (dl < 0.0) amax = fmin(amax, -l / dl);
+      if (ds < 0.0) ratio_min(s, -ds);
+      if (dl < 0.0) ratio_min(l, -dl);
     }
-    const double alpha = fmin(1.0, 0.995 * block_min<NW>(amax, red));
+    const double alpha = fmin(1.0, 0.995 * block_min<NW>(anum / aden, red));
 
     for (int j = tid; j < n; j += NTH) z[j] += alpha * dz[j];
     for (int k = tid; k < T3; k += NTH) y[k] += alpha * yd[k];
@@ -915,6 +1155,9 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // problem itself.  The result is kept only if it is a verified KKT point: every row within
   // tol_p and lambda >= -tol_d (stationarity holds by construction), which also makes a
   // stalled IPM's answer exact and leaves infeasible problems reported as such.
+#ifdef CCMPC_QP_TRACE
+  const uint64_t tk2 = wall_clock64();
+#endif
   if (A.polish && !infeasible) {
     double *Wm = lds + lay.pw, *Sm = lds + lay.ps, *act = lds + lay.pact,
            *sdinv = lds + lay.pdinv;
@@ -953,138 +1196,274 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       na = tot;
       qp_sync<NW>();
     }
-    // factor H once; y0 = -L^{-1} f
-    if (w == 0) {
-      const bool fail = wave_cholesky(M, n, ldm, dinv, false);
-      double b[2];
-      wave_load2(fu, n, b);
-      b[0] = -b[0];
-      b[1] = -b[1];
-      wave_forward(M, n, ldm, dinv, b);
-      wave_store2(y0, n, b);
-      if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
-    }
-    qp_sync<NW>();
-    const bool h_ok = red[8 * kQpWaves - 1] == 0.0;
-    if (!h_ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
-    // up to 4 rounds of active-set correction, as the oracle's polish does: drop rows whose
-    // multiplier comes out negative, else add the most violated row
-    for (int round = 0; h_ok && round < 4 && na <= n; ++round) {
-      // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
-      for (int a = w; a < na; a += NW) {
-        const int64_t r = static_cast<int64_t>(act[a]);
-        double b[2];
+    if constexpr (NM > 0 && NW == 1) {
+      // One wave, n <= 16: the same polish with every factor in registers (identity-padded
+      // to 16 x 16, straight-line; reg_cholesky without the pivot skip), the L^T columns read
+      // ahead of each backward chain, the vectors moved between lanes by readlane.
+      wave_sync();
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = lane + 64 * h;
-          double g = 0.0;
-          if (j < n) {
-            if (r < nbox) {
-              g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
-            } else if (r < nbox + nv) {
-              const int t = static_cast<int>((r - nbox) >> 1);
-              g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
-            } else {
-              // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
-              const int64_t o = r - nbox - nv;
-              const int t = static_cast<int>(rw.t[o]);
-              g = rw.a0[o] * Gs[(3 * t) * n + j] + rw.a1[o] * Gs[(3 * t + 1) * n + j];
-            }
+      for (int k = 0; k < NR; ++k) {
+        const double v = M[(lane < n ? lane : 0) * ldm + (k < n ? k : 0)];
+        La[k] = (lane < n && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
+      }
+      const bool hfail = reg_cholesky<NR, false>(La, Ldl);
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+        if (k < n && lane < n && k <= lane) M[lane * ldm + k] = La[k];
+      wave_sync();
+      double ltH[NR];
+      reg_load_lt(M, ldm, n, ltH);
+      const double y0r = reg_forward(La, Ldl, lane < n ? -fu[lane] : 0.0);  // y0 = -L^{-1} f
+      if (lane < n) y0[lane] = y0r;
+      if (hfail) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
+      for (int round = 0; !hfail && round < 4 && na <= n; ++round) {
+        // W rows w_a = L^{-1} g_a (g on lane = control), rs_a = w_a . y0 - h_a
+        for (int a = 0; a < na; ++a) {
+          const int64_t r = static_cast<int64_t>(act[a]);
+          const int j = lane < n ? lane : 0;
+          double g;
+          if (r < nbox) {
+            g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
+          } else if (r < nbox + nv) {
+            const int t = static_cast<int>((r - nbox) >> 1);
+            g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
+          } else {
+            const int64_t o = r - nbox - nv;
+            const int t = rw.ix[2 * (nbox + nv + o)] / 3;
+            g = oa0[o] * Gs[(3 * t) * n + j] + oa1[o] * Gs[(3 * t + 1) * n + j];
           }
-          b[h] = g;
+          const double bw_ = reg_forward(La, Ldl, lane < n ? g : 0.0);
+          if (lane < n) Wm[a * n + lane] = bw_;
+          const double d = wave_sum(lane < n ? bw_ * y0r : 0.0);
+          if (lane == 0) rs[a] = d + row_const(r);
         }
-        wave_forward(M, n, ldm, dinv, b);
-        wave_store2(Wm + a * n, n, b);
-        double d = 0.0;
+        wave_sync();
+        // S = W W^T: lane (i, kq) = (lane & 15, lane >> 4) forms S[i][kq + 4 m]
+        {
+          const int i = lane & 15, kq = lane >> 4, ic = i < na ? i : 0;
+          double wi[NR];
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          if (lane + 64 * h < n) d += b[h] * y0[lane + 64 * h];
-        d = wave_sum(d);
-        if (lane == 0) rs[a] = d + row_const(r);
-      }
-      qp_sync<NW>();
-      for (int e = tid; e < na * na; e += NTH) {
-        const int i = e / na, j = e % na;
-        if (j > i) continue;
-        double v = 0.0;
-        for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
-        Sm[i * ldm + j] = v;
-      }
-      qp_sync<NW>();
-      if (w == 0) {
-        const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
-        double b[2];
-        if (!fail) {
-          wave_load2(rs, na, b);
-          wave_forward(Sm, na, ldm, sdinv, b);
-          wave_backward(Sm, na, ldm, sdinv, b);
-          wave_store2(lam, na, b);
+          for (int k = 0; k < NR; ++k) wi[k] = Wm[ic * n + (k < n ? k : 0)];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int jr = kq + 4 * m, jc = jr < na ? jr : 0;
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < NR; ++k)
+              v = k < n ? fma(wi[k], Wm[jc * n + (k < n ? k : 0)], v) : v;
+            if (i < na && jr <= i) Sm[i * ldm + jr] = v;
+          }
         }
+        wave_sync();
+        double Ls[NR], Sdl = 0.0;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          const double v = Sm[(lane < na ? lane : 0) * ldm + (k < na ? k : 0)];
+          Ls[k] = (lane < na && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
+        }
+        const bool sfail = reg_cholesky<NR, false>(Ls, Sdl);
+        if (sfail) break;  // dependent active rows
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+          if (k < na && lane < na && k <= lane) Sm[lane * ldm + k] = Ls[k];
+        wave_sync();
+        const double lamr = reg_solve(Ls, Sm, ldm, Sdl, na, lane < na ? rs[lane] : 0.0);
+        if (lane < na) lam[lane] = lamr;
+        // z = L^{-T}(y0 - W^T lambda)
+        double v = y0r;
+        {
+          const int j = lane < n ? lane : 0;
+#pragma unroll
+          for (int a = 0; a < NR; ++a)
+            v = fma(-Wm[(a < na ? a : 0) * n + j], lane_bcast(lamr, a), v);  // lamr = 0 past na
+        }
+        const double zpr = reg_backward(ltH, Ldl, lane < n ? v : 0.0);
+        if (lane < n) zp[lane] = zpr;
+        {
+          const int kk = lane < T3 ? lane : 0;
+          double yv = 0.0;
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            yv = fma(Gs[kk * n + (j < n ? j : 0)], lane_bcast(zpr, j), yv);
+          if (lane < T3) yp[lane] = yv;
+        }
+        wave_sync();
+        double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
+        for (int64_t r = tid; r < mrows; r += NTH) {
+          const double g = row_g(r, yp, zp);
+          if (!isfinite(g)) bad = 1.0;
+          if (g > viol) {
+            viol = g;
+            vrow = static_cast<double>(r);
+          }
+        }
+        if (lane < na) {
+          if (!isfinite(lamr)) bad = 1.0;
+          lneg = -lamr;
+        }
+        block_argmax<NW>(viol, vrow, red);
+        block_max2<NW>(lneg, bad, red);
+        if (bad != 0.0) break;
+        if (viol <= tol_p && lneg <= tol_d) {
+          if (lane < n) z[lane] = zpr;
+          status = 0;
+          wave_sync();
+          break;
+        }
+        // next active set (lane 0; na <= n entries)
+        if (lane == 0) {
+          int m2 = 0;
+          if (lneg > tol_d) {
+            for (int a = 0; a < na; ++a)
+              if (lam[a] >= -tol_d) act[m2++] = act[a];
+          } else {
+            m2 = na;
+            if (na < n) act[m2++] = vrow;
+            else m2 = n + 1;  // nowhere to add: give up
+          }
+          red[8 * kQpWaves - 2] = static_cast<double>(m2);
+        }
+        wave_sync();
+        na = static_cast<int>(red[8 * kQpWaves - 2]);
+        wave_sync();
+      }
+    } else {
+      // factor H once; y0 = -L^{-1} f
+      if (w == 0) {
+        const bool fail = wave_cholesky(M, n, ldm, dinv, false);
+        double b[2];
+        wave_load2(fu, n, b);
+        b[0] = -b[0];
+        b[1] = -b[1];
+        wave_forward(M, n, ldm, dinv, b);
+        wave_store2(y0, n, b);
         if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
       }
       qp_sync<NW>();
-      if (red[8 * kQpWaves - 1] != 0.0) break;  // dependent active rows
-      // z = L^{-T}(y0 - W^T lambda)
-      for (int j = tid; j < n; j += NTH) {
-        double v = y0[j];
-        for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
-        zp[j] = v;
-      }
-      qp_sync<NW>();
-      if (w == 0) {
-        double b[2];
-        wave_load2(zp, n, b);
-        wave_backward(M, n, ldm, dinv, b);
-        wave_store2(zp, n, b);
-      }
-      qp_sync<NW>();
-      for (int k = tid; k < T3; k += NTH) {
-        double v = 0.0;
-        for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
-        yp[k] = v;
-      }
-      qp_sync<NW>();
-      double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
-      for (int64_t r = tid; r < mrows; r += NTH) {
-        const double g = row_g(r, yp, zp);
-        if (!isfinite(g)) bad = 1.0;
-        if (g > viol) {
-          viol = g;
-          vrow = static_cast<double>(r);
+      const bool h_ok = red[8 * kQpWaves - 1] == 0.0;
+      if (!h_ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
+      // up to 4 rounds of active-set correction, as the oracle's polish does: drop rows whose
+      // multiplier comes out negative, else add the most violated row
+      for (int round = 0; h_ok && round < 4 && na <= n; ++round) {
+        // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
+        for (int a = w; a < na; a += NW) {
+          const int64_t r = static_cast<int64_t>(act[a]);
+          double b[2];
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = lane + 64 * h;
+            double g = 0.0;
+            if (j < n) {
+              if (r < nbox) {
+                g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
+              } else if (r < nbox + nv) {
+                const int t = static_cast<int>((r - nbox) >> 1);
+                g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
+              } else {
+                // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
+                const int64_t o = r - nbox - nv;
+                const int t = rw.ix[2 * (nbox + nv + o)] / 3;
+                g = oa0[o] * Gs[(3 * t) * n + j] + oa1[o] * Gs[(3 * t + 1) * n + j];
+              }
+            }
+            b[h] = g;
+          }
+          wave_forward(M, n, ldm, dinv, b);
+          wave_store2(Wm + a * n, n, b);
+          double d = 0.0;
+  #pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (lane + 64 * h < n) d += b[h] * y0[lane + 64 * h];
+          d = wave_sum(d);
+          if (lane == 0) rs[a] = d + row_const(r);
         }
-      }
-      for (int a = tid; a < na; a += NTH) {
-        if (!isfinite(lam[a])) bad = 1.0;
-        lneg = fmax(lneg, -lam[a]);
-      }
-      block_argmax<NW>(viol, vrow, red);
-      block_max2<NW>(lneg, bad, red);
-      if (bad != 0.0) break;
-      if (viol <= tol_p && lneg <= tol_d) {
-        for (int j = tid; j < n; j += NTH) z[j] = zp[j];
-        status = 0;
         qp_sync<NW>();
-        break;
-      }
-      // next active set (thread 0; na <= n entries)
-      if (tid == 0) {
-        int m2 = 0;
-        if (lneg > tol_d) {
-          for (int a = 0; a < na; ++a)
-            if (lam[a] >= -tol_d) act[m2++] = act[a];
-        } else {
-          m2 = na;
-          if (na < n) act[m2++] = vrow;
-          else m2 = n + 1;  // nowhere to add: give up
+        for (int e = tid; e < na * na; e += NTH) {
+          const int i = e / na, j = e % na;
+          if (j > i) continue;
+          double v = 0.0;
+          for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
+          Sm[i * ldm + j] = v;
         }
-        red[8 * kQpWaves - 2] = static_cast<double>(m2);
+        qp_sync<NW>();
+        if (w == 0) {
+          const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
+          double b[2];
+          if (!fail) {
+            wave_load2(rs, na, b);
+            wave_forward(Sm, na, ldm, sdinv, b);
+            wave_backward(Sm, na, ldm, sdinv, b);
+            wave_store2(lam, na, b);
+          }
+          if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+        }
+        qp_sync<NW>();
+        if (red[8 * kQpWaves - 1] != 0.0) break;  // dependent active rows
+        // z = L^{-T}(y0 - W^T lambda)
+        for (int j = tid; j < n; j += NTH) {
+          double v = y0[j];
+          for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
+          zp[j] = v;
+        }
+        qp_sync<NW>();
+        if (w == 0) {
+          double b[2];
+          wave_load2(zp, n, b);
+          wave_backward(M, n, ldm, dinv, b);
+          wave_store2(zp, n, b);
+        }
+        qp_sync<NW>();
+        for (int k = tid; k < T3; k += NTH) {
+          double v = 0.0;
+          for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
+          yp[k] = v;
+        }
+        qp_sync<NW>();
+        double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
+        for (int64_t r = tid; r < mrows; r += NTH) {
+          const double g = row_g(r, yp, zp);
+          if (!isfinite(g)) bad = 1.0;
+          if (g > viol) {
+            viol = g;
+            vrow = static_cast<double>(r);
+          }
+        }
+        for (int a = tid; a < na; a += NTH) {
+          if (!isfinite(lam[a])) bad = 1.0;
+          lneg = fmax(lneg, -lam[a]);
+        }
+        block_argmax<NW>(viol, vrow, red);
+        block_max2<NW>(lneg, bad, red);
+        if (bad != 0.0) break;
+        if (viol <= tol_p && lneg <= tol_d) {
+          for (int j = tid; j < n; j += NTH) z[j] = zp[j];
+          status = 0;
+          qp_sync<NW>();
+          break;
+        }
+        // next active set (thread 0; na <= n entries)
+        if (tid == 0) {
+          int m2 = 0;
+          if (lneg > tol_d) {
+            for (int a = 0; a < na; ++a)
+              if (lam[a] >= -tol_d) act[m2++] = act[a];
+          } else {
+            m2 = na;
+            if (na < n) act[m2++] = vrow;
+            else m2 = n + 1;  // nowhere to add: give up
+          }
+          red[8 * kQpWaves - 2] = static_cast<double>(m2);
+        }
+        qp_sync<NW>();
+        na = static_cast<int>(red[8 * kQpWaves - 2]);
+        qp_sync<NW>();
       }
-      qp_sync<NW>();
-      na = static_cast<int>(red[8 * kQpWaves - 2]);
-      qp_sync<NW>();
     }
   }
 
+#ifdef CCMPC_QP_TRACE
+  const uint64_t tk3 = wall_clock64();
+#endif
   // ---- outputs: u, X = Gamma_f u + const (all four state rows), the objective value ----------
   for (int j = tid; j < n; j += NTH) A.out_u[sc * n + j] = z[j];
   double part = 0.0;
@@ -1126,6 +1505,12 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     A.out_status[sc] = status | (sk > 0.0 ? CCMPC_QP_SKIPPED_ROWS : 0);
     A.out_iter[sc] = it;
   }
+#ifdef CCMPC_QP_TRACE
+  const uint64_t tk4 = wall_clock64();
+  if (tid == 0 && sc == 0)
+    printf("qp phases (10ns): setup %d iterations %d polish %d outputs %d\n", int(tk1 - tk0),
+           int(tk2 - tk1), int(tk3 - tk2), int(tk4 - tk3));
+#endif
 }
 
 // Where the per-scene state lives: the polish step's matrices come first (they make the
@@ -1184,7 +1569,7 @@ extern "C" size_t ccmpc_mpc_qp_workspace_bytes(int64_t n_scenes, int64_t T,
   const int64_t R = max_cells_per_scene * qp_rows_per_cell(static_cast<int>(T), rec_kind);
   if (qp_plan(static_cast<int>(T), R).rows_lds) return 16;  // rows live in LDS
   const int64_t m = 4 * T + 2 * T + R;
-  return static_cast<size_t>(n_scenes * (4 * m + 4 * R)) * sizeof(double) + 16;
+  return static_cast<size_t>(n_scenes * kQpRowDoubles * m) * sizeof(double) + 16;
 }
 
 extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamma,

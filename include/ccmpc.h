@@ -106,6 +106,21 @@ int ccmpc_copy_async(void *dst, const void *src, size_t bytes, ccmpc_stream_t st
  * kernel node rather than a memcpy node); bytes and both pointers 16-byte aligned. */
 int ccmpc_copy_kernel_async(void *dst, const void *src, size_t bytes, ccmpc_stream_t stream);
 
+/* Stream-ordered signal: *host_word (pinned) = *value (device), visible to the host only after
+ * every write this stream made before it (a system-scope release).  A captured step's host side
+ * polls the word rather than synchronising the stream. */
+int ccmpc_signal_host(int64_t *host_word, const int64_t *value, ccmpc_stream_t stream);
+
+/* Graph capture of a planning step (ccmpc/step.py): begin / end a relaxed-mode capture on
+ * `stream` (the library calls and event record / wait pairs issued in between become the
+ * graph; end instantiates it into *out_exec), replay it on a stream, release it.  The graph
+ * holds the buffer addresses it was captured with: keep them alive while it exists, and let
+ * its last replay finish before destroying it or them. */
+int ccmpc_graph_capture_begin(ccmpc_stream_t stream);
+int ccmpc_graph_capture_end(ccmpc_stream_t stream, void **out_exec);
+int ccmpc_graph_launch(void *exec, ccmpc_stream_t stream);
+int ccmpc_graph_destroy(void *exec);
+
 /* ---------------------------------------------------------------------------------------
  * Moment (Gram) reduction.  Replaces every np.mean / np.cov over particle clouds on the path:
  *   v8ideal/__init__.py:864-875 (t=0 stats), :896 + makeconstraint.py:41-70 predict_moments

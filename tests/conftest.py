@@ -18,6 +18,11 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests proper")
+    if os.environ.get("CCMPC_SEGV_BT") == "1":      # debug aid: native backtrace on SIGSEGV
+        import ctypes
+        import faulthandler
+        faulthandler.enable()
+        ctypes.CDLL(os.path.join(ROOT, "tools", "libsegvbt.so")).segv_bt_install()
 
 
 @pytest.fixture(scope="session")

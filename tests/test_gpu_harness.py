@@ -83,6 +83,27 @@ def test_harness_episode_through_run_step(gpu, per_particle):
         assert ref_agent.last_records.tobytes() == s["records"].tobytes(), s["frame"]
 
 
+def test_next_episode_takes_the_destroyed_agents_graphs(gpu):
+    """The harness builds a fresh agent per episode and destroys the last (tests/Hz20/
+    __init__.py:383-399): the next agent takes the released step graphs from the pool (its
+    steps replay them, captured) and plans the same episode to the same bytes."""
+    from ccmpc import step
+    scen = _scenario(gpu, False, run_interval=10, n_ov=1, N=2000)
+    step._POOL.clear()
+    scen.episode(0)
+    first_ids = {id(g) for lst in step._POOL.values() for g in lst}
+    first = [(s["records"].tobytes(), s["speeds"].tobytes(), s["angles"].tobytes())
+             for s in scen.steps]
+    assert len(first_ids) >= 9          # T = 8 .. 1 and the receding affine shape at least
+    scen.episode(0)                     # same seeds: the same episode again
+    again = [(s["records"].tobytes(), s["speeds"].tobytes(), s["angles"].tobytes())
+             for s in scen.steps]
+    assert again == first
+    assert {id(g) for lst in step._POOL.values() for g in lst} == first_ids
+    assert all(g.graphs is not None for lst in step._POOL.values() for g in lst
+               if g.generation >= 2)
+
+
 def test_harness_steps_match_oracle_chain(gpu):
     """Minkowski records of the harness's shrinking steps against the oracle chain, and the
     planning QP against the oracle QP on the oracle's records."""
@@ -174,6 +195,8 @@ def test_filter_pmf_reaches_every_stage(gpu):
                                               ref[-1] + [4.0, 0.5], ref)
         except planner.InSimulationException:
             pass                                     # the QP may fail; the records are set
+        except ValueError as e:                      # T < ph after a failed T == ph QP: no
+            assert "needs u_prev" in str(e)          # executed controls; records still set
         ovs, out = agent.last_generator_output
         assert [ov.n_states for ov in ovs] == K.tolist()
         per_cell = T * (T - 1) // 2 if shrinking else T

@@ -124,3 +124,30 @@ def test_graph_step_refuses_a_different_mode_split(gpu):
     with pytest.raises(ValueError):
         g.set_inputs(1, init, pmf, gmm, minpos, _ref(0), np.zeros((sum(K) + O, 3)),
                      np.zeros((sum(K) + O, 2)), np.zeros((sum(K) + O, 2)))
+
+
+def test_graph_replay_equals_its_first_eager_launch(gpu):
+    """A step graph's first launch runs its calls eagerly (StepGraph.capture_at), the second is
+    the captured graph: with the same inputs (same frame, seed and saved moments) both give the
+    same bytes, for every step kind -- full-horizon Minkowski, shrinking (ideal rollout) and
+    receding affine."""
+    from ccmpc import episode, planner
+    init, pmf, gmm, minpos, pasts, K, eps = _inputs()
+    ag = planner.MidlevelAgent(prediction_horizon=PH, n_ideal=200_000, device=gpu)
+    for frame, T, affine in ((0, PH, False), (10, PH - 1, False), (20, PH, True)):
+        params = episode.Params(O, K, frame)
+        sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=77 + frame)
+        fn = ag.predict_and_constrain_affine if affine else ag.predict_and_constrain
+        got = []
+        for _ in range(2):
+            ovs, out = fn(params, sampler, eps, T, _ref(frame), minpos, pasts)
+            g = list(ag._graphs.values())[-1]           # this frame's graph (most recent)
+            L4 = list(g.l4_outputs(g.generation).values())
+            got.append((np.array(ag.last_records).view(np.uint8), L4,
+                        [np.array(p) for ov in ovs for p in ov.pred_positions]))
+        (r0, l0, p0), (r1, l1, p1) = got
+        np.testing.assert_array_equal(r0, r1)
+        for a, b in zip(l0 + p0, l1 + p1):
+            np.testing.assert_array_equal(a, b)
+    assert len(ag._graphs) == 3
+    assert all(g.graphs is not None and g.generation == 2 for g in ag._graphs.values())

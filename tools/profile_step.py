@@ -45,7 +45,7 @@ def main():
     g = next(iter(agent._graphs.values()))
     t0 = time.perf_counter()
     for i in range(a.steps):
-        g.graph.replay()
+        g.graphs[0].replay()
         torch.cuda.current_stream().synchronize()
     print(f"replay + sync: {(time.perf_counter() - t0) / a.steps * 1e6:.1f} us")
     g.bind()
@@ -64,7 +64,7 @@ def main():
     print(f"direct launches, host only: {(time.perf_counter() - t0) / a.steps * 1e6:.1f} us")
     t0 = time.perf_counter()
     for i in range(a.steps):
-        g.graph.replay()
+        g.graphs[0].replay()
     torch.cuda.current_stream().synchronize()
     print(f"graph replays, host only: {(time.perf_counter() - t0) / a.steps * 1e6:.1f} us")
     t0 = time.perf_counter()
