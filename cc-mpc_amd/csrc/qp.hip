@@ -409,13 +409,15 @@ __device__ __forceinline__ bool reg_cholesky(double (&a)[NM], double &dl) {
 #pragma unroll
   for (int k = 0; k < NM; ++k)
     if (k == lane) diag0 = a[k];
+  fail = __ballot(lane < NM && !isfinite(diag0)) != 0;
 #pragma unroll
   for (int j = 0; j < NM; ++j) {
     {
       double d = lane_bcast(a[j], j);
-      const double ajj = lane_bcast(diag0, j);
-      fail = fail || !isfinite(d) || !isfinite(ajj);
-      if (!(d > 1e-30 * ajj)) {  // pivot skip (the IPM), or a failure (SKIP = false)
+      // lane j's pivot against its own original diagonal, as a ballot bit (no broadcast)
+      const bool tiny = (__ballot(!(a[j] > 1e-30 * diag0)) >> j) & 1;
+      fail = fail || !isfinite(d);
+      if (tiny) {  // pivot skip (the IPM), or a failure (SKIP = false)
         fail = fail || !SKIP;
         d = 1e128;
       }
@@ -454,7 +456,7 @@ __device__ __forceinline__ double reg_forward(const double (&a)[NM], double dl, 
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < NM; ++j) {
-    const double yj = lane_bcast(b, j) * lane_bcast(dl, j);
+    const double yj = lane_bcast(b * dl, j);  // lane j's b is final: one broadcast
     const double upd = fma(-a[j], yj, b);
     b = lane == j ? yj : (lane > j ? upd : b);
   }
@@ -465,7 +467,7 @@ __device__ __forceinline__ double reg_backward(const double (&lt)[NM], double dl
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = NM - 1; j >= 0; --j) {
-    const double xj = lane_bcast(b, j) * lane_bcast(dl, j);
+    const double xj = lane_bcast(b * dl, j);
     const double upd = fma(-lt[j], xj, b);
     b = lane == j ? xj : (lane < j ? upd : b);
   }
@@ -531,6 +533,10 @@ __device__ __forceinline__ double hctrl_mul(const double *z, int i, int T, int o
 // takes the ~30 workgroup barriers per IPM iteration off the chain.
 template <bool ROWS_LDS, int NM, int NW>
 __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
+  // multiply-adds fused in the solver (the library builds with -ffp-contract=off for the
+  // moments' reference arithmetic; the IPM's iterates carry no such contract, and its answer
+  // is the verified polish / KKT point, tested against the oracle QP to a tolerance)
+#pragma clang fp contract(fast)
   constexpr int NTH = 64 * NW;
   extern __shared__ double lds[];
   const int64_t sc = blockIdx.x;
