@@ -85,10 +85,11 @@ class Pack:
         """Zero-copy NumPy view of the pinned host field."""
         return self._h[name]
 
-    def snapshot(self):
-        """One copy of the whole host buffer; returns {field: view of the copy} (outputs that
-        must outlive the next replay, for one memcpy instead of one per field)."""
-        raw = self.host.numpy().copy()
+    def snapshot(self, device=False):
+        """One copy of the whole host buffer (device=True: of the device buffer, synchronously);
+        returns {field: view of the copy} (outputs that must outlive the next replay, for one
+        memcpy instead of one per field)."""
+        raw = self.dev.cpu().numpy() if device else self.host.numpy().copy()
         nd = np.ndarray
         return {name: nd(shape, dt, raw, off) for name, shape, dt, off in self._views}
 
@@ -218,7 +219,7 @@ class StepGraph:
         self.out_l4s = [Pack([("A", (C, ph_, 4, 2), f64), ("b", (C, ph_, 4), f64),
                               ("yaw_mean", (C, ph_), f64), ("yaw0_var", (C,), f64)], self.device)
                         for _ in range(2)]
-        # pinned signal words: [0] the record path's generation, [2 + 2 p] parity p's L4
+        # pinned signal word [0]: the record path's generation
         self.flags = torch.zeros(8, dtype=i64, pin_memory=True)
         self._flags = self.flags.numpy()
         # small clouds: sampler + bucketing in three short launches (ccmpc_sample_bucket), whose
@@ -254,7 +255,7 @@ class StepGraph:
         # fork / join events per parity graph, alive as long as the graphs are: an event
         # recorded into a capture and destroyed before the graph (what wait_stream's temporary
         # does) left a dangling reference that crashed the replay once the memory was reused
-        self._ev = [{k: torch.cuda.Event() for k in ("fork", "join", "l4f", "l4j")}
+        self._ev = [{k: torch.cuda.Event() for k in ("fork", "join")}
                     for _ in range(2)]
         if kind == "ideal":         # its own: the rollout runs beside the scene's moments
             self.ideal_ws = engine.Workspace(self.device)
@@ -336,11 +337,6 @@ class StepGraph:
                     p(o.d("pl")), engine._stream()), "ccmpc_ideal_minkowski_cycle_ex")
         for fn, args in self._sample_calls(s):
             chk(fn(*args), fn.__name__)
-        # L4 only reads the bucketed store: a branch beside the generator
-        ev["l4f"].record(main)
-        self.side.wait_event(ev["l4f"])
-        with torch.cuda.stream(self.side):
-            self._enqueue_l4(parity)
         mws = self.ws.buf
         if self.kind == "minkowski":
             chk(lib.ccmpc_minkowski_cycle(
@@ -360,15 +356,18 @@ class StepGraph:
                 main.wait_event(ev["join"])
         chk(copy(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
         chk(lib.ccmpc_signal_host(p(self.flags), p(i.d("gen")), s), "ccmpc_signal_host")
-        ev["l4j"].record(self.side)
-        main.wait_event(ev["l4j"])
+        # L4 (which only reads the bucketed store) after the record path's signal, on the same
+        # stream: the host's wait ends before it, and a linear graph launches in a fraction of
+        # the host time a forked one takes (one branch for L4 cost ~25 us more per
+        # hipGraphLaunch; with L4's nodes captured first, the cycle also started only after
+        # L4's first pass, profiles/r04/probe_step_l4_first.log)
+        self._enqueue_l4(parity)
 
     def _enqueue_l4(self, parity):
-        """The L4 branch on the current stream: L4 over the bucketed store, its copy-out into
-        the parity's pack, its signal."""
+        """The L4 branch on the current stream: L4 over the bucketed store into the parity's
+        device pack (read back on access: two graph nodes, no copy-out or signal to launch)."""
         lib, p, s = _lib.load(), engine._p, engine._stream()
         i, o, q, st = self.inp, self.out, self.out_l4s[parity], self.store
-        copy = lib.ccmpc_copy_kernel_async if self.copy_kernel else lib.ccmpc_copy_async
         lws = self.l4_ws.buf
         chk = engine._lib.check
         chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, self.ph, p(st.origin),
@@ -376,9 +375,6 @@ class StepGraph:
                                p(i.d("past")), p(i.d("bbox")), p(lws), lws.numel(),
                                p(q.d("A")), p(q.d("b")), p(q.d("yaw_mean")),
                                p(q.d("yaw0_var")), None, None, s), "ccmpc_l4_split")
-        chk(copy(p(q.host), p(q.dev), q.nbytes, s), "ccmpc_copy_async")
-        chk(lib.ccmpc_signal_host(p(self.flags[2 + 2 * parity:]), p(i.d("gen")), s),
-            "ccmpc_signal_host")
 
     def capture(self):
         """Record the two parity graphs (after one eager run that warms every kernel).
@@ -572,8 +568,10 @@ class StepGraph:
         if gen < 1 or gen < self.generation - 1 or gen > self.generation:
             raise RuntimeError(f"stale planning-step data: the L4 outputs of launch {gen} were "
                                f"overwritten (this graph is at launch {self.generation})")
-        self._poll(2 + 2 * (gen & 1), gen, "L4")
-        snap = self.out_l4s[gen & 1].snapshot()
+        # the parity's pack is not rewritten before launch gen + 2: the stream's work up to now
+        # includes gen's L4 branch (a step's graph joins its branches)
+        torch.cuda.current_stream(self.device).synchronize()
+        snap = self.out_l4s[gen & 1].snapshot(device=True)
         self._l4_snap = {k: v for k, v in self._l4_snap.items() if k >= self.generation - 1}
         self._l4_snap[gen] = snap
         return snap

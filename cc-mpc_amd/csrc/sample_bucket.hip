@@ -256,11 +256,11 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
 
 __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   __shared__ double2 gp_s[kFGroups * kMaxKept];   // the OV's centre partials [g][k]
-  __shared__ int hist[kFusedMaxBins];             // rare particles per bin, all of the OV
+  __shared__ int hist[kFusedMaxBins];             // rare particles per bin in slots >= r0
   __shared__ int pre[kFusedMaxBins];              // ... in rare-list slots before this block's
   __shared__ int bstart[kFusedMaxBins];           // bin start relative to the region
   __shared__ int wcnt[kRWaves][kFusedMaxBins];
-  __shared__ int okey[kRThreads];
+  __shared__ __attribute__((aligned(16))) int okey[kRThreads];
   __shared__ int keep_s[64], tot_s[kMaxKept + 1];
   __shared__ int64_t cst_s[kMaxKept];
   __shared__ double cen_s[kMaxKept][2];
@@ -300,6 +300,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   }
   const int nbins = K * (L + 1);
   for (int b = tid; b < nbins; b += kRThreads) hist[b] = pre[b] = 0;
+  okey[tid] = -1;                                 // not one of this block's rare slots
   __syncthreads();
   FUSED_TS(2, 1);
   const int R = tot_s[K];
@@ -327,8 +328,8 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   }
   __syncthreads();
   FUSED_TS(2, 2);
-  // every rare particle's key (owner (L + 1) + 1 + z), counted per bin: in total, and before
-  // this block's first slot; this block's own keys kept
+  // every rare particle's key (owner (L + 1) + 1 + z), counted per bin before this block's
+  // first slot (pre) and from it on (hist): one LDS atomic per key; this block's own keys kept
   for (int q0 = 0; q0 < R; q0 += kB * kRThreads) {
     if (q0 > 0) load_batch(q0);
 #pragma unroll
@@ -337,8 +338,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
       if (q < R) {
         const int kq = key_staged(__builtin_bit_cast(int, f[j].z), static_cast<double>(f[j].x) + mx,
                                   static_cast<double>(f[j].y) + my, keep_s, cen_s, K, L);
-        atomicAdd(&hist[kq], 1);
-        if (q < r0) atomicAdd(&pre[kq], 1);
+        atomicAdd(q < r0 ? &pre[kq] : &hist[kq], 1);
         if (q >= r0 && q < r0 + kRThreads) okey[q - r0] = kq;
       }
     }
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
     const int upto = gi == 0 ? L : gi - 1;  // gi == 0 (the natives' bin): every rare bin of k
     int s = 0;
 #pragma unroll 8
-    for (int zz = 0; zz < upto; ++zz) s += hist[hb + zz];
+    for (int zz = 0; zz < upto; ++zz) s += hist[hb + zz] + pre[hb + zz];
     if (gi > 0) {
       bstart[b] = static_cast<int>(cst_s[k] - reg) + tot_s[k] + s;
     } else if (blockIdx.x == 0) {
@@ -367,19 +367,27 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
     }
   }
   FUSED_TS(2, 4);
-  // this block's stable ranks: lanes in order within a wave, waves in order
-  const int kr = own ? okey[tid] : -1;
-  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  int rank = 0;
-  unsigned long long todo = __ballot(own);
-  while (todo) {
-    const int leader = __ffsll(static_cast<long long>(todo)) - 1;
-    const int kl = __shfl(kr, leader, 64);
-    const unsigned long long m = __ballot(own && kr == kl);
-    if (own && kr == kl) rank = __popcll(m & below);
-    if (lane == leader) wcnt[w][kl] = __popcll(m);
-    todo &= ~m;
+  // this block's stable ranks: lanes in order within a wave, waves in order.  Every lane scans
+  // its wave's 64 keys (broadcast LDS reads, 16 bytes at a time): the same-key lanes before it
+  // (its rank) and in all (the wave's count, written by the last such lane) -- a fixed 16
+  // reads, where a ballot round per distinct key took up to ~30 dependent rounds
+  const int kr = okey[tid];
+  int rank = 0, cnt = 0;
+  {
+    const int4 *wk = reinterpret_cast<const int4 *>(okey + w * 64);
+#pragma unroll
+    for (int j4 = 0; j4 < 16; ++j4) {
+      const int4 k4 = wk[j4];
+      const int kk[4] = {k4.x, k4.y, k4.z, k4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool same = kk[e] == kr;
+        rank += (same && 4 * j4 + e < lane) ? 1 : 0;
+        cnt += same ? 1 : 0;
+      }
+    }
   }
+  if (own && rank == cnt - 1) wcnt[w][kr] = cnt;
   __syncthreads();
   FUSED_TS(2, 5);
   if (own) {

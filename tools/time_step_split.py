@@ -24,8 +24,9 @@ def wrap(name, f):
         t0 = time.perf_counter(); r = f(*a, **k); marks[name] = marks.get(name, 0) + time.perf_counter() - t0; return r
     return w
 g.launch, g.wait, g.out.snapshot, g.set_inputs = wrap("launch", orig_launch), wrap("wait", orig_wait), wrap("snapshot", orig_snap), wrap("set_inputs", orig_set)
-agent._state_stats = wrap("state_stats", agent._state_stats)
-agent._cell_risk_host = wrap("cell_risk", agent._cell_risk_host)
+for name in ("_cell_risk_host", "_step_tuple", "_src_cells_host"):
+    if hasattr(agent, name):
+        setattr(agent, name, wrap(name.strip("_"), getattr(agent, name)))
 n = 300
 t0 = time.perf_counter()
 for i in range(n):
