@@ -140,3 +140,71 @@ class PlanningQP:
         if self.u_order == U_ORDER_F:
             return u.reshape(-1, 2, self.T).transpose(1, 2)
         return u.reshape(-1, self.T, 2)
+
+
+class PlanningQPStep:
+    """One scene's planning QP as the planner calls it every frame, with its host traffic in
+    two pinned packs (ccmpc/step.py's Pack): the frame's x_init, reference, goal and executed
+    controls go up in one copy kernel, the LTV model (when the frame rebuilds it) and the solve
+    run on the device on the generator's device records, and u, X, cost and status come back
+    in one copy kernel followed by ccmpc_signal_host, which the host polls -- one wait for the
+    whole solve instead of a synchronising copy per tensor (~10 us each).
+
+    The LTV buffers (xbar [1, 4 ph], gamma [1, 4 ph, 2 ph]) belong to the caller: they are
+    rebuilt at Tsh == ph and kept below it (v8ideal/__init__.py:2858-2891)."""
+
+    def __init__(self, n_cells, T, T_full, kind=REC_HALFSPACE, params=None, u_order=U_ORDER_F,
+                 device="cuda"):
+        from . import step
+        self.T, self.T_full = int(T), int(T_full)
+        T, Tf = self.T, self.T_full
+        self.device = engine.require_device(device)
+        self.u_order = int(u_order)
+        f64, i32, i64 = torch.float64, torch.int32, torch.int64
+        self.inp = step.Pack([("gen", (2,), i64), ("x0", (1, 4), f64), ("ref", (1, T, 2), f64),
+                              ("goal", (1, 2), f64), ("uprev", (1, max(2 * (Tf - T), 1)), f64)],
+                             self.device)
+        self.out = step.Pack([("u", (1, 2 * T), f64), ("X", (1, T, 4), f64), ("cost", (1,), f64),
+                              ("status", (1,), i32), ("iters", (1,), i32)], self.device)
+        self.qp = PlanningQP([n_cells], T, T_full=Tf, kind=kind, params=params,
+                             u_order=u_order, device=self.device)
+        o = self.out        # the solve writes straight into the output pack's device half
+        self.qp.u, self.qp.X, self.qp.cost = o.d("u"), o.d("X"), o.d("cost")
+        self.qp.status, self.qp.iters = o.d("status"), o.d("iters")
+        self.flags = torch.zeros(2, dtype=i64, pin_memory=True)
+        self._flags = self.flags.numpy()
+        self.generation = 0
+
+    def solve(self, x_init, goal, ref_traj, rec, xbar, gamma, u_prev=None, ltv=False, Ts=0.5,
+              lon=3.7):
+        """Enqueue the frame on the current stream and wait for its answer on the host:
+        {cost, U_star (T, 2), X_star (T, 4), u (2T,), status, iters}.  ltv: rebuild xbar /
+        gamma from x_init first (Tsh == ph)."""
+        from . import step
+        T, Tf = self.T, self.T_full
+        i, o, lib, p = self.inp, self.out, _lib.load(), engine._p
+        i.h("x0")[0] = np.asarray(x_init, np.float64).reshape(4)
+        i.h("ref")[0] = np.asarray(ref_traj, np.float64)[:T].reshape(T, 2)
+        i.h("goal")[0] = np.asarray(goal, np.float64).reshape(2)
+        if T < Tf:
+            if u_prev is None:
+                raise ValueError("u_prev (the executed controls) is required when T < T_full")
+            i.h("uprev")[0] = np.asarray(u_prev, np.float64).reshape(2 * (Tf - T))
+        self.generation += 1
+        gen = self.generation
+        i.h("gen")[0] = gen
+        s = engine._stream()
+        chk = _lib.check
+        chk(lib.ccmpc_copy_kernel_async(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
+        if ltv:
+            chk(lib.ccmpc_mpc_ltv(p(i.d("x0")), 1, Tf, float(Ts), 0.5 * float(lon), float(lon),
+                                  p(xbar), p(gamma), s), "ccmpc_mpc_ltv")
+        self.qp.solve(gamma, xbar, i.d("goal"), i.d("ref"), rec,
+                      u_prev=i.d("uprev") if T < Tf else None)
+        chk(lib.ccmpc_copy_kernel_async(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
+        chk(lib.ccmpc_signal_host(p(self.flags), p(i.d("gen")), s), "ccmpc_signal_host")
+        step.poll_word(self._flags, 0, gen, self.device, f"planning QP {gen}: the")
+        u = o.h("u")[0].copy()
+        U = u.reshape(2, T).T.copy() if self.u_order == U_ORDER_F else u.reshape(T, 2).copy()
+        return {"cost": float(o.h("cost")[0]), "U_star": U, "X_star": o.h("X")[0].copy(),
+                "u": u, "status": int(o.h("status")[0]), "iters": int(o.h("iters")[0])}

@@ -1194,33 +1194,31 @@ class MidlevelAgent:
         if int(Tsh) != T:
             raise ValueError(f"records are for T = {T}, not Tsh = {Tsh}")
         ph = self.prediction_horizon
-        if T == ph or self._ltv is None:
-            self._ltv = mpc.ltv(np.asarray(x_init, np.float64)[None], ph, Ts=self.steptime,
-                                lon=lon)
+        if self._ltv is None:               # device buffers, rebuilt in place at Tsh == ph
+            self._ltv = (torch.empty((1, 4 * ph), dtype=torch.float64, device=self.device),
+                         torch.empty((1, 4 * ph, 2 * ph), dtype=torch.float64,
+                                     device=self.device))
+            self._ltv_built = False
         xbar, gamma = self._ltv
         key = (rec.shape[0], T, kind, u_order)
-        qp = self._qp.get(key)
-        if qp is None:
-            qp = mpc.PlanningQP([rec.shape[0]], T, T_full=ph, kind=kind,
-                                params=self.mpc_params, u_order=u_order, device=self.device)
-            self._qp[key] = qp
-        dev = self.device
-        ref = torch.as_tensor(np.asarray(ref_traj, np.float64)[None, :T], device=dev)
-        goal_t = torch.as_tensor(np.asarray(goal, np.float64).reshape(1, 2), device=dev)
-        up = None
-        if T < ph:
-            if u_prev is None:
-                raise ValueError(f"Tsh = {T} < ph = {ph} needs u_prev, the controls executed "
-                                 "since the first shrinking step (:3186)")
-            up = torch.as_tensor(np.asarray(u_prev, np.float64).reshape(1, 2 * (ph - T)),
-                                 device=dev)
-        u, X, cost, status, _ = qp.solve(gamma, xbar, goal_t, ref, rec, u_prev=up)
-        st = int(status[0])
+        run = self._qp.get(key)
+        if run is None:
+            run = mpc.PlanningQPStep(rec.shape[0], T, ph, kind=kind, params=self.mpc_params,
+                                     u_order=u_order, device=self.device)
+            self._qp[key] = run
+        if T < ph and u_prev is None:
+            raise ValueError(f"Tsh = {T} < ph = {ph} needs u_prev, the controls executed "
+                             "since the first shrinking step (:3186)")
+        build = T == ph or not self._ltv_built
+        res = run.solve(x_init, goal, ref_traj, rec, xbar, gamma, u_prev=u_prev, ltv=build,
+                        Ts=self.steptime, lon=lon)
+        self._ltv_built = True
+        st = res["status"]
         if st & (mpc.QP_MAXITER | mpc.QP_NUMERIC):
             raise InSimulationException("Optimizer failed to find a solution")
-        return {"cost": float(cost[0]), "U_star": qp.U(u)[0].cpu().numpy(),
-                "X_star": X[0].cpu().numpy(), "goal": np.asarray(goal, np.float64),
-                "u": u[0].cpu().numpy(), "skipped_rows": bool(st & mpc.QP_SKIPPED_ROWS)}
+        return {"cost": res["cost"], "U_star": res["U_star"], "X_star": res["X_star"],
+                "goal": np.asarray(goal, np.float64), "u": res["u"],
+                "skipped_rows": bool(st & mpc.QP_SKIPPED_ROWS)}
 
     def _loaded_tangents(self, loaded, mean, K, T, x_init, ref):
         """The previous frame's slopes / tangent indices for every (cell, t) of this frame

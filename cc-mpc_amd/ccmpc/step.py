@@ -132,6 +132,26 @@ class HipGraph:
             self.exec = None
 
 
+def poll_word(words, slot, gen, device, what):
+    """Spin until the pinned signal word words[slot] (written by ccmpc_signal_host) reaches
+    `gen`.  A word that does not arrive within 5 s (a faulted kernel never signals)
+    synchronises the device, which raises the error, or else reports the missing signal."""
+    if words[slot] >= gen:
+        return
+    deadline, n = None, 0
+    while words[slot] < gen:
+        n += 1
+        if n & 0x3FF == 0:
+            now = time.perf_counter()
+            if deadline is None:
+                deadline = now + 5.0
+            elif now > deadline:
+                torch.cuda.synchronize(device)
+                if words[slot] < gen:
+                    raise RuntimeError(f"{what} signal never came (word {slot} = "
+                                       f"{int(words[slot])}, expected {gen})")
+
+
 class StepGraph:
     """Sampler -> bucketing -> the step's generator kernels and, as a parallel branch, L4, for
     one shape.
@@ -528,24 +548,7 @@ class StepGraph:
             g.replay(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _poll(self, slot, gen, what):
-        """Spin until the pinned signal word `slot` reaches `gen`.  A word that does not arrive
-        within 5 s (a faulted kernel never signals) synchronises the device, which raises the
-        error, or else reports the missing signal."""
-        f = self._flags
-        if f[slot] >= gen:
-            return
-        deadline, n = None, 0
-        while f[slot] < gen:
-            n += 1
-            if n & 0x3FF == 0:
-                now = time.perf_counter()
-                if deadline is None:
-                    deadline = now + 5.0
-                elif now > deadline:
-                    torch.cuda.synchronize(self.device)
-                    if f[slot] < gen:
-                        raise RuntimeError(f"planning step {gen}: the {what} signal never came "
-                                           f"(word {slot} = {int(f[slot])})")
+        poll_word(self._flags, slot, gen, self.device, f"planning step {gen}: the {what}")
 
     def wait(self):
         """Return when the launched step's output pack (records, moments, counts) is on the

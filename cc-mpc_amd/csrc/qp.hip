@@ -1280,8 +1280,11 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         {
           const int j = lane < n ? lane : 0;
 #pragma unroll
-          for (int a = 0; a < NR; ++a)
-            v = fma(-Wm[(a < na ? a : 0) * n + j], lane_bcast(lamr, a), v);  // lamr = 0 past na
+          for (int a = 0; a < NR; ++a) {  // rows past na are never written (with na = 0 not
+            // even row 0): select, never multiply, what may be stale LDS
+            const double wa = Wm[(a < na ? a : 0) * n + j];
+            v = a < na ? fma(-wa, lane_bcast(lamr, a), v) : v;
+          }
         }
         const double zpr = reg_backward(ltH, Ldl, lane < n ? v : 0.0);
         if (lane < n) zp[lane] = zpr;

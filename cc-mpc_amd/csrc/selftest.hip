@@ -75,9 +75,34 @@ __global__ __launch_bounds__(64) void selftest_kernel(int kind, int64_t n,
   }
 }
 
+// Fills the whole LDS of every CU with one value (test aid): a kernel that reads LDS before
+// writing it would see it.  160 KB per workgroup, enough workgroups to visit every CU.
+__global__ __launch_bounds__(1024) void poison_lds_kernel(double value) {
+  extern __shared__ double lds_all[];
+  const int n = static_cast<int>(160 * 1024 / sizeof(double));
+  for (int i = threadIdx.x; i < n; i += blockDim.x) lds_all[i] = value;
+  __syncthreads();
+  // keep the stores (a never-true read so the compiler cannot drop them)
+  if (lds_all[threadIdx.x] != value && value == value) lds_all[0] = 0.0;
+}
+
 }  // namespace ccmpc
 
 using namespace ccmpc;
+
+extern "C" int ccmpc_poison_lds(double value, ccmpc_stream_t stream) {
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(poison_lds_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+  if (e != hipSuccess) {
+    set_error(std::string("ccmpc_poison_lds: ") + hipGetErrorString(e));
+    return CCMPC_ERR_LAUNCH;
+  }
+  hipLaunchKernelGGL(poison_lds_kernel, dim3(4096), dim3(1024), 160 * 1024, as_stream(stream),
+                     value);
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}
 
 extern "C" int ccmpc_selftest(int kind, int64_t n, const double *in, double *out, double tol,
                               int32_t maxiter, ccmpc_stream_t stream) {

@@ -488,6 +488,11 @@ int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamm
 int ccmpc_selftest(int kind, int64_t n, const double *in, double *out, double tol,
                    int32_t maxiter, ccmpc_stream_t stream);
 
+/* Test aid: fill every CU's LDS with `value` (tests/test_gpu_lds_poison.py runs the kernels
+ * after NaN and after zero fills and requires the same bits: no kernel reads LDS it did not
+ * write). */
+int ccmpc_poison_lds(double value, ccmpc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
