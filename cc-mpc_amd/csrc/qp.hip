@@ -24,8 +24,10 @@ namespace ccmpc {
 
 #ifdef CCMPC_QP_TRACE
 #define QP_MARK(i) (tmark[i] = wall_clock64())
+#define PQ_MARK(i) (pmark[i] = pmark[i] ? pmark[i] : wall_clock64())
 #else
 #define QP_MARK(i) ((void)0)
+#define PQ_MARK(i) ((void)0)
 #endif
 
 constexpr int kQpThreads = 256;
@@ -698,12 +700,27 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     rw.ix[2 * r + 1] = i0;
   }
   qp_sync<NW>();
-  // f = Gs^T qf (for the scaling of the dual residual)
+  // f = Gs^T qf (the scaling of the dual residual; kept in LDS for the polish)
   double fmax_ = 0.0;
-  for (int j = tid; j < n; j += NTH) {
+  if constexpr (NW == 1) {  // a quad per control, DPP sum (as the IPM's rd)
+    const int j = lane >> 2, kq = lane & 3, jj = j < n ? j : 0;
     double v = 0.0;
-    for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * qf[k];
-    fmax_ = fmax(fmax_, fabs(v));
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int k = kq + 4 * i, kk = k < T3 ? k : 0;
+      const double g = Gs[kk * n + jj], qk = qf[kk];
+      v = k < T3 ? fma(g, qk, v) : v;
+    }
+    v = sum4(v);
+    if (kq == 0 && j < n) lds[lay.f + j] = v;
+    fmax_ = j < n ? fabs(v) : 0.0;
+  } else {
+    for (int j = tid; j < n; j += NTH) {
+      double v = 0.0;
+      for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * qf[k];
+      lds[lay.f + j] = v;
+      fmax_ = fmax(fmax_, fabs(v));
+    }
   }
   // initial point: z = 0 (inside the control box), s = max(-g(0), 1), lambda = 1
   // g(z) = row_lin(r, Gs z, z) + row_const(r): the linear part in the state's output rows
@@ -779,6 +796,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   bool infeasible = false;
 #ifdef CCMPC_QP_TRACE
   uint64_t tmark[8] = {};
+  uint64_t pmark[8] = {};  // polish: first pass through each point
   const uint64_t tk1 = wall_clock64();
 #endif
   constexpr int NR = NM > 0 ? NM : 1;
@@ -1168,23 +1186,45 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     double *Wm = lds + lay.pw, *Sm = lds + lay.ps, *act = lds + lay.pact,
            *sdinv = lds + lay.pdinv;
     double *fu = lds + lay.f, *y0 = rh, *rs = e2, *lam = q, *zp = dz, *yp = yd;
-    // H (no barrier terms) into M; f in control space
-    for (int e = tid; e < n * n; e += NTH) {
-      const int i = e / n, j = e % n;
-      if (j > i) continue;
-      double v = hctrl(i, j, T, order, p);
-      for (int t = 0; t < T; ++t) {
+    PQ_MARK(0);
+    // H (no barrier terms) into M; f in control space (fu) is the setup's
+    if constexpr (NW == 1) {  // as the IPM's M: lane column jm, rows (lane >> 4) + 4 m
+      const int jm = lane & 15, jc = jm < n ? jm : 0;
+      double hx[8], hy[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int tt = t < T ? t : 0;
         const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
-        v += wp * (Gs[(3 * t) * n + i] * Gs[(3 * t) * n + j] +
-                   Gs[(3 * t + 1) * n + i] * Gs[(3 * t + 1) * n + j]);
+        hx[t] = t < T ? wp * Gs[(3 * tt) * n + jc] : 0.0;
+        hy[t] = t < T ? wp * Gs[(3 * tt + 1) * n + jc] : 0.0;
       }
-      M[i * ldm + j] = v;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int im = (lane >> 4) + 4 * m;
+        const bool on = im < n && jm <= im;
+        const int ic = on ? im : 0;
+        double v = Hc[ic * n + jc];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int tt = t < T ? t : 0;
+          v = fma(Gs[(3 * tt) * n + ic], hx[t], fma(Gs[(3 * tt + 1) * n + ic], hy[t], v));
+        }
+        if (on) M[im * ldm + jm] = v;
+      }
+    } else {
+      for (int e = tid; e < n * n; e += NTH) {
+        const int i = e / n, j = e % n;
+        if (j > i) continue;
+        double v = hctrl(i, j, T, order, p);
+        for (int t = 0; t < T; ++t) {
+          const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+          v += wp * (Gs[(3 * t) * n + i] * Gs[(3 * t) * n + j] +
+                     Gs[(3 * t + 1) * n + i] * Gs[(3 * t + 1) * n + j]);
+        }
+        M[i * ldm + j] = v;
+      }
     }
-    for (int j = tid; j < n; j += NTH) {
-      double v = 0.0;
-      for (int k = 0; k < T3; ++k) v += Gs[k * n + j] * qf[k];
-      fu[j] = v;
-    }
+    PQ_MARK(1);
     // active rows, compacted in row order (ballot + prefix: deterministic)
     int na = 0;
     for (int64_t base = 0; base < mrows; base += NTH) {
@@ -1203,6 +1243,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       qp_sync<NW>();
     }
     if constexpr (NM > 0 && NW == 1) {
+      PQ_MARK(2);
       // One wave, n <= 16: the same polish with every factor in registers (identity-padded
       // to 16 x 16, straight-line; reg_cholesky without the pivot skip), the L^T columns read
       // ahead of each backward chain, the vectors moved between lanes by readlane.
@@ -1223,27 +1264,41 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       if (lane < n) y0[lane] = y0r;
       if (hfail) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
       for (int round = 0; !hfail && round < 4 && na <= n; ++round) {
-        // W rows w_a = L^{-1} g_a (g on lane = control), rs_a = w_a . y0 - h_a
-        for (int a = 0; a < na; ++a) {
+        PQ_MARK(3);
+        // W rows w_a = L^{-1} g_a, rs_a = w_a . y0 - h_a: one active row per lane (na <= n),
+        // each lane's own forward substitution (L's entries are the same address on every
+        // lane: broadcast LDS reads), so all rows advance together instead of one triangular
+        // solve per row.  The row's gradient from its one-form (c0, c1, i0, i1): d v[i] / d z_j
+        // is Gs[i][j] for an output row i < T3, else [i - T3 == j].
+        {
+          const int a = lane < na ? lane : 0;
           const int64_t r = static_cast<int64_t>(act[a]);
-          const int j = lane < n ? lane : 0;
-          double g;
-          if (r < nbox) {
-            g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
-          } else if (r < nbox + nv) {
-            const int t = static_cast<int>((r - nbox) >> 1);
-            g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
-          } else {
-            const int64_t o = r - nbox - nv;
-            const int t = rw.ix[2 * (nbox + nv + o)] / 3;
-            g = oa0[o] * Gs[(3 * t) * n + j] + oa1[o] * Gs[(3 * t + 1) * n + j];
+          const int2 ix = reinterpret_cast<const int2 *>(rw.ix)[r];
+          const double c0 = rw.c0[r], c1 = rw.c1[r];
+          const int x0c = ix.x < T3 ? ix.x : 0, x1c = ix.y < T3 ? ix.y : 0;
+          double wv[NR];
+          double d = 0.0;
+#pragma unroll
+          for (int j = 0; j < NR; ++j) {
+            const int jc = j < n ? j : 0;
+            const double ga = Gs[x0c * n + jc], gb = Gs[x1c * n + jc];
+            const double g0 = ix.x < T3 ? ga : (ix.x - T3 == j ? 1.0 : 0.0);
+            const double g1 = ix.y < T3 ? gb : (ix.y - T3 == j ? 1.0 : 0.0);
+            double v = c0 * g0 + c1 * g1;
+#pragma unroll
+            for (int k = 0; k < j; ++k) v = fma(-M[jc * ldm + k], wv[k], v);
+            wv[j] = j < n ? v * lane_bcast(Ldl, j) : 0.0;
+            d = fma(wv[j], lane_bcast(y0r, j), d);
           }
-          const double bw_ = reg_forward(La, Ldl, lane < n ? g : 0.0);
-          if (lane < n) Wm[a * n + lane] = bw_;
-          const double d = wave_sum(lane < n ? bw_ * y0r : 0.0);
-          if (lane == 0) rs[a] = d + row_const(r);
+          if (lane < na) {
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+              if (j < n) Wm[lane * n + j] = wv[j];
+            rs[lane] = d + row_const(r);
+          }
         }
         wave_sync();
+        PQ_MARK(4);
         // S = W W^T: lane (i, kq) = (lane & 15, lane >> 4) forms S[i][kq + 4 m]
         {
           const int i = lane & 15, kq = lane >> 4, ic = i < na ? i : 0;
@@ -1275,6 +1330,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         wave_sync();
         const double lamr = reg_solve(Ls, Sm, ldm, Sdl, na, lane < na ? rs[lane] : 0.0);
         if (lane < na) lam[lane] = lamr;
+        PQ_MARK(5);
         // z = L^{-T}(y0 - W^T lambda)
         double v = y0r;
         {
@@ -1297,6 +1353,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
           if (lane < T3) yp[lane] = yv;
         }
         wave_sync();
+        PQ_MARK(6);
         double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
         for (int64_t r = tid; r < mrows; r += NTH) {
           const double g = row_g(r, yp, zp);
@@ -1517,8 +1574,11 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk4 = wall_clock64();
   if (tid == 0 && sc == 0)
-    printf("qp phases (10ns): setup %d iterations %d polish %d outputs %d\n", int(tk1 - tk0),
-           int(tk2 - tk1), int(tk3 - tk2), int(tk4 - tk3));
+    printf("qp phases (10ns): setup %d iterations %d polish %d outputs %d\n"
+           "   polish (first round): H %d act %d factor %d W %d S %d z %d\n", int(tk1 - tk0),
+           int(tk2 - tk1), int(tk3 - tk2), int(tk4 - tk3), int(pmark[1] - pmark[0]),
+           int(pmark[2] - pmark[1]), int(pmark[3] - pmark[2]), int(pmark[4] - pmark[3]),
+           int(pmark[5] - pmark[4]), int(pmark[6] - pmark[5]));
 #endif
 }
 
