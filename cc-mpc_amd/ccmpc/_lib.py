@@ -62,6 +62,7 @@ SIGNATURES = {
     "ccmpc_graph_capture_end": (ctypes.c_int, [_P, _P]),
     "ccmpc_graph_launch": (ctypes.c_int, [_P, _P]),
     "ccmpc_signal_host": (ctypes.c_int, [_P, _P, _P]),
+    "ccmpc_copy_signal_async": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _P]),
     "ccmpc_graph_destroy": (ctypes.c_int, [_P]),
     "ccmpc_moments_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "ccmpc_moments": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64, _I64, _P,

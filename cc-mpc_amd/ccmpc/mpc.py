@@ -201,8 +201,8 @@ class PlanningQPStep:
                                   p(xbar), p(gamma), s), "ccmpc_mpc_ltv")
         self.qp.solve(gamma, xbar, i.d("goal"), i.d("ref"), rec,
                       u_prev=i.d("uprev") if T < Tf else None)
-        chk(lib.ccmpc_copy_kernel_async(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
-        chk(lib.ccmpc_signal_host(p(self.flags), p(i.d("gen")), s), "ccmpc_signal_host")
+        chk(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
+                                        p(i.d("gen")), s), "ccmpc_copy_signal_async")
         step.poll_word(self._flags, 0, gen, self.device, f"planning QP {gen}: the")
         u = o.h("u")[0].copy()
         U = u.reshape(2, T).T.copy() if self.u_order == U_ORDER_F else u.reshape(T, 2).copy()

@@ -20,19 +20,17 @@ cell counts on the device.  ``StepGraph`` captures, per kind,
                          moments (the t = 0 statistics, :864-875) } -> copy-out
     affine    (T == ph)  copy-in -> sampler -> bucketing -> moments -> GMM-affine -> copy-out
 
-with the L4 outer approximation (vertices / A_union / b_union and the heading statistics,
-:627-736) as a second branch of the same graph, forked off once the store is bucketed:
+each as one linear graph that ends with the L4 outer approximation (vertices / A_union /
+b_union and the heading statistics, :627-736):
 
-    ... bucketing -+-> generator -> copy-out -> signal A
-                   +-> L4 -> L4 copy-out -> signal B       (side stream, joined at the end)
+    ... generator -> copy-out -> signal -> L4          (one stream; one hipGraphLaunch)
 
-The host does not synchronise the stream: each branch ends with ccmpc_signal_host, which writes
-the step's generation number into a pinned word after everything the branch wrote, and the
-host polls that word.  So the records, moments and counts are read as soon as their copy-out
-lands, while L4 (only returned by the generator, never fed to the QP, :951-952) is still
-running; its outputs are read lazily, on access.  Two graphs alternate by the generation's
-parity, each with its own L4 output buffers, so the previous step's L4 stays readable while the
-next step runs.
+The host does not synchronise the stream: after the copy-out, ccmpc_signal_host writes the
+step's generation number into a pinned word behind every output byte, and the host polls that
+word.  So the records, moments and counts are read as soon as they land, while L4 (only
+returned by the generator, never fed to the QP, :951-952) still runs; its device outputs are
+read back on first access.  Two graphs alternate by the generation's parity, each with its own
+L4 output buffers, so the previous step's L4 stays readable while the next step runs.
 
 A step is: write the inputs into pinned memory, launch one graph, poll, read the outputs
 through NumPy views of one snapshot.  The Philox seeds travel in the packed inputs (ccmpc_sample_unicycle_ex
@@ -291,6 +289,11 @@ class StepGraph:
         # (CCMPC_STEP_COPY_KERNEL=0) as memcpy nodes (a runtime blit of ~4.8 us each): the
         # kernels take ~8 us off a step (profiles/r02/v33_step_copy_kernel.txt)
         self.copy_kernel = os.environ.get("CCMPC_STEP_COPY_KERNEL", "1") == "1"
+        # the multi-block copy kernel followed by ccmpc_signal_host, or (=1) both as one
+        # single-workgroup launch: one CU's copy of the ~50 KB pack costs more than the launch
+        # it saves (C2 step 100.4 vs 102.6 us, profiles/r04/ab_fused_signal.log); the QP's
+        # sub-KB pack takes the fused form
+        self.fused_signal = os.environ.get("CCMPC_STEP_FUSED_SIGNAL", "0") == "1"
         self.graphs = None                  # [parity 0, parity 1]
         # launches before this one run eagerly (the same calls, no capture): a shape used once
         # -- each shrinking horizon of an episode on a fresh agent -- never pays the capture
@@ -374,8 +377,12 @@ class StepGraph:
             elif self.ideal_fork:
                 ev["join"].record(self.aux)
                 main.wait_event(ev["join"])
-        chk(copy(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
-        chk(lib.ccmpc_signal_host(p(self.flags), p(i.d("gen")), s), "ccmpc_signal_host")
+        if self.copy_kernel and self.fused_signal:   # one single-workgroup launch
+            chk(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
+                                            p(i.d("gen")), s), "ccmpc_copy_signal_async")
+        else:
+            chk(copy(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
+            chk(lib.ccmpc_signal_host(p(self.flags), p(i.d("gen")), s), "ccmpc_signal_host")
         # L4 (which only reads the bucketed store) after the record path's signal, on the same
         # stream: the host's wait ends before it, and a linear graph launches in a fraction of
         # the host time a forked one takes (one branch for L4 cost ~25 us more per

@@ -79,6 +79,52 @@ __global__ __launch_bounds__(64) void signal_host_kernel(int64_t *dst, const int
   __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Copy-out and signal in one single-workgroup kernel: every wave copies its share, waits for
+// its stores (vmcnt(0)), the workgroup meets at a barrier, then one thread makes everything the
+// CU wrote visible at system scope (the release writes back this XCD's L2, where all of this
+// kernel's stores went) and stores the value.  One launch less on a planning step's critical
+// path than ccmpc_copy_kernel_async followed by ccmpc_signal_host.
+__global__ __launch_bounds__(1024) void copy16_signal_kernel(uint4 *__restrict__ dst,
+                                                             const uint4 *__restrict__ src,
+                                                             size_t n, int64_t *host_word,
+                                                             const int64_t *value) {
+  constexpr int U = 4;  // 4 loads in flight per thread before the stores (64 KB in one pass)
+  for (size_t base = 0; base < n; base += U * blockDim.x) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      if (i < n) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      if (i < n) dst[i] = v[u];
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores have landed in L2
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t v = __hip_atomic_load(value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope
+    __hip_atomic_store(host_word, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+extern "C" int ccmpc_copy_signal_async(void *dst, const void *src, size_t bytes,
+                                       int64_t *host_word, const int64_t *value,
+                                       ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(dst && src && host_word && value, "null pointer");
+  CCMPC_REQUIRE(bytes % 16 == 0 && ccmpc::aligned(dst, 16) && ccmpc::aligned(src, 16) &&
+                    ccmpc::aligned(host_word, 8) && ccmpc::aligned(value, 8),
+                "bytes and pointers must be 16-byte (words 8-byte) aligned");
+  hipLaunchKernelGGL(copy16_signal_kernel, dim3(1), dim3(1024), 0, ccmpc::as_stream(stream),
+                     static_cast<uint4 *>(dst), static_cast<const uint4 *>(src), bytes / 16,
+                     host_word, value);
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}
+
 extern "C" int ccmpc_signal_host(int64_t *host_word, const int64_t *value, ccmpc_stream_t stream) {
   CCMPC_REQUIRE(host_word && value, "null pointer");
   CCMPC_REQUIRE(ccmpc::aligned(host_word, 8) && ccmpc::aligned(value, 8),

@@ -110,6 +110,10 @@ int ccmpc_copy_kernel_async(void *dst, const void *src, size_t bytes, ccmpc_stre
  * every write this stream made before it (a system-scope release).  A captured step's host side
  * polls the word rather than synchronising the stream. */
 int ccmpc_signal_host(int64_t *host_word, const int64_t *value, ccmpc_stream_t stream);
+/* ccmpc_copy_kernel_async (device -> pinned host) and ccmpc_signal_host in one single-workgroup
+ * launch: *host_word = *value becomes visible only after the copied bytes. */
+int ccmpc_copy_signal_async(void *dst, const void *src, size_t bytes, int64_t *host_word,
+                            const int64_t *value, ccmpc_stream_t stream);
 
 /* Graph capture of a planning step (ccmpc/step.py): begin / end a relaxed-mode capture on
  * `stream` (the library calls and event record / wait pairs issued in between become the
