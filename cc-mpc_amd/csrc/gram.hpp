@@ -400,12 +400,50 @@ struct Quad<float> {
   }
 };
 
+// The stream loop's particle loads with the nontemporal hint: the store is read exactly once, so
+// it need not displace what the caches hold.  Measured (profiles/r04/ab_nt_loads.log): the
+// Scheme4 kernel's 16-byte row loads (load_pair, T = 9..12) gain -- the 64-scene C4 batch 218 ->
+// 211 us warm, 211 -> 200 us cold (0.58 -> 0.61 of 8 TB/s), the per-GPU batch 36-37 -> 33.6 us
+// cold -- while the 16x16-tile kernel's quad loads lose at T = 40 (C5 80 -> 88 us) and are
+// neutral at T = 8: so pairs on, quads off.
+#ifndef CCMPC_NT_PAIR
+#define CCMPC_NT_PAIR 1
+#endif
+#ifndef CCMPC_NT_QUAD
+#define CCMPC_NT_QUAD 0
+#endif
+typedef double ccmpc_d2v __attribute__((ext_vector_type(2)));
+typedef float ccmpc_f2v __attribute__((ext_vector_type(2)));
+typedef float ccmpc_f4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ double2 stream_load2(const double *p) {
+  if constexpr (NT) {
+    const ccmpc_d2v t = __builtin_nontemporal_load(reinterpret_cast<const ccmpc_d2v *>(p));
+    return make_double2(t.x, t.y);
+  } else {
+    return *reinterpret_cast<const double2 *>(p);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ float2 stream_load2(const float *p) {
+  if constexpr (NT) {
+    const ccmpc_f2v t = __builtin_nontemporal_load(reinterpret_cast<const ccmpc_f2v *>(p));
+    return make_float2(t.x, t.y);
+  } else {
+    return *reinterpret_cast<const float2 *>(p);
+  }
+}
 __device__ __forceinline__ void load_quad(const double *__restrict__ p, Quad<double> &q) {
-  q.lo = *reinterpret_cast<const double2 *>(p);
-  q.hi = *reinterpret_cast<const double2 *>(p + 2);
+  q.lo = stream_load2<CCMPC_NT_QUAD != 0>(p);
+  q.hi = stream_load2<CCMPC_NT_QUAD != 0>(p + 2);
 }
 __device__ __forceinline__ void load_quad(const float *__restrict__ p, Quad<float> &q) {
-  q.v = *reinterpret_cast<const float4 *>(p);
+  if constexpr (CCMPC_NT_QUAD != 0) {
+    const ccmpc_f4v t = __builtin_nontemporal_load(reinterpret_cast<const ccmpc_f4v *>(p));
+    q.v = make_float4(t.x, t.y, t.z, t.w);
+  } else {
+    q.v = *reinterpret_cast<const float4 *>(p);
+  }
 }
 
 // 16-byte write-through (sc1) buffer accesses: one dwordx4 transaction per lane instead of two

@@ -150,10 +150,10 @@ struct Pair<float> {
   }
 };
 __device__ __forceinline__ void load_pair(const double *__restrict__ p, Pair<double> &q) {
-  q.v = *reinterpret_cast<const double2 *>(p);
+  q.v = stream_load2<CCMPC_NT_PAIR != 0>(p);
 }
 __device__ __forceinline__ void load_pair(const float *__restrict__ p, Pair<float> &q) {
-  q.v = *reinterpret_cast<const float2 *>(p);
+  q.v = stream_load2<CCMPC_NT_PAIR != 0>(p);
 }
 
 template <typename P, int W>
