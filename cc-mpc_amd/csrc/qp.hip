@@ -35,6 +35,12 @@ constexpr int kQpWaves = kQpThreads / 64;
 constexpr int kQpMaxT = 40;
 constexpr size_t kQpLdsBytes = 160 * 1024;
 constexpr int kQpRowDoubles = 10;  // doubles per constraint row in the row store (Rows)
+// the IPM tries its one early polish once mu <= kEarlyPolish * max(mu0, 1) (the regular stop is
+// at mu <= 1e-3 tol, ~1e-12)
+#ifndef CCMPC_QP_EARLY_POLISH
+#define CCMPC_QP_EARLY_POLISH 1e-5
+#endif
+constexpr double kEarlyPolish = CCMPC_QP_EARLY_POLISH;
 
 // ---- the LTV model ---------------------------------------------------------------------------
 // About u = 0 the bicycle model's nominal trajectory is straight at constant speed
@@ -794,6 +800,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   int status = 0, it = 0;
   double mu = 0.0, mu0 = 0.0;
   bool infeasible = false;
+  bool polished = false, early_tried = false;
 #ifdef CCMPC_QP_TRACE
   uint64_t tmark[8] = {};
   uint64_t pmark[8] = {};  // polish: first pass through each point
@@ -801,6 +808,367 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #endif
   constexpr int NR = NM > 0 ? NM : 1;
   double La[NR], Ldl = 0.0;  // wave 0: L of the current M (register path, NM > 0)
+  // ---- polish: the equality-constrained QP on the IPM's active set ---------------------------
+  // (as OSQP polishes an ADMM iterate).  Rows with s < lambda are taken as active; the KKT
+  // system of  min 1/2 z^T H z + f^T z  s.t.  G_A z = h_A  is solved through H = L L^T and
+  // S = W^T W, W = L^{-1} G_A^T:  lambda = S^{-1}(W^T y0 - h_A), y0 = -L^{-1} f,
+  // z = L^{-T}(y0 - W lambda).  H carries no barrier weights, so this is as accurate as the
+  // problem itself.  The result is kept only if it is a verified KKT point: every row within
+  // tol_p and lambda >= -tol_d (stationarity holds by construction), which also makes a
+  // stalled IPM's answer exact and leaves infeasible problems reported as such.  It depends on
+  // the iterate only through the active set, and touches none of the state the next IPM
+  // iteration reads (z only on success), so the IPM can try it early: once mu is small the
+  // active set is usually settled, and a verified answer ends the solve several iterations
+  // before the interior point would.  Returns true on a verified answer (z, status = 0).
+  auto polish = [&]() -> bool {
+    bool ok = false;
+    double *Wm = lds + lay.pw, *Sm = lds + lay.ps, *act = lds + lay.pact,
+           *sdinv = lds + lay.pdinv;
+    double *fu = lds + lay.f, *y0 = rh, *rs = e2, *lam = q, *zp = dz, *yp = yd;
+    PQ_MARK(0);
+    // H (no barrier terms) into M; f in control space (fu) is the setup's
+    if constexpr (NW == 1) {  // as the IPM's M: lane column jm, rows (lane >> 4) + 4 m
+      const int jm = lane & 15, jc = jm < n ? jm : 0;
+      double hx[8], hy[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int tt = t < T ? t : 0;
+        const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+        hx[t] = t < T ? wp * Gs[(3 * tt) * n + jc] : 0.0;
+        hy[t] = t < T ? wp * Gs[(3 * tt + 1) * n + jc] : 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int im = (lane >> 4) + 4 * m;
+        const bool on = im < n && jm <= im;
+        const int ic = on ? im : 0;
+        double v = Hc[ic * n + jc];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int tt = t < T ? t : 0;
+          v = fma(Gs[(3 * tt) * n + ic], hx[t], fma(Gs[(3 * tt + 1) * n + ic], hy[t], v));
+        }
+        if (on) M[im * ldm + jm] = v;
+      }
+    } else {
+      for (int e = tid; e < n * n; e += NTH) {
+        const int i = e / n, j = e % n;
+        if (j > i) continue;
+        double v = hctrl(i, j, T, order, p);
+        for (int t = 0; t < T; ++t) {
+          const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+          v += wp * (Gs[(3 * t) * n + i] * Gs[(3 * t) * n + j] +
+                     Gs[(3 * t + 1) * n + i] * Gs[(3 * t + 1) * n + j]);
+        }
+        M[i * ldm + j] = v;
+      }
+    }
+    PQ_MARK(1);
+    // active rows, compacted in row order (ballot + prefix: deterministic)
+    int na = 0;
+    for (int64_t base = 0; base < mrows; base += NTH) {
+      const int64_t r = base + tid;
+      const bool on = r < mrows && rw.s[r] < rw.l[r];
+      const uint64_t mask = __ballot(on);
+      if (lane == 0) red[w] = static_cast<double>(__popcll(mask));
+      qp_sync<NW>();
+      int off = na;
+      for (int k = 0; k < w; ++k) off += static_cast<int>(red[k]);
+      int tot = na;
+      for (int k = 0; k < NW; ++k) tot += static_cast<int>(red[k]);
+      const int pos = off + __popcll(mask & ((uint64_t(1) << lane) - 1));
+      if (on && pos < n) act[pos] = static_cast<double>(r);
+      na = tot;
+      qp_sync<NW>();
+    }
+    if constexpr (NM > 0 && NW == 1) {
+      PQ_MARK(2);
+      // One wave, n <= 16: the same polish with every factor in registers (identity-padded
+      // to 16 x 16, straight-line; reg_cholesky without the pivot skip), the L^T columns read
+      // ahead of each backward chain, the vectors moved between lanes by readlane.
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const double v = M[(lane < n ? lane : 0) * ldm + (k < n ? k : 0)];
+        La[k] = (lane < n && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
+      }
+      const bool hfail = reg_cholesky<NR, false>(La, Ldl);
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+        if (k < n && lane < n && k <= lane) M[lane * ldm + k] = La[k];
+      wave_sync();
+      double ltH[NR];
+      reg_load_lt(M, ldm, n, ltH);
+      const double y0r = reg_forward(La, Ldl, lane < n ? -fu[lane] : 0.0);  // y0 = -L^{-1} f
+      if (lane < n) y0[lane] = y0r;
+      if (hfail) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
+      for (int round = 0; !hfail && round < 4 && na <= n; ++round) {
+        PQ_MARK(3);
+        // W rows w_a = L^{-1} g_a, rs_a = w_a . y0 - h_a: one active row per lane (na <= n),
+        // each lane's own forward substitution (L's entries are the same address on every
+        // lane: broadcast LDS reads), so all rows advance together instead of one triangular
+        // solve per row.  The row's gradient from its one-form (c0, c1, i0, i1): d v[i] / d z_j
+        // is Gs[i][j] for an output row i < T3, else [i - T3 == j].
+        {
+          const int a = lane < na ? lane : 0;
+          const int64_t r = static_cast<int64_t>(act[a]);
+          const int2 ix = reinterpret_cast<const int2 *>(rw.ix)[r];
+          const double c0 = rw.c0[r], c1 = rw.c1[r];
+          const int x0c = ix.x < T3 ? ix.x : 0, x1c = ix.y < T3 ? ix.y : 0;
+          double wv[NR];
+          double d = 0.0;
+#pragma unroll
+          for (int j = 0; j < NR; ++j) {
+            const int jc = j < n ? j : 0;
+            const double ga = Gs[x0c * n + jc], gb = Gs[x1c * n + jc];
+            const double g0 = ix.x < T3 ? ga : (ix.x - T3 == j ? 1.0 : 0.0);
+            const double g1 = ix.y < T3 ? gb : (ix.y - T3 == j ? 1.0 : 0.0);
+            double v = c0 * g0 + c1 * g1;
+#pragma unroll
+            for (int k = 0; k < j; ++k) v = fma(-M[jc * ldm + k], wv[k], v);
+            wv[j] = j < n ? v * lane_bcast(Ldl, j) : 0.0;
+            d = fma(wv[j], lane_bcast(y0r, j), d);
+          }
+          if (lane < na) {
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+              if (j < n) Wm[lane * n + j] = wv[j];
+            rs[lane] = d + row_const(r);
+          }
+        }
+        wave_sync();
+        PQ_MARK(4);
+        // S = W W^T: lane (i, kq) = (lane & 15, lane >> 4) forms S[i][kq + 4 m]
+        {
+          const int i = lane & 15, kq = lane >> 4, ic = i < na ? i : 0;
+          double wi[NR];
+#pragma unroll
+          for (int k = 0; k < NR; ++k) wi[k] = Wm[ic * n + (k < n ? k : 0)];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int jr = kq + 4 * m, jc = jr < na ? jr : 0;
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < NR; ++k)
+              v = k < n ? fma(wi[k], Wm[jc * n + (k < n ? k : 0)], v) : v;
+            if (i < na && jr <= i) Sm[i * ldm + jr] = v;
+          }
+        }
+        wave_sync();
+        double Ls[NR], Sdl = 0.0;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          const double v = Sm[(lane < na ? lane : 0) * ldm + (k < na ? k : 0)];
+          Ls[k] = (lane < na && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
+        }
+        const bool sfail = reg_cholesky<NR, false>(Ls, Sdl);
+        if (sfail) break;  // dependent active rows
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+          if (k < na && lane < na && k <= lane) Sm[lane * ldm + k] = Ls[k];
+        wave_sync();
+        const double lamr = reg_solve(Ls, Sm, ldm, Sdl, na, lane < na ? rs[lane] : 0.0);
+        if (lane < na) lam[lane] = lamr;
+        PQ_MARK(5);
+        // z = L^{-T}(y0 - W^T lambda)
+        double v = y0r;
+        {
+          const int j = lane < n ? lane : 0;
+#pragma unroll
+          for (int a = 0; a < NR; ++a) {  // rows past na are never written (with na = 0 not
+            // even row 0): select, never multiply, what may be stale LDS
+            const double wa = Wm[(a < na ? a : 0) * n + j];
+            v = a < na ? fma(-wa, lane_bcast(lamr, a), v) : v;
+          }
+        }
+        const double zpr = reg_backward(ltH, Ldl, lane < n ? v : 0.0);
+        if (lane < n) zp[lane] = zpr;
+        {
+          const int kk = lane < T3 ? lane : 0;
+          double yv = 0.0;
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            yv = fma(Gs[kk * n + (j < n ? j : 0)], lane_bcast(zpr, j), yv);
+          if (lane < T3) yp[lane] = yv;
+        }
+        wave_sync();
+        PQ_MARK(6);
+        double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
+        for (int64_t r = tid; r < mrows; r += NTH) {
+          const double g = row_g(r, yp, zp);
+          if (!isfinite(g)) bad = 1.0;
+          if (g > viol) {
+            viol = g;
+            vrow = static_cast<double>(r);
+          }
+        }
+        if (lane < na) {
+          if (!isfinite(lamr)) bad = 1.0;
+          lneg = -lamr;
+        }
+        block_argmax<NW>(viol, vrow, red);
+        block_max2<NW>(lneg, bad, red);
+        if (bad != 0.0) break;
+        if (viol <= tol_p && lneg <= tol_d) {
+          if (lane < n) z[lane] = zpr;
+          status = 0;
+          ok = true;
+          wave_sync();
+          break;
+        }
+        // next active set (lane 0; na <= n entries)
+        if (lane == 0) {
+          int m2 = 0;
+          if (lneg > tol_d) {
+            for (int a = 0; a < na; ++a)
+              if (lam[a] >= -tol_d) act[m2++] = act[a];
+          } else {
+            m2 = na;
+            if (na < n) act[m2++] = vrow;
+            else m2 = n + 1;  // nowhere to add: give up
+          }
+          red[8 * kQpWaves - 2] = static_cast<double>(m2);
+        }
+        wave_sync();
+        na = static_cast<int>(red[8 * kQpWaves - 2]);
+        wave_sync();
+      }
+    } else {
+      // factor H once; y0 = -L^{-1} f
+      if (w == 0) {
+        const bool fail = wave_cholesky(M, n, ldm, dinv, false);
+        double b[2];
+        wave_load2(fu, n, b);
+        b[0] = -b[0];
+        b[1] = -b[1];
+        wave_forward(M, n, ldm, dinv, b);
+        wave_store2(y0, n, b);
+        if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+      }
+      qp_sync<NW>();
+      const bool h_ok = red[8 * kQpWaves - 1] == 0.0;
+      if (!h_ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
+      // up to 4 rounds of active-set correction, as the oracle's polish does: drop rows whose
+      // multiplier comes out negative, else add the most violated row
+      for (int round = 0; h_ok && round < 4 && na <= n; ++round) {
+        // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
+        for (int a = w; a < na; a += NW) {
+          const int64_t r = static_cast<int64_t>(act[a]);
+          double b[2];
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = lane + 64 * h;
+            double g = 0.0;
+            if (j < n) {
+              if (r < nbox) {
+                g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
+              } else if (r < nbox + nv) {
+                const int t = static_cast<int>((r - nbox) >> 1);
+                g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
+              } else {
+                // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
+                const int64_t o = r - nbox - nv;
+                const int t = rw.ix[2 * (nbox + nv + o)] / 3;
+                g = oa0[o] * Gs[(3 * t) * n + j] + oa1[o] * Gs[(3 * t + 1) * n + j];
+              }
+            }
+            b[h] = g;
+          }
+          wave_forward(M, n, ldm, dinv, b);
+          wave_store2(Wm + a * n, n, b);
+          double d = 0.0;
+  #pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (lane + 64 * h < n) d += b[h] * y0[lane + 64 * h];
+          d = wave_sum(d);
+          if (lane == 0) rs[a] = d + row_const(r);
+        }
+        qp_sync<NW>();
+        for (int e = tid; e < na * na; e += NTH) {
+          const int i = e / na, j = e % na;
+          if (j > i) continue;
+          double v = 0.0;
+          for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
+          Sm[i * ldm + j] = v;
+        }
+        qp_sync<NW>();
+        if (w == 0) {
+          const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
+          double b[2];
+          if (!fail) {
+            wave_load2(rs, na, b);
+            wave_forward(Sm, na, ldm, sdinv, b);
+            wave_backward(Sm, na, ldm, sdinv, b);
+            wave_store2(lam, na, b);
+          }
+          if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
+        }
+        qp_sync<NW>();
+        if (red[8 * kQpWaves - 1] != 0.0) break;  // dependent active rows
+        // z = L^{-T}(y0 - W^T lambda)
+        for (int j = tid; j < n; j += NTH) {
+          double v = y0[j];
+          for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
+          zp[j] = v;
+        }
+        qp_sync<NW>();
+        if (w == 0) {
+          double b[2];
+          wave_load2(zp, n, b);
+          wave_backward(M, n, ldm, dinv, b);
+          wave_store2(zp, n, b);
+        }
+        qp_sync<NW>();
+        for (int k = tid; k < T3; k += NTH) {
+          double v = 0.0;
+          for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
+          yp[k] = v;
+        }
+        qp_sync<NW>();
+        double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
+        for (int64_t r = tid; r < mrows; r += NTH) {
+          const double g = row_g(r, yp, zp);
+          if (!isfinite(g)) bad = 1.0;
+          if (g > viol) {
+            viol = g;
+            vrow = static_cast<double>(r);
+          }
+        }
+        for (int a = tid; a < na; a += NTH) {
+          if (!isfinite(lam[a])) bad = 1.0;
+          lneg = fmax(lneg, -lam[a]);
+        }
+        block_argmax<NW>(viol, vrow, red);
+        block_max2<NW>(lneg, bad, red);
+        if (bad != 0.0) break;
+        if (viol <= tol_p && lneg <= tol_d) {
+          for (int j = tid; j < n; j += NTH) z[j] = zp[j];
+          status = 0;
+          ok = true;
+          qp_sync<NW>();
+          break;
+        }
+        // next active set (thread 0; na <= n entries)
+        if (tid == 0) {
+          int m2 = 0;
+          if (lneg > tol_d) {
+            for (int a = 0; a < na; ++a)
+              if (lam[a] >= -tol_d) act[m2++] = act[a];
+          } else {
+            m2 = na;
+            if (na < n) act[m2++] = vrow;
+            else m2 = n + 1;  // nowhere to add: give up
+          }
+          red[8 * kQpWaves - 2] = static_cast<double>(m2);
+        }
+        qp_sync<NW>();
+        na = static_cast<int>(red[8 * kQpWaves - 2]);
+        qp_sync<NW>();
+      }
+    }
+    return ok;
+  };
+
   for (; it <= A.max_iter; ++it) {
     QP_MARK(0);
     // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
@@ -972,6 +1340,14 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     if (it == A.max_iter || !isfinite(mu) || !isfinite(rpmax) || !isfinite(rdmax)) {
       status = CCMPC_QP_MAXITER;
       break;
+    }
+    // one early polish attempt once mu has fallen by kEarlyPolish (below)
+    if (A.polish && !early_tried && it >= 2 && mu <= kEarlyPolish * fmax(mu0, 1.0)) {
+      early_tried = true;
+      if (polish()) {
+        polished = true;
+        break;
+      }
     }
     QP_MARK(2);
     // ---- I3: Cholesky on wave 0 (left-looking, lane = row) ---------------------------------
@@ -1171,362 +1547,10 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #endif
   }
 
-  // ---- polish: the equality-constrained QP on the IPM's active set ---------------------------
-  // (as OSQP polishes an ADMM iterate).  Rows with s < lambda are taken as active; the KKT
-  // system of  min 1/2 z^T H z + f^T z  s.t.  G_A z = h_A  is solved through H = L L^T and
-  // S = W^T W, W = L^{-1} G_A^T:  lambda = S^{-1}(W^T y0 - h_A), y0 = -L^{-1} f,
-  // z = L^{-T}(y0 - W lambda).  H carries no barrier weights, so this is as accurate as the
-  // problem itself.  The result is kept only if it is a verified KKT point: every row within
-  // tol_p and lambda >= -tol_d (stationarity holds by construction), which also makes a
-  // stalled IPM's answer exact and leaves infeasible problems reported as such.
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk2 = wall_clock64();
 #endif
-  if (A.polish && !infeasible) {
-    double *Wm = lds + lay.pw, *Sm = lds + lay.ps, *act = lds + lay.pact,
-           *sdinv = lds + lay.pdinv;
-    double *fu = lds + lay.f, *y0 = rh, *rs = e2, *lam = q, *zp = dz, *yp = yd;
-    PQ_MARK(0);
-    // H (no barrier terms) into M; f in control space (fu) is the setup's
-    if constexpr (NW == 1) {  // as the IPM's M: lane column jm, rows (lane >> 4) + 4 m
-      const int jm = lane & 15, jc = jm < n ? jm : 0;
-      double hx[8], hy[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int tt = t < T ? t : 0;
-        const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
-        hx[t] = t < T ? wp * Gs[(3 * tt) * n + jc] : 0.0;
-        hy[t] = t < T ? wp * Gs[(3 * tt + 1) * n + jc] : 0.0;
-      }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int im = (lane >> 4) + 4 * m;
-        const bool on = im < n && jm <= im;
-        const int ic = on ? im : 0;
-        double v = Hc[ic * n + jc];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int tt = t < T ? t : 0;
-          v = fma(Gs[(3 * tt) * n + ic], hx[t], fma(Gs[(3 * tt + 1) * n + ic], hy[t], v));
-        }
-        if (on) M[im * ldm + jm] = v;
-      }
-    } else {
-      for (int e = tid; e < n * n; e += NTH) {
-        const int i = e / n, j = e % n;
-        if (j > i) continue;
-        double v = hctrl(i, j, T, order, p);
-        for (int t = 0; t < T; ++t) {
-          const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
-          v += wp * (Gs[(3 * t) * n + i] * Gs[(3 * t) * n + j] +
-                     Gs[(3 * t + 1) * n + i] * Gs[(3 * t + 1) * n + j]);
-        }
-        M[i * ldm + j] = v;
-      }
-    }
-    PQ_MARK(1);
-    // active rows, compacted in row order (ballot + prefix: deterministic)
-    int na = 0;
-    for (int64_t base = 0; base < mrows; base += NTH) {
-      const int64_t r = base + tid;
-      const bool on = r < mrows && rw.s[r] < rw.l[r];
-      const uint64_t mask = __ballot(on);
-      if (lane == 0) red[w] = static_cast<double>(__popcll(mask));
-      qp_sync<NW>();
-      int off = na;
-      for (int k = 0; k < w; ++k) off += static_cast<int>(red[k]);
-      int tot = na;
-      for (int k = 0; k < NW; ++k) tot += static_cast<int>(red[k]);
-      const int pos = off + __popcll(mask & ((uint64_t(1) << lane) - 1));
-      if (on && pos < n) act[pos] = static_cast<double>(r);
-      na = tot;
-      qp_sync<NW>();
-    }
-    if constexpr (NM > 0 && NW == 1) {
-      PQ_MARK(2);
-      // One wave, n <= 16: the same polish with every factor in registers (identity-padded
-      // to 16 x 16, straight-line; reg_cholesky without the pivot skip), the L^T columns read
-      // ahead of each backward chain, the vectors moved between lanes by readlane.
-      wave_sync();
-#pragma unroll
-      for (int k = 0; k < NR; ++k) {
-        const double v = M[(lane < n ? lane : 0) * ldm + (k < n ? k : 0)];
-        La[k] = (lane < n && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
-      }
-      const bool hfail = reg_cholesky<NR, false>(La, Ldl);
-#pragma unroll
-      for (int k = 0; k < NR; ++k)
-        if (k < n && lane < n && k <= lane) M[lane * ldm + k] = La[k];
-      wave_sync();
-      double ltH[NR];
-      reg_load_lt(M, ldm, n, ltH);
-      const double y0r = reg_forward(La, Ldl, lane < n ? -fu[lane] : 0.0);  // y0 = -L^{-1} f
-      if (lane < n) y0[lane] = y0r;
-      if (hfail) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
-      for (int round = 0; !hfail && round < 4 && na <= n; ++round) {
-        PQ_MARK(3);
-        // W rows w_a = L^{-1} g_a, rs_a = w_a . y0 - h_a: one active row per lane (na <= n),
-        // each lane's own forward substitution (L's entries are the same address on every
-        // lane: broadcast LDS reads), so all rows advance together instead of one triangular
-        // solve per row.  The row's gradient from its one-form (c0, c1, i0, i1): d v[i] / d z_j
-        // is Gs[i][j] for an output row i < T3, else [i - T3 == j].
-        {
-          const int a = lane < na ? lane : 0;
-          const int64_t r = static_cast<int64_t>(act[a]);
-          const int2 ix = reinterpret_cast<const int2 *>(rw.ix)[r];
-          const double c0 = rw.c0[r], c1 = rw.c1[r];
-          const int x0c = ix.x < T3 ? ix.x : 0, x1c = ix.y < T3 ? ix.y : 0;
-          double wv[NR];
-          double d = 0.0;
-#pragma unroll
-          for (int j = 0; j < NR; ++j) {
-            const int jc = j < n ? j : 0;
-            const double ga = Gs[x0c * n + jc], gb = Gs[x1c * n + jc];
-            const double g0 = ix.x < T3 ? ga : (ix.x - T3 == j ? 1.0 : 0.0);
-            const double g1 = ix.y < T3 ? gb : (ix.y - T3 == j ? 1.0 : 0.0);
-            double v = c0 * g0 + c1 * g1;
-#pragma unroll
-            for (int k = 0; k < j; ++k) v = fma(-M[jc * ldm + k], wv[k], v);
-            wv[j] = j < n ? v * lane_bcast(Ldl, j) : 0.0;
-            d = fma(wv[j], lane_bcast(y0r, j), d);
-          }
-          if (lane < na) {
-#pragma unroll
-            for (int j = 0; j < NR; ++j)
-              if (j < n) Wm[lane * n + j] = wv[j];
-            rs[lane] = d + row_const(r);
-          }
-        }
-        wave_sync();
-        PQ_MARK(4);
-        // S = W W^T: lane (i, kq) = (lane & 15, lane >> 4) forms S[i][kq + 4 m]
-        {
-          const int i = lane & 15, kq = lane >> 4, ic = i < na ? i : 0;
-          double wi[NR];
-#pragma unroll
-          for (int k = 0; k < NR; ++k) wi[k] = Wm[ic * n + (k < n ? k : 0)];
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const int jr = kq + 4 * m, jc = jr < na ? jr : 0;
-            double v = 0.0;
-#pragma unroll
-            for (int k = 0; k < NR; ++k)
-              v = k < n ? fma(wi[k], Wm[jc * n + (k < n ? k : 0)], v) : v;
-            if (i < na && jr <= i) Sm[i * ldm + jr] = v;
-          }
-        }
-        wave_sync();
-        double Ls[NR], Sdl = 0.0;
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-          const double v = Sm[(lane < na ? lane : 0) * ldm + (k < na ? k : 0)];
-          Ls[k] = (lane < na && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
-        }
-        const bool sfail = reg_cholesky<NR, false>(Ls, Sdl);
-        if (sfail) break;  // dependent active rows
-#pragma unroll
-        for (int k = 0; k < NR; ++k)
-          if (k < na && lane < na && k <= lane) Sm[lane * ldm + k] = Ls[k];
-        wave_sync();
-        const double lamr = reg_solve(Ls, Sm, ldm, Sdl, na, lane < na ? rs[lane] : 0.0);
-        if (lane < na) lam[lane] = lamr;
-        PQ_MARK(5);
-        // z = L^{-T}(y0 - W^T lambda)
-        double v = y0r;
-        {
-          const int j = lane < n ? lane : 0;
-#pragma unroll
-          for (int a = 0; a < NR; ++a) {  // rows past na are never written (with na = 0 not
-            // even row 0): select, never multiply, what may be stale LDS
-            const double wa = Wm[(a < na ? a : 0) * n + j];
-            v = a < na ? fma(-wa, lane_bcast(lamr, a), v) : v;
-          }
-        }
-        const double zpr = reg_backward(ltH, Ldl, lane < n ? v : 0.0);
-        if (lane < n) zp[lane] = zpr;
-        {
-          const int kk = lane < T3 ? lane : 0;
-          double yv = 0.0;
-#pragma unroll
-          for (int j = 0; j < NR; ++j)
-            yv = fma(Gs[kk * n + (j < n ? j : 0)], lane_bcast(zpr, j), yv);
-          if (lane < T3) yp[lane] = yv;
-        }
-        wave_sync();
-        PQ_MARK(6);
-        double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
-        for (int64_t r = tid; r < mrows; r += NTH) {
-          const double g = row_g(r, yp, zp);
-          if (!isfinite(g)) bad = 1.0;
-          if (g > viol) {
-            viol = g;
-            vrow = static_cast<double>(r);
-          }
-        }
-        if (lane < na) {
-          if (!isfinite(lamr)) bad = 1.0;
-          lneg = -lamr;
-        }
-        block_argmax<NW>(viol, vrow, red);
-        block_max2<NW>(lneg, bad, red);
-        if (bad != 0.0) break;
-        if (viol <= tol_p && lneg <= tol_d) {
-          if (lane < n) z[lane] = zpr;
-          status = 0;
-          wave_sync();
-          break;
-        }
-        // next active set (lane 0; na <= n entries)
-        if (lane == 0) {
-          int m2 = 0;
-          if (lneg > tol_d) {
-            for (int a = 0; a < na; ++a)
-              if (lam[a] >= -tol_d) act[m2++] = act[a];
-          } else {
-            m2 = na;
-            if (na < n) act[m2++] = vrow;
-            else m2 = n + 1;  // nowhere to add: give up
-          }
-          red[8 * kQpWaves - 2] = static_cast<double>(m2);
-        }
-        wave_sync();
-        na = static_cast<int>(red[8 * kQpWaves - 2]);
-        wave_sync();
-      }
-    } else {
-      // factor H once; y0 = -L^{-1} f
-      if (w == 0) {
-        const bool fail = wave_cholesky(M, n, ldm, dinv, false);
-        double b[2];
-        wave_load2(fu, n, b);
-        b[0] = -b[0];
-        b[1] = -b[1];
-        wave_forward(M, n, ldm, dinv, b);
-        wave_store2(y0, n, b);
-        if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
-      }
-      qp_sync<NW>();
-      const bool h_ok = red[8 * kQpWaves - 1] == 0.0;
-      if (!h_ok) status = CCMPC_QP_NUMERIC;  // H itself is not positive definite (bad weights)
-      // up to 4 rounds of active-set correction, as the oracle's polish does: drop rows whose
-      // multiplier comes out negative, else add the most violated row
-      for (int round = 0; h_ok && round < 4 && na <= n; ++round) {
-        // W rows (one per active row a, wave per row): w_a = L^{-1} g_a;  rs_a = w_a . y0 - h_a
-        for (int a = w; a < na; a += NW) {
-          const int64_t r = static_cast<int64_t>(act[a]);
-          double b[2];
-  #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int j = lane + 64 * h;
-            double g = 0.0;
-            if (j < n) {
-              if (r < nbox) {
-                g = (j == static_cast<int>(r >> 1)) ? ((r & 1) ? -1.0 : 1.0) : 0.0;
-              } else if (r < nbox + nv) {
-                const int t = static_cast<int>((r - nbox) >> 1);
-                g = ((r - nbox) & 1) ? -Gs[(3 * t + 2) * n + j] : Gs[(3 * t + 2) * n + j];
-              } else {
-                // the row's gradient in control space: a . (Gs_x, Gs_y) of its step
-                const int64_t o = r - nbox - nv;
-                const int t = rw.ix[2 * (nbox + nv + o)] / 3;
-                g = oa0[o] * Gs[(3 * t) * n + j] + oa1[o] * Gs[(3 * t + 1) * n + j];
-              }
-            }
-            b[h] = g;
-          }
-          wave_forward(M, n, ldm, dinv, b);
-          wave_store2(Wm + a * n, n, b);
-          double d = 0.0;
-  #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            if (lane + 64 * h < n) d += b[h] * y0[lane + 64 * h];
-          d = wave_sum(d);
-          if (lane == 0) rs[a] = d + row_const(r);
-        }
-        qp_sync<NW>();
-        for (int e = tid; e < na * na; e += NTH) {
-          const int i = e / na, j = e % na;
-          if (j > i) continue;
-          double v = 0.0;
-          for (int k = 0; k < n; ++k) v += Wm[i * n + k] * Wm[j * n + k];
-          Sm[i * ldm + j] = v;
-        }
-        qp_sync<NW>();
-        if (w == 0) {
-          const bool fail = na > 0 && wave_cholesky(Sm, na, ldm, sdinv, false);
-          double b[2];
-          if (!fail) {
-            wave_load2(rs, na, b);
-            wave_forward(Sm, na, ldm, sdinv, b);
-            wave_backward(Sm, na, ldm, sdinv, b);
-            wave_store2(lam, na, b);
-          }
-          if (lane == 0) red[8 * kQpWaves - 1] = fail ? 1.0 : 0.0;
-        }
-        qp_sync<NW>();
-        if (red[8 * kQpWaves - 1] != 0.0) break;  // dependent active rows
-        // z = L^{-T}(y0 - W^T lambda)
-        for (int j = tid; j < n; j += NTH) {
-          double v = y0[j];
-          for (int a = 0; a < na; ++a) v -= Wm[a * n + j] * lam[a];
-          zp[j] = v;
-        }
-        qp_sync<NW>();
-        if (w == 0) {
-          double b[2];
-          wave_load2(zp, n, b);
-          wave_backward(M, n, ldm, dinv, b);
-          wave_store2(zp, n, b);
-        }
-        qp_sync<NW>();
-        for (int k = tid; k < T3; k += NTH) {
-          double v = 0.0;
-          for (int j = 0; j < n; ++j) v += Gs[k * n + j] * zp[j];
-          yp[k] = v;
-        }
-        qp_sync<NW>();
-        double viol = -1e300, vrow = 0.0, lneg = 0.0, bad = 0.0;
-        for (int64_t r = tid; r < mrows; r += NTH) {
-          const double g = row_g(r, yp, zp);
-          if (!isfinite(g)) bad = 1.0;
-          if (g > viol) {
-            viol = g;
-            vrow = static_cast<double>(r);
-          }
-        }
-        for (int a = tid; a < na; a += NTH) {
-          if (!isfinite(lam[a])) bad = 1.0;
-          lneg = fmax(lneg, -lam[a]);
-        }
-        block_argmax<NW>(viol, vrow, red);
-        block_max2<NW>(lneg, bad, red);
-        if (bad != 0.0) break;
-        if (viol <= tol_p && lneg <= tol_d) {
-          for (int j = tid; j < n; j += NTH) z[j] = zp[j];
-          status = 0;
-          qp_sync<NW>();
-          break;
-        }
-        // next active set (thread 0; na <= n entries)
-        if (tid == 0) {
-          int m2 = 0;
-          if (lneg > tol_d) {
-            for (int a = 0; a < na; ++a)
-              if (lam[a] >= -tol_d) act[m2++] = act[a];
-          } else {
-            m2 = na;
-            if (na < n) act[m2++] = vrow;
-            else m2 = n + 1;  // nowhere to add: give up
-          }
-          red[8 * kQpWaves - 2] = static_cast<double>(m2);
-        }
-        qp_sync<NW>();
-        na = static_cast<int>(red[8 * kQpWaves - 2]);
-        qp_sync<NW>();
-      }
-    }
-  }
-
+  if (A.polish && !infeasible && !polished) polished = polish();
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk3 = wall_clock64();
 #endif
