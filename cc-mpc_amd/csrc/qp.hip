@@ -36,9 +36,12 @@ constexpr int kQpMaxT = 40;
 constexpr size_t kQpLdsBytes = 160 * 1024;
 constexpr int kQpRowDoubles = 10;  // doubles per constraint row in the row store (Rows)
 // the IPM tries its one early polish once mu <= kEarlyPolish * max(mu0, 1) (the regular stop is
-// at mu <= 1e-3 tol, ~1e-12)
+// at mu <= 1e-3 tol, ~1e-12).  Measured (profiles/r04/qp_early_polish_ab.log): 1e-3 is too
+// early (the active set not settled: a failed attempt, 11 iterations, 232 us for the single
+// T = 8 solve), 1e-4 133 us (5 iterations), 1e-5 / 1e-6 152 us (7); a C1 episode's 12 QPs
+// 2.10 ms at 1e-4 against 2.21 at 1e-5
 #ifndef CCMPC_QP_EARLY_POLISH
-#define CCMPC_QP_EARLY_POLISH 1e-5
+#define CCMPC_QP_EARLY_POLISH 1e-4
 #endif
 constexpr double kEarlyPolish = CCMPC_QP_EARLY_POLISH;
 
@@ -1341,7 +1344,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       status = CCMPC_QP_MAXITER;
       break;
     }
-    // one early polish attempt once mu has fallen by kEarlyPolish (below)
+    // one early polish attempt once mu has fallen by kEarlyPolish
     if (A.polish && !early_tried && it >= 2 && mu <= kEarlyPolish * fmax(mu0, 1.0)) {
       early_tried = true;
       if (polish()) {
