@@ -293,3 +293,37 @@ def test_qp_refuses_malformed_inputs(gpu):
         mpc.PlanningQP(cps, 5, T_full=8).solve(gamma, xbar, g_t, r_t[:, :5], rec)
     qp.solve(gamma, xbar, g_t, r_t, rec)          # the well-formed call still runs
     assert np.all(qp.status.cpu().numpy() >= 0)
+
+
+@pytest.mark.parametrize("T", [8, 5])
+def test_planning_qp_step_equals_the_direct_solve(gpu, T):
+    """mpc.PlanningQPStep (what solve_planning_qp runs: inputs up in one pinned pack, LTV on the
+    device at T == T_full, outputs back in one copy + a polled signal) gives the bytes of the
+    plain PlanningQP.solve on the same inputs, per scene, for the full and a shrinking horizon."""
+    Tf = 8
+    for s in _feasible(2) + _infeasible(1):
+        ovs, cells, K, ref, goal, x0 = crossing_scene(s, T=Tf)
+        cells_t = [c[:, :T] for c in cells]
+        store = engine.ParticleStore.from_cells(cells_t, device=gpu)
+        cyc = cycle.MinkowskiCycle(store, K, ref[:T])
+        cyc.run()
+        u_prev = np.linspace(-0.2, 0.3, 2 * (Tf - T)) if T < Tf else None
+        xbar, gamma = mpc.ltv(x0[None], Tf, lon=LON)
+        qp = mpc.PlanningQP([len(cells)], T, T_full=Tf, device=gpu)
+        u, X, cost, st, it = qp.solve(
+            gamma, xbar, torch.as_tensor(goal[None], device=gpu),
+            torch.as_tensor(ref[None, :T], device=gpu), cyc.rec,
+            u_prev=None if u_prev is None else torch.as_tensor(u_prev[None], device=gpu))
+        run = mpc.PlanningQPStep(len(cells), T, Tf, device=gpu)
+        xb2 = torch.empty_like(xbar)
+        ga2 = torch.empty_like(gamma)
+        if T < Tf:      # the shrinking step reuses the full step's model
+            xb2.copy_(xbar)
+            ga2.copy_(gamma)
+        res = run.solve(x0, goal, ref, cyc.rec, xb2, ga2, u_prev=u_prev, ltv=T == Tf,
+                        lon=LON)
+        assert res["status"] == int(st[0]) and res["iters"] == int(it[0])
+        assert res["u"].tobytes() == u[0].cpu().numpy().tobytes()
+        assert res["X_star"].tobytes() == X[0].cpu().numpy().tobytes()
+        assert res["cost"] == float(cost[0])
+        np.testing.assert_array_equal(res["U_star"], qp.U(u)[0].cpu().numpy())
