@@ -39,6 +39,9 @@ inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_
 constexpr int kWave = 64;  // CDNA wavefront
 
 // ---- Philox4x32-10 (mirrors oracle/philox.py) ----------------------------------------------
+#ifndef CCMPC_PHILOX_MAD
+#define CCMPC_PHILOX_MAD 1
+#endif
 constexpr uint32_t STREAM_IDEAL_Z = 0x1DEA0001u;
 constexpr uint32_t STREAM_IDEAL_X0 = 0x1DEA0002u;
 constexpr uint32_t STREAM_SAMPLER_EPS = 0x5A4D0001u;
@@ -53,6 +56,18 @@ __device__ __forceinline__ u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c
   uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
+#if CCMPC_PHILOX_MAD
+    // one 32x32->64 product per multiplier (v_mad_u64_u32) instead of separate lo / hi
+    // multiplies: both are quarter-rate, so this halves the integer multiply issue
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c0;
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c2;
+    const uint32_t n0 = static_cast<uint32_t>(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = static_cast<uint32_t>(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0;
+    c1 = static_cast<uint32_t>(p1);
+    c2 = n2;
+    c3 = static_cast<uint32_t>(p0);
+#else
     const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
     const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
     const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
@@ -60,6 +75,7 @@ __device__ __forceinline__ u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c
     c1 = lo1;
     c2 = n2;
     c3 = lo0;
+#endif
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }

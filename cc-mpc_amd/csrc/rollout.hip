@@ -17,6 +17,17 @@
 #include "constraints.hpp"
 #include "gram.hpp"
 
+// ideal_gram_kernel's work items per launch (all cells): 512 keeps a 1- or 2-cell launch to one
+// round of workgroups (tools/time_ideal.py: T = 1 41 -> 33 us, T = 4 68 -> 62 us against 1024)
+#ifndef CCMPC_IDEAL_ITEMS
+#define CCMPC_IDEAL_ITEMS 512
+#endif
+// size the plan / lower-bound tables for the instance's horizon (T <= 8 RB) instead of kMaxT:
+// at RB = 1 the kernel's LDS drops from 54 to 47 KB, three workgroups per CU instead of two
+#ifndef CCMPC_IDEAL_LDS_SHRINK
+#define CCMPC_IDEAL_LDS_SHRINK 1
+#endif
+
 namespace ccmpc {
 
 struct StepPlan {
@@ -160,13 +171,21 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
   constexpr int D = 16 * RB;
   constexpr int E = slab_doubles(RB);
   constexpr int NW = ideal_waves(RB);
+#if CCMPC_IDEAL_LDS_SHRINK
+  __shared__ StepPlan plan[8 * RB];
+#else
   __shared__ StepPlan plan[40];
+#endif
   __shared__ double stage_all[NW * D * kStageStride];
   __shared__ double xch[combine_xch_doubles(RB, NW)];
   __shared__ double shift_s[D];
   __shared__ double S_lds[D];
   __shared__ double mean_lds[D];
+#if CCMPC_IDEAL_LDS_SHRINK
+  __shared__ double lb_s[MINK ? (8 * RB) * (8 * RB - 1) / 2 : 1];
+#else
   __shared__ double lb_s[MINK ? 40 * 39 / 2 : 1];
+#endif
   __shared__ int status_s;
   __shared__ int flag;
   const int lane = threadIdx.x & 63;
@@ -224,13 +243,16 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
     const int64_t i = base + lane;
     const bool valid = i < p1;
     double x = x0x, y = x0y;
+    auto put = [&](int t) {
+      stage[(2 * t) * kStageStride + lane] = valid ? x - shift_s[2 * t] : 0.0;
+      stage[(2 * t + 1) * kStageStride + lane] = valid ? y - shift_s[2 * t + 1] : 0.0;
+    };
     for (int t = 0; t < T; ++t) {
       double z0, z1;
       normal_pair(static_cast<uint32_t>(i), static_cast<uint32_t>(t), rng, STREAM_IDEAL_Z, seed, z0,
                   z1);
       advance(plan[t], z0, z1, x, y);
-      stage[(2 * t) * kStageStride + lane] = valid ? x - shift_s[2 * t] : 0.0;
-      stage[(2 * t + 1) * kStageStride + lane] = valid ? y - shift_s[2 * t + 1] : 0.0;
+      put(t);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
@@ -271,9 +293,9 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
   if (MINK) minkowski_cell(cov, mean_lds, T, cell, mp, lb_s, threadIdx.x, blockDim.x);
 }
 
-// samples per work item (multiple of 256 = 4 waves x 64): >= ~1024 items for 1e6-sample cells
+// samples per work item (multiple of 256 = 4 waves x 64): ~CCMPC_IDEAL_ITEMS items per launch
 inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
-  int64_t c = (n_cells * n + 1023) / 1024;
+  int64_t c = (n_cells * n + CCMPC_IDEAL_ITEMS - 1) / CCMPC_IDEAL_ITEMS;
   c = ((c + 255) / 256) * 256;
   if (c < 256) c = 256;
   if (c > 16384) c = 16384;
