@@ -156,10 +156,15 @@ __global__ __launch_bounds__(256) void ideal_rollout_kernel(
 
 constexpr int kStageStride = 66;  // doubles per LDS row: bank-conflict-free both ways
 
-__host__ __device__ constexpr int ideal_waves(int rb) { return rb <= 2 ? 4 : 2; }
+#ifndef CCMPC_IDEAL_WAVES1
+#define CCMPC_IDEAL_WAVES1 4
+#endif
+__host__ __device__ constexpr int ideal_waves(int rb) {
+  return rb == 1 ? CCMPC_IDEAL_WAVES1 : rb <= 2 ? 4 : 2;
+}
 
 template <int RB, bool MINK>
-__global__ __launch_bounds__(256) void ideal_gram_kernel(
+__global__ __launch_bounds__(64 * ideal_waves(RB)) void ideal_gram_kernel(
     const double *__restrict__ prev_mean, const double *__restrict__ prev_cov, int T_src,
     const int32_t *__restrict__ src_cell, int T, int64_t n, int64_t chunk, int64_t items_per_cell,
     const double *__restrict__ x0, uint64_t seed_arg, const uint64_t *__restrict__ seed_dev,
@@ -296,8 +301,9 @@ __global__ __launch_bounds__(256) void ideal_gram_kernel(
 // samples per work item (multiple of 256 = 4 waves x 64): ~CCMPC_IDEAL_ITEMS items per launch
 inline int64_t ideal_chunk(int64_t n_cells, int64_t n) {
   int64_t c = (n_cells * n + CCMPC_IDEAL_ITEMS - 1) / CCMPC_IDEAL_ITEMS;
-  c = ((c + 255) / 256) * 256;
-  if (c < 256) c = 256;
+  constexpr int64_t q = 64 * (CCMPC_IDEAL_WAVES1 > 4 ? CCMPC_IDEAL_WAVES1 : 4);
+  c = ((c + q - 1) / q) * q;
+  if (c < q) c = q;
   if (c > 16384) c = 16384;
   return c;
 }
