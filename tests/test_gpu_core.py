@@ -225,6 +225,23 @@ def test_ideal_moments_fused_equals_materialised(gpu):
         assert fro_rel(c_b.cpu().numpy(), c_a.cpu().numpy()) < 1e-10
 
 
+@pytest.mark.parametrize("T_src", [2, 9, 10, 17, 40])   # T = 1, 8 | 9, 16 | 17, 39
+def test_ideal_moments_fused_equals_materialised_across_row_blocks(gpu, T_src):
+    """Every row-block instance's edges (the fused kernel's plan table holds 8 RB steps), three
+    cells from two sources, sample counts that leave ragged waves and a ragged last item."""
+    eng = ccmpc()
+    _, mean, cov = _source_moments(gpu, T_src=T_src)
+    Tn = T_src - 1
+    src = torch.tensor([1, 0, 1], dtype=torch.int32, device=gpu)
+    for ns in (777, 70_001):
+        store, st = eng.ideal_rollout(mean, cov, src, Tn, ns, seed=31)
+        m_a, c_a = eng.moments(store)
+        m_b, c_b, st_b = eng.ideal_moments(mean, cov, src, Tn, ns, seed=31)
+        assert st.cpu().numpy().tolist() == [0, 0, 0] and st_b.cpu().numpy().tolist() == [0, 0, 0]
+        np.testing.assert_allclose(m_b.cpu().numpy(), m_a.cpu().numpy(), rtol=1e-12)
+        assert fro_rel(c_b.cpu().numpy(), c_a.cpu().numpy()) < 1e-10
+
+
 def test_ideal_moments_full_size_properties(gpu):
     """BASELINE size (1e6 samples per cell): the sample moments of the rollout reproduce the
     conditional-Gaussian model it samples (mean_{t+1} + A (x0-mean_t) ...) to sampling error,

@@ -138,11 +138,14 @@ def test_empty_and_singleton_cells_give_nan_like_numpy(gpu):
     assert torch.isfinite(c[2]).all()
 
 
-def test_ideal_cycle_equals_ideal_moments_plus_minkowski(gpu):
+@pytest.mark.parametrize("T_src", [8, 9, 17, 40])   # T = 7 / 8 | 16 | 39: the row-block edges
+def test_ideal_cycle_equals_ideal_moments_plus_minkowski(gpu, T_src):
+    """The fused cycle's half-space tables are sized per row-block instance (T <= 8 RB,
+    CCMPC_IDEAL_LDS_SHRINK): the cycle equals ideal_moments + minkowski bit for bit at each
+    instance's largest T."""
     from ccmpc import risk
     e = eng()
     rng = np.random.default_rng(4)
-    T_src = 8
     cells = [190 + np.cumsum(rng.normal(0, 0.4, size=(n, T_src, 2)), axis=1) for n in (900, 1500)]
     store = e.ParticleStore.from_cells(cells, device=gpu)
     mean, cov = e.moments(store)
