@@ -127,7 +127,7 @@ def sweep(dev, seed):
     ws = engine.Workspace(dev)
     fn = lambda: engine.ideal_minkowski_cycle(mean, cov, src, 7, 1_000_000, reft, cr, seed=3,
                                               workspace=ws)
-    t = time_kernel_live(fn, dev, per_graph=4, replays=3)
+    t = time_kernel_live(fn, dev, per_graph=4, replays=10)
     rows.append({"config": "ideal rollout 2 cells x 1e6 samples T=7 (fused rollout+moments+"
                            "half-spaces; 0 HBM bytes for trajectories)",
                  "particles": 2_000_000, "T": 7, "kernel_us": round(t * 1e6, 2),
