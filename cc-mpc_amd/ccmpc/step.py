@@ -300,8 +300,6 @@ class StepGraph:
         # and instantiation (two graphs, ~2-3 ms), a shape that recurs is graphed from its
         # second launch on
         self.capture_at = int(os.environ.get("CCMPC_STEP_CAPTURE_AT", "2"))
-        # the library's own capture (HipGraph), or (CCMPC_STEP_TORCH_GRAPH=1) torch.cuda.CUDAGraph
-        self.torch_graph = os.environ.get("CCMPC_STEP_TORCH_GRAPH", "0") == "1"
         self._static_set = False
         self._l4_snap = {}                  # generation -> snapshot of its L4 outputs
 
@@ -406,28 +404,28 @@ class StepGraph:
     def capture(self):
         """Record the two parity graphs (after one eager run that warms every kernel).
 
-        torch hands out streams from a small pool, so this graph's capture / aux / side
-        streams can be another graph's streams, which may still hold that graph's last L4
-        replay: the device is drained first, so no stream joins a capture with work pending
-        (a fork into a stream with pending uncaptured work corrupted the captured graph:
-        segfaults in the first replay once the pool had wrapped)."""
-        torch.cuda.synchronize(self.device)
+        torch hands out streams from a small pool, so this graph's capture / aux streams can be
+        another graph's streams, which may still hold that graph's last L4 replay.  A fork into
+        a stream with pending uncaptured work corrupted the captured graph (segfaults in the
+        first replay once the pool had wrapped), so every stream the capture
+        touches is drained first -- those streams only, not the device: another agent's work on
+        other streams keeps running."""
+        main = torch.cuda.current_stream(self.device)
         s = torch.cuda.Stream(device=self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
+        used = [s, main] + [x for x in (getattr(self, "aux", None),) if x is not None]
+        for x in used:
+            x.synchronize()
+        s.wait_stream(main)
         with torch.cuda.stream(s):
             self._enqueue(0)
-        torch.cuda.synchronize(self.device)
-        graphs = []
-        for par in range(2):
-            if self.torch_graph:    # A/B: torch's graph object around the same capture
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=s):
-                    self._enqueue(par)
-            else:
-                g = HipGraph(self.device, lambda par=par: self._enqueue(par), s)
-            graphs.append(g)
-        self.graphs = graphs
-        torch.cuda.synchronize(self.device)
+        for x in used:
+            x.synchronize()
+        # the warm-up ran the whole step, including the signal of THIS launch's generation:
+        # step the word back, so the poll can only be satisfied by the replay (ADVICE r04: else
+        # wait() returned at once and the host read the output pack while the replay rewrote it)
+        self._flags[0] = self.generation - 1
+        self.graphs = [HipGraph(self.device, lambda par=par: self._enqueue(par), s)
+                       for par in range(2)]
         return self
 
     # ---------------------------------------------------------------------------------------
@@ -548,11 +546,7 @@ class StepGraph:
             return
         if self.graphs is None:
             self.capture()
-        g = self.graphs[gen & 1]
-        if self.torch_graph:
-            g.replay()
-        else:
-            g.replay(torch.cuda.current_stream(self.device).cuda_stream)
+        self.graphs[gen & 1].replay(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _poll(self, slot, gen, what):
         poll_word(self._flags, slot, gen, self.device, f"planning step {gen}: the {what}")

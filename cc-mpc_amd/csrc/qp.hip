@@ -40,10 +40,10 @@ constexpr int kQpRowDoubles = 10;  // doubles per constraint row in the row stor
 // early (the active set not settled: a failed attempt, 11 iterations, 232 us for the single
 // T = 8 solve), 1e-4 133 us (5 iterations), 1e-5 / 1e-6 152 us (7); a C1 episode's 12 QPs
 // 2.10 ms at 1e-4 against 2.21 at 1e-5
-#ifndef CCMPC_QP_EARLY_POLISH
-#define CCMPC_QP_EARLY_POLISH 1e-4
-#endif
-constexpr double kEarlyPolish = CCMPC_QP_EARLY_POLISH;
+// (the env var CCMPC_QP_EARLY_POLISH overrides it per call: 0 = no early attempt; a negative
+// value -x attempts at x but discards even a verified answer, the test hook that checks a failed
+// attempt leaves the IPM bit-identical to a solve without one)
+constexpr double kEarlyPolish = 1e-4;
 
 // ---- the LTV model ---------------------------------------------------------------------------
 // About u = 0 the bicycle model's nominal trajectory is straight at constant speed
@@ -104,8 +104,9 @@ __global__ void mpc_ltv_kernel(const double *__restrict__ x_init, int64_t S, int
 struct QpArgs {
   int64_t S;
   int T, Tf, n_ref, u_order, rec_kind, max_iter, rows_in_lds, polish;
+  int early_discard;  // test hook: attempt the early polish, never keep its answer
   int64_t max_cells;
-  double tol;
+  double tol, early;  // early: the early polish threshold on mu / max(mu0, 1) (0 = none)
   const double *gamma, *xbar, *ubar, *u_prev, *goal, *ref;
   const unsigned char *rec;
   const int64_t *scene_cell;
@@ -128,7 +129,8 @@ struct QpLayout {
     int o = 0;
     gs = o; o += T3 * n;
     m = o; o += n * ldm;
-    hc = o; o += n * n;  // H_ctrl (constant over the iterations)
+    hc = o;  // H_ctrl (constant over the iterations): only the one-wave path (n <= 16)
+    if (n <= 16) o += n * n;  // reads the table; the four-wave paths evaluate hctrl()
     c3 = o; o += T3;
     y = o; o += T3;
     z = o; o += n;   // right behind y: the rows index [y | z] as one vector
@@ -636,7 +638,8 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     lb[j] = c == 0 ? p.min_a : -p.max_delta;
     z[j] = 0.0;
   }
-  for (int e = tid; e < n * n; e += NTH) Hc[e] = hctrl(e / n, e % n, T, order, p);
+  if constexpr (NW == 1)  // launched only for n <= 16, where the layout reserves the table
+    for (int e = tid; e < n * n; e += NTH) Hc[e] = hctrl(e / n, e % n, T, order, p);
   qp_sync<NW>();
   for (int k = tid; k < T3; k += NTH) {
     // objective's linear term in output space: 2 (w_ref (c - ref_t) + [t = T-1] w_final (c - g))
@@ -819,11 +822,11 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // problem itself.  The result is kept only if it is a verified KKT point: every row within
   // tol_p and lambda >= -tol_d (stationarity holds by construction), which also makes a
   // stalled IPM's answer exact and leaves infeasible problems reported as such.  It depends on
-  // the iterate only through the active set, and touches none of the state the next IPM
-  // iteration reads (z only on success), so the IPM can try it early: once mu is small the
-  // active set is usually settled, and a verified answer ends the solve several iterations
-  // before the interior point would.  Returns true on a verified answer (z, status = 0).
-  auto polish = [&]() -> bool {
+  // the iterate only through the active set; it overwrites M (H and its factor), which the
+  // early call site rebuilds on failure, and writes z only on success, so the IPM can try it
+  // early: once mu is small the active set is usually settled, and a verified answer ends the
+  // solve several iterations before the interior point would.  Returns true on a verified answer (z, status = 0).
+  auto polish = [&](bool commit) -> bool {
     bool ok = false;
     double *Wm = lds + lay.pw, *Sm = lds + lay.ps, *act = lds + lay.pact,
            *sdinv = lds + lay.pdinv;
@@ -1013,7 +1016,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         block_max2<NW>(lneg, bad, red);
         if (bad != 0.0) break;
         if (viol <= tol_p && lneg <= tol_d) {
-          if (lane < n) z[lane] = zpr;
+          if (commit && lane < n) z[lane] = zpr;
           status = 0;
           ok = true;
           wave_sync();
@@ -1145,7 +1148,8 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         block_max2<NW>(lneg, bad, red);
         if (bad != 0.0) break;
         if (viol <= tol_p && lneg <= tol_d) {
-          for (int j = tid; j < n; j += NTH) z[j] = zp[j];
+          if (commit)
+            for (int j = tid; j < n; j += NTH) z[j] = zp[j];
           status = 0;
           ok = true;
           qp_sync<NW>();
@@ -1170,6 +1174,60 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       }
     }
     return ok;
+  };
+
+  // M = H_ctrl + D_box + sum_t Gs_t^T B_t Gs_t (the barrier-weighted normal matrix of I2).
+  // A lambda so a failed early polish, which factors H in M's storage, can rebuild it.
+  auto normal_matrix = [&]() {
+    if constexpr (NW == 1) {
+      // lane column jm = lane & 15 (its weighted Gs columns in registers), rows
+      // im = (lane >> 4) + 4 m
+      const int jm = lane & 15, jc = jm < n ? jm : 0;
+      double wx[8], wy[8], wv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int tt = t < T ? t : 0;
+        const double xj = Gs[(3 * tt) * n + jc], yj = Gs[(3 * tt + 1) * n + jc],
+                     vj = Gs[(3 * tt + 2) * n + jc];
+        const double b0 = bw[4 * tt], b1 = bw[4 * tt + 1], b2 = bw[4 * tt + 2],
+                     b3 = bw[4 * tt + 3];
+        wx[t] = t < T ? fma(b0, xj, b1 * yj) : 0.0;
+        wy[t] = t < T ? fma(b1, xj, b2 * yj) : 0.0;
+        wv[t] = t < T ? b3 * vj : 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int im = (lane >> 4) + 4 * m;
+        const bool on = im < n && jm <= im;
+        const int ic = on ? im : 0;
+        double v2 = Hc[ic * n + jc];
+        if (ic == jc) v2 += rw.l[2 * ic] * rw.is[2 * ic] + rw.l[2 * ic + 1] * rw.is[2 * ic + 1];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int tt = t < T ? t : 0;
+          const double xi = Gs[(3 * tt) * n + ic], yi = Gs[(3 * tt + 1) * n + ic],
+                       vi = Gs[(3 * tt + 2) * n + ic];
+          v2 = fma(xi, wx[t], fma(yi, wy[t], fma(vi, wv[t], v2)));
+        }
+        if (on) M[im * ldm + jm] = v2;
+      }
+    } else {
+      for (int e = tid; e < n * n; e += NTH) {
+        const int i = e / n, j = e % n;
+        if (j > i) continue;
+        double v = hctrl(i, j, T, order, p);
+        if (i == j) v += rw.l[2 * i] * rw.is[2 * i] + rw.l[2 * i + 1] * rw.is[2 * i + 1];
+        for (int t = 0; t < T; ++t) {
+          const double xi = Gs[(3 * t) * n + i], yi = Gs[(3 * t + 1) * n + i],
+                       vi = Gs[(3 * t + 2) * n + i];
+          const double xj = Gs[(3 * t) * n + j], yj = Gs[(3 * t + 1) * n + j],
+                       vj = Gs[(3 * t + 2) * n + j];
+          v += xi * (bw[4 * t] * xj + bw[4 * t + 1] * yj) + yi * (bw[4 * t + 1] * xj +
+               bw[4 * t + 2] * yj) + bw[4 * t + 3] * vi * vj;
+        }
+        M[i * ldm + j] = v;
+      }
+    }
   };
 
   for (; it <= A.max_iter; ++it) {
@@ -1263,37 +1321,6 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       v = sum4(v) + (rw.l[2 * jj] - rw.l[2 * jj + 1]);
       if (kq == 0 && j < n) rd[j] = v;
       rdmax = j < n ? fabs(v) : 0.0;
-      // M = H_ctrl + D_box + sum_t Gs_t^T B_t Gs_t: lane column jm = lane & 15 (its weighted
-      // Gs columns in registers), rows im = (lane >> 4) + 4 m
-      const int jm = lane & 15, jc = jm < n ? jm : 0;
-      double wx[8], wy[8], wv[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int tt = t < T ? t : 0;
-        const double xj = Gs[(3 * tt) * n + jc], yj = Gs[(3 * tt + 1) * n + jc],
-                     vj = Gs[(3 * tt + 2) * n + jc];
-        const double b0 = bw[4 * tt], b1 = bw[4 * tt + 1], b2 = bw[4 * tt + 2],
-                     b3 = bw[4 * tt + 3];
-        wx[t] = t < T ? fma(b0, xj, b1 * yj) : 0.0;
-        wy[t] = t < T ? fma(b1, xj, b2 * yj) : 0.0;
-        wv[t] = t < T ? b3 * vj : 0.0;
-      }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int im = (lane >> 4) + 4 * m;
-        const bool on = im < n && jm <= im;
-        const int ic = on ? im : 0;
-        double v2 = Hc[ic * n + jc];
-        if (ic == jc) v2 += rw.l[2 * ic] * rw.is[2 * ic] + rw.l[2 * ic + 1] * rw.is[2 * ic + 1];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int tt = t < T ? t : 0;
-          const double xi = Gs[(3 * tt) * n + ic], yi = Gs[(3 * tt + 1) * n + ic],
-                       vi = Gs[(3 * tt + 2) * n + ic];
-          v2 = fma(xi, wx[t], fma(yi, wy[t], fma(vi, wv[t], v2)));
-        }
-        if (on) M[im * ldm + jm] = v2;
-      }
     } else {
     for (int j = tid; j < n; j += NTH) {
       double v = hctrl_mul(z, j, T, order, p) + rw.l[2 * j] - rw.l[2 * j + 1];
@@ -1301,22 +1328,8 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       rd[j] = v;
       rdmax = fmax(rdmax, fabs(v));
     }
-    for (int e = tid; e < n * n; e += NTH) {
-      const int i = e / n, j = e % n;
-      if (j > i) continue;
-      double v = hctrl(i, j, T, order, p);
-      if (i == j) v += rw.l[2 * i] * rw.is[2 * i] + rw.l[2 * i + 1] * rw.is[2 * i + 1];
-      for (int t = 0; t < T; ++t) {
-        const double xi = Gs[(3 * t) * n + i], yi = Gs[(3 * t + 1) * n + i],
-                     vi = Gs[(3 * t + 2) * n + i];
-        const double xj = Gs[(3 * t) * n + j], yj = Gs[(3 * t + 1) * n + j],
-                     vj = Gs[(3 * t + 2) * n + j];
-        v += xi * (bw[4 * t] * xj + bw[4 * t + 1] * yj) + yi * (bw[4 * t + 1] * xj +
-             bw[4 * t + 2] * yj) + bw[4 * t + 3] * vi * vj;
-      }
-      M[i * ldm + j] = v;
     }
-    }
+    normal_matrix();
     block_max2<NW>(rpmax, rdmax, red);
     mu = block_sum<NW>(sl, red) / static_cast<double>(mrows);
 #ifdef CCMPC_QP_TRACE
@@ -1344,13 +1357,20 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       status = CCMPC_QP_MAXITER;
       break;
     }
-    // one early polish attempt once mu has fallen by kEarlyPolish
-    if (A.polish && !early_tried && it >= 2 && mu <= kEarlyPolish * fmax(mu0, 1.0)) {
+    // one early polish attempt once mu has fallen by A.early (kEarlyPolish)
+    if (A.polish && A.early > 0.0 && !early_tried && it >= 2 && mu <= A.early * fmax(mu0, 1.0)) {
       early_tried = true;
-      if (polish()) {
+      if (polish(!A.early_discard) && !A.early_discard) {
         polished = true;
         break;
       }
+      // the polish factored H in M's storage (and may have set a status): restore the
+      // barrier-weighted normal matrix this iteration's factor needs, so a failed attempt
+      // leaves the IPM exactly where it was
+      status = 0;
+      qp_sync<NW>();
+      normal_matrix();
+      qp_sync<NW>();
     }
     QP_MARK(2);
     // ---- I3: Cholesky on wave 0 (left-looking, lane = row) ---------------------------------
@@ -1553,7 +1573,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk2 = wall_clock64();
 #endif
-  if (A.polish && !infeasible && !polished) polished = polish();
+  if (A.polish && !infeasible && !polished) polished = polish(true);
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk3 = wall_clock64();
 #endif
@@ -1711,6 +1731,12 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   a.max_iter = max_iter;
   a.rows_in_lds = in_lds;
   a.polish = plan.polish;
+  {
+    const char *e = getenv("CCMPC_QP_EARLY_POLISH");  // per call (a test switches it)
+    const double v = e ? atof(e) : kEarlyPolish;
+    a.early = fabs(v);
+    a.early_discard = v < 0.0;
+  }
   a.max_cells = max_cells_per_scene;
   a.tol = tol;
   a.gamma = gamma;

@@ -327,3 +327,69 @@ def test_planning_qp_step_equals_the_direct_solve(gpu, T):
         assert res["X_star"].tobytes() == X[0].cpu().numpy().tobytes()
         assert res["cost"] == float(cost[0])
         np.testing.assert_array_equal(res["U_star"], qp.U(u)[0].cpu().numpy())
+
+
+def _solve_with_env(monkeypatch, value, seeds, T, gpu, rec_in=None):
+    if value is None:
+        monkeypatch.delenv("CCMPC_QP_EARLY_POLISH", raising=False)
+    else:
+        monkeypatch.setenv("CCMPC_QP_EARLY_POLISH", value)
+    rec, cps, o_recs, refs, goals, x0s = rec_in or _scene_inputs(seeds, T, gpu)
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    out = mpc.PlanningQP(cps, T).solve(gamma, xbar, torch.as_tensor(goals, device=gpu),
+                                       torch.as_tensor(refs, device=gpu), rec)
+    return [o.cpu().numpy().copy() for o in out], (rec, cps, o_recs, refs, goals, x0s)
+
+
+@pytest.mark.parametrize("T", [8, 12])
+def test_failed_early_polish_leaves_the_ipm_untouched(gpu, monkeypatch, T):
+    """The early polish factors H in the normal matrix's storage.  A failed attempt must rebuild
+    the barrier-weighted matrix before the IPM's own factor: with the attempt forced
+    to fail (CCMPC_QP_EARLY_POLISH = -x: attempted at x, its answer discarded) every scene's
+    status, iteration count and u are the bytes of a solve with no early attempt (= 0), at an
+    early threshold (1e-1) where the active set is not yet settled and at the default one."""
+    seeds = list(range(100, 124)) if T == 8 else list(range(200, 212))
+    none, inp = _solve_with_env(monkeypatch, "0", seeds, T, gpu)
+    for x in ("-1e-1", "-1e-2", "-1e-4"):
+        forced, _ = _solve_with_env(monkeypatch, x, seeds, T, gpu, inp)
+        for a, b in zip(none, forced):
+            assert a.tobytes() == b.tobytes(), x
+    # a real early attempt at 1e-1 either ends the solve sooner with a verified answer or fails
+    # and leaves the IPM's path unchanged; either way the same minimiser and status
+    early, _ = _solve_with_env(monkeypatch, "1e-1", seeds, T, gpu, inp)
+    dflt, _ = _solve_with_env(monkeypatch, None, seeds, T, gpu, inp)
+    for got in (early, dflt):
+        assert np.array_equal(got[3], none[3])
+        assert np.all(got[4] <= none[4])
+        ok = none[3] == mpc.QP_OK
+        scale = 1.0 + np.abs(none[0][ok]).max(axis=1, keepdims=True)
+        assert np.all(np.abs(got[0][ok] - none[0][ok]) <= 1e-9 * scale)
+    assert np.any(none[3] == mpc.QP_OK) and np.any(none[3] == mpc.QP_MAXITER)
+
+
+def test_qp_at_the_longest_horizon(gpu):
+    """T = 40 (the C5 horizon, the ABI's maximum): the LDS image must fit (the one-wave H_ctrl
+    table is reserved only for n <= 16), and every solved scene is a KKT point of
+    the oracle's own (H, f, G, h)."""
+    T = 40
+    seeds = [300, 301, 302]
+    rec, cps, o_recs, refs, goals, x0s = _scene_inputs(seeds, T, gpu)
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    u, X, cost, status, iters = mpc.PlanningQP(cps, T).solve(
+        gamma, xbar, torch.as_tensor(goals, device=gpu), torch.as_tensor(refs, device=gpu), rec)
+    u, status = u.cpu().numpy(), status.cpu().numpy()
+    prm = _params_dict(mpc.MPCParams.reference_defaults())
+    n_ok = 0
+    for i in range(len(seeds)):
+        Gf, c = mo.state_map(gamma[i].cpu().numpy(), xbar[i].cpu().numpy(), T, T)
+        rows = mo.obstacle_rows(o_recs[i], "halfspace", T)
+        H, f, _, G, h = mo.assemble_qp(Gf, c, T, goals[i], refs[i], rows, prm)
+        feasible = mo.is_feasible(G, h)
+        if not feasible:
+            assert status[i] == mpc.QP_MAXITER, (seeds[i], status[i])
+            continue
+        assert status[i] == mpc.QP_OK, (seeds[i], status[i])
+        prim, stat, comp, _ = mo.kkt_residuals(H, f, G, h, u[i])
+        assert prim <= 1e-8 and stat <= 1e-5 and comp <= 1e-6, (prim, stat, comp)
+        n_ok += 1
+    assert n_ok >= 1

@@ -151,3 +151,30 @@ def test_graph_replay_equals_its_first_eager_launch(gpu):
             np.testing.assert_array_equal(a, b)
     assert len(ag._graphs) == 3
     assert all(g.graphs is not None and g.generation == 2 for g in ag._graphs.values())
+
+
+def test_first_replay_is_not_signalled_by_the_capture_warmup(gpu, monkeypatch):
+    """capture() runs the whole step eagerly once (warm-up), signal included, with the
+    generation of the launch that captures.  The signal word must be stepped back after it, so
+    wait() returns only once the REPLAY has signalled (otherwise the host read the
+    output pack while the replay's copy-out rewrote it).  The replay is held back here: the word
+    must still be one generation behind; replaying then satisfies the poll."""
+    import torch
+    from ccmpc import episode, planner, step
+    init, pmf, gmm, minpos, pasts, K, eps = _inputs()
+    ag = planner.MidlevelAgent(prediction_horizon=PH, device=gpu)
+    params = episode.Params(O, K, 0)
+    sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=5)
+    ag.predict_and_constrain(params, sampler, eps, PH, _ref(0), minpos, pasts)   # eager
+    g = list(ag._graphs.values())[-1]
+    assert g.graphs is None and g.generation == 1
+    held = []
+    monkeypatch.setattr(step.HipGraph, "replay", lambda self, stream=None: held.append(self))
+    g.launch()                                            # generation 2: capture, replay held
+    torch.cuda.synchronize(gpu)
+    assert g.graphs is not None and len(held) == 1
+    assert int(g._flags[0]) == 1, int(g._flags[0])        # the warm-up's signal was taken back
+    monkeypatch.undo()
+    held[0].replay(torch.cuda.current_stream(gpu).cuda_stream)
+    g.wait()
+    assert int(g._flags[0]) == 2
