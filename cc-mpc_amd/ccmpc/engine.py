@@ -298,6 +298,37 @@ def sample_unicycle(init_state, latent_pmf, gmm, N, T, dt=0.5, seed=0, device="c
     return out_z, store
 
 
+def load_predictions(predictions, z, n_latent, rows=None, device="cuda"):
+    """generate_vehicle_latents' predictions (nodes, N, T, 2) float32 scene-relative and z
+    (nodes, N) int64 / int32 (prediction.py:93-105; host arrays or device tensors) -> the
+    sample-order F32 store + int32 z that ccmpc_bucket reads (ccmpc_load_predictions), OV o
+    = node rows[o] (default: every node).  Returns (z [O, N] int32, ParticleStore)."""
+    lib = _lib.load()
+    dev = require_device(device)
+    pred = torch.as_tensor(predictions, device=dev)
+    if pred.dtype != torch.float32 or pred.dim() != 4 or pred.shape[3] != 2:
+        raise ValueError("predictions must be (nodes, N, T, 2) float32")
+    pred = pred.contiguous()
+    zt = torch.as_tensor(z, device=dev).contiguous()
+    if zt.dtype not in (torch.int64, torch.int32) or tuple(zt.shape) != tuple(pred.shape[:2]):
+        raise ValueError("z must be (nodes, N) int64 or int32")
+    n_nodes, N, T = int(pred.shape[0]), int(pred.shape[1]), int(pred.shape[2])
+    rows = list(range(n_nodes)) if rows is None else [int(r) for r in rows]
+    if any(r < 0 or r >= n_nodes for r in rows):
+        raise ValueError(f"rows outside [0, {n_nodes})")
+    O = len(rows)
+    t_rows = torch.as_tensor(np.asarray(rows, np.int32), device=dev)
+    store = ParticleStore(T, [N] * O, dtype=torch.float32, device=dev, origin=np.zeros((O, 2)),
+                          align=4)
+    out_z = torch.empty((O, N), dtype=torch.int32, device=dev)
+    stride = store.offsets[1] if O > 1 else N
+    _lib.check(lib.ccmpc_load_predictions(
+        _p(pred), _p(zt), zt.element_size(), _p(t_rows), O, N, T, int(n_latent), _p(store.pos),
+        store.ld, stride, _p(out_z), _stream()), "ccmpc_load_predictions")
+    store._keepalive = (pred, zt, t_rows)
+    return out_z, store
+
+
 def _sampler_inputs(init_state, latent_pmf, gmm, N, T, dev, z, eps, per_particle):
     """Device copies of a sampler call's inputs (ccmpc_sample_unicycle_ex's layouts)."""
     init_state = np.asarray(init_state, np.float64).reshape(-1, 4)

@@ -496,6 +496,14 @@ class MidlevelAgent:
         self._u_prev = []                  # executed controls of this shrinking episode (:3186)
         self.last_generator_output = None
         self.last_ctrl = None
+        # the reference's prediction functions (prediction.py:19-105 and Trajectron++'s
+        # prediction_output_to_trajectories), injectable; do_prediction calls them when eval_stg
+        # is a Trajectron++ model (it has no sample_boundary)
+        from . import prediction
+        self._generate_vehicle_latents = kwargs.get("generate_vehicle_latents",
+                                                    prediction.generate_vehicle_latents)
+        self._prediction_output_to_trajectories = kwargs.get(
+            "prediction_output_to_trajectories", prediction.prediction_output_to_trajectories)
 
     # ------------------------------------------------------------------------------------
     # The harness-facing surface (tests/Hz20/__init__.py:183-359): construction, sensor and
@@ -595,25 +603,71 @@ class MidlevelAgent:
         return timeout
 
     def do_prediction(self, frame):
-        """:414-467: the frame's scene from the scene builder, then generate_vehicle_latents
-        (prediction.py:19-105).  Trajectron++'s encoder and GRU decoder run in eval_stg; what
-        reaches this path is the sampler tail's input (per-OV latent pmf, initial state, GMM
-        parameters, and for Trajectron++'s own boundary the per-sample parameters, z and noise
-        as device tensors).  The rollout itself (GMM2D.rsample + Unicycle) runs inside the
-        planning step on the GPU, so `boundary` stands where the reference's `predictions` /
-        `z` arrays stand."""
+        """:414-467: the frame's scene from the scene builder, then the predictor.
+
+        A Trajectron++ eval_stg (the reference's): generate_vehicle_latents(eval_stg, scene,
+        timesteps, num_samples, ph, z_mode=False, gmm_mode=False, full_dist=False,
+        all_z_sep=False) (prediction.py:19-105; injectable as the agent keyword
+        generate_vehicle_latents) and prediction_output_to_trajectories, returned as the
+        reference's AttrDict (scene, timestep, nodes, predictions, z, latent_probs, past_dict,
+        ground_truth_dict); make_ovehicles then buckets predictions + z on the GPU.
+
+        An eval_stg with sample_boundary (this library's sampler-tail boundary: per-OV latent
+        pmf, initial state and GMM parameters, or Trajectron++'s per-sample parameters, z and
+        noise as device tensors): the rollout itself (GMM2D.rsample + Unicycle) runs inside the
+        planning step on the GPU, and `boundary` stands where `predictions` / `z` stand."""
+        from .standins import AttrDict
         scene = self._scene_builder.get_scene()
         timestep = int((frame - self._first_frame) / self.record_interval)
-        b = self._eval_stg.sample_boundary(scene, timestep, self.n_predictions,
-                                           self.prediction_horizon)
-        return {"scene": scene, "timestep": timestep, "nodes": list(b["nodes"]),
-                "boundary": b, "latent_probs": np.asarray(b["latent_probs"], np.float64),
-                "past_dict": {timestep: scene.past(timestep, max_h=10)}}
+        ph = self.prediction_horizon
+        if hasattr(self._eval_stg, "sample_boundary"):
+            b = self._eval_stg.sample_boundary(scene, timestep, self.n_predictions, ph)
+            return AttrDict(scene=scene, timestep=timestep, nodes=list(b["nodes"]), boundary=b,
+                            latent_probs=np.asarray(b["latent_probs"], np.float64),
+                            past_dict={timestep: scene.past(timestep, max_h=10)})
+        timesteps = np.array([timestep])
+        with torch.no_grad():
+            z, predictions, nodes, predictions_dict, latent_probs = \
+                self._generate_vehicle_latents(self._eval_stg, scene, timesteps,
+                                               num_samples=self.n_predictions, ph=ph,
+                                               z_mode=False, gmm_mode=False, full_dist=False,
+                                               all_z_sep=False)
+        _, past_dict, ground_truth_dict = self._prediction_output_to_trajectories(
+            predictions_dict, dt=scene.dt, max_h=10, ph=ph, map=None)
+        return AttrDict(scene=scene, timestep=timestep, nodes=nodes, predictions=predictions,
+                        z=z, latent_probs=latent_probs, past_dict=past_dict,
+                        ground_truth_dict=ground_truth_dict)
+
+    def make_ovehicles(self, result):
+        """:469-505 (+ OVehicle.from_trajectron, ovehicle.py:24-117) on do_prediction's result:
+        the non-ego nodes' predictions bucketed by z on the GPU (ccmpc_load_predictions +
+        ccmpc_bucket), minpos = (x_min, y_min), pasts / ground truths + minpos, the OV actors'
+        bboxes.  Returns list[OVehicle] (one device store).  The planning step itself
+        (compute_prediction_controls) runs the same stages inside its step graph."""
+        from . import ovehicle
+        if "predictions" not in result:
+            raise ValueError("make_ovehicles takes generate_vehicle_latents' result (this "
+                             "do_prediction was given a sample_boundary eval_stg)")
+        sampler, minpos, pasts, bboxes = self._ov_inputs(result)
+        rows = sampler["rows"]
+        pred, z = sampler["predictions"], sampler["z"]
+        if torch.is_tensor(pred):
+            pred, z = pred.cpu().numpy(), z.cpu().numpy()
+        ovs = ovehicle.make_ovehicles(np.asarray(pred)[rows], np.asarray(z)[rows],
+                                      sampler["latent_pmf"], minpos, pasts, bboxes=bboxes,
+                                      device=self.device)
+        gt, ts, nodes = result.get("ground_truth_dict"), result["timestep"], result["nodes"]
+        for ov, r in zip(ovs, rows):
+            ov.node = nodes[r]
+            if gt is not None:
+                ov.ground_truth = gt[ts][nodes[r]] + minpos
+        return ovs
 
     def _ov_inputs(self, pred):
-        """make_ovehicles (:469-505) up to the bucketing: the non-ego nodes' rows of the sampler
-        boundary, minpos = (x_min, y_min), pasts (+ minpos) and bboxes of the OV actors."""
-        nodes, b, ts = pred["nodes"], pred["boundary"], pred["timestep"]
+        """make_ovehicles (:469-505) up to the bucketing: the non-ego nodes' rows of the
+        predictions + z (or of the sampler boundary), minpos = (x_min, y_min), pasts (+ minpos)
+        and bboxes of the OV actors."""
+        nodes, ts = pred["nodes"], pred["timestep"]
         sel = [i for i, n in enumerate(nodes) if n.id != "ego"]
         scene = pred["scene"]
         minpos = np.array([scene.x_min, scene.y_min])
@@ -624,6 +678,13 @@ class MidlevelAgent:
             ext = a.bounding_box.extent if a is not None else None
             bboxes.append([2.0 * ext.x, 2.0 * ext.y] if ext is not None else [4.5, 2.5])
         idx = np.asarray(sel)
+        if "predictions" in pred:                # the reference's 5-tuple
+            P = pred["predictions"]
+            sampler = {"source": "predictions", "predictions": P, "z": pred["z"], "rows": sel,
+                       "latent_pmf": np.asarray(pred["latent_probs"], np.float64).reshape(
+                           len(nodes), -1)[idx], "N": int(P.shape[1])}
+            return sampler, minpos, pasts, np.asarray(bboxes, np.float64)
+        b = pred["boundary"]
 
         def rows(x):
             if x is None:
@@ -1032,13 +1093,20 @@ class MidlevelAgent:
         record-path outputs.  Returns (ovehicles, graph, outputs, scene, K)."""
         from . import ovehicle, step
         ph = self.prediction_horizon
-        init = np.asarray(sampler["init_state"], np.float64)
+        source = sampler.get("source", "sampler")
         pmf = np.asarray(sampler["latent_pmf"], np.float64)
         O, L = pmf.shape
-        N, seed = int(sampler["N"]), int(sampler["seed"])
-        gmm = sampler["gmm"]
-        pp = bool(sampler.get("per_particle", False))
-        z_in, eps_in = sampler.get("z"), sampler.get("eps")
+        N = int(sampler["N"])
+        if source == "predictions":              # generate_vehicle_latents' 5-tuple
+            init, seed, gmm, pp = None, 0, None, False
+            z_in = eps_in = None
+            pred_dev = torch.is_tensor(sampler["predictions"])
+        else:
+            init = np.asarray(sampler["init_state"], np.float64)
+            seed, gmm = int(sampler["seed"]), sampler["gmm"]
+            pp = bool(sampler.get("per_particle", False))
+            z_in, eps_in = sampler.get("z"), sampler.get("eps")
+            pred_dev = False
         if pp and z_in is None:
             raise ValueError("per-particle GMM parameters need the injected z (prediction.py:103)")
         if not pp and (z_in is not None or eps_in is not None):
@@ -1059,14 +1127,15 @@ class MidlevelAgent:
                 raise KeyError(f"no moments saved for frame {params.frame - self.record_interval}"
                                " (the reference fails to load its pickle here)")
             extra = dict(prev_K=tuple(prev[2]), T_src=int(prev[3]), n_ideal=self.n_ideal)
-        key = (kind, O, N, ph, T, L, tuple(K), pp, eps_in is not None) + tuple(
+        key = (kind, O, N, ph, T, L, tuple(K), pp, eps_in is not None, source, pred_dev) + tuple(
             sorted(extra.items()))
         g = self._graphs.pop(key, None)
         if g is None:
             g = step.pool_take(self.device, key + (self.R,))
         if g is None:
             g = step.StepGraph(O, N, ph, L, K, device=self.device, R=self.R, per_particle=pp,
-                               eps_in=eps_in is not None, kind=kind, T=T, **extra)
+                               eps_in=eps_in is not None, kind=kind, T=T, source=source,
+                               pred_device=pred_dev, **extra)
             while self._graphs and len(self._graphs) >= self.max_graphs:
                 self._graphs.popitem(last=False)           # least recently used
         self._graphs[key] = g                              # most recently used
@@ -1079,6 +1148,8 @@ class MidlevelAgent:
                                (self.seed * 1_000_003 + int(params.frame)) & (2**63 - 1))
         if pp:
             g.set_device_inputs(gmm, z_in, eps_in)
+        if source == "predictions":
+            g.set_predictions(sampler["predictions"], sampler["z"], sampler.get("rows"))
         g.launch()
         # host objects that need no output are built while the graph runs
         st = g.store

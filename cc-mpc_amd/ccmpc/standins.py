@@ -203,8 +203,22 @@ def straight_route(start, heading, length=200.0, step=2.0):
 
 
 class _Node:
-    def __init__(self, node_id):
+    """A Trajectron++ scene node: id, and get(range, state) over the scene builder's track (the
+    call prediction_output_to_trajectories makes): rows for timesteps lo .. hi inclusive, NaN
+    outside the recorded track, as Trajectron++'s Node.get pads."""
+
+    def __init__(self, node_id, tracks=None):
         self.id = node_id
+        self._tracks = tracks
+
+    def get(self, tr_scene, state):
+        lo, hi = int(tr_scene[0]), int(tr_scene[1])
+        tr = self._tracks[self.id]
+        out = np.full((hi - lo + 1, 2), np.nan)
+        for k, ts in enumerate(range(lo, hi + 1)):
+            if 0 <= ts < len(tr):
+                out[k] = tr[ts]
+        return out
 
     def __repr__(self):
         return f"VEHICLE/{self.id}"
@@ -246,8 +260,10 @@ class ReplaySceneBuilder:
         self.record_interval = scene_config.record_interval if scene_config else 10
         self.dt = self.record_interval * ego_vehicle.get_world().get_settings().fixed_delta_seconds
         self.minpos = np.asarray(minpos, np.float64)
-        self.nodes = [_Node("ego")] + [_Node(str(i)) for i in other_vehicles]
-        self.tracks = {n.id: [] for n in self.nodes}
+        self.tracks = {}
+        self.nodes = [_Node("ego", self.tracks)] + [_Node(str(i), self.tracks)
+                                                    for i in other_vehicles]
+        self.tracks.update({n.id: [] for n in self.nodes})
         for n in self.nodes:
             self.tracks[n.id + "/state"] = []
         self.timestep = -1
@@ -346,3 +362,58 @@ def town03_scene(world=None, n_ov=1, ego_xy=(140.0, 81.0), ego_yaw_deg=0.0, ego_
     start = np.array([ego_xy[0], -ego_xy[1]])
     route = straight_route(start, -math.radians(ego_yaw_deg))
     return world, ego, ids, StubMapReader(route)
+
+
+class TrajectronModel:
+    """eval_stg stand-in shaped like a real Trajectron++ model object: it has NO sample_boundary,
+    so MidlevelAgent.do_prediction takes the reference's own route -- generate_vehicle_latents
+    (prediction.py:19-105) -> the 5-tuple -> make_ovehicles on predictions + z.  `inner` (a
+    SyntheticTrajectron) supplies the latent pmfs / GMM parameters that stand where the GRU
+    decoder's outputs would; use it with generate_vehicle_latents below (agent keyword
+    generate_vehicle_latents=standins.generate_vehicle_latents)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.device = inner.device
+
+
+def generate_vehicle_latents(eval_stg, scene, timesteps, num_samples=200, ph=8, z_mode=False,
+                             gmm_mode=False, full_dist=False, all_z_sep=False):
+    """prediction.py:19-105 for a TrajectronModel stand-in: the reference's 5-tuple
+    (z (nodes, N) int64, predictions (nodes, N, ph, 2) float32 scene-relative, nodes,
+    predictions_dict, latent_probs) as numpy arrays, the samples drawn by the library's own
+    sampler tail (ccmpc_sample_unicycle_ex) from the inner stand-in's boundary.  The non-ego
+    nodes are drawn as OVs 0 .. O-1 in node order (the Philox streams the sample_boundary route
+    keys them by), so both routes see the same particles; the ego's row is drawn after them."""
+    from . import engine
+    b = eval_stg.inner.sample_boundary(scene, int(np.asarray(timesteps).reshape(-1)[0]),
+                                       num_samples, ph)
+    nodes = list(b.nodes)
+    N = int(b.N)
+    n = len(nodes)
+    rows = [i for i, nd in enumerate(nodes) if nd.id != "ego"]
+    rows += [i for i, nd in enumerate(nodes) if nd.id == "ego"]
+    pred = np.empty((n, N, ph, 2), np.float32)
+    z = np.empty((n, N), np.int64)
+    sel = np.asarray(rows)
+    pp = bool(b.get("per_particle", False))
+
+    def pick(x):
+        if x is None:
+            return None
+        if isinstance(x, torch.Tensor):
+            return x[torch.as_tensor(sel, device=x.device)]
+        return np.asarray(x)[sel]
+    zs, store = engine.sample_unicycle(
+        np.asarray(b.init_state)[sel], np.asarray(b.latent_probs)[sel], pick(b.gmm), N, ph,
+        seed=b.seed, device=eval_stg.device, z=pick(b.get("z")) if pp else None,
+        eps=pick(b.get("eps")) if pp else None, per_particle=pp)
+    pos = store.pos.cpu().numpy()
+    zh = zs.cpu().numpy()
+    for j, r in enumerate(rows):
+        o = store.offsets[j]
+        pred[r] = pos[:, o:o + N].reshape(ph, 2, N).transpose(2, 0, 1)
+        z[r] = zh[j]
+    ts = int(np.asarray(timesteps).reshape(-1)[0])
+    pdict = {ts: {nd: pred[i][None] for i, nd in enumerate(nodes)}}
+    return z, pred, nodes, pdict, np.asarray(b.latent_probs, np.float64)

@@ -170,12 +170,20 @@ class StepGraph:
                           written into this graph's own device buffers (pp_gmm, pp_z, pp_eps)
                           by set_device_inputs, never through the host.
 
+    source="predictions" takes the reference's own prediction boundary instead of the sampler
+    tail: generate_vehicle_latents' predictions (O, N, ph, 2) float32 scene-relative and z
+    (O, N) latent ids (prediction.py:93-105) -- host arrays written into the packed inputs
+    (pred_device=False), or device tensors copied into the graph's own buffers -- moved into
+    the sample-order store by ccmpc_load_predictions, then bucketed (ccmpc_bucket) as the
+    sampler's output is: make_ovehicles (:469-505) with no sampler in the graph.
+
     ``generation`` counts launches: objects built over this graph's buffers (ScenePredictions)
     record the generation they belong to and refuse reads after a later replay."""
 
     def __init__(self, O, N, ph, L, K, device="cuda", dt=0.5, R=risk.R_COLLISION, tol=1e-8,
                  maxiter=1000, per_particle=False, eps_in=False, kind="minkowski", T=None,
-                 prev_K=None, T_src=None, n_ideal=1_000_000):
+                 prev_K=None, T_src=None, n_ideal=1_000_000, source="sampler",
+                 pred_device=False):
         self.device = engine.require_device(device)
         lib = _lib.load()
         if kind not in ("minkowski", "ideal", "affine"):
@@ -195,10 +203,18 @@ class StepGraph:
         self.per_particle, self.eps_in = bool(per_particle), bool(eps_in)
         if self.eps_in and not self.per_particle:
             raise ValueError("eps_in is part of the per-particle (Trajectron++ boundary) mode")
+        if source not in ("sampler", "predictions"):
+            raise ValueError(f"unknown source {source!r}")
+        self.source, self.pred_device = source, bool(pred_device)
+        if source == "predictions" and self.per_particle:
+            raise ValueError("the predictions source replaces the sampler tail: no per_particle")
         self.generation = 0
         f64, f32, i32, i64, u8 = torch.float64, torch.float32, torch.int32, torch.int64, torch.uint8
         ph_, L_ = self.ph, self.L
-        gmm_field = [] if self.per_particle else [("gmm", (O, L_, ph_, 5), f32)]
+        gmm_field = ([] if self.per_particle or source == "predictions"
+                     else [("gmm", (O, L_, ph_, 5), f32)])
+        if source == "predictions" and not self.pred_device:
+            gmm_field += [("pred", (O, N, ph_, 2), f32), ("zin", (O, N), i64)]
         fields = ([("gen", (2,), i64), ("seed", (1,), i64), ("init", (O, 4), f64),
                    ("cdf", (O, L_), f64)] + gmm_field +
                   [("keep", (O, L_), i32), ("nk", (O,), i32), ("base", (O,), i32),
@@ -222,6 +238,10 @@ class StepGraph:
             self.pp_z = torch.zeros((O, N), dtype=i32, device=self.device)
             if self.eps_in:
                 self.pp_eps = torch.zeros((O, ph_, 2, N), dtype=f32, device=self.device)
+        self.pr_pred = self.pr_z = None
+        if source == "predictions" and self.pred_device:
+            self.pr_pred = torch.zeros((O, N, ph_, 2), dtype=f32, device=self.device)
+            self.pr_z = torch.zeros((O, N), dtype=i64, device=self.device)
         out = [("cnt", (C,), i64), ("off", (C,), i64), ("pmf", (C,), f64),
                ("centre", (C, 2), f64), ("mean", (C, ph_, 2), f64),
                ("cov", (C, 2 * ph_, 2 * ph_), f64)]
@@ -243,7 +263,7 @@ class StepGraph:
         # small clouds: sampler + bucketing in three short launches (ccmpc_sample_bucket), whose
         # cells need K (N + 4) slots per OV; else the sampler's sample-order store + ccmpc_bucket
         fused_ws = lib.ccmpc_sample_bucket_workspace_bytes(O, N, ph_, self.max_k) \
-            if self.max_k * (L_ + 1) <= 512 else 0
+            if self.max_k * (L_ + 1) <= 512 and source == "sampler" else 0
         self.fused = fused_ws > 0
         region, cur, n_bound = [], 0, 0
         for o in range(O):
@@ -310,7 +330,9 @@ class StepGraph:
         i, o, st = self.inp, self.out, self.store
         O, N, T, L = self.O, self.N, self.ph, self.L
         ws = self.bucket_ws
-        if self.per_particle:
+        if self.source == "predictions":
+            gmm = layout = z_in = eps = None
+        elif self.per_particle:
             gmm, layout, z_in, eps = (p(self.pp_gmm), _lib.GMM_PER_PARTICLE, p(self.pp_z),
                                       p(self.pp_eps))
         else:
@@ -323,10 +345,18 @@ class StepGraph:
                 ws.numel(), None, p(st.pos), st.ld, p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")),
                 p(o.d("centre")), s))]
         sm = self.samples
-        return [(lib.ccmpc_sample_unicycle_ex, (
-                    p(i.d("init")), p(i.d("cdf")), L, gmm, layout, z_in,
-                    eps, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld,
-                    s)),
+        if self.source == "predictions":
+            pred, z = ((self.pr_pred, self.pr_z) if self.pred_device
+                       else (i.d("pred"), i.d("zin")))
+            stride = sm.offsets[1] if O > 1 else N
+            first = (lib.ccmpc_load_predictions, (p(pred), p(z), 8, None, O, N, T, L,
+                                                  p(sm.pos), sm.ld, stride, p(self.z), s))
+        else:
+            first = (lib.ccmpc_sample_unicycle_ex, (
+                p(i.d("init")), p(i.d("cdf")), L, gmm, layout, z_in,
+                eps, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld,
+                s))
+        return [first,
                 (lib.ccmpc_bucket, (p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
                                     p(i.d("nk")), p(i.d("base")), self.max_k,
                                     p(i.d("minpos")), p(i.d("region")), p(ws), ws.numel(),
@@ -453,9 +483,13 @@ class StepGraph:
         np.multiply(kc, kept, out=keep, casting="unsafe")
         keep -= 1
         i.h("seed")[0] = _as_i64(seed)
-        i.h("init").reshape(-1)[:] = np.asarray(init_state, np.float64).reshape(-1)
+        if init_state is not None:             # (the predictions source has no sampler)
+            i.h("init").reshape(-1)[:] = np.asarray(init_state, np.float64).reshape(-1)
         np.cumsum(pmf, axis=1, out=i.h("cdf"))
-        if self.per_particle:
+        if self.source == "predictions":
+            if gmm is not None:
+                raise ValueError("the predictions source takes set_predictions, not gmm")
+        elif self.per_particle:
             if gmm is not None:
                 raise ValueError("per-particle graph: pass the device parameters to "
                                  "set_device_inputs, not set_inputs")
@@ -497,6 +531,43 @@ class StepGraph:
         src = src_cell.cpu().numpy() if torch.is_tensor(src_cell) else np.asarray(src_cell)
         i.h("src")[:] = src.reshape(-1)
         i.h("iseed")[0] = _as_i64(seed)
+
+    def set_predictions(self, predictions, z, rows=None):
+        """The predictions source's input for the next launch: generate_vehicle_latents'
+        predictions (nodes, N, ph, 2) float32 scene-relative and z (nodes, N) latent ids
+        (prediction.py:93-105), of which rows[o] is OV o's node (make_ovehicles skips the ego's,
+        :475-477; default: rows 0 .. O-1).  Host arrays go into the pinned input pack (moved by
+        the step's copy-in); device tensors are copied on the current stream into the graph's
+        own buffers (a graph built with pred_device=True).  Values are not validated on the host
+        (that would synchronise): the load kernel clamps z into [0, L)."""
+        if self.source != "predictions":
+            raise ValueError("set_predictions needs a graph built with source='predictions'")
+        O, N, T = self.O, self.N, self.ph
+        rows = list(range(O)) if rows is None else [int(r) for r in rows]
+        if len(rows) != O:
+            raise ValueError(f"{len(rows)} OV rows for a graph of {O} OVs")
+        dev = torch.is_tensor(predictions)
+        if dev != self.pred_device or torch.is_tensor(z) != dev:
+            raise ValueError("predictions / z must both be device tensors on a pred_device "
+                             "graph and host arrays otherwise")
+        if tuple(predictions.shape[1:]) != (N, T, 2) or tuple(z.shape[1:]) != (N,):
+            raise ValueError(f"predictions {tuple(predictions.shape)} / z {tuple(z.shape)}: "
+                             f"expected (nodes, {N}, {T}, 2) / (nodes, {N})")
+        if dev:
+            if predictions.device != self.device or z.device != self.device:
+                raise ValueError("predictions / z must be on the graph's device")
+            if rows == list(range(O)) and predictions.shape[0] == O:
+                self.pr_pred.copy_(predictions)
+                self.pr_z.copy_(z)
+            else:
+                idx = torch.as_tensor(rows, device=self.device)
+                torch.index_select(predictions.to(torch.float32), 0, idx, out=self.pr_pred)
+                torch.index_select(z.to(torch.int64), 0, idx, out=self.pr_z)
+            return
+        hp, hz = self.inp.h("pred"), self.inp.h("zin")
+        for o, r in enumerate(rows):             # straight into the pinned pack, no temporary
+            np.copyto(hp[o], predictions[r], casting="same_kind")
+            np.copyto(hz[o], z[r], casting="unsafe")
 
     def set_device_inputs(self, gmm, z, eps=None):
         """The per-particle mode's device inputs for the next launch, as Trajectron++ leaves

@@ -585,3 +585,67 @@ extern "C" int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }
+
+// ---- the reference's own prediction boundary ---------------------------------------------
+// generate_vehicle_latents (prediction.py:93-105) hands make_ovehicles (v8ideal/__init__.py:
+// 469-505) predictions[node][N][T][2] float32 (scene-relative; particle-major, as numpy's
+// swapaxes(predictions, 0, 1) leaves them) and z[node][N] (int64 argmax of the one-hot sample).
+// load_predictions_kernel gathers the OV rows (rows[o]: the non-ego nodes) into the plane-major
+// sample-order store ccmpc_bucket reads, pos[(2t + c) * ld + o * ov_stride + i], and the latent
+// ids into int32.  A workgroup moves kLoadChunk particles: the chunk's 2T * kLoadChunk floats
+// are one contiguous run of the source, read coalesced into LDS (padded rows: 2T + 1 floats),
+// then written plane by plane, kLoadChunk consecutive floats per plane.
+constexpr int kLoadChunk = 128;
+
+__global__ __launch_bounds__(256) void load_predictions_kernel(
+    const float *__restrict__ pred, const void *__restrict__ z, int z_bytes,
+    const int32_t *__restrict__ rows, int64_t N, int T, int64_t n_latent,
+    float *__restrict__ pos, int64_t ld, int64_t ov_stride, int32_t *__restrict__ z_out) {
+  extern __shared__ float tile[];
+  const int o = blockIdx.y;
+  const int64_t row = rows ? rows[o] : o;
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kLoadChunk;
+  const int n = static_cast<int>(N - b0 < kLoadChunk ? N - b0 : kLoadChunk);
+  const int W = 2 * T, S = W + 1;
+  const float *src = pred + (row * N + b0) * W;
+  for (int e = threadIdx.x; e < n * W; e += 256) {
+    const int p = e / W;
+    tile[p * S + (e - p * W)] = src[e];
+  }
+  if (threadIdx.x < n) {
+    const int64_t i = row * N + b0 + threadIdx.x;
+    int64_t v = z_bytes == 8 ? static_cast<const int64_t *>(z)[i]
+                             : static_cast<int64_t>(static_cast<const int32_t *>(z)[i]);
+    v = v < 0 ? 0 : (v >= n_latent ? n_latent - 1 : v);  // the kernels' clamp of injected ids
+    z_out[o * N + b0 + threadIdx.x] = static_cast<int32_t>(v);
+  }
+  __syncthreads();
+  float *dst = pos + o * ov_stride + b0;
+  for (int e = threadIdx.x; e < W * kLoadChunk; e += 256) {
+    const int r = e / kLoadChunk, p = e % kLoadChunk;
+    if (p < n) dst[r * ld + p] = tile[p * S + r];
+  }
+}
+
+extern "C" int ccmpc_load_predictions(const float *pred, const void *z, int z_bytes,
+                                      const int32_t *rows, int64_t n_ov, int64_t N, int64_t T,
+                                      int64_t n_latent, float *pos_out, int64_t ld_out,
+                                      int64_t ov_stride, int32_t *z_out,
+                                      ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
+  CCMPC_REQUIRE(n_ov >= 0 && N >= 0 && n_ov < 65536, "bad n_ov / N");
+  CCMPC_REQUIRE(z_bytes == 4 || z_bytes == 8, "z must be int32 or int64");
+  CCMPC_REQUIRE(n_latent >= 1, "n_latent must be >= 1");
+  if (n_ov == 0 || N == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(pred && z && pos_out && z_out, "null pointer");
+  CCMPC_REQUIRE(ov_stride >= N && ld_out >= (n_ov - 1) * ov_stride + N, "store too small");
+  const int64_t chunks = (N + kLoadChunk - 1) / kLoadChunk;
+  CCMPC_REQUIRE(chunks < (int64_t(1) << 31), "N too large");
+  const size_t lds = static_cast<size_t>(kLoadChunk) * (2 * T + 1) * sizeof(float);
+  hipLaunchKernelGGL(load_predictions_kernel,
+                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(n_ov)), dim3(256),
+                     lds, as_stream(stream), pred, z, z_bytes, rows, N, static_cast<int>(T),
+                     n_latent, pos_out, ld_out, ov_stride, z_out);
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}

@@ -349,6 +349,25 @@ int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T
                  double *init_center, ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * The reference's own prediction boundary into ccmpc_bucket's input.  Replaces the per-OV
+ * `predictions[idx]` / `z[idx]` reads of make_ovehicles (v8ideal/__init__.py:469-490) on the
+ * 5-tuple generate_vehicle_latents returns (prediction.py:93-105):
+ *  pred[row][N][T][2]  float32, scene-relative (numpy's swapaxes(predictions, 0, 1) layout)
+ *  z[row][N]           latent ids, int64 (z_bytes = 8: np.argmax's dtype) or int32 (4);
+ *                      clamped into [0, n_latent)
+ *  rows[n_ov]          device int32: the node row of OV o (make_ovehicles skips the ego's
+ *                      node); NULL = rows 0 .. n_ov-1
+ *  out: pos_out        F32 sample-order store, OV o at o * ov_stride (ov_stride >= N, 4-aligned
+ *                      for ccmpc_bucket): pos_out[(2t + c) * ld_out + o * ov_stride + i]
+ *       z_out[n_ov][N] int32, as ccmpc_bucket reads it
+ * One launch; traffic 2 x 8 T B per particle.
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_load_predictions(const float *pred, const void *z, int z_bytes, const int32_t *rows,
+                           int64_t n_ov, int64_t N, int64_t T, int64_t n_latent, float *pos_out,
+                           int64_t ld_out, int64_t ov_stride, int32_t *z_out,
+                           ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Sampler + bucketing in three short launches, for clouds of N <= 8192 particles per OV: the same draws
  * as ccmpc_sample_unicycle_ex (same Philox streams, same float32 arithmetic) bucketed as
  * ccmpc_bucket buckets them -- every cell holds the same particles in the same order and the

@@ -201,3 +201,88 @@ def test_filter_pmf_reaches_every_stage(gpu):
         assert [ov.n_states for ov in ovs] == K.tolist()
         per_cell = T * (T - 1) // 2 if shrinking else T
         assert len(out[0]) == K.sum() * per_cell
+
+
+def _latents_route(gpu, per_particle, device_tensors=False, run_interval=10):
+    """The same scenario with an eval_stg shaped like a real Trajectron++ model (no
+    sample_boundary): do_prediction calls generate_vehicle_latents and the step graph takes
+    its predictions + z (source='predictions')."""
+    import torch
+    from ccmpc import standins
+    scen = _scenario(gpu, per_particle, run_interval=run_interval)
+    scen.eval_stg = standins.TrajectronModel(scen.eval_stg)
+    gvl = standins.generate_vehicle_latents
+    if device_tensors:          # a predictor that leaves its outputs on the GPU
+        def gvl(*a, **k):
+            z, pred, nodes, pdict, lp = standins.generate_vehicle_latents(*a, **k)
+            return (torch.as_tensor(z, device=gpu), torch.as_tensor(pred, device=gpu), nodes,
+                    pdict, lp)
+    scen.agent_kwargs["generate_vehicle_latents"] = gvl
+    return scen
+
+
+@pytest.mark.parametrize("per_particle,device_tensors", [(False, False), (True, False),
+                                                         (False, True)],
+                         ids=["per_latent", "per_particle", "device_tensors"])
+def test_reference_predictor_output_drives_run_step(gpu, per_particle, device_tensors):
+    """an eval_stg without sample_boundary takes the reference's route --
+    generate_vehicle_latents (prediction.py:19-105) -> the 5-tuple -> make_ovehicles on
+    predictions + z (v8ideal/__init__.py:469-505) -> generator -> QP, no sampler in the step
+    graph.  With a stand-in predictor whose particles are the sampler's own draws, every planning
+    step's records, speeds and angles are the sample_boundary route's bytes."""
+    from ccmpc import step
+    a = _scenario(gpu, per_particle)
+    a.episode(0)
+    b = _latents_route(gpu, per_particle, device_tensors)
+    b.episode(0)
+    assert len(a.steps) == len(b.steps) == 10
+    for sa, sb in zip(a.steps, b.steps):
+        assert sb["sampler"]["source"] == "predictions"
+        assert sa["frame"] == sb["frame"] and sa["T"] == sb["T"]
+        assert sa["records"].tobytes() == sb["records"].tobytes(), sa["frame"]
+        assert sa["speeds"].tobytes() == sb["speeds"].tobytes()
+        assert sa["angles"].tobytes() == sb["angles"].tobytes()
+    keys = [k for k in step._POOL if k[1][-3] == "predictions"]
+    assert keys, "the predictions-source graphs were not used"
+
+
+def test_make_ovehicles_on_the_reference_5_tuple(gpu):
+    """The agent's make_ovehicles(result) on do_prediction's 5-tuple: bucketed clouds equal the
+    oracle's restatement of :469-505 + from_trajectron on the same predictions + z, and past /
+    ground truth come from prediction_output_to_trajectories (+ minpos)."""
+    from ccmpc import planner, standins
+    scen = _latents_route(gpu, False)
+    world, ego, ids, mr = scen.make_world()
+    agent = planner.MidlevelAgent(ego, mr, ids, scen.eval_stg,
+                                  scene_builder_cls=standins.ReplaySceneBuilder,
+                                  scene_config=standins.OnlineConfig(10), prediction_horizon=8,
+                                  n_predictions=3000, device=gpu, **{
+                                      k: v for k, v in scen.agent_kwargs.items()
+                                      if k != "device"})
+    frame = world.tick()
+    for _ in range(31):
+        agent.run_step(frame)                       # burn-in frames only: no planning yet
+        frame = world.tick()
+    res = agent.do_prediction(agent._first_frame + 30)
+    assert set(res) >= {"scene", "timestep", "nodes", "predictions", "z", "latent_probs",
+                        "past_dict", "ground_truth_dict"}
+    assert res["z"].dtype == np.int64 and res["predictions"].dtype == np.float32
+    ovs = agent.make_ovehicles(res)
+    minpos = np.array([res["scene"].x_min, res["scene"].y_min])
+    rows = [i for i, n in enumerate(res["nodes"]) if n.id != "ego"]
+    assert len(ovs) == len(rows)
+    ts = res["timestep"]
+    pasts = [res["past_dict"][ts][res["nodes"][r]] + minpos for r in rows]
+    want = orc.make_ovehicles(res["predictions"][rows], res["z"][rows],
+                              np.asarray(res["latent_probs"], float)[rows], minpos, pasts,
+                              [np.array([4.5, 2.5])] * len(rows), 8)
+    for ov, w, r, past in zip(ovs, want, rows, pasts):
+        got = ov.pred_positions
+        assert len(got) == len(w.pred_positions)
+        for g, x in zip(got, w.pred_positions):
+            np.testing.assert_array_equal(g, x)
+        np.testing.assert_array_equal(ov.latent_pmf, w.latent_pmf)
+        np.testing.assert_array_equal(ov.past, past)
+        assert ov.node is res["nodes"][r]
+        np.testing.assert_array_equal(ov.ground_truth, res["ground_truth_dict"][ts][
+            res["nodes"][r]] + minpos)

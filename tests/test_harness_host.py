@@ -133,3 +133,43 @@ def test_route_goal_rule():
                                   [14.0, 0.0])       # 14 lies in (12, 14]
     np.testing.assert_array_equal(rb.collect_segs_polytopes_and_goal([30.0, 1.0], 99.0).goal,
                                   [40.0, 0.0])
+
+
+def test_prediction_output_to_trajectories_over_standin_nodes(host_agent_cls):
+    """Trajectron++'s prediction_output_to_trajectories as restated in ccmpc.prediction, over the
+    scene builder's nodes (Node.get pads with NaN outside the track): the history is the track's
+    last max_h + 1 positions (the sample_boundary route's scene.past), the future is empty in a
+    live simulation, the prediction passes through."""
+    from ccmpc import prediction
+    world, ego, agent = _make(host_agent_cls)
+    frame = world.tick()
+    for _ in range(131):                          # 14 recorded timesteps, no planning call
+        agent.run_step(frame) if agent._first_frame is None or \
+            (frame - agent._first_frame) // 10 < 4 else \
+            agent._scene_builder.capture_trajectory(frame)
+        frame = world.tick()
+    scene = agent._scene_builder.get_scene()
+    ts = scene.timestep
+    assert ts == 13
+    preds = {n: np.full((1, 5, 8, 2), float(i)) for i, n in enumerate(scene.nodes)}
+    out, hist, fut = prediction.prediction_output_to_trajectories({ts: preds}, dt=scene.dt,
+                                                                  max_h=10, ph=8)
+    past = scene.past(ts, max_h=10)
+    for n in scene.nodes:
+        np.testing.assert_array_equal(hist[ts][n], past[n])
+        assert hist[ts][n].shape == (11, 2)
+        assert fut[ts][n].shape == (0, 2)
+        assert out[ts][n] is preds[n]
+    # an early timestep: the history is cut at the track's start (NaN rows dropped)
+    _, hist2, _ = prediction.prediction_output_to_trajectories({2: preds}, scene.dt, 10, 8)
+    for n in scene.nodes:
+        np.testing.assert_array_equal(hist2[2][n], scene.past(2, max_h=10)[n])
+        assert hist2[2][n].shape == (3, 2)
+
+
+def test_generate_vehicle_latents_fails_like_the_reference_without_trajectron():
+    """prediction.py:13-17: without the trajectron-plus-plus submodule the reference's import
+    raises; the restated glue raises the same exception when a Trajectron++ eval_stg is used."""
+    from ccmpc import prediction
+    with pytest.raises(Exception, match="trajectron"):
+        prediction.generate_vehicle_latents(object(), None, np.array([0]))
