@@ -157,13 +157,16 @@ def c4_sharded(dev, seed, world, rank, steps=20, warmup=3, cfg=None, return_reco
     store = engine.ParticleStore.from_cells(cells, device=dev)
     cyc = cycle.MinkowskiCycle(store, [k for ks in K for k in ks], np.array(refs), scene_K=K)
     launch = cyc.bind().launch
-    gather = None
+    gather = counts = None
     if world > 1 or _backend() is not None:     # a process group (also world 1: --dist-always)
         import torch.distributed as dist
         gloo = dist.get_backend() == "gloo"
         counts = cdist.record_counts(store.n_cells, "cpu" if gloo else dev)
-        gather = ((lambda: cdist.gather_records(cyc.rec.cpu(), counts=counts)) if gloo else
-                  (lambda: cdist.gather_records(cyc.rec, counts=counts)))
+        # the compact exchange: the QP's fields of each record packed to 32 bytes on the
+        # device (ccmpc_compact_records) and all-gathered (a quarter of the 128-byte records)
+        gather = ((lambda: cdist.gather_records(cdist.compact_records(cyc.rec).cpu(),
+                                                counts=counts)) if gloo else
+                  (lambda: cdist.gather_records(cyc.rec, counts=counts, compact=True)))
     gathered = [cyc.rec]
 
     def step():
@@ -199,7 +202,10 @@ def c4_sharded(dev, seed, world, rank, steps=20, warmup=3, cfg=None, return_reco
         "constraints_per_s": round(n_rec / elapsed, 1),
         "record_gather": ("none (N=1)" if gather is None else
                           ("RCCL" if _backend() == "nccl" else _backend())
-                          + " all_gather of every rank's records, inside the step"),
+                          + " all_gather of every rank's compact (32-byte) records, inside the"
+                          " step"),
+        "gather_bytes_per_step": (None if gather is None else
+                                  int(sum(counts) * (c["T"] * (c["T"] - 1) // 2) * 32)),
         "rank0": {"particles": n_part, "cells": store.n_cells, "alg_bytes_per_launch": alg,
                   "kernel_us_warm": round(t_warm * 1e6, 2),
                   "hbm_frac_warm": round(alg / t_warm / HBM_PEAK, 4)},

@@ -86,6 +86,7 @@ SIGNATURES = {
     "ccmpc_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "ccmpc_bucket": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _I64, _P,
                                     _P, _P, _SZ, _P, _I64, _P, _P, _P, _P, _P]),
+    "ccmpc_compact_records": (ctypes.c_int, [_P, ctypes.c_int, _I64, _P, _P]),
     "ccmpc_load_predictions": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _I64, _I64, _I64, _I64,
                                               _P, _I64, _I64, _P, _P]),
     "ccmpc_sample_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),

@@ -16,6 +16,26 @@ Cells (scene, OV, mode) are independent, so a node runs the path as weak-scaled 
 import torch
 
 REC_BYTES = 128
+COMPACT_BYTES = 32      # ccmpc_gather_rec: n0, n1, rhs, side, status, t_tau
+
+
+def compact_records(rec, kind=0):
+    """The QP-read fields of a record block, packed on the device (ccmpc_compact_records):
+    uint8 (cells, P, 128) -> (cells, P, 32) ccmpc_gather_rec.  kind: 0 half-space, 1 affine
+    (mpc.REC_HALFSPACE / REC_AFFINE).  The QP reads the result in place (mpc.REC_*_COMPACT)."""
+    from . import _lib, engine
+    if rec.dtype != torch.uint8 or rec.dim() != 3 or rec.shape[2] != REC_BYTES:
+        raise ValueError("rec must be a uint8 (cells, P, 128) record block")
+    if rec.device.type != "cuda":
+        raise _lib.CcmpcError("compact_records runs on the GPU (ccmpc_compact_records)")
+    rec = rec.contiguous()
+    out = torch.empty(tuple(rec.shape[:2]) + (COMPACT_BYTES,), dtype=torch.uint8,
+                      device=rec.device)
+    with torch.cuda.device(rec.device):
+        _lib.check(_lib.load().ccmpc_compact_records(
+            engine._p(rec), int(kind), rec.shape[0] * rec.shape[1], engine._p(out),
+            engine._stream()), "ccmpc_compact_records")
+    return out
 
 
 def scene_range(n_scenes, rank, world):
@@ -46,18 +66,24 @@ def record_counts(n_local, device, group=None):
     return [int(x.item()) for x in ns]
 
 
-def gather_records(rec, group=None, counts=None):
+def gather_records(rec, group=None, counts=None, compact=False, kind=0):
     """All-gather every rank's record block.
 
-    rec: uint8 tensor (n_local, P, 128) on this rank's device (CPU under gloo).  Ranks may hold
-    different numbers of cells; blocks are padded to the largest and trimmed after the
-    exchange.  ``counts`` (every rank's n_local, from ``record_counts``) skips the count
-    exchange, so the call enqueues without a host synchronisation.  Returns the (sum n, P, 128)
-    block in rank order, i.e. the global cell order of contiguous ``scene_range`` shards.
+    rec: uint8 tensor (n_local, P, 128) -- or (n_local, P, 32) already-packed ccmpc_gather_rec
+    -- on this rank's device (CPU under gloo).  compact=True packs 128-byte records on the GPU
+    first (compact_records; kind 0 half-space, 1 affine), so a quarter of the bytes cross xGMI.
+    Ranks may hold different numbers of cells; blocks are padded to the largest and trimmed
+    after the exchange.  ``counts`` (every rank's n_local, from ``record_counts``) skips the
+    count exchange, so the call enqueues without a host synchronisation.  Returns the
+    (sum n, P, bytes) block in rank order, i.e. the global cell order of contiguous
+    ``scene_range`` shards.
     """
     import torch.distributed as dist
-    if rec.dtype != torch.uint8 or rec.dim() != 3 or rec.shape[2] != REC_BYTES:
-        raise ValueError("rec must be a uint8 (cells, P, 128) record block")
+    if rec.dtype != torch.uint8 or rec.dim() != 3 or rec.shape[2] not in (REC_BYTES,
+                                                                             COMPACT_BYTES):
+        raise ValueError("rec must be a uint8 (cells, P, 128 or 32) record block")
+    if compact and rec.shape[2] == REC_BYTES:
+        rec = compact_records(rec, kind)
     world = dist.get_world_size(group)
     if counts is None:
         counts = record_counts(rec.shape[0], rec.device, group)

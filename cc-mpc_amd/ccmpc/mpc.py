@@ -22,6 +22,7 @@ from . import _lib, engine
 
 U_ORDER_F, U_ORDER_C = 0, 1            # CCMPC_U_ORDER_*: cvxpy's default reshape is 'F'
 REC_HALFSPACE, REC_AFFINE = 0, 1       # CCMPC_REC_KIND_*
+REC_HALFSPACE_COMPACT, REC_AFFINE_COMPACT = 2, 3   # the same, as 32-byte ccmpc_gather_rec
 QP_OK, QP_MAXITER, QP_NUMERIC, QP_SKIPPED_ROWS = 0, 1, 2, 4
 
 
@@ -104,7 +105,8 @@ class PlanningQP:
 
     def solve(self, gamma, xbar, goal, ref, rec, u_prev=None, ubar=None):
         """Enqueue the S solves.  gamma [S, 4T_full, 2T_full], xbar [S, 4T_full],
-        goal [S, 2], ref [S, n_ref, 2], rec the records (uint8 [cells, P, 128] tensor)."""
+        goal [S, 2], ref [S, n_ref, 2], rec the records (uint8 [cells, P, 128] tensor, or
+        [cells, P, 32] ccmpc_gather_rec for the *_COMPACT kinds)."""
         lib = _lib.load()
         S, T, Tf = self.S, self.T, self.T_full
         ref = ref.reshape(S, -1, 2)
@@ -116,11 +118,13 @@ class PlanningQP:
         self._need(ref, "ref", None)
         if ref.shape[1] < 1:
             raise ValueError("ref: at least one reference point per scene")
-        P = T * (T - 1) // 2 if self.kind == REC_HALFSPACE else T
+        P = T * (T - 1) // 2 if self.kind in (REC_HALFSPACE, REC_HALFSPACE_COMPACT) else T
+        B = 32 if self.kind >= REC_HALFSPACE_COMPACT else 128    # record bytes
         if P > 0 and self.n_cells > 0:
             self._need(rec, "rec", None, torch.uint8)
-            if rec.numel() < self.n_cells * P * 128 or (rec.dim() == 3 and rec.shape[1] != P):
-                raise ValueError(f"rec: [cells >= {self.n_cells}, {P}, 128] records expected")
+            if rec.numel() < self.n_cells * P * B or (rec.dim() == 3 and (
+                    rec.shape[1] != P or rec.shape[2] != B)):
+                raise ValueError(f"rec: [cells >= {self.n_cells}, {P}, {B}] records expected")
         if u_prev is not None and Tf > T:
             self._need(u_prev, "u_prev", (S, 2 * (Tf - T)))
         if ubar is not None:

@@ -184,3 +184,44 @@ extern "C" int ccmpc_graph_destroy(void *exec) {
   }
   return CCMPC_OK;
 }
+
+// ---- compact records for the multi-GPU exchange ---------------------------------------------
+// One thread per record: the five fields the QP reads (n, rhs, side, status, t_tau) out of the
+// 128-byte record into a 32-byte ccmpc_gather_rec, as two 16-byte stores.
+__global__ __launch_bounds__(256) void compact_records_kernel(const unsigned char *__restrict__ rec,
+                                                              int affine, int64_t n,
+                                                              double4 *__restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned char *r = rec + i * 128;
+  const double2 nn = *reinterpret_cast<const double2 *>(r);
+  const double rhs = *reinterpret_cast<const double *>(r + (affine ? 32 : 16));
+  const int4 tail = *reinterpret_cast<const int4 *>(r + 112);  // which, side, status, t_tau
+  const uint32_t ss = (static_cast<uint32_t>(static_cast<uint16_t>(tail.y))) |
+                      (static_cast<uint32_t>(static_cast<uint16_t>(tail.z)) << 16);
+  double4 v;
+  v.x = nn.x;
+  v.y = nn.y;
+  v.z = rhs;
+  v.w = __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(tail.w)) << 32) |
+                                       ss);
+  out[i] = v;
+}
+
+extern "C" int ccmpc_compact_records(const void *rec, int rec_kind, int64_t n_rec,
+                                     ccmpc_gather_rec *out, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(rec_kind == CCMPC_REC_KIND_HALFSPACE || rec_kind == CCMPC_REC_KIND_AFFINE,
+                "rec_kind must be CCMPC_REC_KIND_HALFSPACE or _AFFINE");
+  CCMPC_REQUIRE(n_rec >= 0, "bad n_rec");
+  if (n_rec == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(rec && out, "null pointer");
+  CCMPC_REQUIRE(ccmpc::aligned(rec, 16) && ccmpc::aligned(out, 32), "misaligned records");
+  const int64_t blocks = (n_rec + 255) / 256;
+  CCMPC_REQUIRE(blocks < (int64_t(1) << 31), "too many records");
+  hipLaunchKernelGGL(compact_records_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                     ccmpc::as_stream(stream), static_cast<const unsigned char *>(rec),
+                     rec_kind == CCMPC_REC_KIND_AFFINE ? 1 : 0, n_rec,
+                     reinterpret_cast<double4 *>(out));
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}

@@ -99,6 +99,12 @@ __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + 
 __device__ __forceinline__ int32_t items_of(int64_t n, int lg_chunk) {
   return n > 0 ? static_cast<int32_t>((n + (int64_t(1) << lg_chunk) - 1) >> lg_chunk) : 1;
 }
+// With whole-cell items: a cell of <= whole particles is ONE item (its workgroup's waves deal
+// its load groups round-robin), so its Gram is combined in LDS -- no slabs, no arrival, no
+// root gather; larger cells are cut into chunk-sized items as before.  whole = 0: off.
+__device__ __forceinline__ int32_t items_of(int64_t n, int lg_chunk, int64_t whole) {
+  return n <= whole ? 1 : items_of(n, lg_chunk);
+}
 
 constexpr int kFanIn = 16;
 constexpr int kLgFanIn = 4;
@@ -144,7 +150,8 @@ __device__ __forceinline__ int64_t lane_i64(int64_t v, int l) {
 __device__ __forceinline__ bool locate_item(int32_t item, const int64_t *__restrict__ cnt,
                                             const int64_t *__restrict__ off, int n_cells,
                                             int lg_chunk, ItemLoc &loc,
-                                            const int32_t *__restrict__ cell_ref = nullptr) {
+                                            const int32_t *__restrict__ cell_ref = nullptr,
+                                            int64_t whole = 0) {
   const int lane = threadIdx.x & 63;
   int32_t before = 0;
   for (int base = 0; base < n_cells; base += 64) {
@@ -152,7 +159,7 @@ __device__ __forceinline__ bool locate_item(int32_t item, const int64_t *__restr
     const int64_t n = (c < n_cells) ? cnt[c] : 0;
     const int64_t o = (c < n_cells) ? off[c] : 0;
     const int32_t rs = (cell_ref && c < n_cells) ? cell_ref[c] : 0;  // same round trip
-    const int32_t mine = (c < n_cells) ? items_of(n, lg_chunk) : 0;
+    const int32_t mine = (c < n_cells) ? items_of(n, lg_chunk, whole) : 0;
     const int32_t incl = wave_incl_scan_i32(mine);
     const int32_t total = lane_i32(incl, 63);
     if (item < before + total) {

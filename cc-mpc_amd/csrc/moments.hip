@@ -333,7 +333,8 @@ void moments_kernel(
     const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off,
     const int32_t *__restrict__ cell_ref, int n_cells, const P *__restrict__ pos, int64_t ld,
     int T, const double *__restrict__ origin, int lg_wq, TreeLayout tree,
-    double *__restrict__ out_mean, double *__restrict__ out_cov, MinkParams mp) {
+    double *__restrict__ out_mean, double *__restrict__ out_cov, MinkParams mp,
+    int64_t whole) {
   using G = Geo<RB>;
   constexpr int NT = n_tiles(RB);
   constexpr int NACC = G::NACC;
@@ -367,7 +368,11 @@ void moments_kernel(
     const int g = lane >> 4;
     const int64_t cnt = loc.cnt;
     const double pre = MINK ? prefetch_tail(mp, loc, rows) : 0.0;
-    const WaveRange wr = wave_range<BAL>(a, b, w, G::NW, int64_t(1) << lg_wq, 4 * W * S);
+    // a whole-cell item longer than a chunk deals its load groups round-robin, as balanced
+    // items do, so every wave streams ~1/NW of the cell
+    const bool rr = BAL || (b - a > (int64_t(1) << lg_chunk));
+    const WaveRange wr = rr ? wave_range<true>(a, b, w, G::NW, int64_t(1) << lg_wq, 4 * W * S)
+                            : wave_range<false>(a, b, w, G::NW, int64_t(1) << lg_wq, 4 * W * S);
     const int64_t p1 = wr.p1;
 
     double sh[RB];
@@ -456,12 +461,13 @@ void moments_kernel(
   }
   ItemLoc loc;
   if (!locate_item(blockIdx.x, cell_cnt, cell_off, n_cells, lg_chunk, loc,
-                   cell_ref))
+                   cell_ref, whole))
     return;  // uniform
   PROBE_TS(1);
+  const int32_t nit = items_of(loc.cnt, lg_chunk, whole);
   const int64_t i0 = static_cast<int64_t>(loc.chunk_idx) << lg_chunk;
-  const int64_t i1 = min(i0 + (int64_t(1) << lg_chunk), loc.cnt);
-  item(loc, items_of(loc.cnt, lg_chunk), i0, i1);
+  const int64_t i1 = nit == 1 ? loc.cnt : min(i0 + (int64_t(1) << lg_chunk), loc.cnt);
+  item(loc, nit, i0, i1);
 }
 
 // ---- Scheme4: f64 4x4x4_4b MFMA over 4-row blocks (T <= 12) -------------------------------
@@ -803,6 +809,21 @@ __global__ __launch_bounds__(RootGeo<RB>::THREADS) void root_finalize_kernel(
   }
 }
 
+// Whole-cell items (T <= 8, tiny inputs): a cell of up to CCMPC_WHOLE_CELL_MAX particles is
+// one workgroup's item, combined in LDS -- no slab, arrival or root gather.  One CU's f64 matrix
+// pipes then do the whole cell's Gram (16 x 16 tile per 4 particles, ~1.8 ns per particle), so
+// this pays only for small cells (profiles/r05/ab_whole_cell_cap.log, C2 / C3 cycle, us):
+//   cap      0      1024   1536   2048   3072   4096
+//   C2       11.3   11.4   12.8   13.9   17.6   19.1     (its 5000-particle cell sets the path)
+//   C3 1e3   10.5    9.7    9.8    9.7    9.7    9.7
+// Build knob (0 = off).
+#ifndef CCMPC_WHOLE_CELL_MAX
+#define CCMPC_WHOLE_CELL_MAX 1024
+#endif
+inline int64_t whole_cell_max(int rb, int64_t n_bound) {
+  return (rb == 1 && n_bound <= (int64_t(1) << CCMPC_LG_TINY_INPUT)) ? CCMPC_WHOLE_CELL_MAX : 0;
+}
+
 template <typename P, int RB, bool MINK>
 static int launch(const P *pos, int64_t ld, int T, const double *origin, const int64_t *off,
                   const int64_t *cnt, int n_cells, int64_t n_bound, void *ws, size_t ws_bytes,
@@ -818,7 +839,7 @@ static int launch(const P *pos, int64_t ld, int T, const double *origin, const i
       return CCMPC_ERR_WORKSPACE;
     hipLaunchKernelGGL((moments_kernel<P, RB, MINK, true>), dim3(static_cast<unsigned>(grid)),
                        dim3(threads), 0, s, cnt, off, MINK ? mp.cell_ref : nullptr, n_cells, pos, ld,
-                       T, origin, lg_wq, tree, mean, cov, mp);
+                       T, origin, lg_wq, tree, mean, cov, mp, int64_t(0));
     if (defer_root(RB, MINK, true))
       hipLaunchKernelGGL((root_finalize_kernel<P, RB>),
                          dim3(static_cast<unsigned>(n_cells * n_tiles(RB))), dim3(RootGeo<RB>::THREADS), 0,
@@ -829,7 +850,7 @@ static int launch(const P *pos, int64_t ld, int T, const double *origin, const i
   if (!tree_layout(ws, ws_bytes, items, n_cells, slab_doubles(RB), tree)) return CCMPC_ERR_WORKSPACE;
   hipLaunchKernelGGL((moments_kernel<P, RB, MINK, false>), dim3(static_cast<unsigned>(items)),
                      dim3(threads), 0, s, cnt, off, MINK ? mp.cell_ref : nullptr, n_cells, pos, ld, T,
-                     origin, lg_wq, tree, mean, cov, mp);
+                     origin, lg_wq, tree, mean, cov, mp, whole_cell_max(RB, n_bound));
   return CCMPC_OK;
 }
 

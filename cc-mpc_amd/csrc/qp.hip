@@ -104,6 +104,7 @@ __global__ void mpc_ltv_kernel(const double *__restrict__ x_init, int64_t S, int
 struct QpArgs {
   int64_t S;
   int T, Tf, n_ref, u_order, rec_kind, max_iter, rows_in_lds, polish;
+  int rec_compact;    // records are ccmpc_gather_rec (32 bytes), rec_kind their source kind
   int early_discard;  // test hook: attempt the early polish, never keep its answer
   int64_t max_cells;
   double tol, early;  // early: the early polish threshold on mu / max(mu0, 1) (0 = none)
@@ -658,19 +659,24 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   for (int64_t r = tid; r < R; r += NTH) {
     const int64_t cell = r / P;
     const int pp = static_cast<int>(r - cell * P);
-    const unsigned char *rec = A.rec + (c0 * P + r) * 128;
+    const unsigned char *rec = A.rec + (c0 * P + r) * (A.rec_compact ? 32 : 128);
     const double n0 = *reinterpret_cast<const double *>(rec);
     const double n1 = *reinterpret_cast<const double *>(rec + 8);
-    const double d = *reinterpret_cast<const double *>(
-        rec + (A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? 16 : 32));
-    const int side = *reinterpret_cast<const int32_t *>(rec + 116);
-    const int status = *reinterpret_cast<const int32_t *>(rec + 120);
-    int t;
-    if (A.rec_kind == CCMPC_REC_KIND_HALFSPACE) {
-      t = *reinterpret_cast<const int32_t *>(rec + 124) >> 16;
+    double d;
+    int side, status, tt;
+    if (A.rec_compact) {  // ccmpc_gather_rec: the same fields, packed
+      d = *reinterpret_cast<const double *>(rec + 16);
+      side = *reinterpret_cast<const int16_t *>(rec + 24);
+      status = *reinterpret_cast<const int16_t *>(rec + 26);
+      tt = *reinterpret_cast<const int32_t *>(rec + 28);
     } else {
-      t = *reinterpret_cast<const int32_t *>(rec + 124);
+      d = *reinterpret_cast<const double *>(
+          rec + (A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? 16 : 32));
+      side = *reinterpret_cast<const int32_t *>(rec + 116);
+      status = *reinterpret_cast<const int32_t *>(rec + 120);
+      tt = *reinterpret_cast<const int32_t *>(rec + 124);
     }
+    const int t = A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? tt >> 16 : tt;
     (void)pp;
     const bool ok = status == 0 && isfinite(n0) && isfinite(n1) && isfinite(d) && t >= 0 &&
                     t < T && (side == 1 || side == -1);
@@ -1682,7 +1688,7 @@ extern "C" int ccmpc_mpc_ltv(const double *x_init, int64_t n_scenes, int64_t T, 
 extern "C" size_t ccmpc_mpc_qp_workspace_bytes(int64_t n_scenes, int64_t T,
                                                int64_t max_cells_per_scene, int rec_kind) {
   if (T < 1 || T > kQpMaxT || n_scenes < 0 || max_cells_per_scene < 0) return 0;
-  const int64_t R = max_cells_per_scene * qp_rows_per_cell(static_cast<int>(T), rec_kind);
+  const int64_t R = max_cells_per_scene * qp_rows_per_cell(static_cast<int>(T), rec_kind & 1);
   if (qp_plan(static_cast<int>(T), R).rows_lds) return 16;  // rows live in LDS
   const int64_t m = 4 * T + 2 * T + R;
   return static_cast<size_t>(n_scenes * kQpRowDoubles * m) * sizeof(double) + 16;
@@ -1705,7 +1711,7 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   CCMPC_REQUIRE(out_u && out_x && out_cost && out_status && out_iter, "null pointer");
   CCMPC_REQUIRE(T_full == T || u_prev, "u_prev is required when T < T_full");
   CCMPC_REQUIRE(n_ref >= 1, "n_ref must be >= 1");
-  CCMPC_REQUIRE(rec_kind == CCMPC_REC_KIND_HALFSPACE || rec_kind == CCMPC_REC_KIND_AFFINE,
+  CCMPC_REQUIRE(rec_kind >= CCMPC_REC_KIND_HALFSPACE && rec_kind <= CCMPC_REC_KIND_AFFINE_COMPACT,
                 "bad rec_kind");
   CCMPC_REQUIRE(u_order == CCMPC_U_ORDER_F || u_order == CCMPC_U_ORDER_C, "bad u_order");
   CCMPC_REQUIRE(max_cells_per_scene >= 0, "bad max_cells_per_scene");
@@ -1717,7 +1723,7 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
     return CCMPC_ERR_WORKSPACE;
   }
   const int Ti = static_cast<int>(T);
-  const int64_t R = max_cells_per_scene * qp_rows_per_cell(Ti, rec_kind);
+  const int64_t R = max_cells_per_scene * qp_rows_per_cell(Ti, rec_kind & 1);
   const QpPlan plan = qp_plan(Ti, R);
   const bool in_lds = plan.rows_lds;
   CCMPC_REQUIRE(in_lds || workspace, "null workspace");
@@ -1727,7 +1733,8 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   a.Tf = static_cast<int>(T_full);
   a.n_ref = static_cast<int>(n_ref);
   a.u_order = u_order;
-  a.rec_kind = rec_kind;
+  a.rec_kind = rec_kind & 1;  // the source kind: halfspace (0 / 2) or affine (1 / 3)
+  a.rec_compact = rec_kind >= CCMPC_REC_KIND_HALFSPACE_COMPACT;
   a.max_iter = max_iter;
   a.rows_in_lds = in_lds;
   a.polish = plan.polish;

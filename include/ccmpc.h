@@ -93,6 +93,21 @@ typedef struct ccmpc_affine_rec {
   int32_t which, side, status, t;
 } ccmpc_affine_rec;
 
+/* The fields of a record the QP reads, 32 bytes: what the multi-GPU exchange moves instead of
+ * the 128-byte record (the one collective is a record all-gather; no reference
+ * counterpart -- the reference solves one scene per process).  rhs = the halfspace record's d
+ * or the affine record's rhs; t_tau = the source record's last field. */
+typedef struct ccmpc_gather_rec {
+  double n0, n1, rhs;
+  int16_t side, status;
+  int32_t t_tau;
+} ccmpc_gather_rec;
+
+/* Pack n_rec records of kind CCMPC_REC_KIND_HALFSPACE / _AFFINE into ccmpc_gather_rec
+ * (device pointers; one launch, 128 B read + 32 B written per record). */
+int ccmpc_compact_records(const void *rec, int rec_kind, int64_t n_rec, ccmpc_gather_rec *out,
+                          ccmpc_stream_t stream);
+
 int ccmpc_abi_version(void);
 const char *ccmpc_last_error(void);
 const char *ccmpc_status_string(int status);
@@ -446,6 +461,10 @@ int ccmpc_l4_split(const void *positions, int dtype, int64_t ld, int64_t T, cons
 #define CCMPC_U_ORDER_C 1
 #define CCMPC_REC_KIND_HALFSPACE 0 /* ccmpc_halfspace records [cells][T(T-1)/2] */
 #define CCMPC_REC_KIND_AFFINE 1    /* ccmpc_affine_rec records [cells][T] */
+/* the same records packed as ccmpc_gather_rec (ccmpc_compact_records): what the multi-GPU
+ * record exchange moves, and what the QP can read in place after it */
+#define CCMPC_REC_KIND_HALFSPACE_COMPACT 2
+#define CCMPC_REC_KIND_AFFINE_COMPACT 3
 
 /* QP status per scene */
 #define CCMPC_QP_OK 0
@@ -476,7 +495,9 @@ size_t ccmpc_mpc_qp_workspace_bytes(int64_t n_scenes, int64_t T, int64_t max_cel
  *  gamma[s][4 T_full][2 T_full], xbar[s][4 T_full]  (the full-horizon model of the first step)
  *  ubar[s][2 T_full] or NULL (= 0, u_init = 0);  u_prev[s][2 T_prev] or NULL when T_prev = 0
  *  goal[s][2];  ref[s][n_ref][2] (step t uses ref[min(t, n_ref - 1)], :2492-2501)
- *  rec: records of every scene's cells, scene s owning cells [scene_cell[s], scene_cell[s+1])
+ *  rec: records of every scene's cells, scene s owning cells [scene_cell[s], scene_cell[s+1]),
+ *       128-byte records (rec_kind CCMPC_REC_KIND_HALFSPACE / _AFFINE) or their 32-byte
+ *       ccmpc_gather_rec packing (_HALFSPACE_COMPACT / _AFFINE_COMPACT): the same solve
  *  params: HOST pointer.
  *  out_u[s][2T] (the cvxpy variable u), out_x[s][T][4], out_cost[s], out_status[s],
  *  out_iter[s] (IPM iterations). */

@@ -69,6 +69,22 @@ def _scene_records(scene, T=6):
     return torch.from_numpy(recs.view(np.uint8).reshape(len(recs), P, 128).copy())
 
 
+GATHER_DTYPE = np.dtype([("n0", "<f8"), ("n1", "<f8"), ("rhs", "<f8"), ("side", "<i2"),
+                         ("status", "<i2"), ("t_tau", "<i4")])      # ccmpc_gather_rec
+
+
+def _pack32(block):
+    """The 32-byte ccmpc_gather_rec packing of a half-space block, restated in numpy: what
+    ccmpc_compact_records writes on the GPU (tests/test_gpu_mpc.py checks the kernel against
+    the records' own fields); here only the gather of packed blocks is under test."""
+    h = block.numpy().reshape(-1, 128).view(_lib.HALFSPACE_DTYPE).reshape(-1)
+    out = np.zeros(h.shape, GATHER_DTYPE)
+    for f in ("n0", "n1", "side", "status", "t_tau"):
+        out[f] = h[f]
+    out["rhs"] = h["d"]
+    return torch.from_numpy(out.view(np.uint8).reshape(block.shape[0], block.shape[1], 32).copy())
+
+
 def _worker(rank, world, port, n_scenes, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -78,8 +94,10 @@ def _worker(rank, world, port, n_scenes, out_dir):
         P = local[0].shape[1] if local else 15
         block = torch.cat(local) if local else torch.zeros((0, P, 128), dtype=torch.uint8)
         full = cdist.gather_records(block)
+        compact = cdist.gather_records(_pack32(block))      # the 32-byte exchange
         if rank == 0:
             torch.save(full, os.path.join(out_dir, "gathered.pt"))
+            torch.save(compact, os.path.join(out_dir, "gathered32.pt"))
     finally:
         dist.destroy_process_group()
 
@@ -103,3 +121,8 @@ def test_gather_records_world2_equals_single_rank(tmp_path, n_scenes):
     assert torch.equal(got, want)
     recs = got.numpy().view(_lib.HALFSPACE_DTYPE).reshape(got.shape[:2])
     assert np.all(np.isfinite(recs["d"]))
+    got32 = torch.load(os.path.join(tmp_path, "gathered32.pt"), weights_only=True)
+    assert got32.shape == want.shape[:2] + (32,)
+    assert torch.equal(got32, _pack32(want))           # a quarter of the bytes, the same fields
+    with pytest.raises(ValueError):
+        cdist.gather_records(torch.zeros((1, 3, 64), dtype=torch.uint8))

@@ -393,3 +393,42 @@ def test_qp_at_the_longest_horizon(gpu):
         assert prim <= 1e-8 and stat <= 1e-5 and comp <= 1e-6, (prim, stat, comp)
         n_ok += 1
     assert n_ok >= 1
+
+
+@pytest.mark.parametrize("kind", ["halfspace", "affine"])
+def test_qp_on_compact_records_equals_the_full_records(gpu, kind):
+    """The multi-GPU exchange moves ccmpc_gather_rec (32 bytes: n, rhs, side, status, t_tau)
+    instead of the 128-byte records: the packed fields equal the records' own, and the QP solved
+    in place on the packed block (REC_*_COMPACT) gives the same bytes as on the full records."""
+    from ccmpc import _lib, dist as cdist
+    T = 8
+    seeds = _feasible(4) + _infeasible(1)
+    rec, cps, o_recs, refs, goals, x0s = _scene_inputs(seeds, T, gpu, kind=kind)
+    k_full = mpc.REC_HALFSPACE if kind == "halfspace" else mpc.REC_AFFINE
+    k_comp = mpc.REC_HALFSPACE_COMPACT if kind == "halfspace" else mpc.REC_AFFINE_COMPACT
+    # poison one record's status: the flag must travel too
+    flat = rec.view(-1, 128)
+    flat[3, 120:124] = torch.tensor([-11], dtype=torch.int32).view(torch.uint8).to(gpu)
+    crec = cdist.compact_records(rec, k_full)
+    assert crec.shape == rec.shape[:2] + (32,)
+    full = rec.cpu().numpy().reshape(-1, 128).view(
+        _lib.HALFSPACE_DTYPE if kind == "halfspace" else _lib.AFFINE_DTYPE).reshape(-1)
+    comp = crec.cpu().numpy().reshape(-1, 32).view(np.dtype(
+        [("n0", "<f8"), ("n1", "<f8"), ("rhs", "<f8"), ("side", "<i2"), ("status", "<i2"),
+         ("t_tau", "<i4")])).reshape(-1)
+    assert np.array_equal(comp["n0"], full["n0"]) and np.array_equal(comp["n1"], full["n1"])
+    assert np.array_equal(comp["rhs"], full["d"] if kind == "halfspace" else full["rhs"])
+    assert np.array_equal(comp["side"], full["side"])
+    assert np.array_equal(comp["status"], full["status"]) and comp["status"][3] == -11
+    assert np.array_equal(comp["t_tau"], full["t_tau"] if kind == "halfspace" else full["t"])
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    g_t, r_t = torch.as_tensor(goals, device=gpu), torch.as_tensor(refs, device=gpu)
+    a = [x.cpu().numpy() for x in mpc.PlanningQP(cps, T, kind=k_full).solve(
+        gamma, xbar, g_t, r_t, rec)]
+    b = [x.cpu().numpy() for x in mpc.PlanningQP(cps, T, kind=k_comp).solve(
+        gamma, xbar, g_t, r_t, crec)]
+    for x, y in zip(a, b):
+        assert x.tobytes() == y.tobytes()
+    assert (a[3] & mpc.QP_SKIPPED_ROWS).any()
+    with pytest.raises(ValueError):                  # a full block under a compact kind
+        mpc.PlanningQP(cps, T, kind=k_comp).solve(gamma, xbar, g_t, r_t, rec)

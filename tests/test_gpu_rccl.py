@@ -1,8 +1,8 @@
 """The RCCL branch of the path's one exchange, on one card: a world-size-1 `nccl` process group
 (RCCL; device_id = cuda:0) runs dist.record_counts / gather_records on device tensors, then
-bench.c4_sharded with the record all-gather inside its step -- the code the 8-GPU scaling run
-executes (bench.py c4_sharded, init_dist).  The gathered block must equal the rank's own
-records bit for bit."""
+bench.c4_sharded with the compact record all-gather inside its step -- the code the 8-GPU
+scaling run executes (bench.py c4_sharded, init_dist).  The gathered block must equal the rank's
+own records (128-byte, or packed to 32 bytes by ccmpc_compact_records) bit for bit."""
 import os
 import socket
 
@@ -32,13 +32,16 @@ def _worker(rank, port, out_dir):
         assert dist.get_backend() == "nccl"
         counts = cdist.record_counts(rec0.shape[0], dev)              # device tensors
         got = cdist.gather_records(rec0, counts=counts)
+        got_c = cdist.gather_records(rec0, counts=counts, compact=True)
         torch.cuda.synchronize(dev)
         same_direct = bool(torch.equal(got.cpu(), rec0.cpu()))
+        c0 = cdist.compact_records(rec0)
+        same_compact = bool(torch.equal(got_c.cpu(), c0.cpu())) and got_c.shape[2] == 32
         out1, rec1 = bench.c4_sharded(dev, 99, 1, 0, steps=3, warmup=1, cfg=CFG,
                                       return_records=True)
         torch.cuda.synchronize(dev)
-        res = {"counts": counts, "same_direct": same_direct,
-               "same_step": bool(torch.equal(rec1.cpu(), rec0.cpu())),
+        res = {"counts": counts, "same_direct": same_direct, "same_compact": same_compact,
+               "same_step": bool(torch.equal(rec1.cpu(), c0.cpu())),
                "gather": out1["record_gather"], "gather0": out0["record_gather"],
                "device": str(rec1.device), "records_ok": out1["records_ok"]}
         with open(os.path.join(out_dir, "rccl.json"), "w") as f:
@@ -60,7 +63,7 @@ def test_rccl_world1_record_gather(gpu, tmp_path):
                        start_method="spawn")
     res = json.load(open(os.path.join(tmp_path, "rccl.json")))
     assert res["counts"] == [res["counts"][0]] and res["counts"][0] > 0
-    assert res["same_direct"] and res["same_step"], res
+    assert res["same_direct"] and res["same_compact"] and res["same_step"], res
     assert res["gather0"] == "none (N=1)"
     assert res["gather"].startswith("RCCL"), res
     assert res["device"].startswith("cuda") and res["records_ok"]
