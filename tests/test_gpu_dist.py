@@ -90,7 +90,8 @@ def _bench_worker(rank, world, port, out_dir):
 
 def test_bench_c4_shard_path_gathers_every_scene(gpu, tmp_path):
     """bench.py's c4_sharded (what the driver's SCALE run times at N > 1) on two gloo ranks:
-    the records gathered inside the timed step are the single-rank batch's, bit for bit."""
+    the records gathered inside the timed step are the single-rank batch's (packed to 32 bytes
+    by ccmpc_compact_records), bit for bit."""
     import sys
     import torch.multiprocessing as mp
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -101,4 +102,6 @@ def test_bench_c4_shard_path_gathers_every_scene(gpu, tmp_path):
     got = torch.load(os.path.join(tmp_path, "bench_gathered.pt"), weights_only=True)
     _, want = bench.c4_sharded(gpu, 77, 1, 0, steps=1, warmup=1, cfg=BENCH_CFG,
                                return_records=True)
-    assert torch.equal(got, want.cpu())
+    from ccmpc import dist as cdist
+    assert got.shape[2] == 32           # the step gathers the compact (32-byte) records
+    assert torch.equal(got, cdist.compact_records(want).cpu())
