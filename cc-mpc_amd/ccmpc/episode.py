@@ -16,8 +16,9 @@ fused launch, then the host HalfSpace objects -> the QP on the device records,
 do_highlevel_control :2850-3110).  The ego is not
 simulated: each step plans from a synthetic state on the reference trajectory, and the
 shrinking steps pass the first control of every earlier step as the executed controls
-(U_prev, :3186).  An infeasible QP is logged (the reference raises InSimulationException and
-the episode ends; the replay continues with a zero control for that step).
+(U_prev, :3186).  The ego's lane (EGO_Y) keeps every QP of the default scene feasible; an
+infeasible QP is logged (the reference raises InSimulationException and the episode ends; the
+replay continues with a zero control for that step).
 """
 import time
 
@@ -69,9 +70,14 @@ class EpisodeReplay:
         self.agent = planner.MidlevelAgent(prediction_horizon=ph, n_ideal=n_ideal, seed=seed,
                                            device=self.device)
 
+    # the ego's lane: 22 m north of where the OV's particle cloud crosses it, so the first
+    # planning step's QP is feasible (the oracle's QP on the oracle's records: y = -72 and -60
+    # are infeasible, -55 and -50 feasible) and the schedule is one the reference could run
+    EGO_Y = -50.0
+
     def ref_traj(self, frame):
         """Ego reference over the horizon, placed so ref_y != mean_y."""
-        ego = np.array([165.0 + 0.2 * frame, -72.0])
+        ego = np.array([165.0 + 0.2 * frame, self.EGO_Y])
         return np.array([ego + [4.0 * (t + 1), 0.5 * (t + 1)] for t in range(self.ph)])
 
     def predict(self, frame):

@@ -340,3 +340,128 @@ def solve_step(Gamma_full, xbar_full, T, T_full, goal, ref_traj, records, kind, 
     return dict(feasible=True, u=u, X=X,
                 cost=objective_value(u, Gf, c, T, goal, ref_traj, p, order=order),
                 H=H, f=f, k=k, G=G, h=h, lam=lam, active=active, Gf=Gf, c=c)
+
+
+# ----------------------------------------------------------------------------------------
+# v8's MILP planner (midlevel/v8/__init__.py): the big-M obstacle disjunction over the L4
+# faces (:692-724) and compute_objective (:727-753), road boundaries off (S_big = 0; the
+# reference's own `np.zeros(T, L, dtype=float)` there raises, ccmpc/milp.py), solved exactly
+# by branch and bound over the face choice per (cell, t) -- the problem CPLEX solves at
+# :769-838 (CPLEX itself is absent; parity with its output is unpinned).
+# ----------------------------------------------------------------------------------------
+# v8/__init__.py:73-109 (__make_global_params)
+V8_PARAMS = dict(w_final=3.0, w_ch_accel=0.5, w_ch_turning=2.0, w_ch_joint=0.1, w_accel=0.5,
+                 w_turning=1.0, w_joint=0.2, min_a=-7.0, max_a=3.5, max_v=10.0,
+                 max_delta=0.5 * math.radians(70.0))
+
+
+def v8_compute_objective(X, U, goal, p=V8_PARAMS):
+    """v8/__init__.py:727-753 as written (util.pairwise = consecutive pairs), numeric."""
+    cost = p["w_final"] * (X[-1, 0] - goal[0]) ** 2 + p["w_final"] * (X[-1, 1] - goal[1]) ** 2
+    for u1, u2 in zip(U[:-1, 0], U[1:, 0]):
+        cost += p["w_ch_accel"] * (u1 - u2) * (u1 - u2)
+    for u1, u2 in zip(U[:-1, 1], U[1:, 1]):
+        cost += p["w_ch_turning"] * (u1 - u2) * (u1 - u2)
+    for u1, u2 in zip(U[:-1], U[1:]):
+        d = u1 - u2
+        cost += p["w_ch_joint"] * d[0] * d[1]
+    cost += p["w_accel"] * np.sum(U[:, 0] ** 2)
+    cost += p["w_turning"] * np.sum(U[:, 1] ** 2)
+    cost += 2.0 * p["w_joint"] * np.sum(U[:, 0] * U[:, 1])
+    return float(cost)
+
+
+def v8_qp_params(p=V8_PARAMS):
+    """v8's objective in assemble_qp's form: no reference term (w_ref = 0), R1 as v8ideal's,
+    and R2's off-diagonal w_ch_joint / 2 (v8 adds w_ch_joint du_0 du_1 once, a quadratic form
+    counts the off-diagonal twice).  U = u.reshape(T, nu) of an object array: row-major."""
+    q = dict(p)
+    q.update(w_ref=0.0, w_ch_joint=0.5 * p["w_ch_joint"])
+    return q
+
+
+def _face_rows(fixed, A, rhs):
+    """Rows (t, a, b) in obstacle_rows' `a . x_t <= b` form of the fixed faces: the face
+    a_l . x_t >= rhs_l becomes (-a_l) . x_t <= -rhs_l."""
+    return [(t, -A[c, t, l], -rhs[c, t, l]) for (c, t), l in sorted(fixed.items())]
+
+
+def disjunction_slack(A, rhs, X):
+    """(C, T): min over faces of rhs_l - a_l . x_t -- > 0 where the ego position lies inside
+    every face (the disjunction violated), <= 0 where some face holds."""
+    xy = np.asarray(X)[:, :2]
+    return np.min(rhs - np.einsum("ctlj,tj->ctl", A, xy[:A.shape[1]]), axis=-1)
+
+
+def _node_qp(Gf, c, T, goal, A, rhs, fixed, p, order):
+    H, f, k, G, h = assemble_qp(Gf, c, T, goal, np.asarray(goal).reshape(1, 2),
+                                _face_rows(fixed, A, rhs), p, order=order)
+    if not is_feasible(G, h):
+        return None
+    u, lam, _ = solve_qp(H, f, G, h)
+    return dict(u=u, cost=float(0.5 * u @ H @ u + f @ u + k), X=(Gf @ u + c).reshape(T, 4))
+
+
+def milp_bnb(Gamma_full, xbar_full, T, goal, A, rhs, p=None, order="C", tol=1e-7,
+             max_nodes=20000):
+    """The v8 MILP's exact optimum by best-first branch and bound: a node fixes one face per
+    branched (cell, t); its relaxation is the convex QP with those face rows only (the big-M
+    rows of the unfixed binaries are vacuous at M_big = 1e4); a node whose optimum satisfies
+    every disjunction is feasible for the MILP (Delta = its satisfied faces); else the most
+    violated (cell, t) is branched into its L faces.  Returns dict(u, X, cost, faces (C, T),
+    nodes) or None (infeasible)."""
+    import heapq
+    p = v8_qp_params() if p is None else p
+    Gf, c = state_map(Gamma_full, xbar_full, T, T)
+    A, rhs = np.asarray(A, float)[:, :T], np.asarray(rhs, float)[:, :T]
+    best, nodes, heap, seq = None, 0, [], 0
+    root = _node_qp(Gf, c, T, goal, A, rhs, {}, p, order)
+    if root is None:
+        return None
+    heapq.heappush(heap, (root["cost"], seq, {}, root))
+    while heap:
+        bound, _, fixed, sol = heapq.heappop(heap)
+        nodes += 1
+        if nodes > max_nodes:
+            raise RuntimeError("milp_bnb: node limit")
+        if best is not None and bound >= best["cost"] - 1e-12 * (1 + abs(best["cost"])):
+            continue
+        slack = disjunction_slack(A, rhs, sol["X"])
+        scale = tol * (1.0 + np.abs(rhs).max(-1))
+        viol = slack - scale
+        if viol.max() <= 0:
+            faces = np.argmin(rhs - np.einsum("ctlj,tj->ctl", A, sol["X"][:, :2]), axis=-1)
+            for (cc, t), l in fixed.items():
+                faces[cc, t] = l
+            best = dict(sol, faces=faces)
+            continue
+        cc, t = np.unravel_index(int(np.argmax(viol)), viol.shape)
+        for l in range(A.shape[2]):
+            child = dict(fixed)
+            child[(int(cc), int(t))] = l
+            s = _node_qp(Gf, c, T, goal, A, rhs, child, p, order)
+            if s is None:
+                continue
+            seq += 1
+            heapq.heappush(heap, (s["cost"], seq, child, s))
+    if best is not None:
+        best["nodes"] = nodes
+    return best
+
+
+def milp_enumerate(Gamma_full, xbar_full, T, goal, A, rhs, p=None, order="C"):
+    """Every face assignment (L^(C T) convex QPs): the exact optimum for tiny problems, an
+    independent check of milp_bnb.  Returns dict(u, X, cost, faces) or None."""
+    import itertools
+    p = v8_qp_params() if p is None else p
+    Gf, c = state_map(Gamma_full, xbar_full, T, T)
+    A, rhs = np.asarray(A, float)[:, :T], np.asarray(rhs, float)[:, :T]
+    C, L = A.shape[0], A.shape[2]
+    keys = [(cc, t) for cc in range(C) for t in range(T)]
+    best = None
+    for combo in itertools.product(range(L), repeat=len(keys)):
+        fixed = dict(zip(keys, combo))
+        s = _node_qp(Gf, c, T, goal, A, rhs, fixed, p, order)
+        if s is not None and (best is None or s["cost"] < best["cost"]):
+            best = dict(s, faces=np.array(combo).reshape(C, T))
+    return best

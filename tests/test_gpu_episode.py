@@ -148,6 +148,9 @@ def test_episode_timing_log(gpu):
     assert [s["T"] for s in log] == [8, 7, 6, 5, 4, 3, 2, 1, 8, 8]
     assert all(s["ms"] > 0 for s in log)
     assert log[-1]["generator"] == "affine"
+    # the default scene is one the reference could run: every planning step's QP solves
+    # (the old lane started the C1 schedule with an infeasible QP)
+    assert [s["qp"] for s in log] == ["solved"] * len(log)
     # the default step-graph cache holds the whole schedule: a second episode replays the
     # first one's graphs (an LRU smaller than the schedule would recapture on every step)
     first = {id(g) for g in rep.agent._graphs.values()}

@@ -65,3 +65,61 @@ def test_outside_is_the_best_delta_choice():
     face = np.einsum("ctlj,tj->ctl", rows.A, xy) >= rows.rhs
     # delta = 1 exactly on the faces that hold: feasible iff some face holds
     np.testing.assert_array_equal(rows.satisfied(xy, face.astype(float)), rows.outside(xy))
+
+
+def _box_rows(T, centres, half=(2.0, 1.2), diag=1.0):
+    """L4-shaped rows of axis-aligned boxes: A (C, T, 4, 2), rhs = b + diag (C, T, 4); the
+    obstacle is {x : A x <= b}, a face row asks a_l . x_t >= rhs_l (outside face l)."""
+    A = np.tile(np.array([[1.0, 0.0], [0.0, 1.0], [-1.0, 0.0], [0.0, -1.0]]),
+                (len(centres), T, 1, 1))
+    b = np.zeros((len(centres), T, 4))
+    for c, ctr in enumerate(centres):
+        for t in range(T):
+            px, py = ctr(t)
+            b[c, t] = [px + half[0], py + half[1], -px + half[0], -py + half[1]]
+    return A, b + diag
+
+
+def _ego_model(T, x0=(0.0, 0.0, 0.0, 6.0)):
+    from oracle import mpc_oracle as mo
+    xbar, _, G, _, _ = mo.VehicleModel(T, 0.5, 1.85, 3.7).get_optimization_ltv(
+        np.array(x0), np.zeros(2))
+    return xbar, G
+
+
+def test_v8_objective_is_the_qp_with_v8_weights():
+    """v8's compute_objective (v8/__init__.py:727-753) equals the QP's objective under
+    v8_qp_params (w_ref = 0, R2 off-diagonal w_ch_joint / 2, U row-major), and the product's
+    mirror (ccmpc.milp.compute_objective) is the same expression."""
+    from oracle import mpc_oracle as mo
+    T = 6
+    xbar, G = _ego_model(T)
+    Gf, c = mo.state_map(G, xbar, T, T)
+    goal = np.array([30.0, 1.0])
+    H, f, k, _, _ = mo.assemble_qp(Gf, c, T, goal, goal.reshape(1, 2), [], mo.v8_qp_params(),
+                                   order="C")
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        u = rng.normal(0, 0.5, 2 * T)
+        X, U = (Gf @ u + c).reshape(T, 4), u.reshape(T, 2)
+        want = mo.v8_compute_objective(X, U, goal)
+        assert 0.5 * u @ H @ u + f @ u + k == pytest.approx(want, rel=1e-12)
+        assert milp.compute_objective(X, U, goal) == pytest.approx(want, rel=1e-14)
+
+
+def test_oracle_branch_and_bound_is_the_enumerated_optimum():
+    """The oracle's best-first branch and bound returns the optimum of the enumeration over
+    every face assignment (L^(C T) convex QPs), on a box in the ego's path at every step."""
+    from oracle import mpc_oracle as mo
+    T = 4
+    xbar, G = _ego_model(T)
+    A, rhs = _box_rows(T, [lambda t: (8.0 + 1.5 * t, 0.3)])      # slower, just ahead
+    goal = np.array([20.0, 0.0])
+    e = mo.milp_enumerate(G, xbar, T, goal, A, rhs)
+    b = mo.milp_bnb(G, xbar, T, goal, A, rhs)
+    assert e is not None and b is not None
+    np.testing.assert_allclose(b["u"], e["u"], atol=1e-7)
+    assert b["cost"] == pytest.approx(e["cost"], rel=1e-9)
+    assert b["nodes"] < 4 ** T        # the bound prunes
+    slack = mo.disjunction_slack(A, rhs, b["X"])
+    assert np.all(slack <= 1e-6)      # every disjunction holds at the optimum
