@@ -477,14 +477,46 @@ void moments_kernel(
 // the instruction's A[b][i][k] lane i + 4b + 16k, so ONE register per block is both the A
 // and the B operand of every block pair (I, J), as for the 16x16 tiles.  A group is 32
 // particles per wave.
+// Scheme4's per-lane row load is 16 bytes in either store type: 2 doubles, or 4 floats
+// (CCMPC_F32_WIDE4).  A group is then 16 W particles per wave -- 32 (f64) or 64 (f32) -- so a
+// load ring of the same depth keeps the same BYTES in flight for both stores.  With f32 pairs
+// (8 bytes, 32-particle groups) the f32 store had half the bytes in flight and streamed at half
+// the f64 byte rate: the per-GPU C4 batch took as long on half the bytes (r04 verdict).
+#ifndef CCMPC_F32_WIDE4
+#define CCMPC_F32_WIDE4 1
+#endif
+template <typename P>
+struct Row4 {  // double (and float without CCMPC_F32_WIDE4): one 16 / 8-byte pair per row
+  using type = Pair<P>;
+  static constexpr int W = 2;
+  __device__ static void load(const P *p, type &q) { load_pair(p, q); }
+};
+#if CCMPC_F32_WIDE4
+template <>
+struct Row4<float> {
+  using type = Quad<float>;
+  static constexpr int W = 4;
+  __device__ static void load(const float *p, type &q) {
+    if constexpr (CCMPC_NT_PAIR != 0) {
+      const ccmpc_f4v t = __builtin_nontemporal_load(reinterpret_cast<const ccmpc_f4v *>(p));
+      q.v = make_float4(t.x, t.y, t.z, t.w);
+    } else {
+      q.v = *reinterpret_cast<const float4 *>(p);
+    }
+  }
+};
+#endif
+
 template <typename P, int NB>
-__device__ __forceinline__ void load_group4(Pair<P> (&v)[NB], const P *const (&rowp)[NB],
-                                            int64_t gbase, int64_t p1, int m) {
-  const int64_t qlast = (p1 - 1) & ~int64_t(1);
-  const int64_t q = gbase + 2 * m;
+__device__ __forceinline__ void load_group4(typename Row4<P>::type (&v)[NB],
+                                            const P *const (&rowp)[NB], int64_t gbase, int64_t p1,
+                                            int m) {
+  constexpr int W = Row4<P>::W;
+  const int64_t qlast = (p1 - 1) & ~int64_t(W - 1);
+  const int64_t q = gbase + W * m;
   const int64_t qc = q < qlast ? q : qlast;
 #pragma unroll
-  for (int I = 0; I < NB; ++I) load_pair(rowp[I] + qc, v[I]);
+  for (int I = 0; I < NB; ++I) Row4<P>::load(rowp[I] + qc, v[I]);
 }
 
 // Row-contiguous loads (CCMPC_ROWLOAD4): the matrix-core layout puts 4 rows in every 4
@@ -525,21 +557,23 @@ __device__ __forceinline__ Pair<float> bperm_pair(int addr, const Pair<float> &p
 }
 
 template <typename P, int NB>
-__device__ __forceinline__ void mfma_group4(const Pair<P> (&loaded)[NB], const double (&sh)[NB],
-                                            const bool (&live)[NB], int64_t gbase, int64_t p1,
-                                            int m, int paddr, double (&acc)[n_pairs(NB)],
-                                            double (&s1)[NB]) {
-  const int64_t q = gbase + 2 * m;
+__device__ __forceinline__ void mfma_group4(const typename Row4<P>::type (&loaded)[NB],
+                                            const double (&sh)[NB], const bool (&live)[NB],
+                                            int64_t gbase, int64_t p1, int m, int paddr,
+                                            double (&acc)[n_pairs(NB)], double (&s1)[NB]) {
+  constexpr int W = Row4<P>::W;
+  const int64_t q = gbase + W * m;
 #if CCMPC_ROWLOAD4
+  static_assert(W == 2, "CCMPC_ROWLOAD4 is the pair layout");
   Pair<P> raw[NB];
 #pragma unroll
   for (int I = 0; I < NB; ++I) raw[I] = bperm_pair(paddr, loaded[I]);
 #else
-  const Pair<P>(&raw)[NB] = loaded;
+  const typename Row4<P>::type(&raw)[NB] = loaded;
   (void)paddr;
 #endif
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < W; ++j) {
     double v[NB];  // sub-step j: shifted; out-of-range slots and dead rows become 0
 #pragma unroll
     for (int I = 0; I < NB; ++I) {
@@ -600,7 +634,7 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
     const int paddr = 4 * (16 * c + m);        // matrix lane (c, m) <- loading lane 16 c + m
     const int64_t cnt = loc.cnt;
     const double pre = MINK ? prefetch_tail(mp, loc, rows) : 0.0;
-    const WaveRange wr = wave_range<BAL>(a, b, w, kNW4, int64_t(1) << lg_wq, 32);
+    const WaveRange wr = wave_range<BAL>(a, b, w, kNW4, int64_t(1) << lg_wq, 16 * Row4<P>::W);
     const int64_t p1 = wr.p1;
 
     double sh[NB];
@@ -623,7 +657,7 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
 
     const int64_t ngroups = wr.ngroups, st = wr.stride;
     constexpr int DP = BAL ? kDepth4Bal : kDepth4;
-    Pair<P> buf[DP][NB];
+    typename Row4<P>::type buf[DP][NB];
     if (ngroups > 0) {
 #pragma unroll
       for (int d = 0; d < DP - 1; ++d) load_group4<P, NB>(buf[d], rowp, wr.p0 + d * st, p1, ml);

@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = [("C2", 4, 5000, 8, 1), ("C3-1e3", 1, 1000, 8, 1), ("C3-2e4", 1, 20000, 8, 1),
            ("C3-1e5", 1, 100000, 8, 1), ("C4/8", 4, 20000, 12, 8), ("C4/1", 4, 20000, 12, 64),
-           ("C5", 8, 50000, 40, 1)]
+           ("C5", 8, 50000, 40, 1), ("C4/8-f32", 4, 20000, 12, 8), ("C4/1-f32", 4, 20000, 12, 64)]
 
 
 def child(only):
@@ -27,7 +27,8 @@ def child(only):
         if only and name not in only:
             continue
         row = bench.time_config(dev, 20251015, name, O, N, T, scenes,
-                                cold=N * O * scenes * T * 16 >= (8 << 20))
+                                cold=N * O * scenes * T * 16 >= (8 << 20),
+                                f32=name.endswith("-f32"))
         print(json.dumps(row), flush=True)
         torch.cuda.empty_cache()
 
