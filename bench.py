@@ -762,11 +762,7 @@ def time_graph_replay(g, dev, n=200):
     h = torch.cuda.current_stream(dev).cuda_stream
 
     def one(i):
-        gr = g.graphs[i & 1]
-        if g.torch_graph:
-            gr.replay()
-        else:
-            gr.replay(h)
+        g.graphs[i & 1].replay(h)
 
     for i in range(10):
         one(i)
