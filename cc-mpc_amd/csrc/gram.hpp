@@ -488,8 +488,11 @@ __device__ __forceinline__ void decode_entry(int e, int RB, int &i, int &j) {
 
 // Tiles exchanged per round of combine_waves, and the LDS it needs (doubles).  Up to 5 tiles
 // per round: T = 40's 15 tiles in 3 rounds, 80 KB of LDS at 8 waves.
+#ifndef CCMPC_COMBINE_TPR  // build knob: the most tiles a combine round parks
+#define CCMPC_COMBINE_TPR 5
+#endif
 __host__ __device__ constexpr int combine_tiles_per_round(int rb) {
-  return n_tiles(rb) < 5 ? n_tiles(rb) : 5;
+  return n_tiles(rb) < CCMPC_COMBINE_TPR ? n_tiles(rb) : CCMPC_COMBINE_TPR;
 }
 __host__ __device__ constexpr int combine_xch_doubles(int rb, int nw) {
   // the tile rounds' park area, then the row sums' (every lane's, parked with the first round)
