@@ -75,7 +75,20 @@ def main():
         same = a[k].tobytes() == b[k].tobytes()
         bad += not same
         if not same:
-            print(f"DIFF {k}: {np.count_nonzero(a[k] != b[k])} of {a[k].size} elements differ")
+            x, y = a[k], b[k]
+            if k.endswith("/rec"):             # half-space records: decisions exact?  d, Q rel
+                sys.path[:0] = [os.path.join(ROOT, "cc-mpc_amd")]
+                from ccmpc import _lib
+                x = x.reshape(-1, 128).view(_lib.HALFSPACE_DTYPE).reshape(-1)
+                y = y.reshape(-1, 128).view(_lib.HALFSPACE_DTYPE).reshape(-1)
+                dec = all(np.array_equal(x[f], y[f]) for f in ("which", "side", "status"))
+                rel = max(float(np.max(np.abs(x[f] - y[f]) / (np.abs(x[f]) + 1e-300)))
+                          for f in ("d", "q00", "q11", "r00", "r11"))
+                print(f"DIFF {k}: which/side/status identical: {dec}; max rel d/Q/QR {rel:.2e}")
+            else:
+                rel = float(np.max(np.abs(x - y)) / max(np.max(np.abs(x)), 1e-300))
+                print(f"DIFF {k}: {np.count_nonzero(x != y)} of {x.size} elements differ, "
+                      f"max |diff| / max |a| = {rel:.2e}")
     print(f"{len(a.files) - bad} of {len(a.files)} arrays bit-identical")
     sys.exit(1 if bad else 0)
 
