@@ -7,6 +7,8 @@
                                                               the store: every launch from HBM)
 """
 import os
+
+import numpy as np
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,7 +20,7 @@ from ccmpc import cycle, engine, synthetic  # noqa: E402
 
 CONFIGS = {"C2": (4, 5000, 8, 1), "C3": (1, 100000, 8, 1), "C4": (4, 20000, 12, 8),
            "C5": (8, 50000, 40, 1), "C3-1e3": (1, 1000, 8, 1), "C3-2e4": (1, 20000, 8, 1),
-           "C4full": (4, 20000, 12, 64)}
+           "C4full": (4, 20000, 12, 64), "C4-f32": (4, 20000, 12, 8)}
 
 
 def build(name, dev):
@@ -29,7 +31,12 @@ def build(name, dev):
         cells += [c for o in ovs for c in o]
         K += [len(o) for o in ovs]
         refs.append(ref)
-    store = engine.ParticleStore.from_cells(cells, device=dev)
+    if name.endswith("-f32"):            # the sampler's store format: f32 relative to an origin
+        origin = np.tile(np.array([150.0, -120.0]), (len(cells), 1))
+        store = engine.ParticleStore.from_cells(cells, device=dev, dtype=torch.float32,
+                                                origin=origin)
+    else:
+        store = engine.ParticleStore.from_cells(cells, device=dev)
     return store, cycle.MinkowskiCycle(store, K, refs[0])
 
 
