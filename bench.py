@@ -867,11 +867,30 @@ def ellipsoid_parity(ovs, ref, T, h):
             "order_which_side_exact": bool(exact), "records": len(want), "bar": 1e-5}
 
 
+def spin_sync(local):
+    """hipDeviceScheduleSpin on this rank's device, set before torch creates its context: a
+    host thread waiting in hipDeviceSynchronize / hipStreamSynchronize spins instead of
+    yielding, which is what a latency-bound planner (one ~10 us cycle per step) runs with.  The
+    process has one HIP runtime (torch's libamdhip64.so.7, which libccmpc.so binds to by
+    soname).  CCMPC_BENCH_SPIN=0 leaves the default (auto) schedule.  Returns True if set."""
+    if os.environ.get("CCMPC_BENCH_SPIN", "1") != "1":
+        return False
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so.7")
+    except OSError:
+        return False
+    if hip.hipSetDevice(ctypes.c_int(local)) != 0:
+        return False
+    return hip.hipSetDeviceFlags(ctypes.c_uint(1)) == 0   # hipDeviceScheduleSpin
+
+
 def main():
     args = parse()
     rc = launch_ranks(args)
     if rc is not None:
         sys.exit(rc)
+    spun = False if args.launch_check else spin_sync(int(os.environ.get("LOCAL_RANK", "0")))
     world, rank, local = init_dist(args)
     if args.launch_check:
         launch_check(world, rank)
@@ -932,6 +951,7 @@ def main():
                      else ("torchrun" if world > 1 else "single process")),
         "steps": args.steps,
         "warmup": args.warmup,
+        "host_sync": "spin (hipDeviceScheduleSpin)" if spun else "default",
         "ms_per_step": round(1e3 * elapsed / args.steps, 5),
         "higher_is_better": True,
         "scaling": "weak",
