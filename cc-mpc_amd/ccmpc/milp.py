@@ -301,6 +301,8 @@ class BranchAndBound:
                     continue
                 slack = np.min(self.rhs - np.einsum("ctlj,tj->ctl", self.A, Xi[:, :2]), -1)
                 viol = slack - self.tol * (1.0 + np.abs(self.rhs).max(-1))
+                for key in fixed:                          # a fixed face holds (QP rows):
+                    viol[key] = -np.inf                    # never branch on it again
                 if viol.max() <= 0:                        # every disjunction holds
                     faces = np.argmin(self.rhs - np.einsum("ctlj,tj->ctl", self.A, Xi[:, :2]),
                                       axis=-1)

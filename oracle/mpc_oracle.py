@@ -429,6 +429,8 @@ def milp_bnb(Gamma_full, xbar_full, T, goal, A, rhs, p=None, order="C", tol=1e-7
         slack = disjunction_slack(A, rhs, sol["X"])
         scale = tol * (1.0 + np.abs(rhs).max(-1))
         viol = slack - scale
+        for key in fixed:                  # the node's QP enforces its fixed faces
+            viol[key] = -np.inf
         if viol.max() <= 0:
             faces = np.argmin(rhs - np.einsum("ctlj,tj->ctl", A, sol["X"][:, :2]), axis=-1)
             for (cc, t), l in fixed.items():

@@ -283,3 +283,41 @@ def test_kept_mode_without_draws_fails_like_the_reference(gpu):
     with pytest.raises(IndexError):
         agent.predict_and_constrain(episode.Params(O, [2], 0), s, np.full((1, 2), 0.05), PH,
                                     _ref(0), minpos, pasts)
+
+
+@pytest.mark.parametrize("as_tensors", [False, True], ids=["host_arrays", "device_tensors"])
+def test_predictions_source_at_the_reference_particle_count(gpu, as_tensors):
+    """generate_vehicle_latents' 5-tuple at C1's 100 000 particles per OV (with an ego node in
+    row 0, as the reference's batch has it): the step graph built with source='predictions'
+    (ccmpc_load_predictions -> ccmpc_bucket -> cycle) gives the records, moments and
+    per-cell counts of the sampler route's graph on the same particles, frame after frame, and
+    of the shrinking (ideal) and receding (affine) kinds."""
+    from ccmpc import engine, episode, planner
+    O, N = 1, 100_000
+    init, pmf, gmm, minpos, pasts, K, eps_ura = _scene_inputs(O, seed=20251015)
+    a = planner.MidlevelAgent(prediction_horizon=PH, n_ideal=50_000, device=gpu)
+    b = planner.MidlevelAgent(prediction_horizon=PH, n_ideal=50_000, device=gpu)
+    for frame, T, kind in ((0, PH, "minkowski"), (10, PH - 1, "minkowski"), (20, PH, "affine"),
+                           (30, PH, "minkowski")):
+        seed = 700 + frame
+        sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=N, seed=seed)
+        z, store = engine.sample_unicycle(init, pmf, gmm, N, PH, seed=seed, device=gpu)
+        pred = store.pos[:, :N].reshape(PH, 2, N).permute(2, 0, 1)[None]      # (1, N, T, 2)
+        ego = torch.zeros_like(pred)
+        P = torch.cat([ego, pred]).contiguous()
+        Z = torch.cat([torch.zeros_like(z), z]).to(torch.int64).contiguous()
+        if not as_tensors:
+            P, Z = P.cpu().numpy(), Z.cpu().numpy()
+        lp = np.concatenate([pmf[:1], pmf])
+        psrc = dict(source="predictions", predictions=P, z=Z, rows=[1], latent_pmf=lp[1:],
+                    N=N)
+        params = episode.Params(O, K, frame)
+        fn_a = a.predict_and_constrain_affine if kind == "affine" else a.predict_and_constrain
+        fn_b = b.predict_and_constrain_affine if kind == "affine" else b.predict_and_constrain
+        _, out_a = fn_a(params, sampler, eps_ura, T, _ref(frame), minpos, pasts)
+        rec_a = np.array(a.last_records).tobytes()
+        _, out_b = fn_b(params, psrc, eps_ura, T, _ref(frame), minpos, pasts)
+        assert np.array(b.last_records).tobytes() == rec_a, (frame, kind)
+        np.testing.assert_array_equal(np.asarray(out_a[6][0][0]), np.asarray(out_b[6][0][0]))
+    g = [g for k, g in b._graphs.items() if "predictions" in k]
+    assert g and all(x.source == "predictions" and not x.fused for x in g)
