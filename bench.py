@@ -581,6 +581,105 @@ def episode_c1(dev, cpu_steps=2, with_cpu=True, N=5000):
     return out
 
 
+def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8):
+    """The planning step on the reference's own predictor output: generate_vehicle_latents'
+    5-tuple (prediction.py:93-105) -- predictions (nodes, N, ph, 2) float32 and z (nodes, N)
+    int64 as the host numpy arrays the reference returns, the ego's node in row 0 -- through
+    MidlevelAgent.predict_and_constrain with StepGraph(source="predictions"): the arrays go into
+    the pinned input pack, ccmpc_load_predictions -> ccmpc_bucket (make_ovehicles, :469-505)
+    -> the Minkowski cycle -> L4 -> 9-tuple; no sampler.  `n_sets` precomputed frames of
+    particles (the sampler's own draws) are cycled, a different one each step."""
+    from ccmpc import engine, episode, planner
+    init, pmf, gmm = episode.synthetic_gmm(O, T=ph, seed=20251015)
+    minpos = np.array([150.0, -120.0])
+    pasts = [np.array([[minpos[0] + init[o, 0] - 2.0, minpos[1] + init[o, 1]]])
+             for o in range(O)]
+    K = [int(np.count_nonzero(pmf[o] > 0.1)) for o in range(O)]
+    eps = np.full((O, max(K)), 0.05 / O)
+    ego = np.array([165.0, -72.0])
+    ref = np.array([ego + [4.0 * (t + 1), 0.5 * (t + 1)] for t in range(ph)])
+    sets = []
+    for k in range(n_sets):
+        z, store = engine.sample_unicycle(init, pmf, gmm, N, ph, seed=900 + k, device=dev)
+        pos = store.pos.cpu().numpy()
+        pred = np.zeros((O + 1, N, ph, 2), np.float32)
+        for o in range(O):
+            off = store.offsets[o]
+            pred[o + 1] = pos[:, off:off + N].reshape(ph, 2, N).transpose(2, 0, 1)
+        zz = np.zeros((O + 1, N), np.int64)
+        zz[1:] = z.cpu().numpy()
+        sets.append(dict(source="predictions", predictions=pred, z=zz,
+                         rows=list(range(1, O + 1)), latent_pmf=pmf, N=N))
+    agent = planner.MidlevelAgent(prediction_horizon=ph, device=dev)
+    params = episode.Params(O, K, 0)
+
+    def one(i):
+        return agent.predict_and_constrain(params, sets[i % n_sets], eps, ph, ref, minpos,
+                                           pasts)
+    for i in range(20):
+        one(i)
+    ts = []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        _, out = one(i)
+        ts.append(time.perf_counter() - t0)
+    g = next(iter(agent._graphs.values()))
+    return {"config": f"C2 shape drop-in step on generate_vehicle_latents' 5-tuple: {O} OVs (+ the "
+                      f"ego's node) x np={N} x ph={ph}, K={K}; host numpy predictions / z in the "
+                      "pinned pack -> ccmpc_load_predictions -> ccmpc_bucket -> Minkowski cycle "
+                      "-> L4 -> 9-tuple",
+            "steps": steps, "constraints_per_step": len(out[0]),
+            "graph_branch": f"source={g.source}, fused={g.fused}",
+            "input_pack_bytes": int(g.inp.nbytes),
+            "dropin_step_us_median": round(statistics.median(ts) * 1e6, 1),
+            "dropin_step_us_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
+            "graph_replay_us": round(time_graph_replay(g, dev) * 1e6, 1),
+            "record_path_latency_us": round(time_record_path(g, dev) * 1e6, 1)}
+
+
+def v8_milp(dev, with_cpu=True, seeds=range(20, 28), T=8, O=2):
+    """v8's MILP (v8/__init__.py:692-873, road boundaries off) through
+    MidlevelAgentV8.do_highlevel_control: big-M rows over the device L4 faces of crossing OV
+    clouds, the exact branch and bound on the GPU (each round one batched mpc_qp_kernel launch).
+    Beside it the oracle's branch and bound (SciPy QPs) on the same rows, on one host core."""
+    from ccmpc import milp, ovehicle, synthetic
+    from ccmpc.standins import AttrDict
+    rows_ = []
+    for seed in seeds:
+        cells, K, ref, goal, x_init, pasts = synthetic.crossing_scene(seed, O=O, N=600, T=T, K=1,
+                                                                      lateral=6.0)
+        ovs = ovehicle.scene_from_positions([[c] for c in cells],
+                                            [p.reshape(1, 2) for p in pasts], device=dev)
+        agent = milp.MidlevelAgentV8(prediction_horizon=T, control_horizon=T, device=dev)
+        params = AttrDict(x_init=x_init, goal=goal, diag=milp.ego_diag(3.7, 1.79), O=O, K=K)
+        agent.do_highlevel_control(params, ovs)          # warm: allocations
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        out, err = agent.do_highlevel_control(params, ovs)
+        t_gpu = time.perf_counter() - t0
+        r = {"seed": seed, "feasible": err is None, "ms": round(t_gpu * 1e3, 3),
+             "nodes": agent.last_bnb["nodes"], "launches": agent.last_bnb["launches"]}
+        if with_cpu:
+            from oracle import mpc_oracle as mo
+            rows = agent.compute_obstacle_constraints(params, ovs, None, None, None, None)[0]
+            xb, _, G, _, _ = mo.VehicleModel(T, 0.5, 1.85, 3.7).get_optimization_ltv(
+                x_init, np.zeros(2))
+            t0 = time.perf_counter()
+            want = mo.milp_bnb(G, xb, T, goal, rows.A, rows.rhs)
+            r["oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+            r["same_verdict"] = (want is None) == (err is not None)
+            if want is not None and err is None:
+                r["max_du"] = float(np.abs(out.U_star.reshape(-1) - want["u"]).max())
+        rows_.append(r)
+    solved = [r for r in rows_ if r["feasible"]]
+    return {"config": f"v8 MILP: {O} crossing OVs x np=600, T={T}, L4 faces, big-M disjunction "
+                      "(M_big = 1e4), road boundaries off; exact best-first branch and bound, "
+                      "one batched QP launch per round (do_highlevel_control, host clock)",
+            "scenes": rows_,
+            "ms_median_solved": (round(statistics.median(r["ms"] for r in solved), 3)
+                                 if solved else None)}
+
+
 def harness_episode(dev, N=5000, run_interval=12, episodes=3):
     """The reference harness's own driver sequence (tests/Hz20/__init__.py:183-359) through the
     library: MidlevelAgent's reference constructor, then run_step(frame, offline_index, T,
@@ -1024,6 +1123,8 @@ def main():
         with threadpool_limits(limits=1):
             out["dropin_step_c2"] = dropin_step(dev, with_cpu=not args.no_cpu)
             out["dropin_step_c2_pp"] = dropin_step(dev, with_cpu=False, per_particle=True)
+            # the reference's own predictor output (generate_vehicle_latents' 5-tuple)
+            out["dropin_step_c2_predictions"] = dropin_step_predictions(dev)
             # C1's real particle count (tests/Hz20/params.py:377): the graph's non-fused branch
             out["dropin_step_c1_100k"] = dropin_step(
                 dev, steps=100, with_cpu=not args.no_cpu, O=1, N=100_000, eager_steps=20,
@@ -1033,6 +1134,7 @@ def main():
             # the reference's real particle count at the "np5000" label (params.py:377)
             out["episode_c1_np100k"] = episode_c1(dev, with_cpu=False, N=100_000)
             out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
+            out["v8_milp"] = v8_milp(dev, with_cpu=not args.no_cpu)
     if not args.no_sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)
     if rank == 0:
