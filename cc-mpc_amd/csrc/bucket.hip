@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
 #pragma unroll
   for (int r = 0; r < kPartRounds; ++r) {
     const int t = threadIdx.x + r * kBucketBlock, k = t / kCentreSuper, q = t % kCentreSuper;
-    if (k < K) sup_s[k][q] = pv[r];
+    if (k < K) sup_s[k][q] = q < ng ? pv[r] : double2{-0.0, -0.0};  // lds_row_sum's padding
   }
   int32_t csum = 0;
 #pragma unroll
@@ -181,10 +181,7 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
   const __amdgpu_buffer_rsrc_t rc = raw_rsrc(a.ccnt + static_cast<int64_t>(o) * a.nch * a.L);
   if (threadIdx.x < K) {  // S_ch = 0.0 + P_{64 ch} + P_{64 ch + 1} + ... (bucket.hpp)
     double2 acc = {0.0, 0.0};
-    for (int q = 0; q < ng; ++q) {
-      acc.x += sup_s[threadIdx.x][q].x;
-      acc.y += sup_s[threadIdx.x][q].y;
-    }
+    lds_row_sum(acc, sup_s[threadIdx.x], ng);
     st2_sc1(rs, 16 * (ch * a.max_k + threadIdx.x), acc.x, acc.y);
   }
   if (counter) st1_sc1(rc, 4 * (ch * a.L + threadIdx.x), csum);
@@ -214,17 +211,11 @@ __global__ __launch_bounds__(kBucketBlock) void bucket_stats(BucketArgs a) {
 #pragma unroll
     for (int r = 0; r < kPartRounds; ++r) {
       const int t = threadIdx.x + r * kBucketBlock, k = t / kCentreSuper, q = t % kCentreSuper;
-      if (k < K && q < nc) {
-        sup_s[k][q] = sv[r];
-        atomicAdd(&nk_s[k], nv[r]);
-      }
+      if (k < K) sup_s[k][q] = q < nc ? sv[r] : double2{-0.0, -0.0};
+      if (k < K && q < nc) atomicAdd(&nk_s[k], nv[r]);
     }
     __syncthreads();
-    if (threadIdx.x < K)
-      for (int q = 0; q < nc; ++q) {
-        tot.x += sup_s[threadIdx.x][q].x;
-        tot.y += sup_s[threadIdx.x][q].y;
-      }
+    if (threadIdx.x < K) lds_row_sum(tot, sup_s[threadIdx.x], nc);
     __syncthreads();
   }
   if (threadIdx.x < K) {

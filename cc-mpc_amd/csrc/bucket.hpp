@@ -8,7 +8,8 @@ namespace ccmpc {
 constexpr int kMaxBins = 1024;
 constexpr int kMaxKept = 16;
 constexpr int kCentreGroup = 64;  // particles per centre partial (one wave, sample order)
-constexpr int kCentreSuper = 64;  // partials per sequential superblock
+constexpr int kCentreSuper = 64;  // partials per sequential superblock (a multiple of 16)
+static_assert(kCentreSuper % 16 == 0, "superblock_sum / lds_row_sum read rounds of 16");
 
 // Sum of v over the 64 lanes of a wave (xor butterfly 32, 16, ..., 1: every lane ends with the
 // same value, since each step adds the same two operands on both partners).
@@ -25,7 +26,13 @@ __device__ __forceinline__ double group_sum64(double v) {
 //   S_j  = 0.0 + P_{64 j} + P_{64 j + 1} + ... (left to right over the superblock's partials)
 //   sum  = 0.0 + S_0 + S_1 + ...               (left to right)
 //   centre = sum / n_k
-// superblock_sum(j, G, load) evaluates S_j for partials load(g), g < G.
+// superblock_sum(j, G, load) evaluates S_j for partials load(g, true), g < G; load(g, false)
+// must return -0.0 (an LDS sentinel slot: the address is selected, not the value), the exact
+// identity of IEEE addition (x + -0.0 == x for every x, -0.0 included).  So the chain is one add
+// per partial, and all sixteen reads of a round land in registers of their own before the first
+// add (a predicated add put four selects on the dependent path, and a select of the loaded value
+// let the compiler recycle the landing registers, two reads in flight: ~2.3 us of the rare
+// placement at G = 79).
 template <typename Load>
 __device__ __forceinline__ double2 superblock_sum(int j, int G, Load load) {
   const int g0 = j * kCentreSuper, g1 = min(G, g0 + kCentreSuper);
@@ -33,16 +40,31 @@ __device__ __forceinline__ double2 superblock_sum(int j, int G, Load load) {
   for (int g = g0; g < g1; g += 16) {
     double2 v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = load(g + q < g1 ? g + q : g1 - 1);  // all in flight
+    for (int q = 0; q < 16; ++q) v[q] = load(g + q, g + q < g1);
+    __builtin_amdgcn_sched_barrier(0);  // every read issued before the first add waits
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      if (g + q < g1) {
-        acc.x += v[q].x;
-        acc.y += v[q].y;
-      }
+      acc.x += v[q].x;
+      acc.y += v[q].y;
     }
   }
   return acc;
+}
+
+// acc + row[0] + row[1] + ... + row[n - 1], left to right, as the chain of superblock_sum; the
+// row holds kCentreSuper slots, those past n set to -0.0 by the caller.
+__device__ __forceinline__ void lds_row_sum(double2 &acc, const double2 *row, int n) {
+  for (int q0 = 0; q0 < n; q0 += 16) {
+    double2 v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = row[q0 + q];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc.x += v[q].x;
+      acc.y += v[q].y;
+    }
+  }
 }
 
 // Bucket key of a particle (see bucket.hip): kept mode k's own particle -> k (L + 1); a rare

@@ -26,6 +26,7 @@
 //    LDS -- no kernel boundary between moments and constraints.
 #include "constraints.hpp"
 #include <algorithm>
+#include <type_traits>
 
 #include "gram.hpp"
 
@@ -95,6 +96,10 @@ constexpr int kDepth4 = CCMPC_DEPTH4;
 #define CCMPC_DEPTH4_BAL 3  // C4 per-GPU batch 33.9 -> 32.5 us warm, 38.7 -> 37.0 cold (ab14)
 #endif
 constexpr int kDepth4Bal = CCMPC_DEPTH4_BAL;
+#ifndef CCMPC_DEPTH4_BAL_F32  // the same for the f32 store (64-particle groups, CCMPC_F32_WIDE4)
+#define CCMPC_DEPTH4_BAL_F32 CCMPC_DEPTH4_BAL
+#endif
+constexpr int kDepth4BalF32 = CCMPC_DEPTH4_BAL_F32;
 
 // Progress priority (balanced mode): issue is arbitrated by priority, then age
 // (MI355X_MICROARCH.md, two waves per SIMD), so of two co-resident workgroups the older one
@@ -597,13 +602,23 @@ __device__ __forceinline__ void mfma_group4(const typename Row4<P>::type (&loade
   }
 }
 
-constexpr int kNW4 = 4;  // waves per Scheme4 work item
-#ifndef CCMPC_M4_OCC  // Scheme4 workgroups per CU the register budget must allow (build knob)
-#define CCMPC_M4_OCC(NB) ((NB) <= 5 ? 3 : 2)
+#ifndef CCMPC_NW4  // waves per Scheme4 work item (build knob)
+#define CCMPC_NW4 4
 #endif
+constexpr int kNW4 = CCMPC_NW4;
+#ifndef CCMPC_M4_OCC  // Scheme4 workgroups per CU the register budget must allow (build knob)
+#define CCMPC_M4_OCC(NB) (((NB) <= 5 ? 3 : 2) * 4 / kNW4 > 0 ? ((NB) <= 5 ? 3 : 2) * 4 / kNW4 : 1)
+#endif
+#ifndef CCMPC_M4_OCC_F32  // ... for the f32 store (0: as f64)
+#define CCMPC_M4_OCC_F32 0
+#endif
+template <typename P>
+constexpr int m4_occ(int nb) {
+  return std::is_same_v<P, float> && CCMPC_M4_OCC_F32 > 0 ? CCMPC_M4_OCC_F32 : CCMPC_M4_OCC(nb);
+}
 
 template <typename P, int NB, bool MINK, bool BAL>
-__global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
+__global__ __launch_bounds__(kNW4 * 64, m4_occ<P>(NB)) void moments4_kernel(
     const int64_t *__restrict__ cell_cnt, const int64_t *__restrict__ cell_off,
     const int32_t *__restrict__ cell_ref, int n_cells, const P *__restrict__ pos, int64_t ld,
     int T, const double *__restrict__ origin, int lg_wq, TreeLayout tree,
@@ -656,7 +671,7 @@ __global__ __launch_bounds__(kNW4 * 64, CCMPC_M4_OCC(NB)) void moments4_kernel(
     for (int I = 0; I < NB; ++I) s1[I] = 0.0;
 
     const int64_t ngroups = wr.ngroups, st = wr.stride;
-    constexpr int DP = BAL ? kDepth4Bal : kDepth4;
+    constexpr int DP = BAL ? (std::is_same_v<P, float> ? kDepth4BalF32 : kDepth4Bal) : kDepth4;
     typename Row4<P>::type buf[DP][NB];
     if (ngroups > 0) {
 #pragma unroll

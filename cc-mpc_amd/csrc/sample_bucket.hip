@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
 }
 
 __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
-  __shared__ double2 gp_s[kFGroups * kMaxKept];   // the OV's centre partials [g][k]
+  __shared__ double2 gp_s[kFGroups * kMaxKept + 1];  // the OV's centre partials [g][k], -0.0
   __shared__ int hist[kFusedMaxBins];             // rare particles per bin in slots >= r0
   __shared__ int pre[kFusedMaxBins];              // ... in rare-list slots before this block's
   __shared__ int bstart[kFusedMaxBins];           // bin start relative to the region
@@ -288,6 +288,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   const int ng = a.G * K;
   const double2 *gp = reinterpret_cast<const double2 *>(a.gpart) + static_cast<int64_t>(o) * a.G * a.max_k;
   for (int u = tid; u < ng; u += kRThreads) gp_s[u] = gp[(u / K) * a.max_k + u % K];
+  if (tid == 0) gp_s[kFGroups * kMaxKept] = double2{-0.0, -0.0};  // superblock_sum's sentinel
   // the first batch of rare records too: R is not known yet, so the slots are clamped into the
   // list's storage (a launch's first kB * 256 records cover the C2 shape's whole rare list)
   const float4 *info = reinterpret_cast<const float4 *>(a.rinfo) + static_cast<int64_t>(o) * npad;
@@ -317,8 +318,12 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   if (tid < K) {
     const int k = tid;
     double2 tot = {0.0, 0.0};
+#if defined(CCMPC_PROBE) && (CCMPC_PROBE & 128)  // timing probe: the centre sums left out
+    if (a.G < 0)
+#endif
     for (int j = 0; j * kCentreSuper < a.G; ++j) {
-      const double2 s = superblock_sum(j, a.G, [&](int g) { return gp_s[g * K + k]; });
+      const double2 s = superblock_sum(
+          j, a.G, [&](int g, bool in) { return gp_s[in ? g * K + k : kFGroups * kMaxKept]; });
       tot.x += s.x;
       tot.y += s.y;
     }
