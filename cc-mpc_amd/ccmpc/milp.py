@@ -142,32 +142,38 @@ class MidlevelAgentV8(planner.MidlevelAgent):
         return compute_objective(X, U, goal)
 
     def do_highlevel_control(self, params, ovehicles):
-        """v8/__init__.py:755-873 with road boundaries off: the obstacle big-M rows over the
-        device L4 faces, compute_objective, and the MILP solved by BranchAndBound on the GPU
-        (CPLEX's role).  params: x_init [x, y, psi, v] (make_local_params' state; the LTV model
-        is built about u = 0 on the device) and goal (2,) (compute_segs_polytopes_and_goal's,
-        whose map reader is outside the path); diag as compute_obstacle_constraints reads it.
-        Returns (AttrDict(cost, U_star, X_star, goal, A_union, b_union, vertices, segments=None),
-        None), or with cost / U_star / X_star None and an InSimulationException where the
-        reference's solve fails (:862-873)."""
+        """v8/__init__.py:755-873: the obstacle big-M rows over the device L4 faces,
+        compute_objective, and the MILP solved by BranchAndBound on the GPU (CPLEX's role).
+        params: x_init [x, y, psi, v] (make_local_params' state; the LTV model is built about
+        u = 0 on the device), goal (2,) and, with road_boundary_constraints, segments -- the
+        map reader's compute_segs_polytopes_and_goal payload (polytopes [(A, b)], mask;
+        road.py:639-678), whose Omicron binaries the same branch and bound takes one polytope
+        per step (:676-702); diag as compute_obstacle_constraints reads it.  Returns
+        (AttrDict(cost, U_star, X_star, goal, A_union, b_union, vertices, segments, faces[,
+        polytopes]), None), or with cost / U_star / X_star None and an InSimulationException
+        where the reference's solve fails (:862-873)."""
         from .standins import AttrDict
-        if self.road_boundary_constraints:
-            raise NotImplementedError("the road-boundary variant needs the map reader's segment "
-                                      "polytopes (Omicron binaries, v8/__init__.py:676-690)")
+        segments = getattr(params, "segments", None) if self.road_boundary_constraints else None
+        if self.road_boundary_constraints and segments is None:
+            raise ValueError("road_boundary_constraints: params.segments (the map reader's "
+                             "polytopes and junction mask, v8/__init__.py:759) is required")
         rows, vertices, A_union, b_union = self.compute_obstacle_constraints(
             params, ovehicles, None, None, None, None)
         goal = np.asarray(params.goal, np.float64)
         T = self.control_horizon
         bnb = BranchAndBound(rows, T, params.x_init, goal, lon=self.ego_lon,
-                             params=v8_qp_params(self.mpc_params_steer), device=self.device)
+                             params=v8_qp_params(self.mpc_params_steer), device=self.device,
+                             segments=None if segments is None else RoadSegments(segments))
         sol = bnb.solve()
         self.last_bnb = dict(bnb.stats)
         out = AttrDict(cost=None, U_star=None, X_star=None, goal=goal, A_union=A_union,
-                       b_union=b_union, vertices=vertices, segments=None)
+                       b_union=b_union, vertices=vertices, segments=segments)
         if sol is None:
             return out, planner.InSimulationException("Optimizer failed to find a solution")
         out.update(cost=sol["cost"], U_star=sol["u"].reshape(T, 2), X_star=sol["X"],
                    faces=sol["faces"])
+        if segments is not None:
+            out.polytopes = sol["segments"]          # the Omicron column chosen per step
         return out, None
 
 
@@ -219,114 +225,295 @@ _GATHER = np.dtype([("n0", "<f8"), ("n1", "<f8"), ("rhs", "<f8"), ("side", "<i2"
                     ("status", "<i2"), ("t_tau", "<i4")])       # ccmpc_gather_rec
 
 
-class BranchAndBound:
-    """The v8 MILP (obstacle big-M rows over the L4 faces, road boundaries off) solved exactly
-    on the GPU: best-first branch and bound over the face choice per (cell, t).  A node fixes
-    one face a_l . x_t >= b_l + diag per branched (cell, t); its relaxation is the convex QP
-    with those rows alone (the unfixed binaries' big-M rows are vacuous at M_big = 1e4: the
-    same relaxation CPLEX starts from), solved by mpc_qp_kernel.  Each round pops up to
-    `batch` nodes and solves them as ONE batched launch (a node = a scene of C cells of T
-    compact affine records; unfixed (cell, t) rows carry a nonzero status, so the kernel leaves
-    them out).  A node whose optimum satisfies every disjunction is MILP-feasible (Delta = its
-    satisfied faces) and becomes the incumbent if cheaper; otherwise its most violated
-    (cell, t) is branched into the L faces; nodes whose bound (the parent's optimum) is not
-    below the incumbent are pruned.  Deterministic: the same QP results give the same tree."""
+class RoadSegments:
+    """The map reader's segment payload (road.py:639-678, collect_segs_polytopes_and_goal:
+    polytopes [(A (F, 2), b (F,))] with A x <= b inside, mask True where a polytope covers a
+    junction) as padded arrays: A (I, F, 2), b (I, F), live (I, F), junction (I,)."""
 
-    def __init__(self, rows, T, x_init, goal, lon=3.7, Ts=0.5, params=None, batch=64, tol=1e-7,
-                 max_nodes=100000, device="cuda"):
+    def __init__(self, segments):
+        get = (lambda k: segments[k]) if isinstance(segments, dict) else (
+            lambda k: getattr(segments, k))
+        polys = [(np.asarray(a, np.float64).reshape(-1, 2), np.asarray(b, np.float64).ravel())
+                 for a, b in get("polytopes")]
+        self.I = len(polys)
+        self.junction = np.asarray(get("mask"), bool).reshape(self.I)
+        self.F = max([len(b) for _, b in polys] + [1])
+        self.A = np.zeros((self.I, self.F, 2))
+        self.b = np.zeros((self.I, self.F))
+        self.live = np.zeros((self.I, self.F), bool)
+        for i, (a, b) in enumerate(polys):
+            if a.shape[0] != b.shape[0]:
+                raise ValueError(f"segment {i}: A has {a.shape[0]} rows, b {b.shape[0]}")
+            self.A[i, :len(b)], self.b[i, :len(b)], self.live[i, :len(b)] = a, b, True
+        self.any_open = bool((~self.junction).any())     # some choice relaxes the obstacles
+
+
+class MilpBnB:
+    """Exact best-first branch and bound of the planner's MILPs on the GPU, around
+    mpc_qp_kernel: every node's relaxation is one convex QP, and each round's nodes are ONE
+    batched launch.  The binaries it branches on:
+
+      faces     v8's Delta: one L4 face a_l . x_t + S_t >= rhs_l per (cell, t) (milp.BigMRows)
+      segments  Omicron: one road polytope A_i x_t <= b_i per t (RoadSegments)
+
+    beside `base` rows that every node keeps (the v8ideal generators' half-spaces), of which
+    those flagged sbig carry + S_t on their right-hand side as the affine and scale-ideal
+    generators write it (v8ideal/__init__.py:1503-1515, :2394-2414).  S_t = M_big per chosen
+    non-junction polytope.
+
+    One polytope per t is enough: every Omicron[:, t] with several polytopes is dominated by
+    one of its members (one polytope's rows instead of several, and S_t = M_big already
+    relaxes every obstacle row it touches -- the L4 faces and the '<=' half-spaces lie within
+    metres of the ego, far inside M_big = 1e4 -- while a second non-junction polytope would
+    only tighten the '>=' half-spaces further).  The oracle's literal enumeration over every
+    subset checks this (tests/test_milp.py).
+
+    A node fixes faces {(c, t): l} and polytopes {t: i}.  Its relaxation keeps the rows that
+    hold for every completion: a fixed face only where t's polytope is fixed (or none can
+    relax it), shifted by S_t; a fixed polytope's rows; the base rows with S_t where t's
+    polytope is fixed, else the '>=' rows unshifted and the sbig '<=' rows left out.  A node
+    whose optimum satisfies every step under some polytope (and every (cell, t) disjunction)
+    is feasible for the MILP and becomes the incumbent if cheaper; otherwise its most violated
+    step is branched -- over the polytopes if t's is free, else over the faces of its most
+    violated (cell, t).  Nodes are pruned by their parent's optimum; the objective has no
+    binary terms, so the QP optimum is the MILP cost.  Deterministic: the same QP results give
+    the same tree."""
+
+    def __init__(self, T, gamma, xbar, goal, ref=None, params=None, u_order=None, T_full=None,
+                 u_prev=None, base=None, faces=None, segments=None, M_big=M_BIG, batch=64,
+                 tol=1e-7, max_nodes=100000, device="cuda"):
         from . import engine, mpc
         self.dev = engine.require_device(device)
-        self.T = int(T)
-        self.A = np.asarray(rows.A, np.float64)[:, :self.T]
-        self.rhs = np.asarray(rows.rhs, np.float64)[:, :self.T]
-        self.C, self.L = self.A.shape[0], self.A.shape[2]
+        T_full = int(T_full or T)
+        self.gamma = gamma.reshape(1, 4 * T_full, 2 * T_full).to(self.dev)
+        self.xbar = xbar.reshape(1, 4 * T_full).to(self.dev)
+        self.u_prev = None if u_prev is None else torch.as_tensor(
+            np.asarray(u_prev, np.float64).reshape(1, -1), device=self.dev)
+        if T_full > int(T) and self.u_prev is None:
+            raise ValueError("u_prev (the executed controls) is required when T < T_full")
+        self._host_init(T, goal, ref, params or v8_qp_params(),
+                        mpc.U_ORDER_C if u_order is None else u_order, T_full, base, faces,
+                        segments, M_big, batch, tol, max_nodes)
+
+    def _host_init(self, T, goal, ref, params, u_order, T_full, base, faces, segments, M_big,
+                   batch, tol, max_nodes):
+        """Everything but the device model (the tree logic runs on host arrays)."""
+        self.T, self.T_full = int(T), int(T_full)
         self.goal = np.asarray(goal, np.float64).reshape(2)
-        self.params = params or v8_qp_params()
+        self.ref = np.asarray(self.goal.reshape(1, 2) if ref is None else ref,
+                              np.float64).reshape(-1, 2)
+        self.params, self.u_order = params, int(u_order)
+        self.M = float(M_big)
         self.batch, self.tol, self.max_nodes = int(batch), float(tol), int(max_nodes)
-        self.xbar, self.gamma = mpc.ltv(np.asarray(x_init, np.float64).reshape(1, 4), self.T,
-                                        Ts=Ts, lon=lon)
-        self._qp = {}
-        # per (cell, t, l): the face row as a compact record (side +1: n . x_t >= rhs)
-        c, t, l = np.meshgrid(np.arange(self.C), np.arange(self.T), np.arange(self.L),
-                              indexing="ij")
-        self._face = np.zeros((self.C, self.T, self.L), _GATHER)
-        self._face["n0"], self._face["n1"] = self.A[..., 0], self.A[..., 1]
-        self._face["rhs"], self._face["side"], self._face["t_tau"] = self.rhs, 1, t
+        T = self.T
+        # faces (C, T, L): a_l . x_t >= rhs_l - S_t
+        if faces is not None:
+            self.fA = np.asarray(faces[0], np.float64)[:, :T]
+            self.frhs = np.asarray(faces[1], np.float64)[:, :T]
+        else:
+            self.fA, self.frhs = np.zeros((0, T, 1, 2)), np.zeros((0, T, 1))
+        self.C, self.L = self.frhs.shape[0], self.frhs.shape[2]
+        # base rows (Cb, T): n, rhs, side (+1 '>=', -1 '<='), live, sbig
+        if base is not None:
+            self.bn = np.asarray(base["n"], np.float64).reshape(-1, T, 2)
+            self.brhs = np.asarray(base["rhs"], np.float64).reshape(-1, T)
+            self.bside = np.asarray(base["side"], np.int64).reshape(-1, T)
+            self.blive = np.asarray(base["live"], bool).reshape(-1, T)
+            sb = np.asarray(base.get("sbig", False), bool)
+            self.bsbig = np.broadcast_to(sb[:, None] if sb.ndim == 1 else sb,
+                                         self.brhs.shape).copy()      # per cell or per row
+        else:
+            self.bn, self.brhs = np.zeros((0, T, 2)), np.zeros((0, T))
+            self.bside, self.blive = np.zeros((0, T), np.int64), np.zeros((0, T), bool)
+            self.bsbig = np.zeros((0, T), bool)
+        self.Cb = self.brhs.shape[0]
+        self.seg = segments
+        self.F = segments.F if segments is not None else 0
         self.stats = dict(nodes=0, launches=0, qps=0)
+        self._qp = {}
+
+    # ---- one round -------------------------------------------------------------------------
+    def _records(self, nodes):
+        """(S, Cb + C + F, T) compact affine records of the nodes' relaxations."""
+        S, T, Cb, C = len(nodes), self.T, self.Cb, self.C
+        rec = np.zeros((S, Cb + C + self.F, T), _GATHER)
+        rec["status"] = 1                                   # left out unless set below
+        rec["t_tau"] = np.arange(T)
+        seg = self.seg
+        for s, (faces, segs) in enumerate(nodes):
+            if Cb:
+                shift = np.zeros(T)
+                keep = self.blive.copy()
+                for t in range(T):
+                    if seg is None:
+                        continue
+                    if t in segs:
+                        shift[t] = 0.0 if seg.junction[segs[t]] else self.M
+                    elif seg.any_open:      # a free step: S_t may relax the sbig '<=' rows
+                        keep[:, t] &= ~(self.bsbig[:, t] & (self.bside[:, t] == -1))
+                b = rec[s, :Cb]
+                b["n0"], b["n1"] = self.bn[..., 0], self.bn[..., 1]
+                b["rhs"] = self.brhs + np.where(self.bsbig, shift[None, :], 0.0)
+                b["side"] = self.bside
+                b["status"] = np.where(keep, 0, 1)
+            for (c, t), l in faces.items():
+                if seg is not None and t not in segs and seg.any_open:
+                    continue                                # S_t may relax it
+                st = self.M if (seg is not None and t in segs and not seg.junction[segs[t]]) \
+                    else 0.0
+                r = rec[s, Cb + c, t]
+                r["n0"], r["n1"] = self.fA[c, t, l]
+                r["rhs"], r["side"], r["status"] = self.frhs[c, t, l] - st, 1, 0
+            for t, i in segs.items():
+                r = rec[s, Cb + C:, t]
+                r["n0"], r["n1"] = seg.A[i, :, 0], seg.A[i, :, 1]
+                r["rhs"], r["side"] = seg.b[i], -1
+                r["status"] = np.where(seg.live[i], 0, 1)
+        return rec
 
     def _solve_batch(self, nodes):
         """One mpc_qp_kernel launch over the nodes: (u, X, cost, ok) host arrays."""
         from . import mpc
-        S, C, T = len(nodes), self.C, self.T
-        rec = np.zeros((S, C, T), _GATHER)
-        rec["status"] = 1                                  # unfixed: left out by the kernel
-        rec["t_tau"] = np.arange(T)
-        for s, fixed in enumerate(nodes):
-            for (c, t), l in fixed.items():
-                rec[s, c, t] = self._face[c, t, l]
+        S, T = len(nodes), self.T
+        rec = self._records(nodes)
+        cells = rec.shape[1]
         qp = self._qp.get(S)
         if qp is None:
-            qp = self._qp[S] = mpc.PlanningQP([C] * S, T, kind=mpc.REC_AFFINE_COMPACT,
-                                              params=self.params, u_order=mpc.U_ORDER_C,
-                                              device=self.dev)
-        d_rec = torch.from_numpy(rec.view(np.uint8).reshape(S * C, T, 32)).to(self.dev)
+            qp = self._qp[S] = mpc.PlanningQP([cells] * S, T, T_full=self.T_full,
+                                              kind=mpc.REC_AFFINE_COMPACT, params=self.params,
+                                              u_order=self.u_order, device=self.dev)
+        d_rec = torch.from_numpy(rec.view(np.uint8).reshape(S * cells, T, 32)).to(self.dev)
         goal = torch.as_tensor(np.tile(self.goal, (S, 1)), device=self.dev)
+        ref = torch.as_tensor(np.tile(self.ref[None], (S, 1, 1)), device=self.dev)
+        up = None if self.u_prev is None else self.u_prev.expand(S, -1).contiguous()
         u, X, cost, status, _ = qp.solve(self.gamma.expand(S, -1, -1).contiguous(),
-                                         self.xbar.expand(S, -1).contiguous(), goal,
-                                         goal.reshape(S, 1, 2).contiguous(), d_rec)
+                                         self.xbar.expand(S, -1).contiguous(), goal, ref,
+                                         d_rec, u_prev=up)
         st = status.cpu().numpy() & ~mpc.QP_SKIPPED_ROWS
         self.stats["launches"] += 1
         self.stats["qps"] += S
         return u.cpu().numpy(), X.cpu().numpy(), cost.cpu().numpy(), st == mpc.QP_OK
 
+    # ---- feasibility of a node's optimum -----------------------------------------------------
+    def _violations(self, X, faces, segs):
+        """Per step t: the smallest (over the polytopes t may take) scaled violation of its
+        rows, the polytope that attains it, and per (cell, t) the disjunction's violation under
+        that polytope."""
+        T, xy, seg = self.T, X[:self.T, :2], self.seg
+        nrm = lambda r: 1.0 + np.abs(r)                      # noqa: E731
+        opts = [False, True] if (seg is not None and seg.any_open) else [False]
+        base_v, face_v = {}, {}
+        for open_ in opts:                                   # S_t = M (open) or 0
+            sh = self.M if open_ else 0.0
+            if self.Cb:
+                lhs = np.einsum("ctj,tj->ct", self.bn, xy)
+                rhs = self.brhs + np.where(self.bsbig, sh, 0.0)
+                v = np.where(self.bside == 1, rhs - lhs, lhs - rhs) / nrm(rhs)
+                base_v[open_] = np.where(self.blive, v, -np.inf).max(0)
+            else:
+                base_v[open_] = np.full(T, -np.inf)
+            if self.C:
+                fv = (self.frhs - sh - np.einsum("ctlj,tj->ctl", self.fA, xy)) / nrm(self.frhs)
+                fv = fv.min(-1)
+                for (c, t), l in faces.items():
+                    fv[c, t] = (self.frhs[c, t, l] - sh - self.fA[c, t, l] @ xy[t]) / nrm(
+                        self.frhs[c, t, l])
+                face_v[open_] = fv
+            else:
+                face_v[open_] = np.full((0, T), -np.inf)
+        if seg is None:
+            tv = np.maximum(base_v[False], face_v[False].max(0, initial=-np.inf))
+            return tv, [None] * T, face_v[False]
+        sv = np.einsum("ifj,tj->itf", seg.A, xy) - seg.b[:, None, :]
+        sv = np.where(seg.live[:, None, :], sv / nrm(seg.b)[:, None, :], -np.inf).max(-1)
+        per = np.empty((seg.I, T))                           # (polytope, t)
+        for i in range(seg.I):
+            o = bool(not seg.junction[i])
+            per[i] = np.maximum(sv[i], np.maximum(base_v[o], face_v[o].max(0, initial=-np.inf)))
+        for t, i in segs.items():
+            keep = per[i, t]
+            per[:, t] = np.inf
+            per[i, t] = keep
+        choice = np.argmin(per, 0)
+        tv = per[choice, np.arange(T)]
+        fv = np.stack([face_v[bool(not seg.junction[choice[t]]) and seg.any_open][:, t]
+                       for t in range(T)], 1) if self.C else np.zeros((0, T))
+        return tv, [int(i) for i in choice], fv
+
     def solve(self):
-        """Returns dict(u, X, cost, faces (C, T) chosen face per (cell, t), nodes, launches)
-        or None when the MILP is infeasible (the reference's CPLEX failure path)."""
+        """Returns dict(u, X, cost, faces (C, T), segments (T,) chosen polytope per t, nodes,
+        launches) or None when the MILP is infeasible (the reference's CPLEX failure path)."""
         import heapq
+        if self.seg is not None and self.seg.I == 0:
+            return None                     # sum over an empty Omicron column >= 1 fails
         heap, seq, best = [], 0, None
-        pending = [({}, -np.inf)]                          # (fixed faces, parent bound)
-        while pending or heap:
-            # the next round: the `batch` most promising open nodes (pending are the root /
-            # children whose QPs are not solved yet)
-            nodes = pending[:self.batch]
-            pending = pending[self.batch:]
-            if not nodes:
-                break
-            u, X, cost, ok = self._solve_batch([f for f, _ in nodes])
-            for (fixed, _), ui, Xi, ci, oki in zip(nodes, u, X, cost, ok):
+        pending = [(({}, {}), -np.inf)]
+        tie = lambda c: 1e-12 * (1 + abs(c))                # noqa: E731
+        while pending:
+            u, X, cost, ok = self._solve_batch([n for n, _ in pending])
+            for ((faces, segs), _), ui, Xi, ci, oki in zip(pending, u, X, cost, ok):
                 self.stats["nodes"] += 1
-                if not oki:
-                    continue                               # infeasible subproblem
-                if best is not None and ci >= best["cost"] - 1e-12 * (1 + abs(best["cost"])):
+                if not oki or (best is not None and ci >= best["cost"] - tie(best["cost"])):
                     continue
-                slack = np.min(self.rhs - np.einsum("ctlj,tj->ctl", self.A, Xi[:, :2]), -1)
-                viol = slack - self.tol * (1.0 + np.abs(self.rhs).max(-1))
-                for key in fixed:                          # a fixed face holds (QP rows):
-                    viol[key] = -np.inf                    # never branch on it again
-                if viol.max() <= 0:                        # every disjunction holds
-                    faces = np.argmin(self.rhs - np.einsum("ctlj,tj->ctl", self.A, Xi[:, :2]),
-                                      axis=-1)
-                    for (cc, t), l in fixed.items():
-                        faces[cc, t] = l
-                    best = dict(u=ui, X=Xi, cost=float(ci), faces=faces)
+                tv, choice, fv = self._violations(Xi, faces, segs)
+                if tv.max() <= self.tol:                    # feasible for the MILP
+                    fc = np.zeros((self.C, self.T), np.int64)
+                    if self.C:
+                        xy = Xi[:self.T, :2]
+                        fc = np.argmin(self.frhs - np.einsum("ctlj,tj->ctl", self.fA, xy), -1)
+                        for (c, t), l in faces.items():
+                            fc[c, t] = l
+                    best = dict(u=ui, X=Xi, cost=float(ci), faces=fc,
+                                segments=None if self.seg is None else np.array(choice))
                     continue
-                cc, t = np.unravel_index(int(np.argmax(viol)), viol.shape)
-                for l in range(self.L):
-                    child = dict(fixed)
-                    child[(int(cc), int(t))] = l
+                t = int(np.argmax(tv))
+                kids = []
+                if self.seg is not None and t not in segs:
+                    for i in range(self.seg.I):
+                        kids.append((faces, {**segs, t: i}))
+                else:
+                    v = fv[:, t].copy() if self.C else np.zeros(0)
+                    for (c, tt) in faces:
+                        if tt == t:
+                            v[c] = -np.inf
+                    if v.size and v.max() > self.tol:
+                        c = int(np.argmax(v))
+                        for l in range(self.L):
+                            kids.append(({**faces, (c, t): l}, segs))
+                    elif tv[t] <= 1e-6:                     # rows the QP holds, round-off
+                        best = dict(u=ui, X=Xi, cost=float(ci), faces=None,
+                                    segments=None if self.seg is None else np.array(choice))
+                for kid in kids:
                     seq += 1
-                    heapq.heappush(heap, (float(ci), seq, child))
+                    heapq.heappush(heap, (float(ci), seq, kid))
             if self.stats["nodes"] > self.max_nodes:
                 raise RuntimeError(f"branch and bound: more than {self.max_nodes} nodes")
-            # refill: best-first over the open nodes, bounds pruned against the incumbent
+            pending = []
             while heap and len(pending) < self.batch:
-                bound, _, child = heapq.heappop(heap)
-                if best is not None and bound >= best["cost"] - 1e-12 * (1 + abs(best["cost"])):
-                    heap.clear()                           # every remaining bound is larger
+                bound, _, kid = heapq.heappop(heap)
+                if best is not None and bound >= best["cost"] - tie(best["cost"]):
+                    heap.clear()                            # every remaining bound is larger
                     break
-                pending.append((child, bound))
+                pending.append((kid, bound))
         if best is None:
             return None
         best.update(nodes=self.stats["nodes"], launches=self.stats["launches"])
         return best
 
+
+class BranchAndBound(MilpBnB):
+    """v8's MILP (milp.BigMRows over the device L4 faces; road segments optional) from the
+    planner's state: the LTV model about u = 0 from x_init (make_local_params), v8's objective
+    (no reference term), U row-major.  solve() as MilpBnB's, with faces (C, T) the chosen
+    face per (cell, t)."""
+
+    def __init__(self, rows, T, x_init, goal, lon=3.7, Ts=0.5, params=None, batch=64, tol=1e-7,
+                 max_nodes=100000, device="cuda", segments=None):
+        from . import engine, mpc
+        T = int(T)
+        dev = engine.require_device(device)
+        xbar, gamma = mpc.ltv(np.asarray(x_init, np.float64).reshape(1, 4), T, Ts=Ts, lon=lon)
+        super().__init__(T, gamma, xbar, goal, params=params or v8_qp_params(),
+                         u_order=mpc.U_ORDER_C, faces=(rows.A, rows.rhs), segments=segments,
+                         M_big=rows.M_big, batch=batch, tol=tol, max_nodes=max_nodes,
+                         device=dev)

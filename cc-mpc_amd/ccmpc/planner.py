@@ -480,6 +480,7 @@ class MidlevelAgent:
         self.prob_lower_save = None
         self.last_records = None
         self._last_rec = None              # (device records, kind, T) of the last generator
+        self._last_sbig = False            # do its rows carry S_big (road boundaries)?
         self.mpc_params = mpc.MPCParams.reference_defaults(self.mpc_params_steer)
         self._ltv = None                   # (x_init, T_full) -> (xbar, Gamma), first step's
         self._qp = {}
@@ -749,9 +750,10 @@ class MidlevelAgent:
         x_init = self.make_local_params(frame, Tsh)
         # do_highlevel_control (:2814, :2840): refT, then the route goal
         ref = self.load_refT(int(self.offline_index / 10) + 1, Tsh, x_init)
-        _, goal = self.compute_segs_polytopes_and_goal(x_init, Tsh)
+        segments, goal = self.compute_segs_polytopes_and_goal(x_init, Tsh)
         speeds, angles, timeout = self.compute_prediction_controls(
-            frame, Tsh, shrinking, sampler, minpos, pasts, x_init, goal, ref, bboxes)
+            frame, Tsh, shrinking, sampler, minpos, pasts, x_init, goal, ref, bboxes,
+            segments=segments)
         self.control_horizon_last = Tsh        # __control_horizon = Tsh (:3170)
         c = self.last_ctrl
         self._U_warm, self._X_warm = c["U_star"], c["X_star"]
@@ -763,7 +765,8 @@ class MidlevelAgent:
                         "bboxes": bboxes, "x_init": x_init.copy(), "goal": goal,
                         "ref": np.array(ref), "records": np.array(self.last_records),
                         "speeds": speeds, "angles": angles, "U_star": c["U_star"],
-                        "X_star": c["X_star"], "u": c["u"]})
+                        "X_star": c["X_star"], "u": c["u"], "segments": segments,
+                        "polytopes": c.get("polytopes")})
         return speeds, angles, timeout
 
     # ------------------------------------------------------------------------------------
@@ -859,8 +862,6 @@ class MidlevelAgent:
         """v8ideal/__init__.py:781-964.  Returns the reference's 9-tuple
         (constraints, vertices, A_union, b_union, OVconstraint, direct, ovStateMean_tau_1,
         ovStateCov_tau_1, 0)."""
-        if self.road_boundary_constraints:
-            raise NotImplementedError("road-boundary QP variables are outside the GPU path")
         T, ph = int(Tsh), self.prediction_horizon
         scene = self._scene(ovehicles)
         K = scene.K
@@ -890,6 +891,7 @@ class MidlevelAgent:
         h = engine.halfspaces(rec)[:, :T * (T - 1) // 2]     # T = 1 keeps one unused slot
         self.last_records = h
         self._last_rec = (rec, mpc.REC_HALFSPACE, T)
+        self._last_sbig = False             # the Minkowski rows carry no S_big (:926-939)
         constraints = self._records_to_halfspaces(h, scene, T)
         pl_h = pl.cpu().numpy()
         if T == ph:
@@ -904,10 +906,9 @@ class MidlevelAgent:
 
     def compute_obstacle_constraints_GMM_affine(
             self, params, ovehicles, Delta2, Omicron, temp_x, eps_ura, segments, Tsh, ref_traj):
-        """v8ideal/__init__.py:1378-1539 (the S_big_repeated term is a QP variable, zero when
-        road-boundary constraints are off, and is left to the caller)."""
-        if self.road_boundary_constraints:
-            raise NotImplementedError("road-boundary QP variables are outside the GPU path")
+        """v8ideal/__init__.py:1378-1539.  The S_big_repeated term (zero with road boundaries
+        off; M_big per chosen non-junction road polytope with them on) belongs to the caller's
+        problem: solve_planning_qp adds it (milp.MilpBnB)."""
         T = int(Tsh)
         scene = self._scene(ovehicles)
         K = scene.K
@@ -920,6 +921,7 @@ class MidlevelAgent:
         h = engine.affine_records(rec)
         self.last_records = h
         self._last_rec = (rec, mpc.REC_AFFINE, T)
+        self._last_sbig = True              # + S_big_repeated[0, t] on both sides (:1503-1515)
         cons = []
         for c, (o, k) in enumerate(scene.cell_of):
             for t in range(T):
@@ -955,8 +957,6 @@ class MidlevelAgent:
                                               scaled=False)
 
     def _affine_tangent_generator(self, params, ovehicles, eps_ura, Tsh, ref_traj, scaled):
-        if self.road_boundary_constraints:
-            raise NotImplementedError("road-boundary QP variables are outside the GPU path")
         T, ph = int(Tsh), self.prediction_horizon
         scene = self._scene(ovehicles)
         K = scene.K
@@ -985,6 +985,9 @@ class MidlevelAgent:
         h = engine.affine_records(rec)
         self.last_records = h
         self._last_rec = (rec, mpc.REC_AFFINE, T)
+        # the scale-ideal rows carry + S_big_repeated[0, t] (:2394-2414), the robust ones
+        # do not (:1828-1849)
+        self._last_sbig = bool(scaled)
         cons = []
         O, maxK = scene.O, max(K)
         mean_p0p1 = _object_grid(O, maxK, T)
@@ -1059,6 +1062,7 @@ class MidlevelAgent:
         constraints = HalfSpaceList(h, scene.cell_of, P)
         self.last_records = h[:, :P]
         self._last_rec = (g.out.d("rec"), mpc.REC_HALFSPACE, T)
+        self._last_sbig = False
         return ovs, self._step_tuple(g, o, scene, K, 0, constraints=constraints)
 
     def predict_and_constrain_affine(self, params, sampler, eps_ura, Tsh, ref_traj, minpos,
@@ -1075,6 +1079,7 @@ class MidlevelAgent:
         h = o["rec"].reshape(-1).view(engine._lib.AFFINE_DTYPE).reshape(g.C, T)
         self.last_records = h
         self._last_rec = (g.out.d("rec"), mpc.REC_AFFINE, T)
+        self._last_sbig = True
         st = h["status"]
         if st.any():
             c, t = divmod(int(np.flatnonzero(st.reshape(-1))[0]), T)
@@ -1201,7 +1206,8 @@ class MidlevelAgent:
         return np.asarray(src, np.int32)
 
     def compute_prediction_controls(self, frame, Tsh, shrinking, sampler, minpos, pasts, x_init,
-                                    goal, ref_traj, bboxes=None, apply_robust=True):
+                                    goal, ref_traj, bboxes=None, apply_robust=True,
+                                    segments=None):
         """__compute_prediction_controls (v8ideal/__init__.py:3163-3210) without CARLA: one
         planning frame of the reference harness loop (tests/Hz20/__init__.py:297-359 ->
         run_step :3226-3284) from the sampler inputs on.
@@ -1244,27 +1250,38 @@ class MidlevelAgent:
                                                          minpos, pasts, bboxes, filter_pmf=fp)
         self.last_generator_output = (ovs, out)
         up = np.concatenate(self._u_prev) if (T < ph and self._u_prev) else None
-        ctrl = self.solve_planning_qp(x_init, goal, ref_traj, T, u_prev=up, lon=self.ego_lon)
+        ctrl = self.solve_planning_qp(x_init, goal, ref_traj, T, u_prev=up, lon=self.ego_lon,
+                                      segments=segments)
         self.last_ctrl = ctrl
         self._u_prev.append(np.asarray(ctrl["u"][:2]))        # U_star.T.ravel()[:nu] (:3186)
         X = ctrl["X_star"]
         return X[:, 3].copy(), -X[:, 2], False
 
     def solve_planning_qp(self, x_init, goal, ref_traj, Tsh, u_prev=None, lon=3.7,
-                          u_order=mpc.U_ORDER_F):
+                          u_order=mpc.U_ORDER_F, segments=None):
         """do_highlevel_control's QP (:2850-3043) on the device, on the records of the last
         generator call (read in place, never copied to the host).  The LTV model is the one of
         the first shrinking step (the reference keeps its Gamma/x_bar across T < ph steps,
         :2858-2891): it is recomputed when Tsh == ph and reused, sliced, below it, with u_prev
         the executed controls (the reference's U_prev, :3186).  Returns the reference's
         ctrl_result fields {cost, U_star (T, 2), X_star (T, 4), goal, u}; raises
-        InSimulationException where CPLEX fails (:3099-3110)."""
+        InSimulationException where CPLEX fails (:3099-3110).
+
+        With road_boundary_constraints the problem is the reference's MILP over the Omicron
+        binaries (:2906-2916, compute_road_boundary_constraints :738-758): `segments` (the map
+        reader's polytopes and junction mask, compute_segs_polytopes_and_goal) is required and
+        the solve is milp.MilpBnB's branch and bound over one road polytope per step, the
+        generator's rows carrying S_big where the reference adds it; the result also holds
+        `polytopes`, the polytope chosen per step."""
         if self._last_rec is None:
             raise RuntimeError("no constraint records: call a generator first")
         rec, kind, T = self._last_rec
         if int(Tsh) != T:
             raise ValueError(f"records are for T = {T}, not Tsh = {Tsh}")
         ph = self.prediction_horizon
+        if self.road_boundary_constraints:
+            return self._solve_road_milp(x_init, goal, ref_traj, T, rec, kind, u_prev, lon,
+                                         u_order, segments)
         if self._ltv is None:               # device buffers, rebuilt in place at Tsh == ph
             self._ltv = (torch.empty((1, 4 * ph), dtype=torch.float64, device=self.device),
                          torch.empty((1, 4 * ph, 2 * ph), dtype=torch.float64,
@@ -1290,6 +1307,66 @@ class MidlevelAgent:
         return {"cost": res["cost"], "U_star": res["U_star"], "X_star": res["X_star"],
                 "goal": np.asarray(goal, np.float64), "u": res["u"],
                 "skipped_rows": bool(st & mpc.QP_SKIPPED_ROWS)}
+
+    def _solve_road_milp(self, x_init, goal, ref_traj, T, rec, kind, u_prev, lon, u_order,
+                         segments):
+        """solve_planning_qp with road boundaries: the generator's records packed on the
+        device (ccmpc_compact_records) and read back as rows, a half-space (t, tau) record in
+        pseudo-cell tau at step t; the LTV model as solve_planning_qp keeps it; MilpBnB."""
+        from . import dist, milp
+        if segments is None:
+            raise ValueError("road_boundary_constraints: segments (compute_segs_polytopes_and_"
+                             "goal's polytopes and mask) are required")
+        ph = self.prediction_horizon
+        if T < ph and u_prev is None:
+            raise ValueError(f"Tsh = {T} < ph = {ph} needs u_prev, the controls executed "
+                             "since the first shrinking step (:3186)")
+        halfspace = kind == mpc.REC_HALFSPACE
+        P = T * (T - 1) // 2 if halfspace else T
+        C = rec.shape[0]
+        Cb = C * (T - 1) if halfspace else C
+        base = dict(n=np.zeros((Cb, T, 2)), rhs=np.zeros((Cb, T)), side=np.ones((Cb, T), int),
+                    live=np.zeros((Cb, T), bool), sbig=np.full((Cb, T), bool(self._last_sbig)))
+        if C and P:
+            h = dist.compact_records(rec[:, :P].contiguous(), int(halfspace is False))
+            h = h.cpu().numpy().reshape(-1).view(milp._GATHER).reshape(C, P)
+            for c in range(C):
+                for p_ in range(P):
+                    r = h[c, p_]
+                    if halfspace:
+                        t, tau = int(r["t_tau"]) >> 16, int(r["t_tau"]) & 0xFFFF
+                        j = c * (T - 1) + tau
+                    else:
+                        t, j = p_, c
+                    base["n"][j, t] = (r["n0"], r["n1"])
+                    base["rhs"][j, t], base["side"][j, t] = r["rhs"], r["side"]
+                    base["live"][j, t] = r["status"] == 0
+        if self._ltv is None:
+            self._ltv = (torch.empty((1, 4 * ph), dtype=torch.float64, device=self.device),
+                         torch.empty((1, 4 * ph, 2 * ph), dtype=torch.float64,
+                                     device=self.device))
+            self._ltv_built = False
+        xbar, gamma = self._ltv
+        if T == ph or not self._ltv_built:
+            xb, gm = mpc.ltv(np.asarray(x_init, np.float64).reshape(1, 4), ph, Ts=self.steptime,
+                             lon=lon)
+            xbar.copy_(xb)
+            gamma.copy_(gm)
+            self._ltv_built = True
+        bnb = milp.MilpBnB(T, gamma, xbar, goal, ref=np.asarray(ref_traj, np.float64)[:T],
+                           params=self.mpc_params, u_order=u_order, T_full=ph,
+                           u_prev=None if T == ph else u_prev, base=base,
+                           segments=milp.RoadSegments(segments), M_big=self.M_big,
+                           device=self.device)
+        sol = bnb.solve()
+        self.last_bnb = dict(bnb.stats)
+        if sol is None:
+            raise InSimulationException("Optimizer failed to find a solution")
+        u = np.asarray(sol["u"], np.float64)
+        U = u.reshape(2, T).T.copy() if u_order == mpc.U_ORDER_F else u.reshape(T, 2).copy()
+        return {"cost": sol["cost"], "U_star": U, "X_star": sol["X"],
+                "goal": np.asarray(goal, np.float64), "u": u, "skipped_rows": False,
+                "polytopes": sol["segments"]}
 
     def _loaded_tangents(self, loaded, mean, K, T, x_init, ref):
         """The previous frame's slopes / tangent indices for every (cell, t) of this frame

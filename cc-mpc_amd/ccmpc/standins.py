@@ -158,12 +158,37 @@ class PolylineRoadBoundary:
     """RoadBoundaryConstraint over a polyline route (points in the planner's flipped frame):
     collect_segs_polytopes_and_goal's goal rule (road.py:663-666: the route point nearest the
     position, then the first point at or past min(its distance + distance, path length)), and
-    get_point_from_start (:621-637, linear instead of the cubic spline between points)."""
+    get_point_from_start (:621-637, linear instead of the cubic spline between points).  The
+    road segments (cover_along_path_varyingsize, :468-556, sizes from the spline curvature)
+    are restated for a polyline: rectangles of `seg_len` metres along the route (one per run
+    of route edges, `overlap` metres longer at each end so neighbours overlap), `lane_width`
+    wide, in H-form A x <= b; a rectangle whose centre lies within one of the `junctions`
+    (x, y, radius) discs is a junction polytope (mask True)."""
 
-    def __init__(self, points):
+    def __init__(self, points, lane_width=3.5, seg_len=10.0, overlap=0.5, junctions=()):
         self.points = np.asarray(points, np.float64).reshape(-1, 2)
         seg = np.linalg.norm(np.diff(self.points, axis=0), axis=1)
         self.distances = np.concatenate([[0.0], np.cumsum(seg)])
+        self._cover(float(lane_width), float(seg_len), float(overlap), junctions)
+
+    def _cover(self, lane_width, seg_len, overlap, junctions):
+        polys, mask, starts = [], [], []
+        d, hw = self.distances, 0.5 * lane_width
+        s0 = 0.0
+        while s0 < d[-1] - 1e-9:
+            s1 = min(s0 + seg_len, d[-1])
+            p0, p1 = self.get_point_from_start(s0), self.get_point_from_start(s1)
+            e = (p1 - p0) / max(np.linalg.norm(p1 - p0), 1e-12)
+            nrm = np.array([-e[1], e[0]])
+            A = np.stack([e, -e, nrm, -nrm])
+            b = np.array([e @ p1 + overlap, -(e @ p0) + overlap, nrm @ p0 + hw, -(nrm @ p0) + hw])
+            ctr = 0.5 * (p0 + p1)
+            polys.append((A, b))
+            mask.append(any(np.hypot(ctr[0] - jx, ctr[1] - jy) <= r for jx, jy, r in junctions))
+            starts.append(s0)
+            s0 = s1
+        self.road_segs = AttrDict(polytopes=polys, mask=np.asarray(mask, bool),
+                                  distances=np.asarray(starts))
 
     @property
     def path_length(self):
@@ -176,24 +201,34 @@ class PolylineRoadBoundary:
         return np.array([np.interp(distance, d, self.points[:, 0]),
                          np.interp(distance, d, self.points[:, 1])])
 
+    def _poly_id(self, dist):
+        return int(np.searchsorted(self.road_segs.distances, dist, side="right")) - 1
+
     def collect_segs_polytopes_and_goal(self, position, distance):
         beg_idx = int(np.argmin(np.linalg.norm(self.points - np.asarray(position)[:2], axis=1)))
-        end_dist = min(self.distances[beg_idx] + distance, self.path_length)
+        beg_dist = self.distances[beg_idx]
+        end_dist = min(beg_dist + distance, self.path_length)
         # distance_to_point is indexed by the right-closed intervals (d[j-1], d[j]] -> point j
         j = max(int(np.searchsorted(self.distances, end_dist, side="left")), 1)
-        return AttrDict(polytopes=[], polytope_ids=[], mask=np.zeros(0, bool),
-                        goal=self.points[j].copy())
+        n = len(self.road_segs.polytopes)
+        beg_id = max(self._poly_id(beg_dist) - 1, 0)                # road.py:667-671
+        end_id = min(self._poly_id(end_dist) + 1, n - 1)
+        return AttrDict(polytopes=self.road_segs.polytopes[beg_id:end_id],
+                        polytope_ids=list(range(beg_id, end_id)),
+                        mask=self.road_segs.mask[beg_id:end_id], goal=self.points[j].copy())
 
 
 class StubMapReader:
     """MapQuerier.road_boundary_constraints_from_actor (map/__init__.py:392) returning a
-    PolylineRoadBoundary along the given route."""
+    PolylineRoadBoundary along the given route (road_kwargs: its lane width, segment length
+    and junction discs)."""
 
-    def __init__(self, route_points):
+    def __init__(self, route_points, **road_kwargs):
         self.route_points = np.asarray(route_points, np.float64)
+        self.road_kwargs = road_kwargs
 
     def road_boundary_constraints_from_actor(self, actor, max_distance, choices=(), flip_y=True):
-        return PolylineRoadBoundary(self.route_points)
+        return PolylineRoadBoundary(self.route_points, **self.road_kwargs)
 
 
 def straight_route(start, heading, length=200.0, step=2.0):

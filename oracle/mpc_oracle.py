@@ -467,3 +467,88 @@ def milp_enumerate(Gamma_full, xbar_full, T, goal, A, rhs, p=None, order="C"):
         if s is not None and (best is None or s["cost"] < best["cost"]):
             best = dict(s, faces=np.array(combo).reshape(C, T))
     return best
+
+
+# ----------------------------------------------------------------------------------------
+# Road boundaries on (road_boundary_constraints=True): the Omicron binaries of v8's
+# do_highlevel_control (v8/__init__.py:676-702) and v8ideal's (v8ideal/__init__.py:738-758,
+# :2906-2916).  Per segment polytope i (A_i x <= b_i, road.py:639-678) and step t:
+#     A_i . X[t, :2] - M_big (1 - Omicron[i, t]) <= b_i,     sum_i Omicron[i, t] >= 1
+# and S_t = M_big * sum_i Omicron[i, t] over the non-junction polytopes (segments.mask False),
+# added to the obstacle rows: v8's face rows (a . x + M (1 - Delta) + S_t >= b + diag) and, in
+# v8ideal, the affine (:1503-1515) and scale-ideal (:2394-2414) rows, both sides
+# (n . x >= d + g + S_t, n . x <= d - g + S_t as written); the Minkowski (:926-939) and robust
+# (:1828-1849) generators leave S out.  Enumerated literally here: every non-empty Omicron[:, t]
+# subset, every unchosen row kept with its + M relaxation.
+# ----------------------------------------------------------------------------------------
+def road_rows(base, faces, segs, mask, M, seg_choice, face_choice, T):
+    """obstacle_rows-form rows (t, a, b: a . x_t <= b) of one assignment.  base: rows dicts
+    (t, n, rhs, side +1 '>=' / -1 '<=', sbig); faces (A (C, T, L, 2), rhs (C, T, L)) or None;
+    segs [(A_i, b_i)], mask (I,); seg_choice {t: tuple of chosen i} (None without segments);
+    face_choice {(c, t): l}."""
+    S = np.zeros(T)
+    if segs is not None:
+        for t in range(T):
+            S[t] = M * sum(1 for i in seg_choice[t] if not mask[i])
+    rows = []
+    for r in base:
+        t = int(r["t"])
+        b = float(r["rhs"]) + (S[t] if r.get("sbig", False) else 0.0)
+        n = np.asarray(r["n"], np.float64)
+        rows.append((t, -n, -b) if int(r["side"]) == 1 else (t, n, b))
+    if faces is not None:
+        A, rhs = faces
+        C, _, L = rhs.shape
+        for c in range(C):
+            for t in range(T):
+                for l in range(L):      # a . x + M (1 - delta) + S >= rhs
+                    relax = 0.0 if face_choice[(c, t)] == l else M
+                    rows.append((t, -A[c, t, l], -(rhs[c, t, l] - relax - S[t])))
+    if segs is not None:
+        for t in range(T):
+            for i, (Ai, bi) in enumerate(segs):
+                relax = 0.0 if i in seg_choice[t] else M
+                for f in range(len(bi)):
+                    rows.append((t, np.asarray(Ai[f], np.float64), float(bi[f]) + relax))
+    return rows
+
+
+def _road_node(Gf, c, T, goal, ref, rows, p, order):
+    H, f, k, G, h = assemble_qp(Gf, c, T, goal, ref, rows, p, order=order)
+    if not is_feasible(G, h):
+        return None
+    u, _, _ = solve_qp(H, f, G, h)
+    return dict(u=u, cost=float(0.5 * u @ H @ u + f @ u + k), X=(Gf @ u + c).reshape(T, 4))
+
+
+def road_milp_enumerate(Gamma_full, xbar_full, T, goal, ref, p, base=(), faces=None, segs=None,
+                        mask=None, M=10_000.0, order="F", T_full=None, u_prev=None,
+                        subsets=True):
+    """The MILP's optimum over every assignment: Omicron[:, t] any non-empty subset (subsets)
+    or one polytope, Delta one face per (cell, t).  Returns dict(u, X, cost, segs, faces) or
+    None (infeasible: no polytope, or no assignment with a feasible QP)."""
+    import itertools
+    Gf, c = state_map(Gamma_full, xbar_full, T, T_full or T, u_prev=u_prev)
+    if segs is not None and len(segs) == 0:
+        return None                    # sum over an empty Omicron column >= 1
+    if segs is None:
+        seg_opts = [None]
+    elif subsets:
+        I = len(segs)
+        seg_opts = [s for k in range(1, I + 1) for s in itertools.combinations(range(I), k)]
+    else:
+        seg_opts = [(i,) for i in range(len(segs))]
+    keys = []
+    if faces is not None:
+        C, _, L = faces[1].shape
+        keys = [(cc, t) for cc in range(C) for t in range(T)]
+    best = None
+    for sc in itertools.product(seg_opts, repeat=T):
+        seg_choice = dict(enumerate(sc))
+        for fc in itertools.product(*(range(faces[1].shape[2]) for _ in keys)):
+            face_choice = dict(zip(keys, fc))
+            rows = road_rows(base, faces, segs, mask, M, seg_choice, face_choice, T)
+            s = _road_node(Gf, c, T, goal, ref, rows, p, order)
+            if s is not None and (best is None or s["cost"] < best["cost"] - 1e-12):
+                best = dict(s, segs=sc, faces=dict(face_choice))
+    return best

@@ -286,3 +286,49 @@ def test_make_ovehicles_on_the_reference_5_tuple(gpu):
         assert ov.node is res["nodes"][r]
         np.testing.assert_array_equal(ov.ground_truth, res["ground_truth_dict"][ts][
             res["nodes"][r]] + minpos)
+
+
+@pytest.mark.parametrize("junction", [True, False], ids=["junction_road", "open_road"])
+def test_harness_episode_with_road_boundaries(gpu, junction):
+    """road_boundary_constraints=True through run_step (v8ideal/__init__.py:2906-2916): every
+    planning step is the road MILP over the stand-in map's polytopes (one per step, chosen by
+    the branch and bound), each plan inside the polytopes it chose.  On a junction road
+    (S_big = 0) the wide lane does not bind and the plans equal the road-free episode's; on an
+    open road the affine receding steps' '>=' rows carry S_big = M_big (as the reference writes
+    them), which no plan can meet, so those steps fail as the reference's solve would."""
+    from ccmpc import harness, standins
+
+    def make_world():
+        world, ego, ids, mr = standins.town03_scene(n_ov=1, ego_xy=(60.0, 81.76),
+                                                    ego_speed=8.0, ov_gap=20.0, ov_speed=8.0,
+                                                    ov_lateral=40.0)
+        r = mr.route_points
+        disc = [(float(r[0, 0]), float(r[0, 1]), 1e4)] if junction else []
+        return world, ego, ids, standins.StubMapReader(r, lane_width=6.0, junctions=disc)
+
+    runs = {}
+    for road in (False, True):
+        route = make_world()[3].route_points
+        stg = standins.SyntheticTrajectron(L=25, ph=8, seed=5, device=gpu)
+        scen = harness.MonteCarloScenario(
+            harness.ScenarioParameters(n_burn_interval=4, run_interval=10),
+            harness.CtrlParameters(n_predictions=2000, prediction_horizon=8, control_horizon=8),
+            make_world, stg, agent_kwargs=dict(n_ideal=N_IDEAL, reference_trajectory=route[::2],
+                                               road_boundary_constraints=road, device=gpu))
+        runs[road] = (scen.episode(0), scen.steps)
+    (st0, steps0), (st1, steps1) = runs[False], runs[True]
+    assert not st0.infeasibility
+    for s in steps1:
+        assert s["polytopes"] is not None and len(s["polytopes"]) == s["T"]
+        for t, i in enumerate(s["polytopes"]):
+            A, b = s["segments"].polytopes[i]
+            assert np.all(A @ s["X_star"][t, :2] <= b + 1e-6)
+    if junction:
+        assert not st1.infeasibility and len(steps1) == len(steps0)
+        for a, b in zip(steps0, steps1):
+            tol = 1e-6 * (1.0 + np.abs(a["u"]).max())
+            assert np.abs(a["u"] - b["u"]).max() <= tol, a["frame"]
+    else:
+        shrink = [s for s in steps1 if s["shrinking"]]
+        assert len(shrink) == 8                        # the Minkowski steps plan
+        assert st1.infeasibility                       # the first affine step cannot

@@ -118,3 +118,134 @@ def test_v8_do_highlevel_control_on_device_l4(gpu, O, T):
                                          rel=1e-9)
         n_cmp += 1
     assert n_cmp >= 2
+
+
+def _road_segments():
+    from ccmpc import milp
+    from test_milp import _road_scene
+    segs, mask = _road_scene(0)
+    return segs, mask, milp.RoadSegments(dict(polytopes=segs, mask=mask))
+
+
+@pytest.mark.parametrize("T,sbig", [(3, True), (3, False), (4, True), (5, True)])
+def test_road_milp_on_halfspaces_matches_oracle(gpu, T, sbig):
+    """Road boundaries on a v8ideal-style QP (the reference objective with its trajectory
+    term, cvxpy's column-major U): the generator's half-spaces plus one road polytope per step
+    (Omicron), the affine / scale-ideal rows carrying S_t (sbig) or not -- MilpBnB on the GPU
+    against the oracle's literal MILP over every Omicron subset."""
+    from ccmpc import milp, mpc
+    from test_milp import _road_base
+    segs, mask, rs = _road_segments()
+    goal, base = _road_base(T, sbig)
+    xbar, G = _ego_model(T, X0)
+    ref = np.stack([np.linspace(1.0, goal[0], T), np.zeros(T)], 1)
+    want = mo.road_milp_enumerate(G, xbar, T, goal, ref, mo.DEFAULT_PARAMS, base=base,
+                                  segs=segs, mask=mask, subsets=True)
+    rows = dict(n=np.zeros((2, T, 2)), rhs=np.zeros((2, T)), side=np.ones((2, T), int),
+                live=np.zeros((2, T), bool), sbig=np.full((2, T), sbig))
+    slot = {-1: 0, 1: 1}
+    for r in base:
+        j, t = slot[r["side"]], r["t"]
+        rows["n"][j, t], rows["rhs"][j, t], rows["side"][j, t] = r["n"], r["rhs"], r["side"]
+        rows["live"][j, t] = True
+    g_xbar, g_gamma = mpc.ltv(np.array(X0).reshape(1, 4), T)
+    got = milp.MilpBnB(T, g_gamma, g_xbar, goal, ref=ref,
+                       params=mpc.MPCParams.reference_defaults(), u_order=mpc.U_ORDER_F,
+                       base=rows, segments=rs, device=gpu).solve()
+    assert got is not None and want is not None
+    assert np.abs(got["u"] - want["u"]).max() <= 1e-6 * (1.0 + np.abs(want["u"]).max())
+    assert got["cost"] == pytest.approx(want["cost"], rel=1e-8)
+    # the GPU's polytope per step holds its optimum
+    for t, i in enumerate(got["segments"]):
+        A, b = segs[i]
+        assert np.all(A @ got["X"][t, :2] <= b + 1e-6)
+
+
+@pytest.mark.parametrize("T", [3])
+def test_v8_road_milp_matches_oracle(gpu, T):
+    """v8's MILP with road boundaries: the L4-face disjunctions (Delta) and the road polytopes
+    (Omicron, S_t = M_big per non-junction polytope on the face rows, v8/__init__.py:676-702)
+    branched together by BranchAndBound against the oracle's enumeration of both."""
+    from ccmpc import milp
+    segs, mask, rs = _road_segments()
+    A, rhs = _box_rows(T, [lambda t: (6.5 + 1.0 * t, 0.6)])
+    goal = np.array([14.0, 0.0])
+    xbar, G = _ego_model(T, X0)
+    want = mo.road_milp_enumerate(G, xbar, T, goal, goal.reshape(1, 2), mo.v8_qp_params(),
+                                  faces=(A, rhs), segs=segs, mask=mask, order="C",
+                                  subsets=False)
+    got = milp.BranchAndBound(_rows(A, rhs), T, X0, goal, segments=rs, device=gpu).solve()
+    assert got is not None and want is not None
+    assert np.abs(got["u"] - want["u"]).max() <= 1e-6 * (1.0 + np.abs(want["u"]).max())
+    assert got["cost"] == pytest.approx(want["cost"], rel=1e-8)
+    plain = milp.BranchAndBound(_rows(A, rhs), T, X0, goal, device=gpu).solve()
+    assert plain is None or plain["cost"] != pytest.approx(got["cost"], rel=1e-6)
+
+
+def _planner_road_case(gpu, affine, seed):
+    """One planning frame of MidlevelAgent(road_boundary_constraints=True) at ph = 4 through
+    compute_prediction_controls, and the oracle's literal road MILP on the frame's records."""
+    from ccmpc import episode, mpc, planner
+    from ccmpc.standins import AttrDict
+    ph, O = 4, 2
+    init, pmf, gmm = episode.synthetic_gmm(O, T=ph, seed=seed)
+    minpos = np.array([150.0, -120.0])
+    pasts = [np.array([[minpos[0] + init[o, 0] - 2.0, minpos[1] + init[o, 1]]])
+             for o in range(O)]
+    x_init = np.array([172.0, -96.0, 0.0, 5.0])
+    ref = np.stack([172.0 + 2.5 * np.arange(1, ph + 1), np.linspace(-95.0, -92.0, ph)], 1)
+    goal = np.array([186.0, -91.0])        # up the junction box, out of the lane
+    lane = (np.array([[1.0, 0.0], [-1.0, 0.0], [0.0, 1.0], [0.0, -1.0]]),
+            np.array([180.0, -160.0, -96.0 + 0.6, 96.0 + 0.6]))
+    box = (np.array([[1.0, 0.0], [-1.0, 0.0], [0.0, 1.0], [0.0, -1.0]]),
+           np.array([230.0, -178.0, -96.0 + 8.0, 96.0 + 8.0]))
+    segments = AttrDict(polytopes=[lane, box], mask=np.array([False, True]), goal=goal)
+    agent = planner.MidlevelAgent(prediction_horizon=ph, road_boundary_constraints=True,
+                                  device=gpu)
+    sampler = dict(init_state=init, latent_pmf=pmf, gmm=gmm, N=2000, seed=seed)
+    err = None
+    try:
+        agent.compute_prediction_controls(0, ph, not affine, sampler, minpos, pasts, x_init,
+                                          goal, ref, segments=segments)
+    except planner.InSimulationException as e:
+        err = e
+    h = agent.last_records
+    base = []
+    for c in range(h.shape[0]):
+        for r in h[c]:
+            if int(r["status"]) != 0:
+                continue
+            if affine:
+                t, d = int(r["t"]), float(r["rhs"])
+            else:
+                t, d = int(r["t_tau"]) >> 16, float(r["d"])
+            base.append(dict(t=t, n=np.array([r["n0"], r["n1"]]), rhs=d, side=int(r["side"]),
+                             sbig=affine))
+    xb, _, G, _, _ = mo.VehicleModel(ph, 0.5, 1.85, 3.7).get_optimization_ltv(x_init,
+                                                                               np.zeros(2))
+    want = mo.road_milp_enumerate(G, xb, ph, goal, ref, mpc.MPCParams.reference_defaults()
+                                  .as_dict(), base=base, segs=segments.polytopes,
+                                  mask=segments.mask, subsets=True)
+    return agent, err, want
+
+
+@pytest.mark.parametrize("affine", [False, True], ids=["minkowski", "affine"])
+def test_planner_road_boundaries_match_oracle_milp(gpu, affine):
+    """road_boundary_constraints=True on the v8ideal planner (it used to refuse): the frame's
+    generator records (Minkowski: no S_big; affine: + S_big on both sides) and the road
+    polytopes as one MILP -- solve_planning_qp's branch and bound against the oracle's literal
+    enumeration, the polytope per step holding the plan."""
+    n_feasible = 0
+    for seed in (3, 11):
+        agent, err, want = _planner_road_case(gpu, affine, seed)
+        if want is None:
+            assert err is not None
+            continue
+        assert err is None, err
+        got = agent.last_ctrl
+        assert np.abs(got["u"] - want["u"]).max() <= 1e-6 * (1.0 + np.abs(want["u"]).max())
+        assert got["cost"] == pytest.approx(want["cost"], rel=1e-8)
+        assert list(got["polytopes"]) == [0, 1, 1, 1]     # the lane, then the junction box
+        assert agent.last_bnb["nodes"] > 1                 # the road binds: it branched
+        n_feasible += 1
+    assert n_feasible >= 1

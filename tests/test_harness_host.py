@@ -135,6 +135,28 @@ def test_route_goal_rule():
                                   [40.0, 0.0])
 
 
+def test_road_segments_cover_the_route():
+    """The stand-in's road polytopes (road.py:468-556 restated for a polyline): every route
+    point lies in some polytope, neighbours overlap, a junction disc marks its polytopes, and
+    collect_segs_polytopes_and_goal slices [id(beg) - 1, id(end) + 1) as road.py:667-678."""
+    from ccmpc import standins
+    route = np.stack([np.arange(0.0, 81.0, 2.0), 0.5 * np.arange(0.0, 81.0, 2.0) ** 0.5], 1)
+    rb = standins.PolylineRoadBoundary(route, lane_width=3.5, seg_len=10.0,
+                                       junctions=[(45.0, 3.3, 6.0)])
+    polys, mask = rb.road_segs.polytopes, rb.road_segs.mask
+    for p in route:
+        assert any(np.all(A @ p <= b + 1e-9) for A, b in polys)
+    for i, ((A0, b0), (A1, b1)) in enumerate(zip(polys, polys[1:])):   # a shared point
+        q = rb.get_point_from_start(rb.road_segs.distances[i + 1])
+        assert np.all(A0 @ q <= b0 + 1e-9) and np.all(A1 @ q <= b1 + 1e-9)
+    assert mask.any() and not mask.all()
+    seg = rb.collect_segs_polytopes_and_goal([21.0, 2.0], 25.0)
+    i0 = int(np.searchsorted(rb.road_segs.distances, rb.distances[10], side="right")) - 1
+    assert seg.polytope_ids[0] == max(i0 - 1, 0)
+    assert len(seg.polytopes) == len(seg.mask) == len(seg.polytope_ids)
+    np.testing.assert_array_equal(seg.mask, mask[seg.polytope_ids])
+
+
 def test_prediction_output_to_trajectories_over_standin_nodes(host_agent_cls):
     """Trajectron++'s prediction_output_to_trajectories as restated in ccmpc.prediction, over the
     scene builder's nodes (Node.get pads with NaN outside the track): the history is the track's

@@ -123,3 +123,133 @@ def test_oracle_branch_and_bound_is_the_enumerated_optimum():
     assert b["nodes"] < 4 ** T        # the bound prunes
     slack = mo.disjunction_slack(A, rhs, b["X"])
     assert np.all(slack <= 1e-6)      # every disjunction holds at the optimum
+
+
+def _road_scene(T):
+    """Two road polytopes along x (A x <= b): a narrow non-junction lane and a wide junction
+    box overlapping it, and the ego model of _ego_model."""
+    lane = (np.array([[1.0, 0.0], [-1.0, 0.0], [0.0, 1.0], [0.0, -1.0]]),
+            np.array([9.0, 5.0, 1.8, 1.8]))
+    box = (np.array([[1.0, 0.0], [-1.0, 0.0], [0.0, 1.0], [0.0, -1.0]]),
+           np.array([60.0, -6.0, 6.0, 6.0]))
+    return [lane, box], np.array([False, True])
+
+
+def _road_base(T, sbig):
+    """Half-spaces that make the polytope choice matter: a '<=' row slowing the ego (x_t <=
+    2.5 + 3.2 t, which the junction box x >= 6 cannot meet before t = 1) and from t = 2 a '>='
+    row below it; with sbig the lane's S_t = M_big relaxes the first and breaks the second."""
+    base = []
+    for t in range(T):
+        base.append(dict(t=t, n=np.array([1.0, 0.0]), rhs=2.5 + 3.2 * t, side=-1, sbig=sbig))
+        if t >= 2:
+            base.append(dict(t=t, n=np.array([0.0, 1.0]), rhs=-1.0 - 0.1 * t, side=1,
+                             sbig=sbig))
+    return np.array([3.0 * T + 4.0, 3.0]), base
+
+
+@pytest.mark.parametrize("T,sbig", [(2, True), (3, True), (3, False), (4, True)])
+def test_one_polytope_per_step_is_enough(T, sbig):
+    """MilpBnB branches on ONE road polytope per step; the reference's Omicron[:, t] may take
+    any non-empty subset.  The oracle's literal MILP (every subset, every unchosen row with its
+    + M_big relaxation) has the same optimum as the one-polytope restriction, on a scene whose
+    half-spaces carry S_t (sbig: the affine / scale-ideal rows, both sides) or not."""
+    from oracle import mpc_oracle as mo
+    segs, mask = _road_scene(T)
+    xbar, G = _ego_model(T, (0.0, 0.0, 0.0, 6.0))
+    goal, base = _road_base(T, sbig)
+    p = mo.DEFAULT_PARAMS
+    ref = np.stack([np.linspace(1.0, goal[0], T), np.zeros(T)], 1)
+    full = mo.road_milp_enumerate(G, xbar, T, goal, ref, p, base=base, segs=segs, mask=mask,
+                                  subsets=True)
+    one = mo.road_milp_enumerate(G, xbar, T, goal, ref, p, base=base, segs=segs, mask=mask,
+                                 subsets=False)
+    assert full is not None and one is not None
+    assert one["cost"] == pytest.approx(full["cost"], rel=1e-9, abs=1e-9)
+    np.testing.assert_allclose(one["u"], full["u"], atol=1e-6)
+
+
+def test_road_segments_padding():
+    segs, mask = _road_scene(2)
+    tri = (np.array([[1.0, 0.0], [0.0, 1.0], [-1.0, -1.0]]), np.array([1.0, 1.0, 0.0]))
+    rs = milp.RoadSegments(dict(polytopes=segs + [tri], mask=[False, True, True]))
+    assert (rs.I, rs.F) == (3, 4)
+    assert rs.live.sum() == 11 and not rs.live[2, 3]
+    assert rs.any_open
+    with pytest.raises(ValueError):
+        milp.RoadSegments(dict(polytopes=[(np.zeros((2, 2)), np.zeros(3))], mask=[False]))
+
+
+class _OracleBnB(milp.MilpBnB):
+    """MilpBnB's tree with each node's relaxation solved by the oracle's QP from the very
+    records the GPU launch would get (host-only: the branching, relaxation and feasibility
+    logic on CPU)."""
+
+    def __init__(self, G, xbar, T, goal, ref, p, order, **kw):
+        from oracle import mpc_oracle as mo
+        self._mo, self._p, self._order = mo, p, order
+        self._Gf, self._c = mo.state_map(G, xbar, T, T)
+        self._host_init(T, goal, ref, None, 0, T, kw.get("base"), kw.get("faces"),
+                        kw.get("segments"), kw.get("M_big", milp.M_BIG), 64, 1e-7, 100000)
+
+    def _solve_batch(self, nodes):
+        mo, T = self._mo, self.T
+        rec = self._records(nodes)
+        out = []
+        for r in rec:
+            rows = [(int(x["t_tau"]), (-1.0 if x["side"] == 1 else 1.0) * np.array(
+                [x["n0"], x["n1"]]), (-1.0 if x["side"] == 1 else 1.0) * float(x["rhs"]))
+                for x in r.reshape(-1) if x["status"] == 0]
+            s = mo._road_node(self._Gf, self._c, T, self.goal, self.ref, rows, self._p,
+                              self._order)
+            out.append(s)
+        ok = np.array([s is not None for s in out])
+        u = np.array([s["u"] if s else np.zeros(2 * T) for s in out])
+        X = np.array([s["X"] if s else np.zeros((T, 4)) for s in out])
+        cost = np.array([s["cost"] if s else np.inf for s in out])
+        self.stats["launches"] += 1
+        return u, X, cost, ok
+
+
+@pytest.mark.parametrize("T,sbig", [(3, True), (3, False), (4, True)])
+def test_bnb_tree_on_oracle_qps_halfspaces(T, sbig):
+    """The branch and bound's relaxation / branching / incumbent logic with oracle QPs: the
+    same optimum as the oracle's literal MILP over every Omicron subset."""
+    from oracle import mpc_oracle as mo
+    segs, mask = _road_scene(T)
+    goal, base = _road_base(T, sbig)
+    xbar, G = _ego_model(T, (0.0, 0.0, 0.0, 6.0))
+    ref = np.stack([np.linspace(1.0, goal[0], T), np.zeros(T)], 1)
+    want = mo.road_milp_enumerate(G, xbar, T, goal, ref, mo.DEFAULT_PARAMS, base=base,
+                                  segs=segs, mask=mask, subsets=True)
+    rows = dict(n=np.zeros((2, T, 2)), rhs=np.zeros((2, T)), side=np.ones((2, T), int),
+                live=np.zeros((2, T), bool), sbig=np.array([sbig, sbig]))
+    for r in base:
+        j, t = (0 if r["side"] == -1 else 1), r["t"]
+        rows["n"][j, t], rows["rhs"][j, t], rows["side"][j, t] = r["n"], r["rhs"], r["side"]
+        rows["live"][j, t] = True
+    got = _OracleBnB(G, xbar, T, goal, ref, mo.DEFAULT_PARAMS, "F", base=rows,
+                     segments=milp.RoadSegments(dict(polytopes=segs, mask=mask))).solve()
+    assert got["cost"] == pytest.approx(want["cost"], rel=1e-9)
+    np.testing.assert_allclose(got["u"], want["u"], atol=1e-6)
+
+
+def test_bnb_tree_on_oracle_qps_v8_faces_and_road():
+    """v8's face disjunctions and the road polytopes branched together (oracle QPs) against
+    the oracle's enumeration of both; and the faces alone against milp_bnb."""
+    from oracle import mpc_oracle as mo
+    T = 3
+    segs, mask = _road_scene(T)
+    A, rhs = _box_rows(T, [lambda t: (6.5 + 1.0 * t, 0.6)])
+    goal = np.array([14.0, 0.0])
+    xbar, G = _ego_model(T, (0.0, 0.0, 0.0, 6.0))
+    p = mo.v8_qp_params()
+    want = mo.road_milp_enumerate(G, xbar, T, goal, goal.reshape(1, 2), p, faces=(A, rhs),
+                                  segs=segs, mask=mask, order="C", subsets=False)
+    got = _OracleBnB(G, xbar, T, goal, None, p, "C", faces=(A, rhs),
+                     segments=milp.RoadSegments(dict(polytopes=segs, mask=mask))).solve()
+    assert got["cost"] == pytest.approx(want["cost"], rel=1e-9)
+    np.testing.assert_allclose(got["u"], want["u"], atol=1e-6)
+    plain = _OracleBnB(G, xbar, T, goal, None, p, "C", faces=(A, rhs)).solve()
+    ref = mo.milp_bnb(G, xbar, T, goal, A, rhs)
+    assert plain["cost"] == pytest.approx(ref["cost"], rel=1e-9)
