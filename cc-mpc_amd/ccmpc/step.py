@@ -185,6 +185,8 @@ class StepGraph:
                  prev_K=None, T_src=None, n_ideal=1_000_000, source="sampler",
                  pred_device=False):
         self.device = engine.require_device(device)
+        self._dev_index = (self.device.index if self.device.index is not None
+                           else torch.cuda.current_device())
         lib = _lib.load()
         if kind not in ("minkowski", "ideal", "affine"):
             raise ValueError(f"unknown step kind {kind!r}")
@@ -617,7 +619,7 @@ class StepGraph:
             return
         if self.graphs is None:
             self.capture()
-        self.graphs[gen & 1].replay(torch.cuda.current_stream(self.device).cuda_stream)
+        self.graphs[gen & 1].replay(engine._stream(self._dev_index))
 
     def _poll(self, slot, gen, what):
         poll_word(self._flags, slot, gen, self.device, f"planning step {gen}: the {what}")
