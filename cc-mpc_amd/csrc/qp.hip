@@ -19,6 +19,7 @@
 // wave-synchronous, with no workgroup barrier per column.
 #include "ccmpc_common.hpp"
 #include <cstdlib>
+#include <cstring>
 
 namespace ccmpc {
 
@@ -44,6 +45,10 @@ constexpr int kQpRowDoubles = 10;  // doubles per constraint row in the row stor
 // value -x attempts at x but discards even a verified answer, the test hook that checks a failed
 // attempt leaves the IPM bit-identical to a solve without one)
 constexpr double kEarlyPolish = 1e-4;
+// the default method: the active-set solve where it applies (one wave, n <= 16): a T = 8
+// frame's QP 133.8 -> 47.8 us, the 64-scene batch 359 -> 281 us, the same minimiser and
+// verdict on every tested scene (profiles/r05/ab_qp_method.log, tests/test_gpu_qp_gi.py)
+constexpr int kQpDefaultMethod = CCMPC_QP_METHOD_GI;
 
 // ---- the LTV model ---------------------------------------------------------------------------
 // About u = 0 the bicycle model's nominal trajectory is straight at constant speed
@@ -106,6 +111,7 @@ struct QpArgs {
   int T, Tf, n_ref, u_order, rec_kind, max_iter, rows_in_lds, polish;
   int rec_compact;    // records are ccmpc_gather_rec (32 bytes), rec_kind their source kind
   int early_discard;  // test hook: attempt the early polish, never keep its answer
+  int method;         // CCMPC_QP_METHOD_IPM, or _GI (one wave, n <= 16; else the IPM)
   int64_t max_cells;
   double tol, early;  // early: the early polish threshold on mu / max(mu0, 1) (0 = none)
   const double *gamma, *xbar, *ubar, *u_prev, *goal, *ref;
@@ -545,7 +551,7 @@ __device__ __forceinline__ double hctrl_mul(const double *z, int i, int T, int o
 // NW waves per scene: 4 (the general form), or 1 for n = 2T <= 16 (the reference's ph = 8):
 // every barrier is then a wave-level ordering and every reduction a wave butterfly, which
 // takes the ~30 workgroup barriers per IPM iteration off the chain.
-template <bool ROWS_LDS, int NM, int NW>
+template <bool ROWS_LDS, int NM, int NW, bool GI = false>
 __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // multiply-adds fused in the solver (the library builds with -ffp-contract=off for the
   // moments' reference arithmetic; the IPM's iterates carry no such contract, and its answer
@@ -1236,7 +1242,418 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     }
   };
 
-  for (; it <= A.max_iter; ++it) {
+  // ---- Goldfarb-Idnani dual active-set solve (one wave, n <= 16; CCMPC_QP_METHOD_GI) --------
+  // The strictly convex QP  min 1/2 z^T H z + f^T z  s.t.  g_r(z) <= 0  from its unconstrained
+  // minimum: the most violated row (normalised by its gradient's norm) enters the active set,
+  // primal steps along J2 d2 and dual steps along R^{-1} d1 keep the active multipliers >= 0
+  // (dropping a row whose multiplier reaches 0), until no row is violated beyond tol_p (an
+  // exact KKT point: the active rows hold as equalities, every multiplier >= 0) or no step
+  // exists (the rows are infeasible: CCMPC_QP_MAXITER, the reference's solve failure).  H =
+  // L L^T, J = L^{-T} rotated so that J^T N_A = [R; 0] (Givens rotations as rows enter and
+  // leave).  J lives in M's storage (row-major, stride ldm), R in the polish's S (row-major,
+  // upper triangle), the active rows and multipliers in the polish's act / dinv slots, the
+  // row norms and active flags in the IPM's row arrays is / dl.  A solve that exceeds its step
+  // budget or meets a non-finite value hands the problem to the IPM (returns false, z = y = 0).
+  // Each active-set change is a handful of wave-wide LDS phases, and a T = 8 frame enters only
+  // a few rows, where the IPM spends ~5 iterations and a polish (~130 us).
+  bool gi_done = false;
+  if constexpr (GI && NW == 1 && NM == 16) {
+    auto gi_solve = [&]() -> bool {
+#ifdef CCMPC_QP_TRACE
+      uint64_t gmark[6] = {}, gacc[6] = {}, gt = 0;
+#define GI_MARK(i) (gmark[i] = wall_clock64())
+#define GI_T0() (gt = wall_clock64())
+#define GI_ACC(k)                         \
+  do {                                    \
+    const uint64_t gn_ = wall_clock64();  \
+    gacc[k] += gn_ - gt;                  \
+    gt = gn_;                             \
+  } while (0)
+#else
+#define GI_MARK(i) ((void)0)
+#define GI_T0() ((void)0)
+#define GI_ACC(k) ((void)0)
+#endif
+      GI_MARK(0);
+      double *Jm = M, *Rm = lds + lay.ps, *actv = lds + lay.pact, *uact = lds + lay.pdinv;
+      const double *fu = lds + lay.f;
+      double *inorm = rw.is, *aflag = rw.dl;
+      const int li = lane < n ? lane : 0;
+      auto gcol = [&](int i, int j) -> double {  // d v[i] / d z_j
+        return i < T3 ? Gs[i * n + j] : (i - T3 == j ? 1.0 : 0.0);
+      };
+      auto update_y = [&]() {  // y = Gs z (the output rows' linear part)
+        wave_sync();
+        if (lane < T3) {
+          double v = 0.0;
+  #pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (j < n) v = fma(Gs[lane * n + j], z[j], v);
+          y[lane] = v;
+        }
+        wave_sync();
+      };
+      auto give_up = [&]() -> bool {  // back to the IPM's starting point
+        wave_sync();
+        if (lane < n) z[lane] = 0.0;
+        if (lane < T3) y[lane] = 0.0;
+        for (int64_t r = lane; r < mrows; r += 64) rw.is[r] = 1.0 / rw.s[r];
+        wave_sync();
+        return false;
+      };
+      // H (no barrier terms) into M's lower triangle, as the polish builds it
+      {
+        const int jm = lane & 15, jc = jm < n ? jm : 0;
+        double hx[8], hy[8];
+  #pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int tt = t < T ? t : 0;
+          const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+          hx[t] = t < T ? wp * Gs[(3 * tt) * n + jc] : 0.0;
+          hy[t] = t < T ? wp * Gs[(3 * tt + 1) * n + jc] : 0.0;
+        }
+  #pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int im = (lane >> 4) + 4 * m;
+          const bool on = im < n && jm <= im;
+          const int ic = on ? im : 0;
+          double v = Hc[ic * n + jc];
+  #pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int tt = t < T ? t : 0;
+            v = fma(Gs[(3 * tt) * n + ic], hx[t], fma(Gs[(3 * tt + 1) * n + ic], hy[t], v));
+          }
+          if (on) M[im * ldm + jm] = v;
+        }
+      }
+      wave_sync();
+      double La[16], Ldl = 0.0;
+  #pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const double v = M[li * ldm + (k < n ? k : 0)];
+        La[k] = (lane < n && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
+      }
+      if (reg_cholesky<16, false>(La, Ldl)) return give_up();
+      GI_MARK(1);
+      // L (rows) and 1 / L_ii into R's storage (free until the first row enters) for the
+      // column-parallel inverse below
+      double *Ls = Rm, *Ldi = lds + lay.dinv;
+      if (lane < n) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k <= lane && k < n) Ls[lane * ldm + k] = La[k];
+        Ldi[lane] = Ldl;
+      }
+      wave_sync();  // (every read of H is done too: J overwrites it)
+      GI_MARK(2);
+      // J = L^{-T}: lane c solves L x = e_c (all columns at once, L's entries broadcast from
+      // LDS), x_k = L^{-1}[k][c] = J[c][k] -- lane c ends with row c of J
+      double Jrow[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        double acc = (k == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = 0; j < k; ++j)
+          if (k < n) acc = fma(-Ls[k * ldm + j], Jrow[j], acc);
+        Jrow[k] = k < n ? acc * Ldi[k < n ? k : 0] : 0.0;
+      }
+      if (lane < n) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k < n) Jm[lane * ldm + k] = Jrow[k];
+      }
+      // row gradient norms (the violation's scale) from each step's output-row Gram: an
+      // obstacle row's gradient is a0 Gs_x(t) + a1 Gs_y(t), a speed row's +-Gs_v(t), a box
+      // row's +-e_j
+      double *Ngr = bw;  // (the IPM's per-step weights: recomputed in its I1)
+      if (lane < T) {
+        double xx = 0.0, xy = 0.0, yy = 0.0, vv = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (j >= n) continue;
+          const double gx = Gs[(3 * lane) * n + j], gy = Gs[(3 * lane + 1) * n + j],
+                       gv = Gs[(3 * lane + 2) * n + j];
+          xx = fma(gx, gx, xx);
+          xy = fma(gx, gy, xy);
+          yy = fma(gy, gy, yy);
+          vv = fma(gv, gv, vv);
+        }
+        Ngr[4 * lane] = xx;
+        Ngr[4 * lane + 1] = xy;
+        Ngr[4 * lane + 2] = yy;
+        Ngr[4 * lane + 3] = vv;
+      }
+      wave_sync();
+      for (int64_t r = lane; r < mrows; r += 64) {
+        const int2 ix = reinterpret_cast<const int2 *>(rw.ix)[r];
+        const double a0 = rw.c0[r], a1 = rw.c1[r];
+        double s2;
+        if (ix.x >= T3) {
+          s2 = a0 * a0 + a1 * a1;                        // a box row (i0 == i1)
+        } else {
+          const int t = ix.x / 3;
+          s2 = (ix.x % 3 == 2) ? (a0 + a1) * (a0 + a1) * Ngr[4 * t + 3]
+                               : a0 * a0 * Ngr[4 * t] + 2.0 * a0 * a1 * Ngr[4 * t + 1] +
+                                     a1 * a1 * Ngr[4 * t + 2];
+        }
+        inorm[r] = s2 > 0.0 ? 1.0 / sqrt(s2) : 0.0;
+        aflag[r] = 0.0;
+      }
+      GI_MARK(3);
+      // the unconstrained minimum z = -J L^{-1} f (the forward solve on lane = row, then each
+      // lane's row of J against it)
+      {
+        const double y0 = reg_forward<16>(La, Ldl, lane < n ? fu[lane] : 0.0);
+        double zi = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k < n) zi = fma(Jrow[k], lane_bcast(y0, k), zi);
+        wave_sync();
+        if (lane < n) z[lane] = -zi;
+      }
+      update_y();
+      GI_MARK(4);
+      int q = 0, steps = 0;
+      const int max_steps = 8 * (n + 16);
+      double *Rdi = lds + lay.dinv;  // 1 / R[k][k] (L's reciprocals are no longer needed)
+      // J stays in registers (lane i: row i, every rotation local); its LDS mirror serves the
+      // column reads of d = J^T m
+      auto store_j = [&]() {
+        if (lane < n) {
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (k < n) Jm[lane * ldm + k] = Jrow[k];
+        }
+      };
+      // a Givens rotation zeroing b against a: c = a / h, s = b / h, h = |(a, b)|, from the
+      // hardware rsqrt with one Newton step (the rotation chain is serial; IEEE sqrt and two
+      // divisions per rotation were most of an active-set change)
+      auto givens = [](double a, double b, double &c, double &s, double &h) {
+        const double n2 = fma(a, a, b * b);
+        if (!(n2 > 0.0)) {
+          c = 1.0;
+          s = 0.0;
+          h = 0.0;
+          return;
+        }
+        double y = __builtin_amdgcn_rsq(n2);
+        y = y * fma(-0.5 * n2 * y, y, 1.5);
+        c = a * y;
+        s = b * y;
+        h = n2 * y;
+      };
+      while (true) {
+        GI_T0();
+        // the most violated row (normalised by its gradient), inactive rows only
+        double best = 0.0, bidx = -1.0, cviol = 0.0;
+#pragma unroll 2
+        for (int64_t r = lane; r < mrows; r += 64) {
+          const int2 ix = reinterpret_cast<const int2 *>(rw.ix)[r];
+          const double g = row_g(r, y, z);
+          const double inr = inorm[r];
+          const bool on = aflag[r] == 0.0 && g > tol_p;
+          if (!isfinite(g)) cviol = 2.0;
+          if (on && inr == 0.0) cviol = fmax(cviol, 1.0);  // a violated constant row
+          const double v = g * inr;
+          if (on && v > best) {
+            best = v;
+            bidx = static_cast<double>(r);
+          }
+          (void)ix;
+        }
+        block_argmax<1>(best, bidx, red);
+        const double cv = wave_max(cviol);
+        GI_ACC(0);
+        if (cv >= 2.0) return give_up();
+        if (cv > 0.0) {  // no point satisfies it: infeasible
+          status = CCMPC_QP_MAXITER;
+          infeasible = true;
+          it = steps;
+          return true;
+        }
+        if (bidx < 0.0) break;  // every row holds: optimal
+        const int64_t pr = static_cast<int64_t>(bidx);
+        const int2 pix = reinterpret_cast<const int2 *>(rw.ix)[pr];
+        const double pc0 = rw.c0[pr], pc1 = rw.c1[pr];
+        // the entering row as m . z >= beta (m = -grad g): m_j on lane j
+        const double mj = lane < n ? -(pc0 * gcol(pix.x, li) + pc1 * gcol(pix.y, li)) : 0.0;
+        double sp = -row_g(pr, y, z);  // its slack (< 0)
+        double uplus = 0.0;
+        double mm[16];  // m, uniform (fixed while this row enters)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mm[i] = lane_bcast(mj, i);
+        while (true) {
+          if (++steps > max_steps) return give_up();
+          // d = J^T m (lane j), r = R^{-1} d[:q] (lane k < q)
+          double dj = 0.0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (i < n) dj = fma(Jm[i * ldm + li], mm[i], dj);
+          double rhs = dj, rk = 0.0;
+          for (int j = q - 1; j >= 0; --j) {
+            const double xj = lane_bcast(rhs, j) * Rdi[j];
+            if (lane == j) rk = xj;
+            if (lane < j) rhs = fma(-Rm[lane * ldm + j], xj, rhs);
+          }
+          GI_ACC(1);
+          double dd[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) dd[k] = lane_bcast(dj, k);
+          double d2 = 0.0, dn2 = 0.0, zi = 0.0;
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            if (k >= n) continue;
+            dn2 = fma(dd[k], dd[k], dn2);
+            if (k >= q) {
+              d2 = fma(dd[k], dd[k], d2);
+              zi = fma(Jrow[k], dd[k], zi);  // J2 d2: the primal direction
+            }
+          }
+          if (!isfinite(dn2)) return give_up();
+          const bool zero_step = !(d2 > 1e-24 * dn2);
+          // partial step: the first active multiplier to reach 0 (smallest lane on ties)
+          const double ratio =
+              (lane < q && rk > 0.0) ? uact[lane < q ? lane : 0] / rk : INFINITY;
+          const double t1 = wave_min(ratio);
+          const int l =
+              t1 < INFINITY
+                  ? __ffsll(static_cast<long long>(__ballot(lane < q && ratio == t1))) - 1
+                  : -1;
+          const double t2 = zero_step ? INFINITY : -sp / d2;
+          if (!(t1 < INFINITY) && !(t2 < INFINITY)) {  // no step: infeasible
+            status = CCMPC_QP_MAXITER;
+            infeasible = true;
+            it = steps;
+            return true;
+          }
+          GI_ACC(2);
+          const double t = fmin(t1, t2);
+          wave_sync();
+          if (lane < q) uact[lane] -= t * rk;
+          if (!zero_step && lane < n) z[lane] += t * zi;
+          uplus += t;
+          if (!zero_step) sp = fma(t, d2, sp);
+          const bool full = !zero_step && t2 <= t1;
+          if (full) {
+            // add the row: rotate d[q:] onto d[q] (J's columns q .. n-1), R's new column
+            double dv[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dv[k] = dd[k];
+#pragma unroll
+            for (int j = 15; j >= 1; --j) {
+              if (j >= n || j <= q) continue;
+              double c, s, h;
+              givens(dv[j - 1], dv[j], c, s, h);
+              dv[j - 1] = h;
+              dv[j] = 0.0;
+              const double x0 = Jrow[j - 1], x1 = Jrow[j];
+              Jrow[j - 1] = fma(c, x0, s * x1);
+              Jrow[j] = fma(-s, x0, c * x1);
+            }
+            double rqq = 0.0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+              if (k == q) rqq = dv[k];
+            if (rqq < 0.0) {
+              rqq = -rqq;
+#pragma unroll
+              for (int k = 0; k < 16; ++k)
+                if (k == q) Jrow[k] = -Jrow[k];
+            }
+            if (!(rqq > 1e-300)) return give_up();  // dependent row with a primal step
+            wave_sync();
+            store_j();
+            if (lane < q) Rm[lane * ldm + q] = dj;
+            if (lane == q) {
+              Rm[q * ldm + q] = rqq;
+              Rdi[q] = 1.0 / rqq;
+              actv[q] = static_cast<double>(pr);
+              uact[q] = uplus;
+            }
+            if (lane == 0) aflag[pr] = 1.0;
+            ++q;
+            GI_ACC(3);
+            update_y();
+            GI_ACC(5);
+            break;
+          }
+          // drop active row l: R's columns l+1 .. q-1 shift left (lane = column), then
+          // rotations on rows (k, k+1), k = l .. q-2, restore the triangle; J's columns
+          // (k, k+1) likewise
+          double Rc[16];
+          {
+            const int col = (lane >= l && lane < q - 1) ? lane + 1 : (lane < q ? lane : 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) Rc[i] = (i < q) ? Rm[i * ldm + col] : 0.0;
+          }
+          for (int k = l; k < q - 1; ++k) {
+            double a = 0.0, b = 0.0;
+#pragma unroll
+            for (int i = 0; i < 15; ++i)
+              if (i == k) {
+                a = Rc[i];
+                b = Rc[i + 1];
+              }
+            double c, s, h;
+            givens(lane_bcast(a, k), lane_bcast(b, k), c, s, h);
+#pragma unroll
+            for (int i = 0; i < 15; ++i)
+              if (i == k) {
+                const double r0 = Rc[i], r1 = Rc[i + 1];
+                Rc[i] = fma(c, r0, s * r1);
+                Rc[i + 1] = fma(-s, r0, c * r1);
+                const double x0 = Jrow[i], x1 = Jrow[i + 1];
+                Jrow[i] = fma(c, x0, s * x1);
+                Jrow[i + 1] = fma(-s, x0, c * x1);
+              }
+          }
+          double rdg = 1.0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (i == lane) rdg = Rc[i];
+          const double act_next = actv[(lane + 1 < q ? lane + 1 : 0)];
+          const double u_next = uact[(lane + 1 < q ? lane + 1 : 0)];
+          const double dropped = actv[l];
+          wave_sync();
+          if (lane < q - 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (i <= lane) Rm[i * ldm + lane] = Rc[i];
+            Rdi[lane] = 1.0 / rdg;
+            if (lane >= l) {
+              actv[lane] = act_next;
+              uact[lane] = u_next;
+            }
+          }
+          store_j();
+          if (lane == 0) aflag[static_cast<int64_t>(dropped)] = 0.0;
+          --q;
+          GI_ACC(4);
+          update_y();
+          GI_ACC(5);
+          if (!zero_step) sp = -row_g(pr, y, z);  // the entering row's slack at the new point
+        }
+      }
+      status = 0;
+      it = steps;
+#ifdef CCMPC_QP_TRACE
+      GI_MARK(5);
+      if (tid == 0 && sc == 0)
+        printf("gi phases (10ns): H+chol %d L %d J+norms %d z0 %d loop %d (steps %d, q %d)\n"
+               "   loop: scan %d d+r %d dir+ratios %d add %d drop %d update_y %d\n",
+               int(gmark[1] - gmark[0]), int(gmark[2] - gmark[1]), int(gmark[3] - gmark[2]),
+               int(gmark[4] - gmark[3]), int(gmark[5] - gmark[4]), steps, q, int(gacc[0]),
+               int(gacc[1]), int(gacc[2]), int(gacc[3]), int(gacc[4]), int(gacc[5]));
+#endif
+#undef GI_MARK
+#undef GI_T0
+#undef GI_ACC
+      return true;
+    };
+    if (A.polish) gi_done = gi_solve();
+  }
+
+  for (; !gi_done && it <= A.max_iter; ++it) {
     QP_MARK(0);
     // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
     double rpmax = 0.0, sl = 0.0;
@@ -1579,7 +1996,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk2 = wall_clock64();
 #endif
-  if (A.polish && !infeasible && !polished) polished = polish(true);
+  if (A.polish && !infeasible && !polished && !gi_done) polished = polish(true);
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk3 = wall_clock64();
 #endif
@@ -1651,18 +2068,18 @@ inline QpPlan qp_plan(int T, int64_t R) {
   return {false, false};
 }
 
-template <bool ROWS_LDS, int NM, int NW>
+template <bool ROWS_LDS, int NM, int NW, bool GI = false>
 hipError_t launch_qp(dim3 grid, size_t lds, hipStream_t s, const QpArgs &a) {
   const dim3 block(64 * NW);
   // the dynamic-LDS limit is a per-device attribute: set it on every launch (cheap), so a
   // process that drives several devices raises it on each, and report a failure as such
   if (lds > 48 * 1024) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM, NW>),
+        reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM, NW, GI>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kQpLdsBytes));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM, NW>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM, NW, GI>), grid, block, lds, s, a);
   return hipSuccess;
 }
 
@@ -1739,6 +2156,11 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   a.rows_in_lds = in_lds;
   a.polish = plan.polish;
   {
+    const char *e = getenv("CCMPC_QP_METHOD");  // per call (tests switch it)
+    a.method = (e && strcmp(e, "ipm") == 0) ? CCMPC_QP_METHOD_IPM
+               : (e && strcmp(e, "gi") == 0) ? CCMPC_QP_METHOD_GI : kQpDefaultMethod;
+  }
+  {
     const char *e = getenv("CCMPC_QP_EARLY_POLISH");  // per call (a test switches it)
     const double v = e ? atof(e) : kEarlyPolish;
     a.early = fabs(v);
@@ -1777,7 +2199,11 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   const dim3 grid(static_cast<unsigned>(n_scenes));
   hipStream_t s = as_stream(stream);
   hipError_t attr;
-  if (in_lds) {
+  const bool gi = one_wave && a.method == CCMPC_QP_METHOD_GI && plan.polish;
+  if (gi) {
+    attr = in_lds ? launch_qp<true, 16, 1, true>(grid, lds, s, a)
+                  : launch_qp<false, 16, 1, true>(grid, lds, s, a);
+  } else if (in_lds) {
     attr = one_wave ? launch_qp<true, 16, 1>(grid, lds, s, a)
                     : (nm == 16 ? launch_qp<true, 16, 4>(grid, lds, s, a)
                                 : launch_qp<true, 0, 4>(grid, lds, s, a));

@@ -473,6 +473,13 @@ int ccmpc_l4_split(const void *positions, int dtype, int64_t ld, int64_t T, cons
 #define CCMPC_QP_NUMERIC 2      /* the objective's Hessian is not positive definite       */
 #define CCMPC_QP_SKIPPED_ROWS 4 /* flag: records with status != 0 were left out */
 
+/* QP method (environment CCMPC_QP_METHOD = "gi" / "ipm", read per ccmpc_mpc_qp call):
+ * the Goldfarb-Idnani dual active-set method for n = 2T <= 16 (one wave per scene), the
+ * Mehrotra interior point + active-set polish otherwise (and where the active-set solve
+ * exceeds its step budget).  Both return the problem's unique minimiser (strictly convex). */
+#define CCMPC_QP_METHOD_IPM 0
+#define CCMPC_QP_METHOD_GI 1
+
 typedef struct ccmpc_mpc_params {
   double w_final, w_ref;                     /* objective weights (:93-102)          */
   double w_accel, w_joint, w_turning;        /* R1                                   */

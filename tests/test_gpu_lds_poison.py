@@ -32,8 +32,10 @@ def _same_under_fills(run):
     return outs[0]
 
 
+@pytest.mark.parametrize("method", ["gi", "ipm"])
 @pytest.mark.parametrize("T,kind", [(8, "halfspace"), (8, "affine"), (12, "halfspace")])
-def test_planning_qp_ignores_stale_lds(gpu, T, kind):
+def test_planning_qp_ignores_stale_lds(gpu, monkeypatch, T, kind, method):
+    monkeypatch.setenv("CCMPC_QP_METHOD", method)      # (n > 16: the interior point either way)
     # binding and infeasible scenes, and one whose obstacles pass far off the path (few or no
     # active rows at the optimum: the polish's empty-active-set case)
     scenes = [(s, 8.0) for s in pick_seeds("binding", 3, T) + pick_seeds("infeasible", 1, T)]

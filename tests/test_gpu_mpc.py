@@ -330,6 +330,7 @@ def test_planning_qp_step_equals_the_direct_solve(gpu, T):
 
 
 def _solve_with_env(monkeypatch, value, seeds, T, gpu, rec_in=None):
+    monkeypatch.setenv("CCMPC_QP_METHOD", "ipm")      # the interior point's own path
     if value is None:
         monkeypatch.delenv("CCMPC_QP_EARLY_POLISH", raising=False)
     else:

@@ -1,0 +1,79 @@
+"""The Goldfarb-Idnani active-set solve of the planning QP (CCMPC_QP_METHOD=gi, one wave per
+scene for n = 2T <= 16) against the interior point + polish (=ipm) and the oracle: the QP is
+strictly convex, so both methods must return its unique minimiser and the same verdict on
+every scene (u within 1e-7 (1 + |u|), the objective within 1e-9 relative)."""
+import numpy as np
+import pytest
+import torch
+
+from ccmpc import mpc
+from test_gpu_mpc import LON, _check, _oracle_solve, _params_dict, _scene_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(monkeypatch, method, cps, T, kind, order, gamma, xbar, goals, refs, rec, **kw):
+    monkeypatch.setenv("CCMPC_QP_METHOD", method)
+    qp = mpc.PlanningQP(cps, T, kind=kind, u_order=order, **kw)
+    out = qp.solve(gamma, xbar, goals, refs, rec, u_prev=kw.get("u_prev_t"))
+    return [o.cpu().numpy() for o in out]
+
+
+@pytest.mark.parametrize("kind", ["halfspace", "affine"])
+@pytest.mark.parametrize("order", [mpc.U_ORDER_F, mpc.U_ORDER_C])
+def test_gi_equals_ipm_on_many_scenes(gpu, monkeypatch, kind, order):
+    T = 8
+    seeds = list(range(100, 148))
+    rec, cps, o_recs, refs, goals, x0s = _scene_inputs(seeds, T, gpu, kind=kind)
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    g_t, r_t = torch.as_tensor(goals, device=gpu), torch.as_tensor(refs, device=gpu)
+    k = mpc.REC_HALFSPACE if kind == "halfspace" else mpc.REC_AFFINE
+    u0, X0, c0, s0, _ = _solve(monkeypatch, "ipm", cps, T, k, order, gamma, xbar, g_t, r_t, rec)
+    u1, X1, c1, s1, i1 = _solve(monkeypatch, "gi", cps, T, k, order, gamma, xbar, g_t, r_t, rec)
+    np.testing.assert_array_equal(s1, s0)
+    ok = s0 == mpc.QP_OK
+    assert ok.sum() >= 4 and (~ok).sum() >= 1          # both verdicts exercised
+    for i in np.flatnonzero(ok):
+        tol = 1e-7 * (1.0 + np.abs(u0[i]).max())
+        assert np.abs(u1[i] - u0[i]).max() <= tol, (seeds[i], np.abs(u1[i] - u0[i]).max())
+        assert c1[i] == pytest.approx(c0[i], rel=1e-9)
+    prm = _params_dict(mpc.MPCParams.reference_defaults())
+    for i in np.flatnonzero(ok)[:8]:
+        want = _oracle_solve(x0s[i], T, goals[i], refs[i], o_recs[i], kind, prm,
+                             order="F" if order == mpc.U_ORDER_F else "C")
+        assert want["feasible"]
+        _check(u1[i], X1[i], float(c1[i]), want, T)
+
+
+def test_gi_shrinking_horizon_with_executed_controls(gpu, monkeypatch):
+    """T < T_full (u_prev in the state's constant part): the same minimiser by both methods."""
+    from ccmpc import cycle, engine
+    from _qp_inputs import crossing_scene as cs
+    Tf, T = 8, 5
+    seeds = list(range(100, 116))
+    rec, cps, goals, refs, x0s = [], [], [], [], []
+    for s in seeds:
+        ovs, cells, K, ref, goal, x0 = cs(s, T=Tf)
+        store = engine.ParticleStore.from_cells([c[:, :T] for c in cells], device=gpu)
+        cyc = cycle.MinkowskiCycle(store, K, ref[:T])
+        cyc.run()
+        rec.append(cyc.rec)
+        cps.append(len(cells))
+        goals.append(goal)
+        refs.append(ref[:T])
+        x0s.append(x0)
+    rec = torch.cat(rec, 0).contiguous()
+    u_prev = torch.as_tensor(np.random.default_rng(3).normal(0, 0.3, (len(seeds), 2 * (Tf - T))),
+                             device=gpu)
+    xbar, gamma = mpc.ltv(np.array(x0s), Tf, lon=LON)
+    g_t = torch.as_tensor(np.array(goals), device=gpu)
+    r_t = torch.as_tensor(np.array(refs), device=gpu)
+    res = {}
+    for m in ("ipm", "gi"):
+        monkeypatch.setenv("CCMPC_QP_METHOD", m)
+        qp = mpc.PlanningQP(cps, T, T_full=Tf)
+        res[m] = [o.cpu().numpy() for o in qp.solve(gamma, xbar, g_t, r_t, rec, u_prev=u_prev)]
+    np.testing.assert_array_equal(res["gi"][3], res["ipm"][3])
+    for i in np.flatnonzero(res["ipm"][3] == mpc.QP_OK):
+        tol = 1e-7 * (1.0 + np.abs(res["ipm"][0][i]).max())
+        assert np.abs(res["gi"][0][i] - res["ipm"][0][i]).max() <= tol
