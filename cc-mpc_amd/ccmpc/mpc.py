@@ -184,9 +184,23 @@ class PlanningQPStep:
         """Enqueue the frame on the current stream and wait for its answer on the host:
         {cost, U_star (T, 2), X_star (T, 4), u (2T,), status, iters}.  ltv: rebuild xbar /
         gamma from x_init first (Tsh == ph)."""
-        from . import step
+        return self.wait(self.launch(x_init, goal, ref_traj, rec, xbar, gamma, u_prev=u_prev,
+                                     ltv=ltv, Ts=Ts, lon=lon))
+
+    def launch(self, x_init, goal, ref_traj, rec, xbar, gamma, u_prev=None, ltv=False, Ts=0.5,
+               lon=3.7):
+        """solve() without the wait: enqueue the frame on the current stream (behind whatever
+        writes `rec` there) and return its generation for wait()."""
+        gen = self.prepare(x_init, goal, ref_traj, u_prev)
+        self.enqueue(rec, xbar, gamma, ltv=ltv, Ts=Ts, lon=lon)
+        return gen
+
+    def prepare(self, x_init, goal, ref_traj, u_prev=None):
+        """The host half of launch(): the frame's inputs into the pinned pack and a new
+        generation (returned); enqueue() -- or a captured graph holding its calls -- moves
+        them to the device."""
         T, Tf = self.T, self.T_full
-        i, o, lib, p = self.inp, self.out, _lib.load(), engine._p
+        i = self.inp
         i.h("x0")[0] = np.asarray(x_init, np.float64).reshape(4)
         i.h("ref")[0] = np.asarray(ref_traj, np.float64)[:T].reshape(T, 2)
         i.h("goal")[0] = np.asarray(goal, np.float64).reshape(2)
@@ -195,8 +209,15 @@ class PlanningQPStep:
                 raise ValueError("u_prev (the executed controls) is required when T < T_full")
             i.h("uprev")[0] = np.asarray(u_prev, np.float64).reshape(2 * (Tf - T))
         self.generation += 1
-        gen = self.generation
-        i.h("gen")[0] = gen
+        i.h("gen")[0] = self.generation
+        return self.generation
+
+    def enqueue(self, rec, xbar, gamma, ltv=False, Ts=0.5, lon=3.7):
+        """The device half of launch() on the current stream (capturable: every call reads
+        the packs at run time): the inputs up, the LTV rebuild (ltv), the QP on `rec`, the
+        answer down and the signal of the pack's generation."""
+        T, Tf = self.T, self.T_full
+        i, o, lib, p = self.inp, self.out, _lib.load(), engine._p
         s = engine._stream()
         chk = _lib.check
         chk(lib.ccmpc_copy_kernel_async(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
@@ -207,6 +228,15 @@ class PlanningQPStep:
                       u_prev=i.d("uprev") if T < Tf else None)
         chk(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
                                         p(i.d("gen")), s), "ccmpc_copy_signal_async")
+
+    def wait(self, gen):
+        """The answer of launch `gen` on the host (it must be the latest launch: the output pack
+        is this step's)."""
+        from . import step
+        T = self.T
+        if gen != self.generation:
+            raise RuntimeError(f"planning QP {gen}: overwritten by launch {self.generation}")
+        o = self.out
         step.poll_word(self._flags, 0, gen, self.device, f"planning QP {gen}: the")
         u = o.h("u")[0].copy()
         U = u.reshape(2, T).T.copy() if self.u_order == U_ORDER_F else u.reshape(T, 2).copy()

@@ -481,6 +481,8 @@ class MidlevelAgent:
         self.last_records = None
         self._last_rec = None              # (device records, kind, T) of the last generator
         self._last_sbig = False            # do its rows carry S_big (road boundaries)?
+        self._qp_request = None            # the frame's QP inputs, set before its step graph
+        self._qp_pending = None            # ((run, gen), records, (T, u_order)) enqueued
         self.mpc_params = mpc.MPCParams.reference_defaults(self.mpc_params_steer)
         self._ltv = None                   # (x_init, T_full) -> (xbar, Gamma), first step's
         self._qp = {}
@@ -539,6 +541,9 @@ class MidlevelAgent:
         for key, g in self._graphs.items():
             step.pool_give(self.device, key + (self.R,), g)
         self._graphs.clear()
+        if self._ltv is not None:
+            step.ltv_give(self.device, self.prediction_horizon, self._ltv)
+            self._ltv = None
 
     def get_goal(self):
         """:344-345: a copy, as an attribute dict (harness code writes goal.x / goal.y)."""
@@ -1134,6 +1139,20 @@ class MidlevelAgent:
             extra = dict(prev_K=tuple(prev[2]), T_src=int(prev[3]), n_ideal=self.n_ideal)
         key = (kind, O, N, ph, T, L, tuple(K), pp, eps_in is not None, source, pred_dev) + tuple(
             sorted(extra.items()))
+        req, self._qp_request = self._qp_request, None
+        if req is not None and (req["T"] != T or (T < ph and req["u_prev"] is None)):
+            req = None
+        if req is not None:
+            # the frame's QP inside the graph, right after the record path (before L4): the
+            # records are final there and the answer is back before the host has built the
+            # 9-tuple.  What the capture bakes in is in the key: the LTV buffers (this agent's,
+            # so a pooled graph only serves the agent that took these buffers), whether the
+            # frame rebuilds them, the QP parameters, Ts and the ego length
+            xbar, gamma = self._ltv_buffers()
+            build = T == ph or not self._ltv_built
+            rec_kind = mpc.REC_AFFINE if kind == "affine" else mpc.REC_HALFSPACE
+            key += ("qp", rec_kind, build, bytes(self.mpc_params), id(xbar),
+                    float(self.steptime), float(req["lon"]))
         g = self._graphs.pop(key, None)
         if g is None:
             g = step.pool_take(self.device, key + (self.R,))
@@ -1144,6 +1163,11 @@ class MidlevelAgent:
             while self._graphs and len(self._graphs) >= self.max_graphs:
                 self._graphs.popitem(last=False)           # least recently used
         self._graphs[key] = g                              # most recently used
+        if req is not None and g.qp is None:
+            g.attach_qp(mpc.PlanningQPStep(g.out.d("rec").shape[0], T, ph, kind=rec_kind,
+                                           params=self.mpc_params, u_order=mpc.U_ORDER_F,
+                                           device=self.device),
+                        xbar, gamma, build, Ts=self.steptime, lon=req["lon"])
         g.set_inputs(seed, init, pmf, None if pp else gmm, minpos, ref_traj,
                      self._cell_risk_host(np.asarray(eps_ura), K), past_last, bboxes,
                      filter_pmf=filter_pmf)
@@ -1155,7 +1179,13 @@ class MidlevelAgent:
             g.set_device_inputs(gmm, z_in, eps_in)
         if source == "predictions":
             g.set_predictions(sampler["predictions"], sampler["z"], sampler.get("rows"))
+        if req is not None:
+            run = g.qp["step"]
+            qgen = run.prepare(req["x_init"], req["goal"], req["ref"], req["u_prev"])
         g.launch()
+        if req is not None:
+            self._ltv_built = True
+            self._qp_pending = ((run, qgen), g.out.d("rec"), (T, mpc.U_ORDER_F))
         # host objects that need no output are built while the graph runs
         st = g.store
         scene = ovehicle.ScenePredictions(st, K, past_last, bboxes)
@@ -1227,13 +1257,27 @@ class MidlevelAgent:
         python-utility is absent, restated), timeout False (the QP has no time limit here).
         Raises InSimulationException where the reference's CPLEX solve fails (:3099-3110).  The
         frame's 9-tuple and QP result stay on the agent (last_generator_output, last_ctrl)."""
-        from . import episode
         T, ph = int(Tsh), self.prediction_horizon
         pmf = np.asarray(sampler["latent_pmf"], np.float64)
-        O = pmf.shape[0]
         fp = float(sampler.get("filter_pmf", 0.1))     # one value for K, the graph and buckets
         if T == ph:
             self._u_prev = []
+        up = np.concatenate(self._u_prev) if (T < ph and self._u_prev) else None
+        self._qp_pending = None
+        if not self.road_boundary_constraints:    # the QP's inputs are known before the step
+            self._qp_request = dict(T=T, x_init=np.asarray(x_init, np.float64), goal=goal,
+                                    ref=ref_traj, u_prev=up, lon=self.ego_lon)
+        try:
+            return self._prediction_controls(frame, T, shrinking, sampler, minpos, pasts,
+                                             x_init, goal, ref_traj, bboxes, apply_robust,
+                                             segments, pmf, fp, up)
+        finally:
+            self._qp_request = None
+
+    def _prediction_controls(self, frame, T, shrinking, sampler, minpos, pasts, x_init, goal,
+                             ref_traj, bboxes, apply_robust, segments, pmf, fp, up):
+        from . import episode
+        O = pmf.shape[0]
         if shrinking and apply_robust:
             K = (pmf > fp).sum(1).tolist()
             eps_ura = np.full((O, max(K)), 0.05 / O)              # :2909-2916
@@ -1249,7 +1293,6 @@ class MidlevelAgent:
             ovs, out = self.predict_and_constrain_affine(params, sampler, eps_ura, T, ref_traj,
                                                          minpos, pasts, bboxes, filter_pmf=fp)
         self.last_generator_output = (ovs, out)
-        up = np.concatenate(self._u_prev) if (T < ph and self._u_prev) else None
         ctrl = self.solve_planning_qp(x_init, goal, ref_traj, T, u_prev=up, lon=self.ego_lon,
                                       segments=segments)
         self.last_ctrl = ctrl
@@ -1282,12 +1325,19 @@ class MidlevelAgent:
         if self.road_boundary_constraints:
             return self._solve_road_milp(x_init, goal, ref_traj, T, rec, kind, u_prev, lon,
                                          u_order, segments)
-        if self._ltv is None:               # device buffers, rebuilt in place at Tsh == ph
-            self._ltv = (torch.empty((1, 4 * ph), dtype=torch.float64, device=self.device),
-                         torch.empty((1, 4 * ph, 2 * ph), dtype=torch.float64,
-                                     device=self.device))
-            self._ltv_built = False
-        xbar, gamma = self._ltv
+        pend, self._qp_pending = self._qp_pending, None
+        if pend is not None and pend[1] is rec and pend[2] == (T, u_order):
+            run, gen = pend[0]            # enqueued behind the step graph (_graph_step)
+        else:
+            run, gen = self._qp_launch(x_init, goal, ref_traj, T, rec, kind, u_prev, lon,
+                                       u_order)
+        return self._qp_result(run.wait(gen), goal)
+
+    def _qp_launch(self, x_init, goal, ref_traj, T, rec, kind, u_prev, lon, u_order):
+        """Enqueue solve_planning_qp's device work on the current stream (no wait): the LTV
+        rebuild at Tsh == ph, the QP on `rec`, the answer's copy-out and signal."""
+        ph = self.prediction_horizon
+        xbar, gamma = self._ltv_buffers()
         key = (rec.shape[0], T, kind, u_order)
         run = self._qp.get(key)
         if run is None:
@@ -1298,9 +1348,25 @@ class MidlevelAgent:
             raise ValueError(f"Tsh = {T} < ph = {ph} needs u_prev, the controls executed "
                              "since the first shrinking step (:3186)")
         build = T == ph or not self._ltv_built
-        res = run.solve(x_init, goal, ref_traj, rec, xbar, gamma, u_prev=u_prev, ltv=build,
-                        Ts=self.steptime, lon=lon)
+        gen = run.launch(x_init, goal, ref_traj, rec, xbar, gamma, u_prev=u_prev, ltv=build,
+                         Ts=self.steptime, lon=lon)
         self._ltv_built = True
+        return run, gen
+
+    def _ltv_buffers(self):
+        """The LTV model's device buffers (xbar [1, 4 ph], Gamma [1, 4 ph, 2 ph]), rebuilt in
+        place at Tsh == ph.  A new agent takes a destroyed agent's from the pool, with them the
+        step graphs whose captured QP reads them."""
+        from . import step
+        if self._ltv is None:
+            ph = self.prediction_horizon
+            self._ltv = step.ltv_take(self.device, ph) or (
+                torch.empty((1, 4 * ph), dtype=torch.float64, device=self.device),
+                torch.empty((1, 4 * ph, 2 * ph), dtype=torch.float64, device=self.device))
+            self._ltv_built = False
+        return self._ltv
+
+    def _qp_result(self, res, goal):
         st = res["status"]
         if st & (mpc.QP_MAXITER | mpc.QP_NUMERIC):
             raise InSimulationException("Optimizer failed to find a solution")
@@ -1341,12 +1407,7 @@ class MidlevelAgent:
                     base["n"][j, t] = (r["n0"], r["n1"])
                     base["rhs"][j, t], base["side"][j, t] = r["rhs"], r["side"]
                     base["live"][j, t] = r["status"] == 0
-        if self._ltv is None:
-            self._ltv = (torch.empty((1, 4 * ph), dtype=torch.float64, device=self.device),
-                         torch.empty((1, 4 * ph, 2 * ph), dtype=torch.float64,
-                                     device=self.device))
-            self._ltv_built = False
-        xbar, gamma = self._ltv
+        xbar, gamma = self._ltv_buffers()
         if T == ph or not self._ltv_built:
             xb, gm = mpc.ltv(np.asarray(x_init, np.float64).reshape(1, 4), ph, Ts=self.steptime,
                              lon=lon)

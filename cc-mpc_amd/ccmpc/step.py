@@ -187,6 +187,7 @@ class StepGraph:
         self.device = engine.require_device(device)
         self._dev_index = (self.device.index if self.device.index is not None
                            else torch.cuda.current_device())
+        self.qp = None                       # attach_qp: the frame's QP inside the graph
         lib = _lib.load()
         if kind not in ("minkowski", "ideal", "affine"):
             raise ValueError(f"unknown step kind {kind!r}")
@@ -413,12 +414,27 @@ class StepGraph:
         else:
             chk(copy(p(o.host), p(o.dev), o.nbytes, s), "ccmpc_copy_async")
             chk(lib.ccmpc_signal_host(p(self.flags), p(i.d("gen")), s), "ccmpc_signal_host")
+        if self.qp is not None:              # the frame's QP on the records, before L4
+            q = self.qp
+            q["step"].enqueue(o.d("rec"), q["xbar"], q["gamma"], ltv=q["ltv"], Ts=q["Ts"],
+                              lon=q["lon"])
         # L4 (which only reads the bucketed store) after the record path's signal, on the same
         # stream: the host's wait ends before it, and a linear graph launches in a fraction of
         # the host time a forked one takes (one branch for L4 cost ~25 us more per
         # hipGraphLaunch; with L4's nodes captured first, the cycle also started only after
         # L4's first pass, profiles/r04/probe_step_l4_first.log)
         self._enqueue_l4(parity)
+
+    def attach_qp(self, qp_step, xbar, gamma, ltv, Ts=0.5, lon=3.7):
+        """Put the planning frame's QP (an mpc.PlanningQPStep over this graph's records) into
+        the step, right after the record path's signal and before L4: its inputs go in with
+        qp_step.prepare() before each launch, its answer comes back with qp_step.wait().
+        xbar / gamma: the LTV buffers (rebuilt by the graph when ltv).  Before the first
+        launch only (the graph captures the calls)."""
+        if self.generation or self.graphs is not None:
+            raise RuntimeError("attach_qp before the graph's first launch")
+        self.qp = dict(step=qp_step, xbar=xbar, gamma=gamma, ltv=bool(ltv), Ts=float(Ts),
+                       lon=float(lon))
 
     def _enqueue_l4(self, parity):
         """The L4 branch on the current stream: L4 over the bucketed store into the parity's
@@ -691,6 +707,24 @@ def pool_give(device, key, g):
         _POOL[k0].pop(0)
         if not _POOL[k0]:
             del _POOL[k0]
+
+
+# The planners' LTV buffers (planner.MidlevelAgent._ltv_buffers), released with the agent's
+# graphs: a graph holding the frame's QP reads one agent's buffers, so the next agent takes
+# both (the graph key names the buffers it was captured with).
+_LTV_POOL = collections.OrderedDict()
+
+
+def ltv_take(device, ph):
+    """A released agent's (xbar, Gamma) for this horizon, or None."""
+    lst = _LTV_POOL.get((str(device), int(ph)))
+    return lst.pop() if lst else None
+
+
+def ltv_give(device, ph, bufs):
+    lst = _LTV_POOL.setdefault((str(device), int(ph)), [])
+    lst.append(bufs)
+    del lst[:-4]
 
 
 def _as_i64(seed):

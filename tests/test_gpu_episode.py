@@ -140,6 +140,48 @@ def test_compute_prediction_controls_drives_the_schedule(gpu):
     assert n_cmp >= 3
 
 
+def test_planning_frame_qp_inside_the_graph_and_the_pool(gpu):
+    """compute_prediction_controls captures the frame's QP inside the step graph (after the
+    record path, before L4) reading the agent's LTV buffers: a destroyed agent's graphs and LTV
+    buffers go to the pool together, and the next agent replays those graphs -- same answers
+    as the first agent and as the eager QP on the same records."""
+    from ccmpc import episode, planner
+    seed = 5
+    rep = episode.EpisodeReplay(O=2, N=3000, ph=8, n_ideal=20_000, receding_steps=1, seed=seed,
+                                device=gpu)
+    sched = [s for s in rep.schedule() if s[2] != "ideal"][:3]
+
+    def run(agent):
+        out = []
+        for frame, T, kind in sched:
+            sampler = dict(init_state=rep.init, latent_pmf=rep.pmf, gmm=rep.gmm, N=rep.N,
+                           seed=rep.seed * 7919 + frame)
+            ref = rep.ref_traj(frame)
+            goal = ref[-1] + [4.0, 0.5]
+            agent.compute_prediction_controls(frame, T, kind == "minkowski", sampler,
+                                              rep.minpos, rep.pasts, rep.x_init(frame), goal, ref)
+            u = agent.last_ctrl["u"].copy()
+            # the eager QP on the same records and LTV model
+            up = np.concatenate(agent._u_prev[:-1]) if T < 8 else None
+            again = agent.solve_planning_qp(rep.x_init(frame), goal, ref, T, u_prev=up,
+                                            lon=agent.ego_lon)["u"]
+            np.testing.assert_array_equal(u, again)
+            out.append(u)
+        return out
+
+    a = planner.MidlevelAgent(prediction_horizon=8, n_ideal=20_000, seed=seed, device=gpu)
+    ua = run(a)
+    qp_graphs = {id(g) for k, g in a._graphs.items() if "qp" in k}
+    assert qp_graphs and all(a._graphs[k].qp is not None for k in a._graphs if "qp" in k)
+    a.destroy()
+    b = planner.MidlevelAgent(prediction_horizon=8, n_ideal=20_000, seed=seed, device=gpu)
+    ub = run(b)
+    assert {id(g) for k, g in b._graphs.items() if "qp" in k} == qp_graphs
+    for x, y in zip(ua, ub):
+        np.testing.assert_array_equal(x, y)
+    b.destroy()
+
+
 def test_episode_timing_log(gpu):
     from ccmpc import episode
     rep = episode.EpisodeReplay(O=1, N=5000, ph=8, n_ideal=100_000, receding_steps=2,

@@ -242,7 +242,7 @@ def test_reference_predictor_output_drives_run_step(gpu, per_particle, device_te
         assert sa["records"].tobytes() == sb["records"].tobytes(), sa["frame"]
         assert sa["speeds"].tobytes() == sb["speeds"].tobytes()
         assert sa["angles"].tobytes() == sb["angles"].tobytes()
-    keys = [k for k in step._POOL if k[1][-3] == "predictions"]
+    keys = [k for k in step._POOL if k[1][9] == "predictions"]
     assert keys, "the predictions-source graphs were not used"
 
 
