@@ -621,6 +621,40 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   auto grow = [&](int k) { return 4 * (Tp + k / 3) + (k % 3 == 2 ? 3 : k % 3); };
 
   // ---- setup -------------------------------------------------------------------------------
+  // The records (fresh from the cycle kernel, so cold) and the reference points are loaded
+  // first, with the model's own reads below, so the setup waits for one round trip of global
+  // loads instead of one per phase: the first kRecPre records of every thread in registers
+  // (n0 n1 as one 16-byte load, then d and side / status / t_tau)
+  constexpr int kRecPre = 4;
+  struct RecIn {
+    double2 nn;
+    int4 a, b;  // full records: d at a.xy (offset 16 or 32), b = bytes 112..127; compact: a
+  };
+  auto load_rec = [&](int64_t r) -> RecIn {
+    const unsigned char *rec = A.rec + (c0 * P + r) * (A.rec_compact ? 32 : 128);
+    RecIn v;
+    v.nn = *reinterpret_cast<const double2 *>(rec);
+    if (A.rec_compact) {
+      v.a = *reinterpret_cast<const int4 *>(rec + 16);
+      v.b = v.a;
+    } else {
+      v.a = *reinterpret_cast<const int4 *>(
+          rec + (A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? 16 : 32));
+      v.b = *reinterpret_cast<const int4 *>(rec + 112);
+    }
+    return v;
+  };
+  RecIn rpre[kRecPre];
+#pragma unroll
+  for (int j = 0; j < kRecPre; ++j) {
+    const int64_t r = tid + static_cast<int64_t>(j) * NTH;
+    if (r < R) rpre[j] = load_rec(r);
+  }
+  double ref_k = 0.0;  // the reference point entry of qf's first row k = tid
+  if (tid < T3 && tid % 3 < 2) {
+    const int t = tid / 3, tr = t < A.n_ref ? t : A.n_ref - 1;
+    ref_k = ref[2 * tr + tid % 3];
+  }
   for (int e = tid; e < T3 * n; e += NTH) {
     const int k = e / n, j = e % n;
     Gs[e] = Gam[static_cast<int64_t>(grow(k)) * ncol + 2 * Tp + j];
@@ -654,7 +688,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     double v = 0.0;
     if (a < 2) {
       const int tr = t < A.n_ref ? t : A.n_ref - 1;
-      v = 2.0 * p.w_ref * (c3[k] - ref[2 * tr + a]);
+      v = 2.0 * p.w_ref * (c3[k] - (k == tid ? ref_k : ref[2 * tr + a]));
       if (t == T - 1) v += 2.0 * p.w_final * (c3[k] - (a == 0 ? g0 : g1));
     }
     qf[k] = v;
@@ -662,28 +696,22 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // obstacle rows: a . (y_xy + c_xy) <= b  ->  a . y_xy <= b' = b - a . c_xy
   int skipped = 0;
   double hmax = 0.0;
-  for (int64_t r = tid; r < R; r += NTH) {
-    const int64_t cell = r / P;
-    const int pp = static_cast<int>(r - cell * P);
-    const unsigned char *rec = A.rec + (c0 * P + r) * (A.rec_compact ? 32 : 128);
-    const double n0 = *reinterpret_cast<const double *>(rec);
-    const double n1 = *reinterpret_cast<const double *>(rec + 8);
-    double d;
+  auto obstacle_row = [&](int64_t r, const RecIn &ri) {
+    const double n0 = ri.nn.x, n1 = ri.nn.y;
+    const double d = __builtin_bit_cast(
+        double, (static_cast<uint64_t>(static_cast<uint32_t>(ri.a.y)) << 32) |
+                    static_cast<uint32_t>(ri.a.x));
     int side, status, tt;
-    if (A.rec_compact) {  // ccmpc_gather_rec: the same fields, packed
-      d = *reinterpret_cast<const double *>(rec + 16);
-      side = *reinterpret_cast<const int16_t *>(rec + 24);
-      status = *reinterpret_cast<const int16_t *>(rec + 26);
-      tt = *reinterpret_cast<const int32_t *>(rec + 28);
+    if (A.rec_compact) {  // ccmpc_gather_rec: the same fields, packed (int16 side, status)
+      side = static_cast<int16_t>(ri.a.z & 0xFFFF);
+      status = static_cast<int16_t>(static_cast<uint32_t>(ri.a.z) >> 16);
+      tt = ri.a.w;
     } else {
-      d = *reinterpret_cast<const double *>(
-          rec + (A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? 16 : 32));
-      side = *reinterpret_cast<const int32_t *>(rec + 116);
-      status = *reinterpret_cast<const int32_t *>(rec + 120);
-      tt = *reinterpret_cast<const int32_t *>(rec + 124);
+      side = ri.b.y;
+      status = ri.b.z;
+      tt = ri.b.w;
     }
     const int t = A.rec_kind == CCMPC_REC_KIND_HALFSPACE ? tt >> 16 : tt;
-    (void)pp;
     const bool ok = status == 0 && isfinite(n0) && isfinite(n1) && isfinite(d) && t >= 0 &&
                     t < T && (side == 1 || side == -1);
     double a0 = 0.0, a1 = 0.0, b = 1.0;
@@ -703,7 +731,14 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     rw.ix[2 * ro] = 3 * ts;
     rw.ix[2 * ro + 1] = 3 * ts + 1;
     hmax = fmax(hmax, fabs(b));
+  };
+#pragma unroll
+  for (int j = 0; j < kRecPre; ++j) {
+    const int64_t r = tid + static_cast<int64_t>(j) * NTH;
+    if (r < R) obstacle_row(r, rpre[j]);
   }
+  for (int64_t r = tid + static_cast<int64_t>(kRecPre) * NTH; r < R; r += NTH)
+    obstacle_row(r, load_rec(r));
   for (int r = tid; r < nbox + nv; r += NTH) {  // box and speed rows
     const bool lo = r & 1;
     int i0;

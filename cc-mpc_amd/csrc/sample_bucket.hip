@@ -45,6 +45,7 @@ constexpr int kFP = 64;                       // particles per P1 block (the cha
 constexpr int kFThreads = 512;                // 8 waves
 constexpr int kFWaves = kFThreads / 64;
 constexpr int kFGroups = kFusedMaxN / kFP;    // centre groups (P1 blocks) per OV at most
+constexpr int kParSteps = 16;                 // P1: horizons whose step terms run in parallel
 constexpr int kRThreads = 256;                // P2: rare-list slots per block
 constexpr int kRWaves = kRThreads / 64;
 // per-OV header: tot[kMaxKept + 1] at h[0..], the int64 cell starts cstart[kMaxKept] at
@@ -141,6 +142,8 @@ __global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
 template <bool PP, bool EPSIN>
 __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
   __shared__ float act[2][40][kFP];
+  // T <= kParSteps: the terms of each step's position update, [x / y][term][t][particle]
+  __shared__ float terms[2][3][kParSteps][kFP];
   __shared__ float gmm_s[64 * 40 * 5 / 4];
   __shared__ int keep_s[64];
   __shared__ int zs[kFP];
@@ -155,6 +158,10 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
   const uint32_t key = a.ov_base + static_cast<uint32_t>(o);
   const int64_t i0 = static_cast<int64_t>(blk) * kFP;
   const double mx = a.minpos[2 * o], my = a.minpos[2 * o + 1];
+  // the OV's initial state (x, y, heading, speed), read here with everything else: a global
+  // read after the barriers below is a round trip of its own on the chain
+  const double4 st0 = {a.init_state[4 * o], a.init_state[4 * o + 1], a.init_state[4 * o + 2],
+                       a.init_state[4 * o + 3]};
   // every load issued together: own latent ids, the groups' category counts, the tables
   if (tid < kFP && i0 + tid < N) zs[tid] = a.zbuf[static_cast<int64_t>(o) * a.Npad + i0 + tid];
   const int nu = a.G * (K + 1);
@@ -203,6 +210,49 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
       draw_action<PP, EPSIN>(t, ip, zs[lane], o, T, L, N, key, seed, a.gmm, gmm_s, staged,
                              a.eps_in, act[0][t][lane], act[1][t][lane]);
   __syncthreads();
+  FUSED_TS(1, 2);
+  // T <= kParSteps: every step's update terms in parallel over the waves (wave w: steps t = w
+  // mod 8).  The heading phi_t and speed v_t are the f32 running sums the chain accumulates
+  // (phi += dphi dt at a turning step, v += a dt), recomputed by each wave in the same order;
+  // sincos_rn(phi_t) is what unicycle_step evaluates (or carries, unchanged, over a straight
+  // step).  What stays on the chain is three adds per coordinate and step, in unicycle_step's
+  // association: x + A + B (+ C), y + A + B (turning: y - A + B - C)
+  const bool par = T <= kParSteps;
+  if (par && valid) {
+    const float dt = a.dt;
+    float phi = static_cast<float>(st0.z);
+    float v = static_cast<float>(st0.w);
+    for (int t = 0; t < T; ++t) {
+      const float dphi = act[0][t][lane], acc = act[1][t][lane];
+      const bool straight = fabsf(dphi) <= 1e-2f;
+      const float phi1 = straight ? phi : phi + dphi * dt;
+      if (t % kFWaves == w) {
+        float s0, c0;
+        sincos_rn(phi, s0, c0);
+        if (straight) {
+          terms[0][0][t][lane] = v * c0 * dt;
+          terms[0][1][t][lane] = (acc / 2.0f) * c0 * dt * dt;
+          terms[1][0][t][lane] = v * s0 * dt;
+          terms[1][1][t][lane] = (acc / 2.0f) * s0 * dt * dt;
+        } else {
+          float s1, c1;
+          sincos_rn(phi1, s1, c1);
+          const float dsin = (s1 - s0) / dphi, dcos = (c1 - c0) / dphi;
+          const float aw = acc / dphi;
+          terms[0][0][t][lane] = aw * dcos;
+          terms[0][1][t][lane] = v * dsin;
+          terms[0][2][t][lane] = aw * s1 * dt;
+          terms[1][0][t][lane] = v * dcos;
+          terms[1][1][t][lane] = aw * dsin;
+          terms[1][2][t][lane] = aw * c1 * dt;
+        }
+      }
+      phi = phi1;
+      v = v + acc * dt;
+    }
+  }
+  __syncthreads();
+  FUSED_TS(1, 3);
   if (blk == 0 && tid <= K) {  // the OV's header for P2 (every block computed the same values)
     int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
     h[tid] = total_s[tid];
@@ -225,24 +275,38 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
   const int rs = native ? 0 : before_s[K] + rank;  // slot in the rare list
   float x = 0.0f, y = 0.0f;
   if (valid) {
-    const double *st = a.init_state + 4 * o;
-    x = static_cast<float>(st[0]);
-    y = static_cast<float>(st[1]);
-    float phi = static_cast<float>(st[2]), v = static_cast<float>(st[3]);
-    float s0, c0;
-    sincos_rn(phi, s0, c0);
+    x = static_cast<float>(st0.x);
+    y = static_cast<float>(st0.y);
     float *op = native ? a.out + dst : rst + rs;
     const int64_t ld = native ? a.ld_out : a.Npad;
-    for (int t = 0; t < T; ++t) {
-      unicycle_step(x, y, phi, v, s0, c0, act[0][t][lane], act[1][t][lane], a.dt);
-      op[(2 * t) * ld] = x;
-      op[(2 * t + 1) * ld] = y;
+    if (par) {
+      for (int t = 0; t < T; ++t) {
+        if (fabsf(act[0][t][lane]) <= 1e-2f) {
+          x = x + terms[0][0][t][lane] + terms[0][1][t][lane];
+          y = y + terms[1][0][t][lane] + terms[1][1][t][lane];
+        } else {
+          x = x + terms[0][0][t][lane] + terms[0][1][t][lane] + terms[0][2][t][lane];
+          y = y - terms[1][0][t][lane] + terms[1][1][t][lane] - terms[1][2][t][lane];
+        }
+        op[(2 * t) * ld] = x;
+        op[(2 * t + 1) * ld] = y;
+      }
+    } else {
+      float phi = static_cast<float>(st0.z), v = static_cast<float>(st0.w);
+      float s0, c0;
+      sincos_rn(phi, s0, c0);
+      for (int t = 0; t < T; ++t) {
+        unicycle_step(x, y, phi, v, s0, c0, act[0][t][lane], act[1][t][lane], a.dt);
+        op[(2 * t) * ld] = x;
+        op[(2 * t + 1) * ld] = y;
+      }
     }
     if (!native) {
       const float4 info = {x, y, __builtin_bit_cast(float, z), 0.0f};
       reinterpret_cast<float4 *>(a.rinfo)[static_cast<int64_t>(o) * npad + rs] = info;
     }
   }
+  FUSED_TS(1, 4);
   // this block is centre group blk: its kept-mode sums of the final world positions
   const double xw = static_cast<double>(x) + mx, yw = static_cast<double>(y) + my;
   double2 *gp = reinterpret_cast<double2 *>(a.gpart) + (static_cast<int64_t>(o) * a.G + blk) * a.max_k;
@@ -251,7 +315,7 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
     const double sx = group_sum64(mine ? xw : 0.0), sy = group_sum64(mine ? yw : 0.0);
     if (lane == 0) gp[k] = double2{sx, sy};
   }
-  FUSED_TS(1, 2);
+  FUSED_TS(1, 5);
 }
 
 __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {

@@ -73,7 +73,7 @@ def main():
         ks = [("sampler", table(lib.ccmpc_probe_sampler_timestamps, 0),
                ["staged", "z", "actions", "chain"]),
               ("latents", table(lib.ccmpc_probe_fused_timestamps, 0, 0), ["drawn"]),
-              ("place", table(lib.ccmpc_probe_fused_timestamps, 1, 0), ["counted", "sampled"]),
+              ("place", table(lib.ccmpc_probe_fused_timestamps, 1, 0), ["counted", "acted", "headings", "chained", "summed"]),
               ("rares", table(lib.ccmpc_probe_fused_timestamps, 2, 0),
                ["loaded", "centres", "keyed", "bins", "ranked", "copied"]),
               ("b.stats", table(lib.ccmpc_probe_bucket_timestamps, 0, 0),
