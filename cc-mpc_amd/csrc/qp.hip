@@ -563,6 +563,10 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   if (sc >= A.S) return;
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk0 = wall_clock64();
+  uint64_t smark[4] = {};
+#define QS_MARK(i) (smark[i] = wall_clock64())
+#else
+#define QS_MARK(i) ((void)0)
 #endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int T = A.T, Tf = A.Tf, Tp = Tf - T;
@@ -655,19 +659,34 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     const int t = tid / 3, tr = t < A.n_ref ? t : A.n_ref - 1;
     ref_k = ref[2 * tr + tid % 3];
   }
-  for (int e = tid; e < T3 * n; e += NTH) {
-    const int k = e / n, j = e % n;
-    Gs[e] = Gam[static_cast<int64_t>(grow(k)) * ncol + 2 * Tp + j];
+  // Gamma's rows in batches of kGsPre loads per thread, every load of a batch issued before
+  // its LDS stores (a store between two loads made each load a round trip of its own: ~6 us
+  // of the one-wave setup at T = 8, where one batch covers all 384 entries)
+  constexpr int kGsPre = 6;
+  for (int e0 = tid; e0 < T3 * n; e0 += kGsPre * NTH) {
+    double gv[kGsPre];
+#pragma unroll
+    for (int q = 0; q < kGsPre; ++q) {
+      const int e = e0 + q * NTH, ee = e < T3 * n ? e : 0;
+      gv[q] = Gam[static_cast<int64_t>(grow(ee / n)) * ncol + 2 * Tp + ee % n];
+    }
+#pragma unroll
+    for (int q = 0; q < kGsPre; ++q)
+      if (e0 + q * NTH < T3 * n) Gs[e0 + q * NTH] = gv[q];
   }
   for (int k = tid; k < T3; k += NTH) {
     // constant part of the state: x_bar + Gamma_p u_prev - Gamma_f u_bar (:2877-2891)
     const int r = grow(k);
     const double *gr = Gam + static_cast<int64_t>(r) * ncol;
     double c = xb[r];
-    if (uprev)
+    if (uprev) {
+#pragma unroll 8
       for (int j = 0; j < 2 * Tp; ++j) c += gr[j] * uprev[j];
-    if (ubar)
+    }
+    if (ubar) {
+#pragma unroll 8
       for (int j = 0; j < n; ++j) c -= gr[2 * Tp + j] * ubar[2 * Tp + j];
+    }
     c3[k] = c;
     y[k] = 0.0;
   }
@@ -682,6 +701,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   if constexpr (NW == 1)  // launched only for n <= 16, where the layout reserves the table
     for (int e = tid; e < n * n; e += NTH) Hc[e] = hctrl(e / n, e % n, T, order, p);
   qp_sync<NW>();
+  QS_MARK(0);
   for (int k = tid; k < T3; k += NTH) {
     // objective's linear term in output space: 2 (w_ref (c - ref_t) + [t = T-1] w_final (c - g))
     const int t = k / 3, a = k % 3;
@@ -759,6 +779,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     rw.ix[2 * r + 1] = i0;
   }
   qp_sync<NW>();
+  QS_MARK(1);
   // f = Gs^T qf (the scaling of the dual residual; kept in LDS for the polish)
   double fmax_ = 0.0;
   if constexpr (NW == 1) {  // a quad per control, DPP sum (as the IPM's rd)
@@ -781,6 +802,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       fmax_ = fmax(fmax_, fabs(v));
     }
   }
+  QS_MARK(2);
   // initial point: z = 0 (inside the control box), s = max(-g(0), 1), lambda = 1
   // g(z) = row_lin(r, Gs z, z) + row_const(r): the linear part in the state's output rows
   // yy = Gs z (or in z itself for the control bounds), constants folded into b' and the bounds
@@ -808,6 +830,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     if (r < nbox + nv) hmax = fmax(hmax, fabs(g));  // bounds' right-hand sides (z = y = 0)
   }
   block_max2<NW>(hmax, fmax_, red);
+  QS_MARK(3);
   const double tol_p = A.tol * (1.0 + hmax), tol_d = A.tol * (1.0 + fmax_);
 
   // Per-step sums over a step's obstacle rows, in a fixed order (wave per step, lane-strided,
@@ -2079,8 +2102,11 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk4 = wall_clock64();
   if (tid == 0 && sc == 0)
-    printf("qp phases (10ns): setup %d iterations %d polish %d outputs %d\n"
-           "   polish (first round): H %d act %d factor %d W %d S %d z %d\n", int(tk1 - tk0),
+    printf("qp setup (10ns): model %d rows %d f %d init %d\n"
+           "qp phases (10ns): setup %d iterations %d polish %d outputs %d\n"
+           "   polish (first round): H %d act %d factor %d W %d S %d z %d\n",
+           int(smark[0] - tk0), int(smark[1] - smark[0]), int(smark[2] - smark[1]),
+           int(smark[3] - smark[2]), int(tk1 - tk0),
            int(tk2 - tk1), int(tk3 - tk2), int(tk4 - tk3), int(pmark[1] - pmark[0]),
            int(pmark[2] - pmark[1]), int(pmark[3] - pmark[2]), int(pmark[4] - pmark[3]),
            int(pmark[5] - pmark[4]), int(pmark[6] - pmark[5]));
