@@ -692,11 +692,17 @@ class MidlevelAgent:
             return sampler, minpos, pasts, np.asarray(bboxes, np.float64)
         b = pred["boundary"]
 
+        run = len(sel) > 0 and sel == list(range(sel[0], sel[0] + len(sel)))
+
         def rows(x):
             if x is None:
                 return None
             if torch.is_tensor(x):
-                return x if len(sel) == x.shape[0] else x[torch.as_tensor(idx, device=x.device)].contiguous()
+                if len(sel) == x.shape[0]:
+                    return x
+                if run:        # the OVs are one run of nodes (the ego first or last): a view,
+                    return x[sel[0]:sel[0] + len(sel)].contiguous()  # no index upload
+                return x[torch.as_tensor(idx, device=x.device)].contiguous()
             return np.asarray(x)[idx]
 
         sampler = {"init_state": rows(b["init_state"]), "latent_pmf": rows(b["latent_probs"]),
