@@ -287,8 +287,9 @@ class MilpBnB:
         T_full = int(T_full or T)
         self.gamma = gamma.reshape(1, 4 * T_full, 2 * T_full).to(self.dev)
         self.xbar = xbar.reshape(1, 4 * T_full).to(self.dev)
+        self.u_prev_h = None if u_prev is None else np.asarray(u_prev, np.float64).reshape(-1)
         self.u_prev = None if u_prev is None else torch.as_tensor(
-            np.asarray(u_prev, np.float64).reshape(1, -1), device=self.dev)
+            self.u_prev_h.reshape(1, -1), device=self.dev)
         if T_full > int(T) and self.u_prev is None:
             raise ValueError("u_prev (the executed controls) is required when T < T_full")
         self._host_init(T, goal, ref, params or v8_qp_params(),
@@ -372,27 +373,22 @@ class MilpBnB:
         return rec
 
     def _solve_batch(self, nodes):
-        """One mpc_qp_kernel launch over the nodes: (u, X, cost, ok) host arrays."""
+        """One mpc_qp_kernel launch over the nodes: (u, X, cost, ok) host arrays.  The round's
+        traffic is one pinned pack each way (records, goal, reference and executed controls up
+        in one copy kernel; u, X, cost, status down in one, then a polled signal), on buffers
+        cached per shape across frames (_RoundIO)."""
         from . import mpc
         S, T = len(nodes), self.T
         rec = self._records(nodes)
-        cells = rec.shape[1]
-        qp = self._qp.get(S)
-        if qp is None:
-            qp = self._qp[S] = mpc.PlanningQP([cells] * S, T, T_full=self.T_full,
-                                              kind=mpc.REC_AFFINE_COMPACT, params=self.params,
-                                              u_order=self.u_order, device=self.dev)
-        d_rec = torch.from_numpy(rec.view(np.uint8).reshape(S * cells, T, 32)).to(self.dev)
-        goal = torch.as_tensor(np.tile(self.goal, (S, 1)), device=self.dev)
-        ref = torch.as_tensor(np.tile(self.ref[None], (S, 1, 1)), device=self.dev)
-        up = None if self.u_prev is None else self.u_prev.expand(S, -1).contiguous()
-        u, X, cost, status, _ = qp.solve(self.gamma.expand(S, -1, -1).contiguous(),
-                                         self.xbar.expand(S, -1).contiguous(), goal, ref,
-                                         d_rec, u_prev=up)
-        st = status.cpu().numpy() & ~mpc.QP_SKIPPED_ROWS
+        io = _RoundIO.get(self, S, rec.shape[1])
+        if io.frame is not self:            # this frame's model on the cached buffers
+            io.set_frame(self)
+        io.rec_h[...] = rec
+        st, u, X, cost = io.run()
+        st = st & ~mpc.QP_SKIPPED_ROWS
         self.stats["launches"] += 1
         self.stats["qps"] += S
-        return u.cpu().numpy(), X.cpu().numpy(), cost.cpu().numpy(), st == mpc.QP_OK
+        return u, X, cost, st == mpc.QP_OK
 
     # ---- feasibility of a node's optimum -----------------------------------------------------
     def _violations(self, X, faces, segs):
@@ -499,6 +495,76 @@ class MilpBnB:
             return None
         best.update(nodes=self.stats["nodes"], launches=self.stats["launches"])
         return best
+
+
+class _RoundIO:
+    """A branch-and-bound round's device side for S nodes of `cells` record cells: the batched
+    PlanningQP, its inputs and outputs as pinned packs (step.Pack), the LTV model repeated S
+    times on the device.  Cached per shape in the process (a frame's rounds and the next
+    frames of the same shape reuse it; the tree runs on one host thread)."""
+    _cache = {}
+
+    @classmethod
+    def get(cls, bnb, S, cells):
+        key = (str(bnb.dev), S, cells, bnb.T, bnb.T_full, bnb.ref.shape[0], bnb.u_order,
+               bytes(bnb.params))
+        io = cls._cache.get(key)
+        if io is None:
+            while len(cls._cache) >= 32:
+                cls._cache.pop(next(iter(cls._cache)))
+            io = cls._cache[key] = cls(bnb, S, cells)
+        return io
+
+    def __init__(self, bnb, S, cells):
+        from . import mpc, step
+        T, Tf, dev = bnb.T, bnb.T_full, bnb.dev
+        f64, i32, i64 = torch.float64, torch.int32, torch.int64
+        self.S, self.T, self.Tf, self.dev = S, T, Tf, dev
+        nref = bnb.ref.shape[0]
+        self.inp = step.Pack([("gen", (2,), i64), ("rec", (S * cells, T, 32), torch.uint8),
+                              ("goal", (S, 2), f64), ("ref", (S, nref, 2), f64),
+                              ("uprev", (S, max(2 * (Tf - T), 1)), f64)], dev)
+        self.out = step.Pack([("u", (S, 2 * T), f64), ("X", (S, T, 4), f64), ("cost", (S,), f64),
+                              ("status", (S,), i32), ("iters", (S,), i32)], dev)
+        self.qp = mpc.PlanningQP([cells] * S, T, T_full=Tf, kind=mpc.REC_AFFINE_COMPACT,
+                                 params=bnb.params, u_order=bnb.u_order, device=dev)
+        o = self.out
+        self.qp.u, self.qp.X, self.qp.cost = o.d("u"), o.d("X"), o.d("cost")
+        self.qp.status, self.qp.iters = o.d("status"), o.d("iters")
+        self.gamma = torch.empty((S, 4 * Tf, 2 * Tf), dtype=f64, device=dev)
+        self.xbar = torch.empty((S, 4 * Tf), dtype=f64, device=dev)
+        self.rec_h = self.inp.h("rec").reshape(-1).view(_GATHER).reshape(S, cells, T)
+        self.flags = torch.zeros(2, dtype=i64, pin_memory=True)
+        self._flags = self.flags.numpy()
+        self.gen, self.frame = 0, None
+
+    def set_frame(self, bnb):
+        """The frame's LTV model (device copies), goal, reference and executed controls."""
+        self.gamma.copy_(bnb.gamma.expand(self.S, -1, -1))
+        self.xbar.copy_(bnb.xbar.expand(self.S, -1))
+        i = self.inp
+        i.h("goal")[...] = bnb.goal
+        i.h("ref")[...] = bnb.ref[None]
+        if self.Tf > self.T:
+            i.h("uprev")[...] = bnb.u_prev_h[None]
+        self.frame = bnb
+
+    def run(self):
+        """Records (already in the pinned pack) up, the batched solve, the answer down; returns
+        host copies (status, u, X, cost)."""
+        from . import _lib, engine, step
+        lib, p, s = _lib.load(), engine._p, engine._stream()
+        i, o = self.inp, self.out
+        self.gen += 1
+        i.h("gen")[0] = self.gen
+        _lib.check(lib.ccmpc_copy_kernel_async(p(i.dev), p(i.host), i.nbytes, s),
+                   "ccmpc_copy_async")
+        self.qp.solve(self.gamma, self.xbar, i.d("goal"), i.d("ref"), i.d("rec"),
+                      u_prev=i.d("uprev") if self.Tf > self.T else None)
+        _lib.check(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
+                                               p(i.d("gen")), s), "ccmpc_copy_signal_async")
+        step.poll_word(self._flags, 0, self.gen, self.dev, "branch-and-bound round")
+        return (o.h("status").copy(), o.h("u").copy(), o.h("X").copy(), o.h("cost").copy())
 
 
 class BranchAndBound(MilpBnB):
