@@ -1402,17 +1402,17 @@ class MidlevelAgent:
         if C and P:
             h = dist.compact_records(rec[:, :P].contiguous(), int(halfspace is False))
             h = h.cpu().numpy().reshape(-1).view(milp._GATHER).reshape(C, P)
-            for c in range(C):
-                for p_ in range(P):
-                    r = h[c, p_]
-                    if halfspace:
-                        t, tau = int(r["t_tau"]) >> 16, int(r["t_tau"]) & 0xFFFF
-                        j = c * (T - 1) + tau
-                    else:
-                        t, j = p_, c
-                    base["n"][j, t] = (r["n0"], r["n1"])
-                    base["rhs"][j, t], base["side"][j, t] = r["rhs"], r["side"]
-                    base["live"][j, t] = r["status"] == 0
+            # record (c, p) -> base row (j, t): pseudo-cell c (T - 1) + tau at step t for a
+            # half-space (t, tau) record, cell c at step p for an affine one (vectorised)
+            if halfspace:
+                tt = h["t_tau"].astype(np.int64)
+                t, j = tt >> 16, np.arange(C)[:, None] * (T - 1) + (tt & 0xFFFF)
+            else:
+                t, j = np.broadcast_to(np.arange(P), (C, P)), np.broadcast_to(
+                    np.arange(C)[:, None], (C, P))
+            base["n"][j, t, 0], base["n"][j, t, 1] = h["n0"], h["n1"]
+            base["rhs"][j, t], base["side"][j, t] = h["rhs"], h["side"]
+            base["live"][j, t] = h["status"] == 0
         xbar, gamma = self._ltv_buffers()
         if T == ph or not self._ltv_built:
             xb, gm = mpc.ltv(np.asarray(x_init, np.float64).reshape(1, 4), ph, Ts=self.steptime,
