@@ -47,6 +47,12 @@ constexpr int kFWaves = kFThreads / 64;
 constexpr int kFGroups = kFusedMaxN / kFP;    // centre groups (P1 blocks) per OV at most
 constexpr int kParSteps = 16;                 // P1: horizons whose step terms run in parallel
 constexpr int kRThreads = 256;                // P2: rare-list slots per block
+// P2: rare records each thread loads per round (kRThreads x this per round; the first round is
+// issued with the kernel's other loads, so a rare list of up to that many takes no further
+// round trip)
+#ifndef CCMPC_RARE_BATCH
+#define CCMPC_RARE_BATCH 8
+#endif
 constexpr int kRWaves = kRThreads / 64;
 // per-OV header: tot[kMaxKept + 1] at h[0..], the int64 cell starts cstart[kMaxKept] at
 // h + 2 * kMaxKept
@@ -356,7 +362,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   // the first batch of rare records too: R is not known yet, so the slots are clamped into the
   // list's storage (a launch's first kB * 256 records cover the C2 shape's whole rare list)
   const float4 *info = reinterpret_cast<const float4 *>(a.rinfo) + static_cast<int64_t>(o) * npad;
-  constexpr int kB = 8;
+  constexpr int kB = CCMPC_RARE_BATCH;
   float4 f[kB];
 #pragma unroll
   for (int j = 0; j < kB; ++j) {
