@@ -110,6 +110,9 @@ SIGNATURES = {
     "ccmpc_mpc_qp": (ctypes.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _I64, _P,
                                     ctypes.c_int, _P, _I64, _P, ctypes.c_int, _I32, _D, _P, _SZ,
                                     _P, _P, _P, _P, _P, _P]),
+    "ccmpc_mpc_qp_ltv": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _I64, _P,
+                                        ctypes.c_int, _P, _I64, _P, ctypes.c_int, _I32, _D, _P,
+                                        _SZ, _P, _P, _P, _P, _P, _P]),
     "ccmpc_selftest": (ctypes.c_int, [ctypes.c_int, _I64, _P, _P, _D, _I32, _P]),
     "ccmpc_poison_lds": (ctypes.c_int, [_D, _P]),
 }

@@ -14,11 +14,15 @@ Every tensor is a torch device tensor; nothing here synchronises except the expl
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
 
 from . import _lib, engine
+
+# the planning frame's LTV rebuild inside the QP's launch (ccmpc_mpc_qp_ltv); 0: its own kernel
+_FUSED_LTV = os.environ.get("CCMPC_QP_FUSED_LTV", "1") == "1"
 
 U_ORDER_F, U_ORDER_C = 0, 1            # CCMPC_U_ORDER_*: cvxpy's default reshape is 'F'
 REC_HALFSPACE, REC_AFFINE = 0, 1       # CCMPC_REC_KIND_*
@@ -59,6 +63,12 @@ def ltv(x_init, T, Ts=0.5, lon=3.7):
                                  float(lon), engine._p(xbar), engine._p(gamma),
                                  engine._stream()), "ccmpc_mpc_ltv")
     return xbar, gamma
+
+
+class QpLtv(ctypes.Structure):
+    """ccmpc_qp_ltv: the fused LTV rebuild's inputs (x_init a device pointer)."""
+    _fields_ = [("x_init", ctypes.c_void_p), ("Ts", ctypes.c_double), ("l_r", ctypes.c_double),
+                ("L", ctypes.c_double)]
 
 
 class PlanningQP:
@@ -103,10 +113,12 @@ class PlanningQP:
         if shape is not None and tuple(t.shape) != tuple(shape):
             raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
 
-    def solve(self, gamma, xbar, goal, ref, rec, u_prev=None, ubar=None):
+    def solve(self, gamma, xbar, goal, ref, rec, u_prev=None, ubar=None, ltv=None):
         """Enqueue the S solves.  gamma [S, 4T_full, 2T_full], xbar [S, 4T_full],
         goal [S, 2], ref [S, n_ref, 2], rec the records (uint8 [cells, P, 128] tensor, or
-        [cells, P, 32] ccmpc_gather_rec for the *_COMPACT kinds)."""
+        [cells, P, 32] ccmpc_gather_rec for the *_COMPACT kinds).  ltv = (x_init [S, 4] device
+        tensor, Ts, lon): rebuild the LTV model about u = 0 in the same launch
+        (ccmpc_mpc_qp_ltv) -- gamma / xbar are then its outputs."""
         lib = _lib.load()
         S, T, Tf = self.S, self.T, self.T_full
         ref = ref.reshape(S, -1, 2)
@@ -130,6 +142,19 @@ class PlanningQP:
         if ubar is not None:
             self._need(ubar, "ubar", (S, 2 * Tf))
         p = engine._p
+        if ltv is not None:
+            x0, Ts, lon = ltv
+            self._need(x0, "x_init", (S, 4))
+            if ubar is not None:
+                raise ValueError("the fused LTV rebuild is the model about u = 0 (no ubar)")
+            spec = QpLtv(x_init=p(x0), Ts=float(Ts), l_r=0.5 * float(lon), L=float(lon))
+            _lib.check(lib.ccmpc_mpc_qp_ltv(
+                ctypes.byref(spec), self.S, self.T, self.T_full, p(gamma), p(xbar), p(u_prev),
+                p(goal), p(ref), ref.shape[1], p(rec), self.kind, p(self.scene_cell),
+                self.max_cells, ctypes.byref(self.params), self.u_order, self.max_iter,
+                self.tol, p(self.ws), self.ws.numel(), p(self.u), p(self.X), p(self.cost),
+                p(self.status), p(self.iters), engine._stream()), "ccmpc_mpc_qp_ltv")
+            return self.u, self.X, self.cost, self.status, self.iters
         _lib.check(lib.ccmpc_mpc_qp(
             self.S, self.T, self.T_full, p(gamma), p(xbar), p(ubar), p(u_prev), p(goal), p(ref),
             ref.shape[1], p(rec), self.kind, p(self.scene_cell), self.max_cells,
@@ -221,11 +246,14 @@ class PlanningQPStep:
         s = engine._stream()
         chk = _lib.check
         chk(lib.ccmpc_copy_kernel_async(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
-        if ltv:
+        # the LTV rebuild (Tsh == ph) fused into the solve's launch, or (CCMPC_QP_FUSED_LTV=0)
+        # as its own kernel first
+        if ltv and not _FUSED_LTV:
             chk(lib.ccmpc_mpc_ltv(p(i.d("x0")), 1, Tf, float(Ts), 0.5 * float(lon), float(lon),
                                   p(xbar), p(gamma), s), "ccmpc_mpc_ltv")
         self.qp.solve(gamma, xbar, i.d("goal"), i.d("ref"), rec,
-                      u_prev=i.d("uprev") if T < Tf else None)
+                      u_prev=i.d("uprev") if T < Tf else None,
+                      ltv=(i.d("x0"), Ts, lon) if (ltv and _FUSED_LTV) else None)
         chk(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
                                         p(i.d("gen")), s), "ccmpc_copy_signal_async")
 

@@ -58,51 +58,71 @@ constexpr int kQpDefaultMethod = CCMPC_QP_METHOD_GI;
 // Ad = I + Ts A, Bd = Ts B + Ts^2/2 A B (cont2discrete 'zoh' = expm of that block matrix).
 // Gamma = A_bar^{-1} B_bar (:296-306) is block lower triangular with block (t, k) =
 // Ad^{t-k} Bd = (I + (t-k) Ts A) Bd.
-__global__ void mpc_ltv_kernel(const double *__restrict__ x_init, int64_t S, int T, double Ts,
-                               double l_r, double L, double *__restrict__ out_xbar,
-                               double *__restrict__ out_gamma) {
-  const int64_t s = blockIdx.x;
-  if (s >= S) return;
-  const double x0 = x_init[4 * s], y0 = x_init[4 * s + 1], psi = x_init[4 * s + 2],
-               v = x_init[4 * s + 3];
-  const double cp = cos(psi), sp = sin(psi);
-  // get_dbeta_ddelta at delta = 0 (:19-24): 1 when l_r == L, else 1 / (L / l_r)
-  const double dbeta = (l_r == L) ? 1.0 : 1.0 / (L / l_r);
-  // A (get_state_matrix :103-115 at delta = 0): nonzeros A[0][2], A[0][3], A[1][2], A[1][3]
-  const double a02 = -v * sp, a03 = cp, a12 = v * cp, a13 = sp;
-  // B (get_input_matrix :117-130 at delta = 0)
-  const double b01 = -v * sp * dbeta, b11 = v * cp * dbeta, b21 = (v / L) * 1.0, b30 = 1.0;
-  // Bd = Ts B + Ts^2/2 A B;  (A B)[r][c] = sum_k A[r][k] B[k][c]
-  const double h = 0.5 * Ts * Ts;
+// The model of one scene, evaluated entry by entry: mpc_ltv_kernel writes every entry, and the
+// QP with a fused LTV rebuild (ccmpc_mpc_qp_ltv) evaluates the ones it reads from the same
+// functions (defined here, outside the QP kernel's fp-contract scope, so both round alike).
+struct LtvModel {
+  double x0, y0, psi, v, cp, sp, Ts;
+  double a02, a03, a12, a13;
   double Bd[4][2];
-  Bd[0][0] = h * (a03 * b30);
-  Bd[0][1] = Ts * b01 + h * (a02 * b21);
-  Bd[1][0] = h * (a13 * b30);
-  Bd[1][1] = Ts * b11 + h * (a12 * b21);
-  Bd[2][0] = 0.0;
-  Bd[2][1] = Ts * b21;
-  Bd[3][0] = Ts * b30;
-  Bd[3][1] = 0.0;
-  const int nx = 4, nu = 2, rows = nx * T, cols = nu * T;
-  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
-    const int r = e / cols, c = e % cols;
-    const int t = r / nx, i = r % nx, k = c / nu, j = c % nu;
+  __device__ LtvModel(const double *x_init, double Ts_, double l_r, double L) {
+    x0 = x_init[0];
+    y0 = x_init[1];
+    psi = x_init[2];
+    v = x_init[3];
+    Ts = Ts_;
+    cp = cos(psi);
+    sp = sin(psi);
+    // get_dbeta_ddelta at delta = 0 (:19-24): 1 when l_r == L, else 1 / (L / l_r)
+    const double dbeta = (l_r == L) ? 1.0 : 1.0 / (L / l_r);
+    // A (get_state_matrix :103-115 at delta = 0): nonzeros A[0][2], A[0][3], A[1][2], A[1][3]
+    a02 = -v * sp;
+    a03 = cp;
+    a12 = v * cp;
+    a13 = sp;
+    // B (get_input_matrix :117-130 at delta = 0)
+    const double b01 = -v * sp * dbeta, b11 = v * cp * dbeta, b21 = (v / L) * 1.0, b30 = 1.0;
+    // Bd = Ts B + Ts^2/2 A B;  (A B)[r][c] = sum_k A[r][k] B[k][c]
+    const double h = 0.5 * Ts * Ts;
+    Bd[0][0] = h * (a03 * b30);
+    Bd[0][1] = Ts * b01 + h * (a02 * b21);
+    Bd[1][0] = h * (a13 * b30);
+    Bd[1][1] = Ts * b11 + h * (a12 * b21);
+    Bd[2][0] = 0.0;
+    Bd[2][1] = Ts * b21;
+    Bd[3][0] = Ts * b30;
+    Bd[3][1] = 0.0;
+  }
+  // Gamma[r][c] (r = 4 t + i, c = 2 k + j): (I + (t - k) Ts A) Bd for k <= t, else 0
+  __device__ double gamma(int r, int c) const {
+    const int t = r >> 2, i = r & 3, k = c >> 1, j = c & 1;
     double g = 0.0;
     if (k <= t) {
-      // (I + m Ts A) Bd, m = t - k
       const double mt = static_cast<double>(t - k) * Ts;
       g = Bd[i][j];
       if (i == 0) g += mt * (a02 * Bd[2][j] + a03 * Bd[3][j]);
       if (i == 1) g += mt * (a12 * Bd[2][j] + a13 * Bd[3][j]);
     }
-    out_gamma[s * rows * cols + e] = g;
+    return g;
   }
-  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
-    const int t = r / nx + 1, i = r % nx;  // X_bar[1:]
+  // X_bar[1:][r]
+  __device__ double xbar(int r) const {
+    const int t = (r >> 2) + 1, i = r & 3;
     const double tt = static_cast<double>(t) * Ts;
-    out_xbar[s * rows + r] = i == 0 ? x0 + v * cp * tt : i == 1 ? y0 + v * sp * tt
-                           : i == 2 ? psi : v;
+    return i == 0 ? x0 + v * cp * tt : i == 1 ? y0 + v * sp * tt : i == 2 ? psi : v;
   }
+};
+
+__global__ void mpc_ltv_kernel(const double *__restrict__ x_init, int64_t S, int T, double Ts,
+                               double l_r, double L, double *__restrict__ out_xbar,
+                               double *__restrict__ out_gamma) {
+  const int64_t s = blockIdx.x;
+  if (s >= S) return;
+  const LtvModel lm(x_init + 4 * s, Ts, l_r, L);
+  const int rows = 4 * T, cols = 2 * T;
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x)
+    out_gamma[s * rows * cols + e] = lm.gamma(e / cols, e % cols);
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) out_xbar[s * rows + r] = lm.xbar(r);
 }
 
 // ---- the QP ---------------------------------------------------------------------------------
@@ -115,6 +135,11 @@ struct QpArgs {
   int64_t max_cells;
   double tol, early;  // early: the early polish threshold on mu / max(mu0, 1) (0 = none)
   const double *gamma, *xbar, *ubar, *u_prev, *goal, *ref;
+  // fused LTV rebuild (ccmpc_mpc_qp_ltv): x_init[S][4] != NULL -> the model is computed here,
+  // written to ltv_xbar / ltv_gamma (= xbar / gamma) and read from registers, not memory
+  const double *ltv_x0;
+  double ltv_Ts, ltv_lr, ltv_L;
+  double *ltv_xbar, *ltv_gamma;
   const unsigned char *rec;
   const int64_t *scene_cell;
   ccmpc_mpc_params p;
@@ -663,6 +688,26 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // its LDS stores (a store between two loads made each load a round trip of its own: ~6 us
   // of the one-wave setup at T = 8, where one batch covers all 384 entries)
   constexpr int kGsPre = 6;
+  if (A.ltv_x0) {
+    // the fused LTV rebuild: this scene's model into the caller's buffers (later frames read
+    // them), Gs and the constant part straight from the model
+    const LtvModel lm(A.ltv_x0 + 4 * sc, A.ltv_Ts, A.ltv_lr, A.ltv_L);
+    const int gr4 = 4 * Tf;
+    double *og = A.ltv_gamma + sc * gr4 * ncol, *ox = A.ltv_xbar + sc * gr4;
+    for (int e = tid; e < gr4 * ncol; e += NTH) og[e] = lm.gamma(e / ncol, e % ncol);
+    for (int r = tid; r < gr4; r += NTH) ox[r] = lm.xbar(r);
+    for (int e = tid; e < T3 * n; e += NTH) Gs[e] = lm.gamma(grow(e / n), 2 * Tp + e % n);
+    for (int k = tid; k < T3; k += NTH) {
+      const int r = grow(k);
+      double c = lm.xbar(r);
+      if (uprev)
+        for (int j = 0; j < 2 * Tp; ++j) c += lm.gamma(r, j) * uprev[j];
+      if (ubar)
+        for (int j = 0; j < n; ++j) c -= lm.gamma(r, 2 * Tp + j) * ubar[2 * Tp + j];
+      c3[k] = c;
+      y[k] = 0.0;
+    }
+  } else {
   for (int e0 = tid; e0 < T3 * n; e0 += kGsPre * NTH) {
     double gv[kGsPre];
 #pragma unroll
@@ -689,6 +734,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     }
     c3[k] = c;
     y[k] = 0.0;
+  }
   }
   for (int j = tid; j < n; j += NTH) {
     // min_u / max_u = vstack((full(T, a), full(T, delta))).T.ravel() (:2874-2875): the bounds
@@ -2172,15 +2218,14 @@ extern "C" size_t ccmpc_mpc_qp_workspace_bytes(int64_t n_scenes, int64_t T,
   return static_cast<size_t>(n_scenes * kQpRowDoubles * m) * sizeof(double) + 16;
 }
 
-extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamma,
-                            const double *xbar, const double *ubar, const double *u_prev,
-                            const double *goal, const double *ref, int64_t n_ref,
-                            const void *rec, int rec_kind, const int64_t *scene_cell,
-                            int64_t max_cells_per_scene, const ccmpc_mpc_params *params,
-                            int u_order, int32_t max_iter, double tol, void *workspace,
-                            size_t workspace_bytes, double *out_u, double *out_x,
-                            double *out_cost, int32_t *out_status, int32_t *out_iter,
-                            ccmpc_stream_t stream) {
+static int mpc_qp_impl(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T, int64_t T_full,
+                       const double *gamma, const double *xbar, const double *ubar,
+                       const double *u_prev, const double *goal, const double *ref,
+                       int64_t n_ref, const void *rec, int rec_kind, const int64_t *scene_cell,
+                       int64_t max_cells_per_scene, const ccmpc_mpc_params *params, int u_order,
+                       int32_t max_iter, double tol, void *workspace, size_t workspace_bytes,
+                       double *out_u, double *out_x, double *out_cost, int32_t *out_status,
+                       int32_t *out_iter, ccmpc_stream_t stream) {
   CCMPC_REQUIRE(T >= 1 && T <= kQpMaxT, "T must be in [1, 40]");
   CCMPC_REQUIRE(T_full >= T && T_full <= kQpMaxT, "T_full must be in [T, 40]");
   CCMPC_REQUIRE(n_scenes >= 0 && n_scenes < (int64_t(1) << 31), "bad n_scenes");
@@ -2244,6 +2289,18 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   a.out_cost = out_cost;
   a.out_status = out_status;
   a.out_iter = out_iter;
+  if (ltv) {
+    CCMPC_REQUIRE(ltv->x_init, "null x_init");
+    CCMPC_REQUIRE(ltv->Ts > 0.0 && ltv->L > 0.0 && ltv->l_r > 0.0,
+                  "Ts, L, l_r must be positive");
+    CCMPC_REQUIRE(!ubar, "the fused LTV rebuild is the model about u = 0 (ubar must be NULL)");
+    a.ltv_x0 = ltv->x_init;
+    a.ltv_Ts = ltv->Ts;
+    a.ltv_lr = ltv->l_r;
+    a.ltv_L = ltv->L;
+    a.ltv_xbar = const_cast<double *>(xbar);
+    a.ltv_gamma = const_cast<double *>(gamma);
+  }
   const size_t lds = static_cast<size_t>(QpLayout(Ti, in_lds ? R : 0, in_lds, plan.polish).total) *
                      sizeof(double);
   CCMPC_REQUIRE(lds <= kQpLdsBytes, "T too large for the LDS image");
@@ -2280,4 +2337,35 @@ extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const d
   }
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
+}
+
+extern "C" int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamma,
+                            const double *xbar, const double *ubar, const double *u_prev,
+                            const double *goal, const double *ref, int64_t n_ref,
+                            const void *rec, int rec_kind, const int64_t *scene_cell,
+                            int64_t max_cells_per_scene, const ccmpc_mpc_params *params,
+                            int u_order, int32_t max_iter, double tol, void *workspace,
+                            size_t workspace_bytes, double *out_u, double *out_x,
+                            double *out_cost, int32_t *out_status, int32_t *out_iter,
+                            ccmpc_stream_t stream) {
+  return mpc_qp_impl(nullptr, n_scenes, T, T_full, gamma, xbar, ubar, u_prev, goal, ref, n_ref,
+                     rec, rec_kind, scene_cell, max_cells_per_scene, params, u_order, max_iter,
+                     tol, workspace, workspace_bytes, out_u, out_x, out_cost, out_status,
+                     out_iter, stream);
+}
+
+extern "C" int ccmpc_mpc_qp_ltv(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T,
+                                int64_t T_full, double *gamma, double *xbar,
+                                const double *u_prev, const double *goal, const double *ref,
+                                int64_t n_ref, const void *rec, int rec_kind,
+                                const int64_t *scene_cell, int64_t max_cells_per_scene,
+                                const ccmpc_mpc_params *params, int u_order, int32_t max_iter,
+                                double tol, void *workspace, size_t workspace_bytes,
+                                double *out_u, double *out_x, double *out_cost,
+                                int32_t *out_status, int32_t *out_iter, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(ltv, "null ltv");
+  return mpc_qp_impl(ltv, n_scenes, T, T_full, gamma, xbar, nullptr, u_prev, goal, ref, n_ref,
+                     rec, rec_kind, scene_cell, max_cells_per_scene, params, u_order, max_iter,
+                     tol, workspace, workspace_bytes, out_u, out_x, out_cost, out_status,
+                     out_iter, stream);
 }

@@ -517,6 +517,24 @@ int ccmpc_mpc_qp(int64_t n_scenes, int64_t T, int64_t T_full, const double *gamm
                  double *out_cost, int32_t *out_status, int32_t *out_iter,
                  ccmpc_stream_t stream);
 
+/* ccmpc_mpc_qp with the LTV rebuild fused in (the planning frame at Tsh == ph: one launch
+ * instead of ccmpc_mpc_ltv then ccmpc_mpc_qp).  Each scene's model about u = 0 is computed from
+ * ltv->x_init[s][4] with ccmpc_mpc_ltv's arithmetic (the same bits), written to gamma / xbar
+ * (OUTPUTS here, [s][4 T_full][2 T_full] and [s][4 T_full]: later frames pass them to
+ * ccmpc_mpc_qp) and used by the solve without reading them back. */
+typedef struct ccmpc_qp_ltv {
+  const double *x_init; /* device, [n_scenes][4] */
+  double Ts, l_r, L;
+} ccmpc_qp_ltv;
+int ccmpc_mpc_qp_ltv(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T, int64_t T_full,
+                     double *gamma, double *xbar, const double *u_prev, const double *goal,
+                     const double *ref, int64_t n_ref, const void *rec, int rec_kind,
+                     const int64_t *scene_cell, int64_t max_cells_per_scene,
+                     const ccmpc_mpc_params *params, int u_order, int32_t max_iter, double tol,
+                     void *workspace, size_t workspace_bytes, double *out_u, double *out_x,
+                     double *out_cost, int32_t *out_status, int32_t *out_iter,
+                     ccmpc_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * TEST ONLY (not a reference interface): the half-space tail's device functions -- the ones
  * ccmpc_minkowski_cycle / ccmpc_minkowski / ccmpc_affine_scale run per record -- on n batched

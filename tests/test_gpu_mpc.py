@@ -433,3 +433,35 @@ def test_qp_on_compact_records_equals_the_full_records(gpu, kind):
     assert (a[3] & mpc.QP_SKIPPED_ROWS).any()
     with pytest.raises(ValueError):                  # a full block under a compact kind
         mpc.PlanningQP(cps, T, kind=k_comp).solve(gamma, xbar, g_t, r_t, rec)
+
+
+@pytest.mark.parametrize("T,kind", [(8, "halfspace"), (6, "halfspace"), (8, "affine")])
+def test_fused_ltv_equals_ltv_then_qp(gpu, T, kind):
+    """ccmpc_mpc_qp_ltv (the LTV rebuild inside the QP's launch, what the planning frame runs at
+    Tsh == ph) writes ccmpc_mpc_ltv's model bit for bit and solves to the bytes of ccmpc_mpc_ltv
+    followed by ccmpc_mpc_qp -- a batch of scenes, the full and a shrinking horizon."""
+    Tf = 8
+    seeds = _feasible(3) + _infeasible(1)
+    rec, cps, _, refs, goals, x0s = _scene_inputs(seeds, Tf, gpu, kind)
+    if T < Tf:                      # the first T steps' records of each cell
+        P = Tf * (Tf - 1) // 2 if kind == "halfspace" else Tf
+        Pt = T * (T - 1) // 2 if kind == "halfspace" else T
+        rec = rec.reshape(rec.shape[0], P, -1)[:, :Pt].contiguous()
+    S = len(seeds)
+    k = mpc.REC_HALFSPACE if kind == "halfspace" else mpc.REC_AFFINE
+    x0_d = torch.as_tensor(x0s, device=gpu)
+    goal = torch.as_tensor(goals, device=gpu)
+    ref = torch.as_tensor(refs[:, :T], device=gpu).contiguous()
+    up = (torch.as_tensor(np.tile(np.linspace(-0.2, 0.3, 2 * (Tf - T)), (S, 1)), device=gpu)
+          if T < Tf else None)
+    xbar, gamma = mpc.ltv(x0s, Tf, Ts=0.5, lon=LON)
+    qa = mpc.PlanningQP(cps, T, T_full=Tf, kind=k, device=gpu)
+    ua, Xa, ca, sa, ia = (t.clone() for t in qa.solve(gamma, xbar, goal, ref, rec, u_prev=up))
+    xb2 = torch.full_like(xbar, float("nan"))
+    ga2 = torch.full_like(gamma, float("nan"))
+    qb = mpc.PlanningQP(cps, T, T_full=Tf, kind=k, device=gpu)
+    ub, Xb, cb, sb, ib = qb.solve(ga2, xb2, goal, ref, rec, u_prev=up, ltv=(x0_d, 0.5, LON))
+    torch.cuda.synchronize(gpu)
+    assert torch.equal(xb2, xbar) and torch.equal(ga2, gamma)
+    for a, b in ((ua, ub), (Xa, Xb), (ca, cb), (sa, sb), (ia, ib)):
+        assert a.cpu().numpy().tobytes() == b.cpu().numpy().tobytes()
