@@ -249,3 +249,36 @@ def test_planner_road_boundaries_match_oracle_milp(gpu, affine):
         assert agent.last_bnb["nodes"] > 1                 # the road binds: it branched
         n_feasible += 1
     assert n_feasible >= 1
+
+
+@pytest.mark.parametrize("T,Tf", [(3, 5), (4, 6)])
+def test_road_milp_shrinking_horizon_matches_oracle(gpu, T, Tf):
+    """The shrinking step's road MILP (Tsh < ph: the first step's LTV model kept, the executed
+    controls u_prev moving the state, :2858-2891 / :3186): MilpBnB with T_full and u_prev --
+    its rounds carry u_prev in their pinned input pack -- against the oracle's literal MILP on
+    the same sliced model."""
+    from ccmpc import milp, mpc
+    from test_milp import _road_base
+    segs, mask, rs = _road_segments()
+    goal, base = _road_base(T, True)
+    xbar, G = _ego_model(Tf, X0)
+    ref = np.stack([np.linspace(1.0, goal[0], T), np.zeros(T)], 1)
+    u_prev = np.tile([0.3, -0.02], Tf - T)
+    want = mo.road_milp_enumerate(G, xbar, T, goal, ref, mo.DEFAULT_PARAMS, base=base,
+                                  segs=segs, mask=mask, subsets=False, T_full=Tf,
+                                  u_prev=u_prev)
+    rows = dict(n=np.zeros((2, T, 2)), rhs=np.zeros((2, T)), side=np.ones((2, T), int),
+                live=np.zeros((2, T), bool), sbig=np.full((2, T), True))
+    slot = {-1: 0, 1: 1}
+    for r in base:
+        j, t = slot[r["side"]], r["t"]
+        rows["n"][j, t], rows["rhs"][j, t], rows["side"][j, t] = r["n"], r["rhs"], r["side"]
+        rows["live"][j, t] = True
+    g_xbar, g_gamma = mpc.ltv(np.array(X0).reshape(1, 4), Tf)
+    got = milp.MilpBnB(T, g_gamma, g_xbar, goal, ref=ref,
+                       params=mpc.MPCParams.reference_defaults(), u_order=mpc.U_ORDER_F,
+                       T_full=Tf, u_prev=u_prev, base=rows, segments=rs, device=gpu).solve()
+    assert (got is None) == (want is None)
+    if want is not None:
+        assert np.abs(got["u"] - want["u"]).max() <= 1e-6 * (1.0 + np.abs(want["u"]).max())
+        assert got["cost"] == pytest.approx(want["cost"], rel=1e-8)
