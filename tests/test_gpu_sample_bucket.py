@@ -72,7 +72,10 @@ def _assert_same(got, want):
     (3, 25, 8, 4097, 2, None),       # a partial last block
     (2, 12, 8, 8192, 3, None),       # the largest fused cloud
     (2, 7, 1, 300, 4, None),         # T = 1
-    (2, 9, 40, 700, 5, None),        # T = 40 (80 coordinate rows)
+    (2, 9, 40, 700, 5, None),        # T = 40 (80 coordinate rows; the serial chain)
+    (2, 9, 16, 900, 11, None),       # T = 16: the parallel step terms' largest horizon
+    (2, 9, 17, 900, 12, None),       # T = 17: the first serial one
+    (3, 12, 12, 2500, 13, None),     # T = 12 (C4's horizon)
     (3, 25, 8, 3000, 6, 1),          # one kept mode: every rare particle is its
     (2, 10, 8, 2000, 7, 8),          # eight kept modes, few rare particles
     (2, 25, 8, 8192, 9, "heavy"),    # ~7000 rare particles: 28 rare-slot blocks per OV
