@@ -350,8 +350,8 @@ def init_dist(args):
         elif backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        else:       # the one-card rehearsal: every rank on device 0 (device_count() may
+            torch.cuda.set_device(0)   # count cards this process cannot open)
             dist.init_process_group(backend)
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     return world, rank, local
@@ -979,9 +979,19 @@ def spin_sync(local):
         hip = ctypes.CDLL("libamdhip64.so.7")
     except OSError:
         return False
-    if hip.hipSetDevice(ctypes.c_int(local)) != 0:
+    n = ctypes.c_int(0)
+    if hip.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value < 1:
+        hip.hipGetLastError()
         return False
-    return hip.hipSetDeviceFlags(ctypes.c_uint(1)) == 0   # hipDeviceScheduleSpin
+    # the one-card rehearsal (--backend gloo) runs every rank on device 0; a failed call would
+    # leave a sticky error that the next torch call reports
+    if hip.hipSetDevice(ctypes.c_int(local % n.value)) != 0:
+        hip.hipGetLastError()
+        return False
+    ok = hip.hipSetDeviceFlags(ctypes.c_uint(1)) == 0   # hipDeviceScheduleSpin
+    if not ok:
+        hip.hipGetLastError()
+    return ok
 
 
 def main():
