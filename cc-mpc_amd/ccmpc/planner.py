@@ -496,6 +496,8 @@ class MidlevelAgent:
         if self.max_graphs < 1:
             raise ValueError(f"max_graphs must be >= 1, got {self.max_graphs}")
         self._risk_memo = {}
+        self._k_key = self._k_val = None   # _kept_counts' last pmf
+        self._eps_memo = {}
         self._u_prev = []                  # executed controls of this shrinking episode (:3186)
         self.last_generator_output = None
         self.last_ctrl = None
@@ -1128,10 +1130,12 @@ class MidlevelAgent:
         if not pp and (z_in is not None or eps_in is not None):
             raise ValueError("injected z / eps go with per_particle=True at the graph step")
         pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
-        past_last = np.array([p[-1] for p in pasts])
+        past_last = np.empty((len(pasts), 2))
+        for j, p in enumerate(pasts):
+            past_last[j] = p[-1]
         bboxes = (_default_bboxes(O) if bboxes is None
                   else np.asarray(bboxes, np.float64).reshape(O, 2))
-        K = (pmf > filter_pmf).sum(1).tolist()
+        K = self._kept_counts(pmf, filter_pmf)
         if min(K) == 0:
             raise ValueError("attempt to get argmin of an empty sequence: an OV has no latent "
                              f"mode with p(z|x) > {filter_pmf} (ovehicle.py:96-97)")
@@ -1280,20 +1284,38 @@ class MidlevelAgent:
         finally:
             self._qp_request = None
 
+    def _kept_counts(self, pmf, fp):
+        """Kept modes per OV, (pmf > fp).sum(1) as a list; memoised on the last pmf (a frame
+        asks twice, and small-array numpy reductions are microseconds each)."""
+        key = (pmf.tobytes(), pmf.shape, fp)
+        if key != self._k_key:
+            self._k_val = (pmf > fp).sum(1).tolist()
+            self._k_key = key
+        return list(self._k_val)
+
+    def _eps_ura(self, O, K):
+        """:2909-2916's eps_ura, np.full((O, max K), 0.05 / O), shared read-only per shape."""
+        key = (O, max(K))
+        e = self._eps_memo.get(key)
+        if e is None:
+            e = self._eps_memo[key] = np.full(key, 0.05 / O)
+            e.setflags(write=False)
+        return e
+
     def _prediction_controls(self, frame, T, shrinking, sampler, minpos, pasts, x_init, goal,
                              ref_traj, bboxes, apply_robust, segments, pmf, fp, up):
         from . import episode
         O = pmf.shape[0]
         if shrinking and apply_robust:
-            K = (pmf > fp).sum(1).tolist()
-            eps_ura = np.full((O, max(K)), 0.05 / O)              # :2909-2916
+            K = self._kept_counts(pmf, fp)
+            eps_ura = self._eps_ura(O, K)                         # :2909-2916
             params = episode.Params(O, K, frame)
             params.x_init = np.asarray(x_init, np.float64)
             ovs, out = self.predict_and_constrain(params, sampler, eps_ura, T, ref_traj, minpos,
                                                   pasts, bboxes, filter_pmf=fp)
         else:
-            K = (pmf > fp).sum(1).tolist()
-            eps_ura = np.full((O, max(K)), 0.05 / O)
+            K = self._kept_counts(pmf, fp)
+            eps_ura = self._eps_ura(O, K)
             params = episode.Params(O, K, frame)
             params.x_init = np.asarray(x_init, np.float64)
             ovs, out = self.predict_and_constrain_affine(params, sampler, eps_ura, T, ref_traj,

@@ -40,6 +40,10 @@ wrap(step.StepGraph, "launch", "launch")
 wrap(step.StepGraph, "wait", "records")
 wrap(mpc.PlanningQPStep, "wait", "qp")
 wrap(planner.MidlevelAgent, "_step_tuple", "tuple")
+wrap(planner.MidlevelAgent, "_graph_step", "graph_step")
+wrap(step.StepGraph, "set_inputs", "set_inputs")
+wrap(mpc.PlanningQPStep, "prepare", "prepare")
+wrap(planner.MidlevelAgent, "_cell_risk_host", "risk")
 
 
 def frame(i):
@@ -57,7 +61,11 @@ for i in range(300):
     frame(100 + i)
     t1 = pc()
     m = dict(marks)
-    seg = {"pre-launch": m["launch>"] - t0, "launch call": m["launch<"] - m["launch>"],
+    seg = {"pre-launch": m["launch>"] - t0, "  to _graph_step": m["graph_step>"] - t0,
+           "  risk": m["risk<"] - m["risk>"], "  set_inputs": m["set_inputs<"] - m["set_inputs>"],
+           "  qp prepare": m["prepare<"] - m["prepare>"],
+           "  rest of _graph_step": (m["launch>"] - m["graph_step>"]) - (m["risk<"] - m["risk>"])
+           - (m["set_inputs<"] - m["set_inputs>"]) - (m["prepare<"] - m["prepare>"]), "launch call": m["launch<"] - m["launch>"],
            "launch -> wait": m["records>"] - m["launch<"],
            "records wait": m["records<"] - m["records>"],
            "records -> tuple": m["tuple>"] - m["records<"],
