@@ -49,6 +49,12 @@ constexpr double kEarlyPolish = 1e-4;
 // frame's QP 133.8 -> 47.8 us, the 64-scene batch 359 -> 281 us, the same minimiser and
 // verdict on every tested scene (profiles/r05/ab_qp_method.log, tests/test_gpu_qp_gi.py)
 constexpr int kQpDefaultMethod = CCMPC_QP_METHOD_GI;
+// the records' first loads: 1 = with the setup's first reads (before the model), 0 = in the rows
+// phase, after the model's barrier (which otherwise waits for them: they sit behind the
+// scene-cell load, two dependent round trips)
+#ifndef CCMPC_QP_REC_PREFETCH
+#define CCMPC_QP_REC_PREFETCH 1
+#endif
 
 // ---- the LTV model ---------------------------------------------------------------------------
 // About u = 0 the bicycle model's nominal trajectory is straight at constant speed
@@ -674,11 +680,13 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     return v;
   };
   RecIn rpre[kRecPre];
+#if CCMPC_QP_REC_PREFETCH
 #pragma unroll
   for (int j = 0; j < kRecPre; ++j) {
     const int64_t r = tid + static_cast<int64_t>(j) * NTH;
     if (r < R) rpre[j] = load_rec(r);
   }
+#endif
   double ref_k = 0.0;  // the reference point entry of qf's first row k = tid
   if (tid < T3 && tid % 3 < 2) {
     const int t = tid / 3, tr = t < A.n_ref ? t : A.n_ref - 1;
@@ -798,6 +806,13 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     rw.ix[2 * ro + 1] = 3 * ts + 1;
     hmax = fmax(hmax, fabs(b));
   };
+#if !CCMPC_QP_REC_PREFETCH
+#pragma unroll
+  for (int j = 0; j < kRecPre; ++j) {
+    const int64_t r = tid + static_cast<int64_t>(j) * NTH;
+    if (r < R) rpre[j] = load_rec(r);
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < kRecPre; ++j) {
     const int64_t r = tid + static_cast<int64_t>(j) * NTH;

@@ -44,6 +44,8 @@ wrap(planner.MidlevelAgent, "_graph_step", "graph_step")
 wrap(step.StepGraph, "set_inputs", "set_inputs")
 wrap(mpc.PlanningQPStep, "prepare", "prepare")
 wrap(planner.MidlevelAgent, "_cell_risk_host", "risk")
+wrap(step.Pack, "snapshot", "snapshot")
+wrap(planner.HalfSpaceList, "__init__", "hslist")
 
 
 def frame(i):
@@ -68,6 +70,11 @@ for i in range(300):
            - (m["set_inputs<"] - m["set_inputs>"]) - (m["prepare<"] - m["prepare>"]), "launch call": m["launch<"] - m["launch>"],
            "launch -> wait": m["records>"] - m["launch<"],
            "records wait": m["records<"] - m["records>"],
+           "  snapshot": m["snapshot<"] - m["snapshot>"],
+           "  records< -> snapshot>": m["snapshot>"] - m["records<"],
+           "  snapshot< -> hslist>": m["hslist>"] - m["snapshot<"],
+           "  hslist": m["hslist<"] - m["hslist>"],
+           "  hslist< -> tuple>": m["tuple>"] - m["hslist<"],
            "records -> tuple": m["tuple>"] - m["records<"],
            "tuple": m["tuple<"] - m["tuple>"], "tuple -> qp wait": m["qp>"] - m["tuple<"],
            "qp wait": m["qp<"] - m["qp>"], "after qp": t1 - m["qp<"], "total": t1 - t0}
