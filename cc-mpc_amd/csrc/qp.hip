@@ -1772,6 +1772,9 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     if (A.polish) gi_done = gi_solve();
   }
 
+#if CCMPC_QP_GI_ONLY  // probe build: the active-set instance without the IPM / polish code
+  if constexpr (!GI) {
+#endif
   for (; !gi_done && it <= A.max_iter; ++it) {
     QP_MARK(0);
     // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
@@ -2116,6 +2119,9 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   const uint64_t tk2 = wall_clock64();
 #endif
   if (A.polish && !infeasible && !polished && !gi_done) polished = polish(true);
+#if CCMPC_QP_GI_ONLY
+  }
+#endif
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk3 = wall_clock64();
 #endif
