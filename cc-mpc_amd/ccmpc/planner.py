@@ -281,9 +281,14 @@ def _default_bboxes(O):
 
 
 @functools.lru_cache(maxsize=64)
+@functools.lru_cache(maxsize=256)
+def _first_cells_t(K):
+    return tuple(sum(K[:o]) for o in range(len(K)))
+
+
 def _first_cells(K):
     """First cell of each OV for kept-mode counts K (a tuple)."""
-    return [sum(K[:o]) for o in range(len(K))]
+    return list(_first_cells_t(tuple(K)))
 
 
 @functools.lru_cache(maxsize=64)
@@ -293,6 +298,8 @@ def _last_cells(K):
 
 
 def _object_grid(*shape):
+    if len(shape) == 1:
+        return [None] * shape[0]
     return np.empty(shape, dtype=object).tolist()
 
 

@@ -40,6 +40,7 @@ Outputs live in the graph's buffers until the next replay of the same graph; wha
 keeps across steps (the saved moments) is copied out.
 """
 import collections
+import collections.abc
 import os
 import time
 
@@ -74,6 +75,13 @@ class Pack:
             self._h[name] = raw[off:off + n].view(npdt).reshape(shape)
         self._views = [(name, shape, self._h[name].dtype, off)
                        for name, (off, shape, dtype, n) in self.spec.items()]
+        self._raw = raw
+        # the whole buffer as one structured record: a snapshot is one copy and one array, its
+        # fields views made on access (numpy's per-view constructor cost was most of it)
+        self._struct = np.dtype({"names": [v[0] for v in self._views],
+                                 "formats": [(v[2], v[1]) for v in self._views],
+                                 "offsets": [v[3] for v in self._views],
+                                 "itemsize": self.nbytes})
 
     def d(self, name):
         """Device view of a field."""
@@ -85,11 +93,29 @@ class Pack:
 
     def snapshot(self, device=False):
         """One copy of the whole host buffer (device=True: of the device buffer, synchronously);
-        returns {field: view of the copy} (outputs that must outlive the next replay, for one
-        memcpy instead of one per field)."""
-        raw = self.dev.cpu().numpy() if device else self.host.numpy().copy()
-        nd = np.ndarray
-        return {name: nd(shape, dt, raw, off) for name, shape, dt, off in self._views}
+        returns a read-only mapping {field: view of the copy} (outputs that must outlive the
+        next replay, for one memcpy instead of one per field)."""
+        raw = self.dev.cpu().numpy() if device else self._raw.copy()
+        return _Snapshot(np.ndarray((), self._struct, raw))
+
+
+class _Snapshot(collections.abc.Mapping):
+    """Pack.snapshot's result: field name -> array view of one copied buffer."""
+    __slots__ = ("_a",)
+
+    def __init__(self, a):
+        self._a = a
+
+    def __getitem__(self, name):
+        if name not in self._a.dtype.fields:
+            raise KeyError(name)
+        return self._a[name]
+
+    def __iter__(self):
+        return iter(self._a.dtype.names)
+
+    def __len__(self):
+        return len(self._a.dtype.names)
 
 
 class HipGraph:
