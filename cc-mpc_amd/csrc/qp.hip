@@ -1598,16 +1598,20 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         const double mj = lane < n ? -(pc0 * gcol(pix.x, li) + pc1 * gcol(pix.y, li)) : 0.0;
         double sp = -row_g(pr, y, z);  // its slack (< 0)
         double uplus = 0.0;
-        double mm[16];  // m, uniform (fixed while this row enters)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mm[i] = lane_bcast(mj, i);
+        // m, fixed while this row enters: broadcast through LDS (the IPM's rh slots, free
+        // here), read as VGPR operands -- sixteen readlane results held in SGPRs were part of
+        // the kernel's SGPR spilling
+        double *mvec = lds + lay.rh, *dvec = lds + lay.e2;
+        wave_sync();
+        if (lane < 16) mvec[lane] = mj;
+        wave_sync();
         while (true) {
           if (++steps > max_steps) return give_up();
           // d = J^T m (lane j), r = R^{-1} d[:q] (lane k < q)
           double dj = 0.0;
 #pragma unroll
           for (int i = 0; i < 16; ++i)
-            if (i < n) dj = fma(Jm[i * ldm + li], mm[i], dj);
+            if (i < n) dj = fma(Jm[i * ldm + li], mvec[i], dj);
           double rhs = dj, rk = 0.0;
           for (int j = q - 1; j >= 0; --j) {
             const double xj = lane_bcast(rhs, j) * Rdi[j];
@@ -1616,8 +1620,11 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
           }
           GI_ACC(1);
           double dd[16];
+          wave_sync();
+          if (lane < 16) dvec[lane] = dj;
+          wave_sync();
 #pragma unroll
-          for (int k = 0; k < 16; ++k) dd[k] = lane_bcast(dj, k);
+          for (int k = 0; k < 16; ++k) dd[k] = dvec[k];
           double d2 = 0.0, dn2 = 0.0, zi = 0.0;
 #pragma unroll
           for (int k = 0; k < 16; ++k) {
