@@ -138,6 +138,8 @@ struct QpArgs {
   int rec_compact;    // records are ccmpc_gather_rec (32 bytes), rec_kind their source kind
   int early_discard;  // test hook: attempt the early polish, never keep its answer
   int method;         // CCMPC_QP_METHOD_IPM, or _GI (one wave, n <= 16; else the IPM)
+  int gi_max_steps;   // the active-set step budget (< 0: 8 (n + 16)); a test hook forces the
+                      // hand-over to the IPM with 0
   int64_t max_cells;
   double tol, early;  // early: the early polish threshold on mu / max(mu0, 1) (0 = none)
   const double *gamma, *xbar, *ubar, *u_prev, *goal, *ref;
@@ -1533,7 +1535,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       update_y();
       GI_MARK(4);
       int q = 0, steps = 0;
-      const int max_steps = 8 * (n + 16);
+      const int max_steps = A.gi_max_steps >= 0 ? A.gi_max_steps : 8 * (n + 16);
       double *Rdi = lds + lay.dinv;  // 1 / R[k][k] (L's reciprocals are no longer needed)
       // J stays in registers (lane i: row i, every rotation local); its LDS mirror serves the
       // column reads of d = J^T m
@@ -2293,6 +2295,10 @@ static int mpc_qp_impl(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T, int
     const char *e = getenv("CCMPC_QP_METHOD");  // per call (tests switch it)
     a.method = (e && strcmp(e, "ipm") == 0) ? CCMPC_QP_METHOD_IPM
                : (e && strcmp(e, "gi") == 0) ? CCMPC_QP_METHOD_GI : kQpDefaultMethod;
+  }
+  {
+    const char *e = getenv("CCMPC_QP_GI_MAX_STEPS");  // per call (test hook)
+    a.gi_max_steps = e ? atoi(e) : -1;
   }
   {
     const char *e = getenv("CCMPC_QP_EARLY_POLISH");  // per call (a test switches it)

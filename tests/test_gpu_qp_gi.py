@@ -77,3 +77,39 @@ def test_gi_shrinking_horizon_with_executed_controls(gpu, monkeypatch):
     for i in np.flatnonzero(res["ipm"][3] == mpc.QP_OK):
         tol = 1e-7 * (1.0 + np.abs(res["ipm"][0][i]).max())
         assert np.abs(res["gi"][0][i] - res["ipm"][0][i]).max() <= tol
+
+
+def test_gi_hands_over_to_the_ipm(gpu, monkeypatch):
+    """A solve that exceeds the active-set step budget (forced here: CCMPC_QP_GI_MAX_STEPS=0)
+    hands the problem to the IPM in the same launch from the setup's state: the scenes that
+    needed an active-set change come back as the IPM alone returns them, byte for byte, the
+    others (the unconstrained minimum is feasible) agree to round-off."""
+    from ccmpc import mpc
+    T = 8
+    seeds = list(range(40, 52))
+    rec, cps, _, refs, goals, x0s = _scene_inputs(seeds, T, gpu, "halfspace")
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    goal = torch.as_tensor(goals, device=gpu)
+    ref = torch.as_tensor(refs, device=gpu)
+
+    def run(method, steps=None):
+        monkeypatch.setenv("CCMPC_QP_METHOD", method)
+        if steps is None:
+            monkeypatch.delenv("CCMPC_QP_GI_MAX_STEPS", raising=False)
+        else:
+            monkeypatch.setenv("CCMPC_QP_GI_MAX_STEPS", str(steps))
+        qp = mpc.PlanningQP(cps, T, device=gpu)
+        out = qp.solve(gamma, xbar, goal, ref, rec)
+        return [t.cpu().numpy().copy() for t in out]
+
+    ipm = run("ipm")
+    forced = run("gi", 0)
+    gi = run("gi")
+    handed = 0
+    for s in range(len(seeds)):
+        if gi[4][s] > 0:          # the normal GI solve took at least one active-set step
+            assert all(a[s].tobytes() == b[s].tobytes() for a, b in zip(forced, ipm)), s
+            handed += 1
+        else:                     # no step needed: the budget never bit
+            assert all(a[s].tobytes() == b[s].tobytes() for a, b in zip(forced, gi)), s
+    assert handed > 0
