@@ -49,6 +49,8 @@ constexpr double kEarlyPolish = 1e-4;
 // frame's QP 133.8 -> 47.8 us, the 64-scene batch 359 -> 281 us, the same minimiser and
 // verdict on every tested scene (profiles/r05/ab_qp_method.log, tests/test_gpu_qp_gi.py)
 constexpr int kQpDefaultMethod = CCMPC_QP_METHOD_GI;
+// internal status bit: the active-set-only instance handed this scene to the IPM pass
+constexpr int kQpNeedIpm = 1 << 20;
 // the records' first loads: 1 = with the setup's first reads (before the model), 0 = in the rows
 // phase, after the model's barrier (which otherwise waits for them: they sit behind the
 // scene-cell load, two dependent round trips)
@@ -140,6 +142,7 @@ struct QpArgs {
   int method;         // CCMPC_QP_METHOD_IPM, or _GI (one wave, n <= 16; else the IPM)
   int gi_max_steps;   // the active-set step budget (< 0: 8 (n + 16)); a test hook forces the
                       // hand-over to the IPM with 0
+  int fallback_only;  // the IPM pass after an active-set-only launch (kQpNeedIpm scenes only)
   int64_t max_cells;
   double tol, early;  // early: the early polish threshold on mu / max(mu0, 1) (0 = none)
   const double *gamma, *xbar, *ubar, *u_prev, *goal, *ref;
@@ -584,7 +587,7 @@ __device__ __forceinline__ double hctrl_mul(const double *z, int i, int T, int o
 // NW waves per scene: 4 (the general form), or 1 for n = 2T <= 16 (the reference's ph = 8):
 // every barrier is then a wave-level ordering and every reduction a wave butterfly, which
 // takes the ~30 workgroup barriers per IPM iteration off the chain.
-template <bool ROWS_LDS, int NM, int NW, bool GI = false>
+template <bool ROWS_LDS, int NM, int NW, bool GI = false, bool GIONLY = false>
 __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // multiply-adds fused in the solver (the library builds with -ffp-contract=off for the
   // moments' reference arithmetic; the IPM's iterates carry no such contract, and its answer
@@ -594,6 +597,8 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   extern __shared__ double lds[];
   const int64_t sc = blockIdx.x;
   if (sc >= A.S) return;
+  // the IPM pass after a GIONLY launch solves only the scenes the active-set pass handed over
+  if (A.fallback_only && !(A.out_status[sc] & kQpNeedIpm)) return;
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk0 = wall_clock64();
   uint64_t smark[4] = {};
@@ -1779,11 +1784,16 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       return true;
     };
     if (A.polish) gi_done = gi_solve();
+    if constexpr (GIONLY) {
+      if (!gi_done) status = kQpNeedIpm;  // the IPM pass launched next takes this scene
+    }
   }
 
-#if CCMPC_QP_GI_ONLY  // probe build: the active-set instance without the IPM / polish code
-  if constexpr (!GI) {
+#ifdef CCMPC_QP_TRACE
+  uint64_t tk2 = 0;
 #endif
+  // the IPM and the polish: compiled out of the active-set-only instance (its registers)
+  if constexpr (!GIONLY) {
   for (; !gi_done && it <= A.max_iter; ++it) {
     QP_MARK(0);
     // ---- I1: residual norms, mu, per-step sums for r_d and M -------------------------------
@@ -2125,12 +2135,10 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   }
 
 #ifdef CCMPC_QP_TRACE
-  const uint64_t tk2 = wall_clock64();
+  tk2 = wall_clock64();
 #endif
   if (A.polish && !infeasible && !polished && !gi_done) polished = polish(true);
-#if CCMPC_QP_GI_ONLY
   }
-#endif
 #ifdef CCMPC_QP_TRACE
   const uint64_t tk3 = wall_clock64();
 #endif
@@ -2205,18 +2213,18 @@ inline QpPlan qp_plan(int T, int64_t R) {
   return {false, false};
 }
 
-template <bool ROWS_LDS, int NM, int NW, bool GI = false>
+template <bool ROWS_LDS, int NM, int NW, bool GI = false, bool GIONLY = false>
 hipError_t launch_qp(dim3 grid, size_t lds, hipStream_t s, const QpArgs &a) {
   const dim3 block(64 * NW);
   // the dynamic-LDS limit is a per-device attribute: set it on every launch (cheap), so a
   // process that drives several devices raises it on each, and report a failure as such
   if (lds > 48 * 1024) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM, NW, GI>),
+        reinterpret_cast<const void *>(mpc_qp_kernel<ROWS_LDS, NM, NW, GI, GIONLY>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kQpLdsBytes));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM, NW, GI>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((mpc_qp_kernel<ROWS_LDS, NM, NW, GI, GIONLY>), grid, block, lds, s, a);
   return hipSuccess;
 }
 
@@ -2352,7 +2360,24 @@ static int mpc_qp_impl(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T, int
   hipStream_t s = as_stream(stream);
   hipError_t attr;
   const bool gi = one_wave && a.method == CCMPC_QP_METHOD_GI && plan.polish;
-  if (gi) {
+  // a batch runs the active-set pass without the IPM's code in its instance (189 instead of
+  // 488 VGPRs, far fewer SGPR spills), then an IPM pass that solves only the scenes it handed
+  // over -- the IPM's own answer, byte for byte, as the combined instance's hand-over gives;
+  // a single scene keeps the combined instance (the second launch would cost it more)
+  static const bool split_env = [] {
+    const char *e = getenv("CCMPC_QP_GI_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  if (gi && n_scenes > 1 && split_env) {
+    attr = in_lds ? launch_qp<true, 16, 1, true, true>(grid, lds, s, a)
+                  : launch_qp<false, 16, 1, true, true>(grid, lds, s, a);
+    if (attr == hipSuccess) {
+      QpArgs f = a;
+      f.fallback_only = 1;
+      attr = in_lds ? launch_qp<true, 16, 1>(grid, lds, s, f)
+                    : launch_qp<false, 16, 1>(grid, lds, s, f);
+    }
+  } else if (gi) {
     attr = in_lds ? launch_qp<true, 16, 1, true>(grid, lds, s, a)
                   : launch_qp<false, 16, 1, true>(grid, lds, s, a);
   } else if (in_lds) {
