@@ -1077,7 +1077,7 @@ class MidlevelAgent:
             self._moments[params.frame] = (o["imean"], o["icov"], list(K), T)   # :960
         else:
             self._moments[params.frame] = (o["mean"], o["cov"], list(K), T)     # :960
-            self.prob_lower_save = list(o["pl"][-1])          # last cell wins (:947, :961)
+            self.prob_lower_save = o["pl"][-1].tolist()       # last cell wins (:947, :961)
         P = T * (T - 1) // 2
         constraints = HalfSpaceList(h, scene.cell_of, P)
         self.last_records = h[:, :P]
@@ -1136,10 +1136,12 @@ class MidlevelAgent:
             raise ValueError("per-particle GMM parameters need the injected z (prediction.py:103)")
         if not pp and (z_in is not None or eps_in is not None):
             raise ValueError("injected z / eps go with per_particle=True at the graph step")
-        pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
+        # only the last past point goes into the step; the full pasts are converted for the
+        # OVehicles after the launch, while the graph runs
         past_last = np.empty((len(pasts), 2))
         for j, p in enumerate(pasts):
-            past_last[j] = p[-1]
+            v = p[-1] if isinstance(p, np.ndarray) and p.ndim == 2 and p.shape[1] == 2 else None
+            past_last[j] = v if v is not None else np.asarray(p, np.float64).reshape(-1, 2)[-1]
         bboxes = (_default_bboxes(O) if bboxes is None
                   else np.asarray(bboxes, np.float64).reshape(O, 2))
         K = self._kept_counts(pmf, filter_pmf)
@@ -1204,6 +1206,7 @@ class MidlevelAgent:
             self._ltv_built = True
             self._qp_pending = ((run, qgen), g.out.d("rec"), (T, mpc.U_ORDER_F))
         # host objects that need no output are built while the graph runs
+        pasts = [np.asarray(p, np.float64).reshape(-1, 2) for p in pasts]
         st = g.store
         scene = ovehicle.ScenePredictions(st, K, past_last, bboxes)
         scene.bind_generation(g)
