@@ -155,7 +155,9 @@ def check_kept_modes_drawn(centre, K):
     no rare particle is ever assigned to it; the drop-in raises the reference's error instead of
     returning that cell.  centre: per-cell init_center (host, (C, 2)), cells in (ov, k) order."""
     centre = np.asarray(centre, np.float64)
-    s = float(centre.sum())       # finite centres sum to a finite value; one NaN makes it NaN
+    # finite centres sum to a finite value; one NaN makes it NaN (a Python sum over the list:
+    # numpy's reduction machinery costs ~2 us on these few values)
+    s = sum(centre.reshape(-1).tolist())
     if s == s:
         return
     bad = np.flatnonzero(np.isnan(centre.reshape(-1, 2)).any(1))

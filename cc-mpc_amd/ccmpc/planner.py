@@ -1068,7 +1068,7 @@ class MidlevelAgent:
         kind = "minkowski" if T == ph else "ideal"
         ovs, g, o, scene, K = self._graph_step(kind, params, sampler, eps_ura, T, ref_traj,
                                                minpos, pasts, bboxes, filter_pmf)
-        h = o["rec"].reshape(-1).view(engine._lib.HALFSPACE_DTYPE).reshape(g.C, g.P)
+        h = o["records"]
         if kind == "ideal":
             st = o["status"]
             if st.any():
@@ -1096,7 +1096,7 @@ class MidlevelAgent:
             raise ValueError("the affine generator runs on the prediction horizon's particles")
         ovs, g, o, scene, K = self._graph_step("affine", params, sampler, eps_ura, T, ref_traj,
                                                minpos, pasts, bboxes, filter_pmf)
-        h = o["rec"].reshape(-1).view(engine._lib.AFFINE_DTYPE).reshape(g.C, T)
+        h = o["records"]
         self.last_records = h
         self._last_rec = (g.out.d("rec"), mpc.REC_AFFINE, T)
         self._last_sbig = True
@@ -1224,8 +1224,7 @@ class MidlevelAgent:
         heading part of the state statistics read graph B's L4 outputs on access."""
         ph = self.prediction_horizon
         if constraints is None:
-            constraints = HalfSpaceList(o["rec"].reshape(-1).view(engine._lib.HALFSPACE_DTYPE)
-                                        .reshape(g.C, g.P), scene.cell_of, g.T * (g.T - 1) // 2)
+            constraints = HalfSpaceList(o["records"], scene.cell_of, g.T * (g.T - 1) // 2)
         gen = g.generation
         l4 = _LazyL4(g, gen)
         mean0, cov0 = o["mean"][:, 0, :], o["cov"][:, 0:2, 0:2]

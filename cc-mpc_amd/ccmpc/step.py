@@ -56,7 +56,10 @@ class Pack:
     """Named, 256-byte aligned fields of one flat device buffer, mirrored in pinned host memory
     (one copy moves all of them)."""
 
-    def __init__(self, fields, device):
+    def __init__(self, fields, device, record_views=None):
+        """record_views: {alias: (field, numpy record dtype)} -- snapshot-only views of a byte
+        field as records (its last axis the record size), so a snapshot hands out the records
+        without a per-call dtype view (~2.3 us each)."""
         self.spec, off = {}, 0
         for name, shape, dtype in fields:
             shape = tuple(int(s) for s in shape)
@@ -77,10 +80,18 @@ class Pack:
                        for name, (off, shape, dtype, n) in self.spec.items()]
         self._raw = raw
         # the whole buffer as one structured record: a snapshot is one copy and one array, its
-        # fields views made on access (numpy's per-view constructor cost was most of it)
-        self._struct = np.dtype({"names": [v[0] for v in self._views],
-                                 "formats": [(v[2], v[1]) for v in self._views],
-                                 "offsets": [v[3] for v in self._views],
+        # fields views made on access (numpy's per-view constructor cost was most of it); a
+        # record view is one more field over the same bytes
+        views = [(name, shape, dt, off) for name, shape, dt, off in self._views]
+        for alias, (field, rdt) in (record_views or {}).items():
+            _, shape, dt, off = next(v for v in self._views if v[0] == field)
+            rdt = np.dtype(rdt)
+            if shape[-1] * dt.itemsize != rdt.itemsize:
+                raise ValueError(f"{field}: last axis is not one {rdt.itemsize}-byte record")
+            views.append((alias, shape[:-1], rdt, off))
+        self._struct = np.dtype({"names": [v[0] for v in views],
+                                 "formats": [(v[2], v[1]) for v in views],
+                                 "offsets": [v[3] for v in views],
                                  "itemsize": self.nbytes})
 
     def d(self, name):
@@ -281,7 +292,8 @@ class StepGraph:
         if kind == "ideal":
             out += [("imean", (C, T, 2), f64), ("icov", (C, 2 * T, 2 * T), f64),
                     ("status", (C,), i32)]
-        self.out = Pack(out, self.device)
+        rdt = engine._lib.AFFINE_DTYPE if kind == "affine" else engine._lib.HALFSPACE_DTYPE
+        self.out = Pack(out, self.device, record_views={"records": ("rec", rdt)})
         # one L4 output pack per generation parity (the two graphs alternate)
         self.out_l4s = [Pack([("A", (C, ph_, 4, 2), f64), ("b", (C, ph_, 4), f64),
                               ("yaw_mean", (C, ph_), f64), ("yaw0_var", (C,), f64)], self.device)
