@@ -280,7 +280,6 @@ def _default_bboxes(O):
     return b
 
 
-@functools.lru_cache(maxsize=64)
 @functools.lru_cache(maxsize=256)
 def _first_cells_t(K):
     return tuple(sum(K[:o]) for o in range(len(K)))
