@@ -178,3 +178,23 @@ def test_first_replay_is_not_signalled_by_the_capture_warmup(gpu, monkeypatch):
     held[0].replay(torch.cuda.current_stream(gpu).cuda_stream)
     g.wait()
     assert int(g._flags[0]) == 2
+
+
+def test_pack_record_view_is_the_byte_field(gpu):
+    """Pack(record_views=...): a snapshot's record field covers the byte field's bytes with the
+    record dtype (what predict_and_constrain hands to HalfSpaceList), in the snapshot's own
+    copy; a byte field whose last axis is not one record is refused."""
+    import torch
+    from ccmpc import engine, step
+    hd = engine._lib.HALFSPACE_DTYPE
+    p = step.Pack([("a", (3,), torch.float64), ("rec", (2, 5, hd.itemsize), torch.uint8)], gpu,
+                  record_views={"records": ("rec", hd)})
+    p.h("rec")[...] = np.random.default_rng(1).integers(0, 256, p.h("rec").shape, dtype=np.uint8)
+    o = p.snapshot()
+    assert o["records"].dtype == hd and o["records"].shape == (2, 5)
+    np.testing.assert_array_equal(o["records"].view(np.uint8).reshape(2, 5, -1), o["rec"])
+    np.testing.assert_array_equal(o["rec"], p.h("rec"))
+    assert not np.shares_memory(o["records"], p.h("rec"))
+    assert set(o) == {"a", "rec", "records"}
+    with pytest.raises(ValueError, match="not one"):
+        step.Pack([("rec", (2, 100), torch.uint8)], gpu, record_views={"r": ("rec", hd)})
