@@ -11,7 +11,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get(
     "CCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libccmpc.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 CCMPC_OK = 0
 CCMPC_F64 = 0
@@ -88,7 +88,10 @@ SIGNATURES = {
                                     _P, _P, _SZ, _P, _I64, _P, _P, _P, _P, _P]),
     "ccmpc_compact_records": (ctypes.c_int, [_P, ctypes.c_int, _I64, _P, _P]),
     "ccmpc_load_predictions": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _I64, _I64, _I64, _I64,
-                                              _P, _I64, _I64, _P, _P]),
+                                              _P, _I64, _I64, _P, _P, _P]),
+    "ccmpc_bucket_predictions": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _I64, _I64, _I64,
+                                                _I64, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P,
+                                                _I64, _P, _P, _P, _P, _P, _P]),
     "ccmpc_sample_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "ccmpc_sample_bucket": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P, _P, _I64, _I64, _I64, _D,
                                            _U64, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P,

@@ -333,11 +333,24 @@ def load_predictions(predictions, z, n_latent, rows=None, device="cuda"):
                           align=4)
     out_z = torch.empty((O, N), dtype=torch.int32, device=dev)
     stride = store.offsets[1] if O > 1 else N
+    z_bad = torch.zeros(O, dtype=torch.int32, device=dev)
     _lib.check(lib.ccmpc_load_predictions(
         _p(pred), _p(zt), zt.element_size(), _p(t_rows), O, N, T, int(n_latent), _p(store.pos),
-        store.ld, stride, _p(out_z), _stream()), "ccmpc_load_predictions")
+        store.ld, stride, _p(out_z), _p(z_bad), _stream()), "ccmpc_load_predictions")
+    raise_bad_latents(z_bad.cpu().numpy(), n_latent)
     store._keepalive = (pred, zt, t_rows)
     return out_z, store
+
+
+def raise_bad_latents(z_bad, n_latent):
+    """IndexError where make_ovehicles' `veh_latent_predictions[zn[jdx]]` (v8ideal/__init__.py:
+    488-491, a list of n_latent entries) raises it: z_bad[o] = OV o's ids outside
+    [-n_latent, n_latent), counted on the device."""
+    bad = [int(b) for b in np.asarray(z_bad).reshape(-1)]
+    if any(bad):
+        o = next(j for j, b in enumerate(bad) if b)
+        raise IndexError(f"list index out of range: {bad[o]} latent id(s) of OV {o} outside "
+                         f"[-{n_latent}, {n_latent}) (make_ovehicles' per-latent list)")
 
 
 def _sampler_inputs(init_state, latent_pmf, gmm, N, T, dev, z, eps, per_particle):
@@ -395,13 +408,13 @@ def _bucket_plan(pmf, filter_pmf, max_k):
     return K, max_k, keep_map, cell_base
 
 
-FUSED_MAX_N = 8192
+FUSED_MAX_N = 1 << 18          # ccmpc_sample_bucket / ccmpc_bucket_predictions
 
 
 def sample_bucket(init_state, latent_pmf, gmm, N, T, minpos, dt=0.5, seed=0, device="cuda",
                   ov_base=0, z=None, eps=None, per_particle=False, filter_pmf=0.1, max_k=None,
                   with_z=False, workspace=None):
-    """Sampler + bucketing in three short launches (ccmpc_sample_bucket, N <= 8192): the draws of
+    """Sampler + bucketing as one placement pass (ccmpc_sample_bucket, N <= 262144): the draws of
     sample_unicycle with the same arguments, bucketed as bucket() buckets them (each cell the
     same particles in the same order, the same pmf / init_center bits; only the cell offsets
     differ).  latent_pmf (O, L) is required (it decides the kept modes).
@@ -451,6 +464,69 @@ def sample_bucket(init_state, latent_pmf, gmm, N, T, minpos, dt=0.5, seed=0, dev
     out._keepalive = (t_init, t_cdf, t_gmm, t_z, t_eps, t_keep, t_nk, t_base, t_min, t_reg, ws)
     if with_z:
         return out_z, out, K, pmf_out, centre
+    return out, K, pmf_out, centre
+
+
+def bucket_predictions(predictions, z, latent_pmf, minpos, rows=None, filter_pmf=0.1,
+                       max_k=None, device="cuda", workspace=None):
+    """make_ovehicles on generate_vehicle_latents' predictions (nodes, N, T, 2) float32 and z
+    (nodes, N) int64 / int32 (prediction.py:93-105; host arrays or device tensors) in one
+    placement pass (ccmpc_bucket_predictions): the cells load_predictions + bucket give, bit
+    for bit (only the cell offsets differ).  OV o = node rows[o] (default: every node);
+    latent_pmf (O, L).  Raises IndexError where the reference's list index does (an id outside
+    [-L, L)).  Returns (bucketed F32 ParticleStore, K per OV, cell_pmf, init_center)."""
+    lib = _lib.load()
+    dev = require_device(device)
+    pred = torch.as_tensor(predictions, device=dev)
+    if pred.dtype != torch.float32 or pred.dim() != 4 or pred.shape[3] != 2:
+        raise ValueError("predictions must be (nodes, N, T, 2) float32")
+    pred = pred.contiguous()
+    zt = torch.as_tensor(z, device=dev).contiguous()
+    if zt.dtype not in (torch.int64, torch.int32) or tuple(zt.shape) != tuple(pred.shape[:2]):
+        raise ValueError("z must be (nodes, N) int64 or int32")
+    n_nodes, N, T = int(pred.shape[0]), int(pred.shape[1]), int(pred.shape[2])
+    rows = list(range(n_nodes)) if rows is None else [int(r) for r in rows]
+    if any(r < 0 or r >= n_nodes for r in rows):
+        raise ValueError(f"rows outside [0, {n_nodes})")
+    pmf = np.asarray(latent_pmf, np.float64)
+    O, L = pmf.shape
+    if O != len(rows):
+        raise ValueError(f"latent_pmf has {O} rows for {len(rows)} OVs")
+    if not 1 <= N <= FUSED_MAX_N:
+        raise ValueError(f"bucket_predictions takes N in [1, {FUSED_MAX_N}]: use "
+                         "load_predictions + bucket beyond")
+    K, max_k, keep_map, cell_base = _bucket_plan(pmf, filter_pmf, max_k)
+    region, cur, n_bound = [], 0, 0
+    for o in range(O):
+        region.append(cur)
+        cur = _round4(cur + K[o] * (N + 4))
+        n_bound = _round4(n_bound + N + 4 * K[o])
+    n_cells = int(sum(K))
+    mp = np.asarray(minpos, np.float64).reshape(-1, 2)
+    mp = np.tile(mp, (O, 1)) if mp.shape[0] == 1 else mp
+    origin = np.repeat(mp, K, axis=0)
+    out = ParticleStore(T, [0] * n_cells, dtype=torch.float32, device=dev, origin=origin,
+                        capacity=cur)
+    out.counts = None
+    out.n_bound = n_bound
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)
+    t_keep, t_nk, t_base = t(keep_map), t(np.asarray(K, np.int32)), t(cell_base)
+    t_min, t_reg = t(mp), t(np.asarray(region, np.int64))
+    t_rows = t(np.asarray(rows, np.int32))
+    pmf_out = torch.empty(n_cells, dtype=torch.float64, device=dev)
+    centre = torch.empty((n_cells, 2), dtype=torch.float64, device=dev)
+    z_bad = torch.empty(O, dtype=torch.int32, device=dev)
+    need = lib.ccmpc_sample_bucket_workspace_bytes(O, N, T, max_k)
+    if need == 0:
+        raise ValueError("shape not supported by ccmpc_bucket_predictions")
+    ws = workspace if workspace is not None else torch.empty(need, dtype=torch.uint8, device=dev)
+    _lib.check(lib.ccmpc_bucket_predictions(
+        _p(pred), _p(zt), zt.element_size(), _p(t_rows), O, N, T, L, _p(t_keep), _p(t_nk),
+        _p(t_base), max_k, _p(t_min), _p(t_reg), _p(ws), ws.numel(), _p(out.pos), out.ld,
+        _p(out.cell_off), _p(out.cell_cnt), _p(pmf_out), _p(centre), _p(z_bad), _stream()),
+        "ccmpc_bucket_predictions")
+    raise_bad_latents(z_bad.cpu().numpy(), L)
+    out._keepalive = (pred, zt, t_rows, t_keep, t_nk, t_base, t_min, t_reg, ws)
     return out, K, pmf_out, centre
 
 

@@ -1212,6 +1212,8 @@ class MidlevelAgent:
         ovs = [ovehicle.OVehicle(scene, j, past=pasts[j]) for j in range(O)]
         g.wait()
         o = g.out.snapshot()            # the record path's outputs in one host copy
+        if source == "predictions":      # make_ovehicles' list index on z (:488-491)
+            engine.raise_bad_latents(o["zbad"][:O], L)
         ovehicle.check_kept_modes_drawn(o["centre"], K)
         st.counts = o["cnt"].tolist()
         st.offsets = o["off"].tolist()
@@ -1290,7 +1292,9 @@ class MidlevelAgent:
                                              x_init, goal, ref_traj, bboxes, apply_robust,
                                              segments, pmf, fp, up)
         finally:
-            self._qp_request = None
+            # a frame that raised after the launch leaves no (run, gen) entry behind for a
+            # later direct solve_planning_qp call to mistake for its own
+            self._qp_request = self._qp_pending = None
 
     def _kept_counts(self, pmf, fp):
         """Kept modes per OV, (pmf > fp).sum(1) as a list; memoised on the last pmf (a frame

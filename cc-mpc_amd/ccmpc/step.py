@@ -255,6 +255,9 @@ class StepGraph:
                      else [("gmm", (O, L_, ph_, 5), f32)])
         if source == "predictions" and not self.pred_device:
             gmm_field += [("pred", (O, N, ph_, 2), f32), ("zin", (O, N), i64)]
+        O4 = -(-O // 4) * 4               # (16-byte copies)
+        if source == "predictions":       # zeroed on the device by every copy-in
+            gmm_field += [("zbad0", (O4,), i32)]
         fields = ([("gen", (2,), i64), ("seed", (1,), i64), ("init", (O, 4), f64),
                    ("cdf", (O, L_), f64)] + gmm_field +
                   [("keep", (O, L_), i32), ("nk", (O,), i32), ("base", (O,), i32),
@@ -292,6 +295,8 @@ class StepGraph:
         if kind == "ideal":
             out += [("imean", (C, T, 2), f64), ("icov", (C, 2 * T, 2 * T), f64),
                     ("status", (C,), i32)]
+        if source == "predictions":       # invalid latent ids per OV (make_ovehicles' index)
+            out += [("zbad", (O4,), i32)]
         rdt = engine._lib.AFFINE_DTYPE if kind == "affine" else engine._lib.HALFSPACE_DTYPE
         self.out = Pack(out, self.device, record_views={"records": ("rec", rdt)})
         # one L4 output pack per generation parity (the two graphs alternate)
@@ -301,10 +306,11 @@ class StepGraph:
         # pinned signal word [0]: the record path's generation
         self.flags = torch.zeros(8, dtype=i64, pin_memory=True)
         self._flags = self.flags.numpy()
-        # small clouds: sampler + bucketing in three short launches (ccmpc_sample_bucket), whose
-        # cells need K (N + 4) slots per OV; else the sampler's sample-order store + ccmpc_bucket
+        # N <= 262144: sampler (or the predictor's output) + bucketing as one placement pass
+        # (ccmpc_sample_bucket / ccmpc_bucket_predictions), whose cells need K (N + 4) slots per
+        # OV; else the sample-order store + ccmpc_bucket
         fused_ws = lib.ccmpc_sample_bucket_workspace_bytes(O, N, ph_, self.max_k) \
-            if self.max_k * (L_ + 1) <= 512 and source == "sampler" else 0
+            if self.max_k * (L_ + 1) <= 512 else 0
         self.fused = fused_ws > 0
         region, cur, n_bound = [], 0, 0
         for o in range(O):
@@ -378,6 +384,14 @@ class StepGraph:
                                       p(self.pp_eps))
         else:
             gmm, layout, z_in, eps = p(i.d("gmm")), _lib.GMM_PER_LATENT, None, None
+        if self.fused and self.source == "predictions":
+            pred, z = ((self.pr_pred, self.pr_z) if self.pred_device
+                       else (i.d("pred"), i.d("zin")))
+            return [(lib.ccmpc_bucket_predictions, (
+                p(pred), p(z), 8, None, O, N, T, L, p(i.d("keep")), p(i.d("nk")), p(i.d("base")),
+                self.max_k, p(i.d("minpos")), p(i.d("region")), p(ws), ws.numel(), p(st.pos),
+                st.ld, p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")), p(o.d("centre")),
+                p(o.d("zbad")), s))]
         if self.fused:
             return [(lib.ccmpc_sample_bucket, (
                 p(i.d("init")), p(i.d("cdf")), L, gmm, layout, z_in, eps,
@@ -391,13 +405,18 @@ class StepGraph:
                        else (i.d("pred"), i.d("zin")))
             stride = sm.offsets[1] if O > 1 else N
             first = (lib.ccmpc_load_predictions, (p(pred), p(z), 8, None, O, N, T, L,
-                                                  p(sm.pos), sm.ld, stride, p(self.z), s))
+                                                  p(sm.pos), sm.ld, stride, p(self.z),
+                                                  p(i.d("zbad0")), s))
         else:
             first = (lib.ccmpc_sample_unicycle_ex, (
                 p(i.d("init")), p(i.d("cdf")), L, gmm, layout, z_in,
                 eps, O, N, T, self.dt, 0, p(i.d("seed")), 0, p(self.z), p(sm.pos), sm.ld,
                 s))
-        return [first,
+        calls = [first]
+        if self.source == "predictions":   # the invalid-id counts into the output pack
+            calls.append((lib.ccmpc_copy_kernel_async, (p(o.d("zbad")), p(i.d("zbad0")),
+                                                        o.d("zbad").numel() * 4, s)))
+        return calls + [
                 (lib.ccmpc_bucket, (p(self.z), p(sm.pos), sm.ld, T, O, N, L, p(i.d("keep")),
                                     p(i.d("nk")), p(i.d("base")), self.max_k,
                                     p(i.d("minpos")), p(i.d("region")), p(ws), ws.numel(),
@@ -510,6 +529,9 @@ class StepGraph:
         # step the word back, so the poll can only be satisfied by the replay (else
         # wait() returned at once and the host read the output pack while the replay rewrote it)
         self._flags[0] = self.generation - 1
+        if self.qp is not None:         # the attached QP signalled its own word the same way
+            q = self.qp["step"]
+            q._flags[0] = q.generation - 1
         self.graphs = [HipGraph(self.device, lambda par=par: self._enqueue(par), s)
                        for par in range(2)]
         return self
@@ -610,8 +632,9 @@ class StepGraph:
         (prediction.py:93-105), of which rows[o] is OV o's node (make_ovehicles skips the ego's,
         :475-477; default: rows 0 .. O-1).  Host arrays go into the pinned input pack (moved by
         the step's copy-in); device tensors are copied on the current stream into the graph's
-        own buffers (a graph built with pred_device=True).  Values are not validated on the host
-        (that would synchronise): the load kernel clamps z into [0, L)."""
+        own buffers (a graph built with pred_device=True).  z is not validated on the host
+        (that would synchronise): the kernels count the ids make_ovehicles' list index would
+        refuse into the output pack's "zbad" (the planner raises IndexError on them)."""
         if self.source != "predictions":
             raise ValueError("set_predictions needs a graph built with source='predictions'")
         O, N, T = self.O, self.N, self.ph
@@ -625,6 +648,12 @@ class StepGraph:
         if tuple(predictions.shape[1:]) != (N, T, 2) or tuple(z.shape[1:]) != (N,):
             raise ValueError(f"predictions {tuple(predictions.shape)} / z {tuple(z.shape)}: "
                              f"expected (nodes, {N}, {T}, 2) / (nodes, {N})")
+        nodes = int(predictions.shape[0])
+        if int(z.shape[0]) != nodes or any(not 0 <= r < nodes for r in rows):
+            # (on the device path an out-of-range row would reach index_select and abort the
+            # process with a device-side assert)
+            raise ValueError(f"OV rows {rows} out of range for {nodes} prediction nodes "
+                             f"(z has {int(z.shape[0])})")
         if dev:
             if predictions.device != self.device or z.device != self.device:
                 raise ValueError("predictions / z must be on the graph's device")

@@ -591,8 +591,10 @@ constexpr int kLoadChunk = 128;
 __global__ __launch_bounds__(256) void load_predictions_kernel(
     const float *__restrict__ pred, const void *__restrict__ z, int z_bytes,
     const int32_t *__restrict__ rows, int64_t N, int T, int64_t n_latent,
-    float *__restrict__ pos, int64_t ld, int64_t ov_stride, int32_t *__restrict__ z_out) {
+    float *__restrict__ pos, int64_t ld, int64_t ov_stride, int32_t *__restrict__ z_out,
+    int32_t *__restrict__ z_bad) {
   extern __shared__ float tile[];
+  int bad = 0;
   const int o = blockIdx.y;
   const int64_t row = rows ? rows[o] : o;
   const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kLoadChunk;
@@ -607,10 +609,16 @@ __global__ __launch_bounds__(256) void load_predictions_kernel(
     const int64_t i = row * N + b0 + threadIdx.x;
     int64_t v = z_bytes == 8 ? static_cast<const int64_t *>(z)[i]
                              : static_cast<int64_t>(static_cast<const int32_t *>(z)[i]);
-    v = v < 0 ? 0 : (v >= n_latent ? n_latent - 1 : v);  // the kernels' clamp of injected ids
+    // make_ovehicles indexes a list by it (v8ideal/__init__.py:488-491): [-L, 0) wraps as a
+    // Python index, anything else outside [0, L) raises IndexError there -- counted in z_bad,
+    // clamped here for memory safety
+    if (v < 0 && v >= -n_latent) v += n_latent;
+    bad = v < 0 || v >= n_latent;
+    v = v < 0 ? 0 : (v >= n_latent ? n_latent - 1 : v);
     z_out[o * N + b0 + threadIdx.x] = static_cast<int32_t>(v);
   }
-  __syncthreads();
+  const int nbad = __syncthreads_count(bad);
+  if (threadIdx.x == 0 && nbad > 0 && z_bad) atomicAdd(z_bad + o, nbad);
   float *dst = pos + o * ov_stride + b0;
   for (int e = threadIdx.x; e < W * kLoadChunk; e += 256) {
     const int r = e / kLoadChunk, p = e % kLoadChunk;
@@ -621,7 +629,7 @@ __global__ __launch_bounds__(256) void load_predictions_kernel(
 extern "C" int ccmpc_load_predictions(const float *pred, const void *z, int z_bytes,
                                       const int32_t *rows, int64_t n_ov, int64_t N, int64_t T,
                                       int64_t n_latent, float *pos_out, int64_t ld_out,
-                                      int64_t ov_stride, int32_t *z_out,
+                                      int64_t ov_stride, int32_t *z_out, int32_t *z_bad,
                                       ccmpc_stream_t stream) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_ov >= 0 && N >= 0 && n_ov < 65536, "bad n_ov / N");
@@ -636,7 +644,7 @@ extern "C" int ccmpc_load_predictions(const float *pred, const void *z, int z_by
   hipLaunchKernelGGL(load_predictions_kernel,
                      dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(n_ov)), dim3(256),
                      lds, as_stream(stream), pred, z, z_bytes, rows, N, static_cast<int>(T),
-                     n_latent, pos_out, ld_out, ov_stride, z_out);
+                     n_latent, pos_out, ld_out, ov_stride, z_out, z_bad);
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

@@ -1653,12 +1653,10 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
                   ? __ffsll(static_cast<long long>(__ballot(lane < q && ratio == t1))) - 1
                   : -1;
           const double t2 = zero_step ? INFINITY : -sp / d2;
-          if (!(t1 < INFINITY) && !(t2 < INFINITY)) {  // no step: infeasible
-            status = CCMPC_QP_MAXITER;
-            infeasible = true;
-            it = steps;
-            return true;
-          }
+          // no step exists: the rows look infeasible.  That test rests on round-off-sensitive
+          // comparisons (zero_step, rk > 0) which near-parallel rows of several cells at one t
+          // can tip, so the verdict is the IPM's: it confirms infeasibility or finds the point
+          if (!(t1 < INFINITY) && !(t2 < INFINITY)) return give_up();
           GI_ACC(2);
           const double t = fmin(t1, t2);
           wave_sync();

@@ -1,25 +1,30 @@
-// Sampler + bucketing for small clouds (N <= 8192 particles per OV): the drop-in step's
-// do_prediction -> make_ovehicles (prediction.py:81-86, v8ideal/__init__.py:469-505,
-// ovehicle.py:24-117) in three short launches instead of the sampler and bucket.hip's three.
+// Sampler + bucketing in one placement pass: the drop-in step's do_prediction -> make_ovehicles
+// (prediction.py:81-86, v8ideal/__init__.py:469-505, ovehicle.py:24-117), and the same placement
+// for the reference's own predictor output (generate_vehicle_latents' predictions + z,
+// prediction.py:93-105) instead of the sampler.
 //
-// What makes the four-launch form slow is not work but dependent memory round trips: each of
-// bucket.hip's kernels re-reads the particles, exchanges partials through memory and ends, and
-// the next starts cold (tools/probe_step.py: ~10 us per kernel).  Here:
+// What makes the sampler -> three-kernel bucketing form slow is not work but dependent memory
+// round trips: each of bucket.hip's kernels re-reads the particles, exchanges partials through
+// memory and ends, and the next starts cold (tools/probe_step.py: ~10 us per kernel).  Here:
 //
-//  P0 latents  one latent id per particle (Philox + CDF count, or the injected z) and each
-//              64-particle group's count per category -- kept mode k or "rare".
-//  P1 place    per block of 64 particles (512 threads): the category counts of the groups before
-//              its own and in total (a few KB of reads summed in LDS; an earlier form redrew every
-//              latent of the OV in every block: 13-20 us of Philox).  No exchange is needed to
-//              know where a kept mode's own particles go: cell k of the OV starts at
+//  P0 latents  one latent id per particle (Philox + CDF count, the injected z, or the predictor's
+//              z, validated: make_ovehicles indexes a list by it) and each 64-particle group's
+//              count per category -- kept mode k or "rare" -- plus every 512-particle block's
+//              totals and its count of invalid ids.
+//  P1 place    per block of 64 NCH particles (512 threads): the category counts before its own
+//              groups and in total (the P0 block totals before its block and the few groups
+//              before it inside it).  No exchange is needed to know where a kept mode's own
+//              particles go: cell k of the OV starts at
 //                  region + sum_{j < k} round4(n_j + R)       (R = the OV's rare count)
 //              so it can take its n_j natives AND, in the worst case, every rare particle; its
 //              natives go to  start_k + (natives of k before this block) + (rank in the block).
-//              Then the sampler's two phases (actions in parallel, then the Unicycle chain on
-//              one wave); the chain writes a native particle's 2T coordinates straight into its
-//              cell, and a rare particle's into a rare list in sample order, with its final
-//              position and latent id; and the block's kept-mode sums of the final world
-//              positions (= one 64-particle centre group, bucket.hpp).
+//              Then the sampler's two phases (actions in parallel, then the Unicycle chain, one
+//              wave per 64 particles) -- or, for the predictor's output, the block's coordinate
+//              run staged through LDS; the chain writes a native particle's 2T coordinates
+//              straight into its cell, and a rare particle's into a rare list in sample order,
+//              with its final position and latent id; and each group's kept-mode sums of the
+//              final world positions (= one 64-particle centre group, bucket.hpp).
+//  small clouds (N <= 8192 per OV):
 //  P2 rares    per block of 256 rare-list slots: the centres in the canonical order (bucket.hpp,
 //              so they equal bucket.hip's bit for bit), the key (owner, latent) of EVERY rare
 //              particle of the OV -- a few KB of L2 reads -- counted per bin in LDS in total and
@@ -27,6 +32,15 @@
 //              particles' stable ranks in sample order without any exchange; then the copy of
 //              its rare particles' coordinates into the owners' cells after the natives.  Block
 //              0 writes cell offsets, counts, pmf and centres.
+//  large clouds (every rare key in every block would be R^2 / 256 keys -- 11 M at N = 100 000):
+//  P2 keys     per block of 1024 rare-list slots: the centres (each superblock's partial sum
+//              by its own thread, then the superblocks left to right: the canonical order), the
+//              keys of its slots (kept for P3) and their histogram over the bins.
+//  P3 copy     per block of 256 slots: every P2 block's histogram (a few KB) -> each bin's
+//              total and its count before this block's P2 block; the keys of the slots before it
+//              in that P2 block; then the bin starts, the stable ranks (a scan of each wave's 64
+//              keys) and the copy into the owners' cells.  Block 0 writes cell offsets, counts
+//              and pmf.
 // (A single launch whose last arriving block ranked and copied every rare particle of the OV
 // was measured at 120 us: that tail is one CU's serial work.)
 //
@@ -39,14 +53,17 @@
 
 namespace ccmpc {
 
-constexpr int kFusedMaxN = 8192;
+constexpr int kFusedMaxN = 8192;             // P2 rares (every rare key per block) up to here
+constexpr int kWideMaxN = 1 << 18;            // the keys + copy form (P2 keys, P3 copy) up to here
 constexpr int kFusedMaxBins = 512;
-constexpr int kFP = 64;                       // particles per P1 block (the chain wave)
+constexpr int kFP = 64;                       // particles per chain wave
 constexpr int kFThreads = 512;                // 8 waves
 constexpr int kFWaves = kFThreads / 64;
 constexpr int kFGroups = kFusedMaxN / kFP;    // centre groups (P1 blocks) per OV at most
 constexpr int kParSteps = 16;                 // P1: horizons whose step terms run in parallel
-constexpr int kRThreads = 256;                // P2: rare-list slots per block
+constexpr int kRThreads = 256;                // P2 / P3: rare-list slots per block (per thread 1)
+constexpr int kKeySlots = 4 * kRThreads;      // P2 keys: rare-list slots per block
+constexpr int kWideMaxSup = (kWideMaxN / kFP + kCentreSuper - 1) / kCentreSuper;
 // P2: rare records each thread loads per round (kRThreads x this per round; the first round is
 // issued with the kernel's other loads, so a rare list of up to that many takes no further
 // round trip)
@@ -57,17 +74,25 @@ constexpr int kRWaves = kRThreads / 64;
 // per-OV header: tot[kMaxKept + 1] at h[0..], the int64 cell starts cstart[kMaxKept] at
 // h + 2 * kMaxKept
 constexpr int kHdrInts = 64;
-// per-group category counts: kept modes 0..K-1, then the rare count
+// per-group / per-P0-block category counts: kept modes 0..K-1, then the rare count; a P0
+// block's row also holds its count of invalid latent ids in the last slot
 constexpr int kCntStride = 32;
+constexpr int kBadSlot = kCntStride - 1;
 static_assert(kMaxKept + 1 <= 2 * kMaxKept, "tot[] must end before the cell starts");
 static_assert(4 * kMaxKept <= kHdrInts, "cell starts (int64) must fit the per-OV header");
-static_assert(kCntStride >= kMaxKept + 1, "group counts: one slot per kept mode + rare");
+static_assert(kCntStride >= kMaxKept + 2, "counts: one slot per kept mode + rare + invalid");
+static_assert(kWideMaxSup <= 64, "P2 keys: the superblock sums of one mode fit one LDS row");
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
-__device__ unsigned long long g_fused_ts[3][kStepProbeWG * kStepProbeSlots];
+__device__ unsigned long long g_fused_ts[5][kStepProbeWG * kStepProbeSlots];
 #define FUSED_TS(kern, k) CCMPC_STEP_TS(g_fused_ts[kern], k)
 #else
 #define FUSED_TS(kern, k) CCMPC_STEP_TS(nullptr, k)
 #endif
+
+// where P0's latent ids come from
+constexpr int kZPhilox = 0;  // Philox inverse CDF of latent_cdf (the synthetic sampler mode)
+constexpr int kZIn = 1;      // injected int32 z_in[o][N] (the sampler's per-particle mode)
+constexpr int kZPred = 2;    // the predictor's z[rows[o]][N], int64 or int32 (list-index rules)
 
 struct FusedArgs {
   // sampler (sampler.hip)
@@ -80,53 +105,90 @@ struct FusedArgs {
   uint64_t seed;
   const uint64_t *seed_dev;
   uint32_t ov_base;
+  // the predictor's output (ccmpc_bucket_predictions): pred[row][N][T][2], z[row][N]
+  const float *pred;
+  const void *zsrc;
+  int z_bytes;
+  const int32_t *rows;
   // bucketing (bucket.hip)
   const int32_t *keep_map, *n_kept, *cell_base;
   int max_k;
   const double *minpos;
   const int64_t *region;
-  // workspace (written by P1, read by P2; the kernel boundary orders them)
+  // workspace (each written by one launch and read by later ones: the kernel boundaries order
+  // them, and nothing needs initialising)
   int32_t *zbuf;   // [n_ov][Npad]: latent ids (P0)
   int32_t *gcnt;   // [n_ov][G][kCntStride]: per 64-particle group category counts (P0)
+  int32_t *bsum;   // [n_ov][nb0][kCntStride]: per 512-particle P0 block totals + invalid ids
   int32_t *hdr;    // [n_ov][kHdrInts]: category totals [K + 1], then cell starts (int64) [K]
   double *gpart;   // [n_ov][G][max_k][2]
   float *rinfo;    // [n_ov][Npad][4]: rare particle's final (x, y), latent id (bits), 0
   float *rstore;   // [n_ov][2T][Npad]: rare particles' coordinates, rare-list order
+  int32_t *kbuf;   // [n_ov][Npad]: rare-list slot keys (P2 keys)
+  int32_t *rhist;  // [n_ov][nkb][kFusedMaxBins]: each P2 keys block's bin histogram
   int64_t Npad;
-  int G;
+  int G, nb0, nkb;
   // outputs
   int32_t *out_z;  // optional sample-order latent ids
   float *out;
   int64_t ld_out;
   int64_t *cell_off, *cell_cnt;
   double *cell_pmf, *init_center;
+  int32_t *z_bad;  // optional [n_ov]: invalid latent ids per OV
 };
 
 __device__ __forceinline__ int64_t *hdr_starts(int32_t *h) {
   return reinterpret_cast<int64_t *>(h + 2 * kMaxKept);
 }
 
-// P0: one latent id per particle (Philox inverse CDF, or the injected z) into the workspace, and
-// each 64-particle group's count per category (kept mode k, or K = rare) -- one wave = one group.
-template <bool ZIN>
+// The OV's count of invalid latent ids (P0's per-block counts; one wave of the OV's block 0 of
+// the last kernel): z_bad[o].
+__device__ __forceinline__ void write_z_bad(const FusedArgs &a, int o) {
+  if (threadIdx.x >= 64) return;
+  int s = 0;
+  for (int b = threadIdx.x; b < a.nb0; b += 64)
+    s += a.bsum[(static_cast<int64_t>(o) * a.nb0 + b) * kCntStride + kBadSlot];
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (threadIdx.x == 0) a.z_bad[o] = s;
+}
+
+// P0: one latent id per particle (Philox inverse CDF, the injected z, or the predictor's z)
+// into the workspace, each 64-particle group's count per category (kept mode k, or K = rare) --
+// one wave = one group -- and the block's totals with its count of invalid ids.  The
+// predictor's ids index make_ovehicles' per-latent list (v8ideal/__init__.py:488-491): an id in
+// [-L, 0) wraps as a Python index does, anything else outside [0, L) is what raises IndexError
+// there -- it is counted (and clamped for memory safety); the injected sampler ids must lie in
+// [0, L).
+template <int ZSRC>
 __global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
   __shared__ double cdf_s[64];
   __shared__ int keep_s[64];
+  __shared__ int wc_s[kFWaves][kMaxKept + 2];   // per wave: categories 0..K, then invalid ids
   FUSED_TS(0, 0);
   const int o = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int K = a.n_kept[o], L = a.L;
   const int64_t N = a.N;
-  if (!ZIN && tid < L) cdf_s[tid] = a.latent_cdf[static_cast<int64_t>(o) * L + tid];
+  if (ZSRC == kZPhilox && tid < L) cdf_s[tid] = a.latent_cdf[static_cast<int64_t>(o) * L + tid];
   if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kFThreads + tid;
   const bool v = i < N;
   int z = 0;
-  if (ZIN && v) {
+  bool bad = false;
+  if (ZSRC == kZIn && v) {
     z = a.z_in[static_cast<int64_t>(o) * N + i];
-    z = z < 0 ? 0 : (z >= L ? L - 1 : z);  // memory safety; the host validates
+    bad = z < 0 || z >= L;
+    z = z < 0 ? 0 : (z >= L ? L - 1 : z);
+  } else if (ZSRC == kZPred && v) {
+    const int64_t e = (a.rows ? static_cast<int64_t>(a.rows[o]) : o) * N + i;
+    int64_t zz = a.z_bytes == 8 ? static_cast<const int64_t *>(a.zsrc)[e]
+                                : static_cast<int64_t>(static_cast<const int32_t *>(a.zsrc)[e]);
+    if (zz < 0 && zz >= -L) zz += L;
+    bad = zz < 0 || zz >= L;
+    z = bad ? 0 : static_cast<int>(zz);
   }
   __syncthreads();
-  if (!ZIN && v)
+  if (ZSRC == kZPhilox && v)
     z = draw_latent(i, a.ov_base + static_cast<uint32_t>(o), a.seed_dev ? *a.seed_dev : a.seed,
                     cdf_s, L);
   if (v) {
@@ -141,8 +203,41 @@ __global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
     const int n = __popcll(__ballot(v && cat == c));
     if (lane == c) mine = n;
   }
+  const int nbad = __popcll(__ballot(v && bad));
   if (g < a.G && lane <= K) a.gcnt[(static_cast<int64_t>(o) * a.G + g) * kCntStride + lane] = mine;
+  if (lane <= K) wc_s[w][lane] = mine;
+  if (lane == 0) wc_s[w][kMaxKept + 1] = nbad;
+  __syncthreads();
+  int32_t *bs = a.bsum + (static_cast<int64_t>(o) * a.nb0 + blockIdx.x) * kCntStride;
+  if (tid <= K || tid == kBadSlot) {
+    const int c = tid <= K ? tid : kMaxKept + 1;
+    int s = 0;
+#pragma unroll
+    for (int u = 0; u < kFWaves; ++u) s += wc_s[u][c];
+    bs[tid] = s;
+  }
   FUSED_TS(0, 1);
+}
+
+// The category counts P1 block `blk` needs, into LDS (zeroed by the caller, the first batch of
+// loads issued before the caller's barrier): total_s[c] over the OV, before_s[c] over the
+// groups before g0 -- the P0 block totals (every row: the total; rows before g0's P0 block: the
+// prefix) and the groups of g0's own P0 block before g0.  Integer-exact in any order.
+__device__ __forceinline__ int count_elem(const FusedArgs &a, int o, int e, int nA, int E,
+                                          int Kp1, int b0, bool &in_total, bool &in_before) {
+  in_total = in_before = false;
+  if (e < nA) {
+    const int row = e / Kp1, c = e - row * Kp1;
+    in_total = true;
+    in_before = row < b0;
+    return a.bsum[(static_cast<int64_t>(o) * a.nb0 + row) * kCntStride + c];
+  }
+  if (e < E) {
+    const int ee = e - nA, gg = b0 * kFWaves + ee / Kp1, c = ee - (ee / Kp1) * Kp1;
+    in_before = true;
+    return a.gcnt[(static_cast<int64_t>(o) * a.G + gg) * kCntStride + c];
+  }
+  return 0;
 }
 
 template <bool PP, bool EPSIN>
@@ -184,7 +279,7 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
   const int gsz = L * T * 5;
   const bool staged = !PP && gsz <= static_cast<int>(sizeof(gmm_s) / sizeof(float));
   if (staged)
-    for (int e = tid; e < gsz; e += kFThreads) gmm_s[e] = a.gmm[static_cast<int64_t>(o) * gsz + e];
+    stage_gmm_coefs(a.gmm + static_cast<int64_t>(o) * gsz, gsz / 5, gmm_s, tid, kFThreads);
   if (tid <= K) before_s[tid] = total_s[tid] = 0;
   __syncthreads();
   // category counts before this block's group and in total (integer-exact in any order)
@@ -324,6 +419,227 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
   FUSED_TS(1, 5);
 }
 
+// P1 as one template over the particle source and the block width: MODE bit 1 = injected
+// noise, 2 = per-particle GMM parameters, 4 = the predictor's coordinates instead of the sampler
+// (no actions: the block's 64 NCH x 2T run of pred staged through LDS); NCH chain waves of 64
+// particles per block (1 for the small clouds, 2 above kFusedMaxN, so a 100 000-particle cloud
+// is 782 blocks).  Dynamic LDS (floats), sized by T:
+//   sampler    act[2][T][PB], T <= kParSteps: sc[2][T + 1][PB] (the headings' sin / cos),
+//              gmm_s[L T 5] (coefficient rows) when staged
+//   predictor  tile[PB][2T + 1]
+// The category counts come from P0's block totals (a few hundred ints, not every group's), and
+// each chain wave's category ranks are taken before the actions.
+template <int MODE, int NCH, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedArgs a,
+                                                                        int staged_gmm) {
+  constexpr bool PRED = (MODE & 4) != 0, PP = (MODE & 2) != 0, EPSIN = (MODE & 1) != 0;
+  constexpr int PB = kFP * NCH, NTH = 64 * NW;
+  static_assert(NCH <= NW, "one wave per chain");
+  extern __shared__ float dyn[];
+  __shared__ int keep_s[64];
+  __shared__ int zs[PB];
+  __shared__ int wc_s[NCH][kMaxKept + 1];   // each chain's category counts
+  __shared__ int before_s[kMaxKept + 1], total_s[kMaxKept + 1];
+  __shared__ double st_s[6];                // the OV's initial state (x, y, heading, speed), minpos
+  FUSED_TS(1, 0);
+  const int o = blockIdx.y, blk = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int K = a.n_kept[o], L = a.L, T = a.T, Kp1 = K + 1;
+  const int64_t N = a.N;
+  const int64_t i0 = static_cast<int64_t>(blk) * PB;
+  const int g0 = blk * NCH, b0 = g0 / kFWaves;
+  const int64_t reg = a.region[o];
+  // every load that needs nothing from another, issued together: own latent ids, the count
+  // rows, the tables, the OV's initial state (a global read after the barriers below is a round
+  // trip of its own on the chain), the predictor's coordinate run
+  if (tid < PB && i0 + tid < N) zs[tid] = a.zbuf[static_cast<int64_t>(o) * a.Npad + i0 + tid];
+  if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
+  const int nA = a.nb0 * Kp1, E = nA + (g0 - b0 * kFWaves) * Kp1;
+  constexpr int kC = 4;
+  int cv[kC];
+  bool ct[kC], cb[kC];
+#pragma unroll
+  for (int j = 0; j < kC; ++j) cv[j] = count_elem(a, o, tid + j * NTH, nA, E, Kp1, b0, ct[j], cb[j]);
+  // (into LDS, read where used: eight VGPRs held across the f64-heavy action phase spilled)
+  if (tid < 4) st_s[tid] = PRED ? 0.0 : a.init_state[4 * o + tid];
+  else if (tid < 6) st_s[tid] = a.minpos[2 * o + tid - 4];
+  const uint64_t seed = PRED ? 0 : (a.seed_dev ? *a.seed_dev : a.seed);
+  const uint32_t key = a.ov_base + static_cast<uint32_t>(o);
+  const int W = 2 * T, S = W + 1;
+  float *act = dyn;                                         // sampler
+  float *sc = dyn + 2 * T * PB;                             // sin / cos of phi_0 .. phi_T
+  const bool par = T <= kParSteps;
+  float *gmm_s = sc + (par ? 2 * (T + 1) * PB : 0);
+  const int gsz = L * T * 5;
+  if (PRED) {
+    const int n = static_cast<int>(N - i0 < PB ? N - i0 : PB);
+    const int64_t row = a.rows ? static_cast<int64_t>(a.rows[o]) : o;
+    const float *src = a.pred + (row * N + i0) * W;
+    for (int e = tid; e < n * W; e += NTH) {
+      const int p = e / W;
+      dyn[p * S + (e - p * W)] = src[e];
+    }
+  } else if (staged_gmm) {
+    stage_gmm_coefs(a.gmm + static_cast<int64_t>(o) * gsz, gsz / 5, gmm_s, tid, NTH);
+  }
+  if (tid <= K) before_s[tid] = total_s[tid] = 0;
+  __syncthreads();
+  FUSED_TS(1, 1);
+  // the counts (further rounds only for clouds of > ~500 000 particles)
+  for (int e0 = 0; e0 < E; e0 += kC * NTH) {
+    if (e0 > 0) {
+#pragma unroll
+      for (int j = 0; j < kC; ++j)
+        cv[j] = count_elem(a, o, e0 + tid + j * NTH, nA, E, Kp1, b0, ct[j], cb[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      const int e = e0 + tid + j * NTH;
+      if (cv[j] == 0) continue;
+      const int c = e < nA ? e % Kp1 : (e - nA) % Kp1;
+      if (ct[j]) atomicAdd(&total_s[c], cv[j]);
+      if (cb[j]) atomicAdd(&before_s[c], cv[j]);
+    }
+  }
+  // the chain waves' own categories and ranks (sample order: chain c's lanes)
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int cat = K, rank_w = 0;
+  bool valid = false;
+  if (w < NCH) {
+    const int q = w * kFP + lane;
+    valid = i0 + q < N;
+    const int kk = valid ? keep_s[zs[q]] : -1;
+    cat = kk >= 0 ? kk : K;
+    int mine = 0;
+    for (int c = 0; c <= K; ++c) {
+      const unsigned long long m = __ballot(valid && cat == c);
+      if (cat == c) rank_w = __popcll(m & below);
+      if (lane == c) mine = __popcll(m);
+    }
+    if (lane <= K) wc_s[w][lane] = mine;
+  }
+  // ---- sampler: actions (all waves), then the headings' sin / cos in parallel --------------
+  if (!PRED) {
+#pragma unroll 1
+    for (int u = w; u < T * NCH; u += NW) {
+      const int t = u / NCH, c = u - t * NCH, q = c * kFP + lane;
+      const int64_t ip = i0 + q;
+      if (ip < N)
+        draw_action<PP, EPSIN>(t, ip, zs[q], o, T, L, N, key, seed, a.gmm, gmm_s,
+                               staged_gmm != 0, a.eps_in, act[t * PB + q], act[(T + t) * PB + q]);
+    }
+  }
+  __syncthreads();
+  FUSED_TS(1, 2);
+  if (!PRED && par) {
+    // T <= kParSteps: the sin / cos of every heading phi_0 .. phi_T, (t, chain) pair u on wave
+    // u mod 8.  phi_t is the f32 running sum the chain accumulates (phi += dphi dt at a turning
+    // step), recomputed in the same order; sincos_rn(phi_t) is what unicycle_step evaluates at
+    // step t (or carries, unchanged, over a straight step: phi_t+1 == phi_t).  One sincos per
+    // heading, where evaluating each step's pair took two
+    const float dt = a.dt;
+#pragma unroll 1
+    for (int u = w; u < (T + 1) * NCH; u += NW) {
+      const int t = u / NCH, c = u - t * NCH, q = c * kFP + lane;
+      if (i0 + q >= N) continue;
+      float phi = static_cast<float>(st_s[2]);
+      for (int s = 0; s < t; ++s) {
+        const float dphi = act[s * PB + q];
+        phi = fabsf(dphi) <= 1e-2f ? phi : phi + dphi * dt;
+      }
+      sincos_rn(phi, sc[t * PB + q], sc[(T + 1 + t) * PB + q]);
+    }
+    __syncthreads();
+    FUSED_TS(1, 3);
+  }
+  const int R = total_s[K];
+  if (blk == 0 && tid <= K) {  // the OV's header for P2 (every block computed the same values)
+    int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
+    h[tid] = total_s[tid];
+    if (tid < K) {
+      int64_t cur = reg;
+      for (int k = 0; k < tid; ++k) cur += (static_cast<int64_t>(total_s[k]) + R + 3) & ~int64_t(3);
+      hdr_starts(h)[tid] = cur;
+    }
+  }
+  if (w >= NCH) return;
+  // ---- chain wave w: particles i0 + 64 w + lane ---------------------------------------------
+  const int q = w * kFP + lane;
+  int rank = rank_w;
+  for (int c = 0; c < w; ++c) rank += wc_s[c][cat];
+  const bool native = cat < K;
+  int64_t dst = 0;
+  if (native) {
+    dst = reg;
+    for (int k = 0; k < cat; ++k) dst += (static_cast<int64_t>(total_s[k]) + R + 3) & ~int64_t(3);
+    dst += before_s[cat] + rank;
+  }
+  const int rs = native ? 0 : before_s[K] + rank;  // slot in the rare list
+  const int npad = static_cast<int>(a.Npad);
+  float x = 0.0f, y = 0.0f;
+  if (valid) {
+    float *op = native ? a.out + dst : a.rstore + static_cast<int64_t>(o) * W * a.Npad + rs;
+    const int64_t ld = native ? a.ld_out : a.Npad;
+    if (PRED) {
+      const float *tp = dyn + q * S;
+      for (int r = 0; r < W; ++r) op[r * ld] = tp[r];
+      x = tp[W - 2];
+      y = tp[W - 1];
+    } else if (par) {
+      // unicycle_step with the headings' sin / cos from LDS: what stays on the dependent path
+      // is the position adds (the terms depend only on LDS values)
+      x = static_cast<float>(st_s[0]);
+      y = static_cast<float>(st_s[1]);
+      float v = static_cast<float>(st_s[3]);
+      const float dt = a.dt;
+      for (int t = 0; t < T; ++t) {
+        const float dphi = act[t * PB + q], acc = act[(T + t) * PB + q];
+        const float s0 = sc[t * PB + q], c0 = sc[(T + 1 + t) * PB + q];
+        if (fabsf(dphi) <= 1e-2f) {
+          x = x + v * c0 * dt + (acc / 2.0f) * c0 * dt * dt;
+          y = y + v * s0 * dt + (acc / 2.0f) * s0 * dt * dt;
+        } else {
+          const float s1 = sc[(t + 1) * PB + q], c1 = sc[(T + 2 + t) * PB + q];
+          const float dsin = (s1 - s0) / dphi, dcos = (c1 - c0) / dphi;
+          const float aw = acc / dphi;
+          x = x + aw * dcos + v * dsin + aw * s1 * dt;
+          y = y - v * dcos + aw * dsin - aw * c1 * dt;
+        }
+        v = v + acc * dt;
+        op[(2 * t) * ld] = x;
+        op[(2 * t + 1) * ld] = y;
+      }
+    } else {
+      x = static_cast<float>(st_s[0]);
+      y = static_cast<float>(st_s[1]);
+      float phi = static_cast<float>(st_s[2]), v = static_cast<float>(st_s[3]);
+      float s0, c0;
+      sincos_rn(phi, s0, c0);
+      for (int t = 0; t < T; ++t) {
+        unicycle_step(x, y, phi, v, s0, c0, act[t * PB + q], act[(T + t) * PB + q], a.dt);
+        op[(2 * t) * ld] = x;
+        op[(2 * t + 1) * ld] = y;
+      }
+    }
+    if (!native) {
+      const float4 info = {x, y, __builtin_bit_cast(float, zs[q]), 0.0f};
+      reinterpret_cast<float4 *>(a.rinfo)[static_cast<int64_t>(o) * npad + rs] = info;
+    }
+  }
+  FUSED_TS(1, 4);
+  // chain wave w is centre group g0 + w: its kept-mode sums of the final world positions
+  const int g = g0 + w;
+  if (g >= a.G) return;
+  const double xw = static_cast<double>(x) + st_s[4], yw = static_cast<double>(y) + st_s[5];
+  double2 *gp = reinterpret_cast<double2 *>(a.gpart) + (static_cast<int64_t>(o) * a.G + g) * a.max_k;
+  for (int k = 0; k < K; ++k) {
+    const bool mine = valid && cat == k;
+    const double sx = group_sum64(mine ? xw : 0.0), sy = group_sum64(mine ? yw : 0.0);
+    if (lane == 0) gp[k] = double2{sx, sy};
+  }
+  FUSED_TS(1, 5);
+}
+
 __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   __shared__ double2 gp_s[kFGroups * kMaxKept + 1];  // the OV's centre partials [g][k], -0.0
   __shared__ int hist[kFusedMaxBins];             // rare particles per bin in slots >= r0
@@ -441,6 +757,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
       a.init_center[2 * cell + 1] = cen_s[k][1];
     }
   }
+  if (blockIdx.x == 0 && a.z_bad) write_z_bad(a, o);
   FUSED_TS(2, 4);
   // this block's stable ranks: lanes in order within a wave, waves in order.  Every lane scans
   // its wave's 64 keys (broadcast LDS reads, 16 bytes at a time): the same-key lanes before it
@@ -476,30 +793,378 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   FUSED_TS(2, 6);
 }
 
+// P2 keys (N > kFusedMaxN): per block of kKeySlots rare-list slots, the centres and the keys.
+// Centres in the canonical order (bucket.hpp): thread (k, j) sums superblock j of mode k's group
+// partials left to right (S_j = 0.0 + P_64j + P_64j+1 + ...), then thread k adds the S_j left to
+// right -- the same additions in the same order as every other form, so the same bits.  Block 0
+// writes the centres (init_center) even when the OV has no rare particle.
+__global__ __launch_bounds__(kRThreads) void rare_key_kernel(FusedArgs a) {
+  __shared__ double2 sup_s[kMaxKept][kWideMaxSup + 16];  // padded to rounds of 16 with -0.0
+  __shared__ int hist[kFusedMaxBins];
+  __shared__ int keep_s[64], tot_s[kMaxKept + 1];
+  __shared__ double cen_s[kMaxKept][2];
+  FUSED_TS(3, 0);
+  const int o = blockIdx.y, tid = threadIdx.x;
+  const int K = a.n_kept[o], L = a.L;
+  const int s0 = blockIdx.x * kKeySlots;
+  const int npad = static_cast<int>(a.Npad);
+  const int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
+  const double mx = a.minpos[2 * o], my = a.minpos[2 * o + 1];
+  if (tid <= K) tot_s[tid] = h[tid];
+  if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
+  // this thread's four rare records (slots clamped into the list's storage; R is not known yet)
+  const float4 *info = reinterpret_cast<const float4 *>(a.rinfo) + static_cast<int64_t>(o) * npad;
+  float4 f[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = s0 + j * kRThreads + tid;
+    f[j] = info[r < npad ? r : npad - 1];
+  }
+  const int nbins = K * (L + 1);
+  for (int b = tid; b < nbins; b += kRThreads) hist[b] = 0;
+  __syncthreads();
+  FUSED_TS(3, 1);
+  const int R = tot_s[K];
+  if (s0 >= R && blockIdx.x != 0) return;  // uniform: no slots here (block 0 writes centres)
+  const int G = a.G, nsup = (G + kCentreSuper - 1) / kCentreSuper;
+  const double2 *gp = reinterpret_cast<const double2 *>(a.gpart) + static_cast<int64_t>(o) * G * a.max_k;
+  for (int u = tid; u < K * nsup; u += kRThreads) {
+    const int k = u / nsup, j = u - k * nsup;
+    const int ga = j * kCentreSuper, gb = min(G, ga + kCentreSuper);
+    double2 acc = {0.0, 0.0};
+    for (int g = ga; g < gb; g += 16) {
+      double2 v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = gp[static_cast<int64_t>(g + q < gb ? g + q : gb - 1) * a.max_k + k];
+      __builtin_amdgcn_sched_barrier(0);  // every read issued before the first add waits
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const bool in = g + q < gb;
+        acc.x += in ? v[q].x : -0.0;      // x + -0.0 == x: the sentinel of bucket.hpp
+        acc.y += in ? v[q].y : -0.0;
+      }
+    }
+    sup_s[k][j] = acc;
+  }
+  for (int u = tid; u < K * 16; u += kRThreads) {
+    const int k = u / 16, j = nsup + (u - k * 16);
+    sup_s[k][j] = double2{-0.0, -0.0};
+  }
+  __syncthreads();
+  FUSED_TS(3, 2);
+  if (tid < K) {
+    double2 tot = {0.0, 0.0};
+    lds_row_sum(tot, sup_s[tid], nsup);
+    const double nk = static_cast<double>(tot_s[tid]);
+    cen_s[tid][0] = tot.x / nk;
+    cen_s[tid][1] = tot.y / nk;
+    if (blockIdx.x == 0) {
+      const int cell = a.cell_base[o] + tid;
+      a.init_center[2 * cell] = cen_s[tid][0];
+      a.init_center[2 * cell + 1] = cen_s[tid][1];
+    }
+  }
+  __syncthreads();
+  FUSED_TS(3, 3);
+  int32_t *kb = a.kbuf + static_cast<int64_t>(o) * npad;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = s0 + j * kRThreads + tid;
+    if (r < R) {
+      const int kq = key_staged(__builtin_bit_cast(int, f[j].z), static_cast<double>(f[j].x) + mx,
+                                static_cast<double>(f[j].y) + my, keep_s, cen_s, K, L);
+      kb[r] = kq;
+      atomicAdd(&hist[kq], 1);
+    }
+  }
+  __syncthreads();
+  if (s0 < R) {
+    int32_t *rh = a.rhist + (static_cast<int64_t>(o) * a.nkb + blockIdx.x) * kFusedMaxBins;
+    for (int b = tid; b < nbins; b += kRThreads) rh[b] = hist[b];
+  }
+  FUSED_TS(3, 4);
+}
+
+// P3 copy (N > kFusedMaxN): per block of kRThreads rare-list slots (one per thread), in the P2
+// keys block B = r0 / kKeySlots.  Every P2 block's histogram gives each bin's total (-> the bin
+// starts) and its count in the P2 blocks before B; the keys of B's slots before r0 add the rest
+// of the count before this block; a scan of each wave's 64 keys gives the stable ranks.  Block 0
+// writes the cells' offsets, counts and pmf (and the invalid-id count).
+__global__ __launch_bounds__(kRThreads) void rare_copy_kernel(FusedArgs a) {
+  __shared__ int binsum[kFusedMaxBins];   // rare particles per bin, whole OV
+  __shared__ int pre[kFusedMaxBins];      // ... in rare-list slots before this block's
+  __shared__ int bstart[kFusedMaxBins];   // bin start relative to the region
+  __shared__ int wcnt[kRWaves][kFusedMaxBins];
+  __shared__ __attribute__((aligned(16))) int okey[kRThreads];
+  __shared__ int tot_s[kMaxKept + 1];
+  __shared__ int64_t cst_s[kMaxKept];
+  FUSED_TS(4, 0);
+  const int o = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int K = a.n_kept[o], L = a.L, T = a.T, rows = 2 * T;
+  const int r0 = blockIdx.x * kRThreads, B = r0 / kKeySlots;
+  const int npad = static_cast<int>(a.Npad);
+  const int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
+  const int64_t reg = a.region[o];
+  if (tid <= K) tot_s[tid] = h[tid];
+  if (tid < K) cst_s[tid] = hdr_starts(const_cast<int32_t *>(h))[tid];
+  const int r = r0 + tid;
+  const int rc = r < npad ? r : npad - 1;
+  const int32_t *kb = a.kbuf + static_cast<int64_t>(o) * npad;
+  const int kown = kb[rc];
+  const float *src = a.rstore + static_cast<int64_t>(o) * rows * a.Npad + rc;
+  float v[80];
+#pragma unroll
+  for (int rr = 0; rr < 80; ++rr)
+    if (rr < rows) v[rr] = src[static_cast<int64_t>(rr) * npad];
+  constexpr int kPre = kKeySlots / kRThreads - 1;  // B's slots before r0: up to 3 per thread
+  int pk[kPre];
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) {
+    const int sl = B * kKeySlots + j * kRThreads + tid;
+    pk[j] = sl < r0 ? kb[sl] : -1;
+  }
+  const int nbins = K * (L + 1);
+  for (int b = tid; b < nbins; b += kRThreads) binsum[b] = pre[b] = 0;
+  for (int b = tid; b < kRWaves * nbins; b += kRThreads) wcnt[b / nbins][b % nbins] = 0;
+  __syncthreads();
+  FUSED_TS(4, 1);
+  const int R = tot_s[K];
+  if (r0 >= R && blockIdx.x != 0) return;  // uniform: no rare slots here (block 0 writes cells)
+  const bool own = r < R;
+  const int nkb = (R + kKeySlots - 1) / kKeySlots;
+  const int32_t *rh = a.rhist + static_cast<int64_t>(o) * a.nkb * kFusedMaxBins;
+  for (int e0 = 0; e0 < nkb * nbins; e0 += 4 * kRThreads) {
+    int hv[4], hb[4], hr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + j * kRThreads + tid;
+      hr[j] = e / nbins;
+      hb[j] = e - hr[j] * nbins;
+      hv[j] = e < nkb * nbins ? rh[static_cast<int64_t>(hr[j]) * kFusedMaxBins + hb[j]] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (hv[j] == 0) continue;
+      atomicAdd(&binsum[hb[j]], hv[j]);
+      if (hr[j] < B) atomicAdd(&pre[hb[j]], hv[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kPre; ++j)
+    if (pk[j] >= 0) atomicAdd(&pre[pk[j]], 1);
+  okey[tid] = own ? kown : -1;
+  __syncthreads();
+  FUSED_TS(4, 2);
+  // bins of kept mode k start after its natives, latents ascending (one thread per bin, its
+  // prefix summed over independent LDS reads); block 0: the cells' outputs
+  for (int b = tid; b < nbins; b += kRThreads) {
+    const int k = b / (L + 1), gi = b - k * (L + 1), hb = k * (L + 1) + 1;
+    const int upto = gi == 0 ? L : gi - 1;  // gi == 0 (the natives' bin): every rare bin of k
+    int s = 0;
+#pragma unroll 8
+    for (int zz = 0; zz < upto; ++zz) s += binsum[hb + zz];
+    if (gi > 0) {
+      bstart[b] = static_cast<int>(cst_s[k] - reg) + tot_s[k] + s;
+    } else if (blockIdx.x == 0) {
+      const int64_t n = tot_s[k] + s;
+      const int cell = a.cell_base[o] + k;
+      a.cell_off[cell] = cst_s[k];
+      a.cell_cnt[cell] = n;
+      a.cell_pmf[cell] = static_cast<double>(n) / static_cast<double>(a.N);
+    }
+  }
+  if (blockIdx.x == 0 && a.z_bad) write_z_bad(a, o);
+  // this block's stable ranks (rare_place's scan of each wave's 64 keys)
+  const int kr = okey[tid];
+  int rank = 0, cnt = 0;
+  {
+    const int4 *wk = reinterpret_cast<const int4 *>(okey + w * 64);
+#pragma unroll
+    for (int j4 = 0; j4 < 16; ++j4) {
+      const int4 k4 = wk[j4];
+      const int kk[4] = {k4.x, k4.y, k4.z, k4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool same = kk[e] == kr;
+        rank += (same && 4 * j4 + e < lane) ? 1 : 0;
+        cnt += same ? 1 : 0;
+      }
+    }
+  }
+  if (own && rank == cnt - 1) wcnt[w][kr] = cnt;
+  __syncthreads();
+  FUSED_TS(4, 3);
+  if (own) {
+    int before = pre[kr] + rank;
+    for (int u = 0; u < w; ++u) before += wcnt[u][kr];
+    float *out = a.out + reg + bstart[kr] + before;
+#pragma unroll
+    for (int rr = 0; rr < 80; ++rr)
+      if (rr < rows) out[static_cast<int64_t>(rr) * a.ld_out] = v[rr];
+  }
+  FUSED_TS(4, 4);
+}
+
 struct FusedWs {
-  size_t zbuf, gcnt, hdr, gpart, rinfo, rstore, total;
+  size_t zbuf, gcnt, bsum, hdr, gpart, rinfo, rstore, kbuf, rhist, total;
+  int64_t G, nb0, nkb, Npad;
 };
 
 inline size_t a256(size_t b) { return (b + 255) / 256 * 256; }
 
 inline FusedWs fused_ws(int64_t n_ov, int64_t N, int64_t T, int64_t max_k) {
-  const int64_t G = (N + kFP - 1) / kFP, Npad = (N + 3) & ~int64_t(3);
   FusedWs w;
+  w.G = (N + kFP - 1) / kFP;
+  w.Npad = (N + 3) & ~int64_t(3);
+  w.nb0 = (N + kFThreads - 1) / kFThreads;
+  w.nkb = (w.Npad + kKeySlots - 1) / kKeySlots;
   size_t o = 0;
   w.zbuf = o;
-  o += a256(sizeof(int32_t) * n_ov * Npad);
+  o += a256(sizeof(int32_t) * n_ov * w.Npad);
   w.gcnt = o;
-  o += a256(sizeof(int32_t) * n_ov * G * kCntStride);
+  o += a256(sizeof(int32_t) * n_ov * w.G * kCntStride);
+  w.bsum = o;
+  o += a256(sizeof(int32_t) * n_ov * w.nb0 * kCntStride);
   w.hdr = o;
   o += a256(sizeof(int32_t) * kHdrInts * n_ov);
   w.gpart = o;
-  o += a256(sizeof(double) * 2 * n_ov * G * max_k);
+  o += a256(sizeof(double) * 2 * n_ov * w.G * max_k);
   w.rinfo = o;
-  o += a256(sizeof(float) * 4 * n_ov * Npad);
+  o += a256(sizeof(float) * 4 * n_ov * w.Npad);
   w.rstore = o;
-  o += a256(sizeof(float) * n_ov * 2 * T * Npad);
+  o += a256(sizeof(float) * n_ov * 2 * T * w.Npad);
+  w.kbuf = o;
+  o += a256(sizeof(int32_t) * n_ov * w.Npad);
+  w.rhist = o;
+  o += a256(sizeof(int32_t) * n_ov * w.nkb * kFusedMaxBins);
   w.total = o;
   return w;
+}
+
+// The rare stage of the small clouds: one pass (rare_place) or the keys + copy pair
+// (CCMPC_RARE_TWO_PASS=1, the large clouds' form, for measurement)
+// (read per call: a launch costs far more than a getenv, and tests switch it)
+inline bool env_on(const char *name) {
+  const char *e = getenv(name);
+  return e && e[0] == '1';
+}
+
+inline bool rare_two_pass(int64_t N) { return N > kFusedMaxN || env_on("CCMPC_RARE_TWO_PASS"); }
+
+// The small clouds' place kernel: the one-chain form of place_kernel (CCMPC_PLACE_V2=1) or the
+// original sample_place_kernel (reads every group's counts)
+inline bool place_v2() { return env_on("CCMPC_PLACE_V2"); }
+
+// Raise a kernel's dynamic LDS limit above the 48 KiB default when a launch needs it (the
+// attribute is per device: set on every such launch; a failure is reported, not launched)
+template <typename Kern>
+inline bool lds_fits(Kern k, size_t bytes) {
+  if (bytes <= 48 * 1024) return true;
+  return hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             static_cast<int>(bytes)) == hipSuccess;
+}
+
+template <int MODE, int NCH, int NW>
+inline int launch_place(const FusedArgs &a, int64_t n_ov, hipStream_t s) {
+  constexpr int PB = kFP * NCH;
+  constexpr bool PRED = (MODE & 4) != 0, PP = (MODE & 2) != 0;
+  const int T = a.T, gsz = a.L * T * 5;
+  size_t floats;
+  int staged = 0;
+  if (PRED) {
+    floats = static_cast<size_t>(PB) * (2 * T + 1);
+  } else {
+    floats = static_cast<size_t>(2 * T) * PB + (T <= kParSteps ? 2 * (T + 1) * PB : 0);
+    staged = !PP && gsz <= 3200;
+    floats += staged ? gsz : 0;
+  }
+  const size_t lds = floats * sizeof(float);
+  if (!lds_fits(&place_kernel<MODE, NCH, NW>, lds)) {
+    set_error("ccmpc_sample_bucket: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    return CCMPC_ERR_LAUNCH;
+  }
+  const dim3 grid(static_cast<unsigned>((a.N + PB - 1) / PB), static_cast<unsigned>(n_ov));
+  hipLaunchKernelGGL((place_kernel<MODE, NCH, NW>), grid, dim3(64 * NW), lds, s, a, staged);
+  return CCMPC_OK;
+}
+
+// The block shape: 8 waves for one chain of 64 particles (small clouds: few blocks, each as
+// parallel as it gets); above kFusedMaxN the phases are issue-bound on the f64 draws and headings,
+// so what matters is that every block is resident at once and the CUs get even shares:
+// 4-wave blocks of one chain (1563 blocks at N = 100 000, 7 per CU), or (CCMPC_PLACE_WIDE2=1)
+// 8-wave blocks of two chains (782 blocks, 3 per CU)
+template <int MODE>
+inline int launch_place_w(const FusedArgs &a, int64_t n_ov, hipStream_t s) {
+  if (a.N > kFusedMaxN) {
+    if (env_on("CCMPC_PLACE_WIDE2")) return launch_place<MODE, 2, 8>(a, n_ov, s);
+    return launch_place<MODE, 1, 4>(a, n_ov, s);
+  }
+  return launch_place<MODE, 1, 8>(a, n_ov, s);
+}
+
+// P0 -> P1 -> the rare stage, for either particle source (pred != nullptr: the predictor's)
+inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s) {
+  const dim3 zgrid(static_cast<unsigned>(a.nb0), static_cast<unsigned>(n_ov));
+  if (a.pred)
+    hipLaunchKernelGGL(latent_count_kernel<kZPred>, zgrid, dim3(kFThreads), 0, s, a);
+  else if (a.z_in)
+    hipLaunchKernelGGL(latent_count_kernel<kZIn>, zgrid, dim3(kFThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(latent_count_kernel<kZPhilox>, zgrid, dim3(kFThreads), 0, s, a);
+  const bool eps = a.eps_in != nullptr;
+  int rc = CCMPC_OK;
+  if (a.pred) {
+    rc = launch_place_w<4>(a, n_ov, s);
+  } else if (a.N > kFusedMaxN || place_v2()) {
+    switch ((pp ? 2 : 0) | (eps ? 1 : 0)) {
+      case 0: rc = launch_place_w<0>(a, n_ov, s); break;
+      case 1: rc = launch_place_w<1>(a, n_ov, s); break;
+      case 2: rc = launch_place_w<2>(a, n_ov, s); break;
+      default: rc = launch_place_w<3>(a, n_ov, s); break;
+    }
+  } else {
+    const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
+#define CCMPC_FUSED(PP, EPSIN) \
+  hipLaunchKernelGGL((sample_place_kernel<PP, EPSIN>), grid, dim3(kFThreads), 0, s, a)
+    switch ((pp ? 2 : 0) | (eps ? 1 : 0)) {
+      case 0: CCMPC_FUSED(false, false); break;
+      case 1: CCMPC_FUSED(false, true); break;
+      case 2: CCMPC_FUSED(true, false); break;
+      default: CCMPC_FUSED(true, true); break;
+    }
+#undef CCMPC_FUSED
+  }
+  if (rc != CCMPC_OK) return rc;
+  if (rare_two_pass(a.N)) {
+    const dim3 kgrid(static_cast<unsigned>(a.nkb), static_cast<unsigned>(n_ov));
+    hipLaunchKernelGGL(rare_key_kernel, kgrid, dim3(kRThreads), 0, s, a);
+    const dim3 cgrid(static_cast<unsigned>((a.Npad + kRThreads - 1) / kRThreads),
+                     static_cast<unsigned>(n_ov));
+    hipLaunchKernelGGL(rare_copy_kernel, cgrid, dim3(kRThreads), 0, s, a);
+  } else {
+    const dim3 rgrid(static_cast<unsigned>((a.N + kRThreads - 1) / kRThreads),
+                     static_cast<unsigned>(n_ov));
+    hipLaunchKernelGGL(rare_place_kernel, rgrid, dim3(kRThreads), 0, s, a);
+  }
+  return CCMPC_OK;
+}
+
+inline void fused_args_ws(FusedArgs &a, const FusedWs &L, void *workspace) {
+  char *ws = static_cast<char *>(workspace);
+  a.zbuf = reinterpret_cast<int32_t *>(ws + L.zbuf);
+  a.gcnt = reinterpret_cast<int32_t *>(ws + L.gcnt);
+  a.bsum = reinterpret_cast<int32_t *>(ws + L.bsum);
+  a.hdr = reinterpret_cast<int32_t *>(ws + L.hdr);
+  a.gpart = reinterpret_cast<double *>(ws + L.gpart);
+  a.rinfo = reinterpret_cast<float *>(ws + L.rinfo);
+  a.rstore = reinterpret_cast<float *>(ws + L.rstore);
+  a.kbuf = reinterpret_cast<int32_t *>(ws + L.kbuf);
+  a.rhist = reinterpret_cast<int32_t *>(ws + L.rhist);
+  a.Npad = L.Npad;
+  a.G = static_cast<int>(L.G);
+  a.nb0 = static_cast<int>(L.nb0);
+  a.nkb = static_cast<int>(L.nkb);
 }
 
 }  // namespace ccmpc
@@ -508,10 +1173,12 @@ using namespace ccmpc;
 
 #if defined(CCMPC_PROBE) && (CCMPC_PROBE & 4)
 // which 0: P0 latents (slots 0 start, 1 done); 1: P1 place (0 start, 1 counted, 2 sampled +
-// published); 2: P2 rares (0 start, 1 loaded, 2 centres, 3 keyed, 4 bin starts, 5 ranked,
-// 6 copied)  (tools/probe_step.py)
+// published; place_kernel: 0 start, 1 loaded, 2 acted, 3 sincos, 4 chained, 5 summed); 2: P2
+// rares (0 start, 1 loaded, 2 centres, 3 keyed, 4 bin starts, 5 ranked, 6 copied); 3: P2 keys
+// (0 start, 1 loaded, 2 superblocks, 3 centres, 4 keyed); 4: P3 copy (0 start, 1 loaded, 2
+// counted, 3 ranked, 4 copied)  (tools/probe_step.py)
 extern "C" int ccmpc_probe_fused_timestamps(void *host, int which, int reset) {
-  if (which < 0 || which > 2) return -1;
+  if (which < 0 || which > 4) return -1;
   const size_t bytes = sizeof(g_fused_ts[0]);
   if (reset) {
     static unsigned long long zeros[kStepProbeWG * kStepProbeSlots];
@@ -525,7 +1192,7 @@ extern "C" int ccmpc_probe_fused_timestamps(void *host, int which, int reset) {
 
 extern "C" size_t ccmpc_sample_bucket_workspace_bytes(int64_t n_ov, int64_t N, int64_t T,
                                                       int64_t max_k) {
-  if (n_ov < 0 || N < 1 || N > kFusedMaxN || T < 1 || T > 40 || max_k < 1 || max_k > kMaxKept)
+  if (n_ov < 0 || N < 1 || N > kWideMaxN || T < 1 || T > 40 || max_k < 1 || max_k > kMaxKept)
     return 0;
   return fused_ws(n_ov, N, T, max_k).total;
 }
@@ -543,7 +1210,7 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
                                    double *cell_pmf, double *init_center, ccmpc_stream_t stream) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
-  CCMPC_REQUIRE(N >= 1 && N <= kFusedMaxN, "N must be in [1, 8192] (bucket.hip beyond)");
+  CCMPC_REQUIRE(N >= 1 && N <= kWideMaxN, "N must be in [1, 262144] (bucket.hip beyond)");
   CCMPC_REQUIRE(max_k >= 1 && max_k <= kMaxKept && max_k * (n_latent + 1) <= kFusedMaxBins,
                 "max_k out of range");
   CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536, "bad n_ov");
@@ -563,8 +1230,7 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
     set_error("ccmpc_sample_bucket: workspace too small or not 256-byte aligned");
     return CCMPC_ERR_WORKSPACE;
   }
-  char *ws = static_cast<char *>(workspace);
-  FusedArgs a;
+  FusedArgs a = {};
   a.init_state = init_state;
   a.latent_cdf = latent_cdf;
   a.gmm = gmm;
@@ -583,14 +1249,7 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
   a.max_k = static_cast<int>(max_k);
   a.minpos = minpos;
   a.region = region;
-  a.zbuf = reinterpret_cast<int32_t *>(ws + L.zbuf);
-  a.gcnt = reinterpret_cast<int32_t *>(ws + L.gcnt);
-  a.hdr = reinterpret_cast<int32_t *>(ws + L.hdr);
-  a.gpart = reinterpret_cast<double *>(ws + L.gpart);
-  a.rinfo = reinterpret_cast<float *>(ws + L.rinfo);
-  a.rstore = reinterpret_cast<float *>(ws + L.rstore);
-  a.Npad = (N + 3) & ~int64_t(3);
-  a.G = static_cast<int>((N + kFP - 1) / kFP);
+  fused_args_ws(a, L, workspace);
   a.out_z = out_z;
   a.out = pos_out;
   a.ld_out = ld_out;
@@ -598,27 +1257,64 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
   a.cell_cnt = cell_cnt;
   a.cell_pmf = cell_pmf;
   a.init_center = init_center;
-  hipStream_t s = as_stream(stream);
-  const dim3 zgrid(static_cast<unsigned>((N + kFThreads - 1) / kFThreads),
-                   static_cast<unsigned>(n_ov));
-  if (z_in)
-    hipLaunchKernelGGL(latent_count_kernel<true>, zgrid, dim3(kFThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL(latent_count_kernel<false>, zgrid, dim3(kFThreads), 0, s, a);
-  const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
-  const int mode = (pp ? 2 : 0) | (eps_in ? 1 : 0);
-#define CCMPC_FUSED(PP, EPSIN) \
-  hipLaunchKernelGGL((sample_place_kernel<PP, EPSIN>), grid, dim3(kFThreads), 0, s, a)
-  switch (mode) {
-    case 0: CCMPC_FUSED(false, false); break;
-    case 1: CCMPC_FUSED(false, true); break;
-    case 2: CCMPC_FUSED(true, false); break;
-    default: CCMPC_FUSED(true, true); break;
+  const int rc = fused_launch(a, n_ov, pp, as_stream(stream));
+  if (rc != CCMPC_OK) return rc;
+  CCMPC_LAUNCH_CHECK();
+  return CCMPC_OK;
+}
+
+extern "C" int ccmpc_bucket_predictions(const float *pred, const void *z, int z_bytes,
+                                        const int32_t *rows, int64_t n_ov, int64_t N, int64_t T,
+                                        int64_t n_latent, const int32_t *keep_map,
+                                        const int32_t *n_kept, const int32_t *cell_base,
+                                        int64_t max_k, const double *minpos,
+                                        const int64_t *region, void *workspace,
+                                        size_t workspace_bytes, float *pos_out, int64_t ld_out,
+                                        int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
+                                        double *init_center, int32_t *z_bad,
+                                        ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
+  CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
+  CCMPC_REQUIRE(N >= 1 && N <= kWideMaxN, "N must be in [1, 262144] (ccmpc_load_predictions + "
+                "ccmpc_bucket beyond)");
+  CCMPC_REQUIRE(z_bytes == 4 || z_bytes == 8, "z must be int32 or int64");
+  CCMPC_REQUIRE(max_k >= 1 && max_k <= kMaxKept && max_k * (n_latent + 1) <= kFusedMaxBins,
+                "max_k out of range");
+  CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536, "bad n_ov");
+  if (n_ov == 0) return CCMPC_OK;
+  CCMPC_REQUIRE(pred && z && keep_map && n_kept && cell_base && minpos && region && pos_out &&
+                    cell_off && cell_cnt && cell_pmf && init_center,
+                "null pointer");
+  CCMPC_REQUIRE(ld_out >= 1 && ld_out * 2 * T < (int64_t(1) << 40), "bad ld_out");
+  const FusedWs L = fused_ws(n_ov, N, T, max_k);
+  if (!workspace || workspace_bytes < L.total || !aligned(workspace, 256)) {
+    set_error("ccmpc_bucket_predictions: workspace too small or not 256-byte aligned");
+    return CCMPC_ERR_WORKSPACE;
   }
-#undef CCMPC_FUSED
-  const dim3 rgrid(static_cast<unsigned>((N + kRThreads - 1) / kRThreads),
-                   static_cast<unsigned>(n_ov));
-  hipLaunchKernelGGL(rare_place_kernel, rgrid, dim3(kRThreads), 0, s, a);
+  FusedArgs a = {};
+  a.pred = pred;
+  a.zsrc = z;
+  a.z_bytes = z_bytes;
+  a.rows = rows;
+  a.L = static_cast<int>(n_latent);
+  a.T = static_cast<int>(T);
+  a.N = N;
+  a.keep_map = keep_map;
+  a.n_kept = n_kept;
+  a.cell_base = cell_base;
+  a.max_k = static_cast<int>(max_k);
+  a.minpos = minpos;
+  a.region = region;
+  fused_args_ws(a, L, workspace);
+  a.out = pos_out;
+  a.ld_out = ld_out;
+  a.cell_off = cell_off;
+  a.cell_cnt = cell_cnt;
+  a.cell_pmf = cell_pmf;
+  a.init_center = init_center;
+  a.z_bad = z_bad;
+  const int rc = fused_launch(a, n_ov, false, as_stream(stream));
+  if (rc != CCMPC_OK) return rc;
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
 }

@@ -75,8 +75,8 @@ __global__ __launch_bounds__(kSampThreads) void sample_unicycle_kernel(
   const int gsz = n_latent * T * 5;
   const bool staged = !PP && gsz <= static_cast<int>(sizeof(gmm_s) / sizeof(float));
   if (staged)
-    for (int e = threadIdx.x; e < gsz; e += blockDim.x)
-      gmm_s[e] = gmm[static_cast<int64_t>(ov) * gsz + e];
+    stage_gmm_coefs(gmm + static_cast<int64_t>(ov) * gsz, gsz / 5, gmm_s, threadIdx.x,
+                    blockDim.x);
   __syncthreads();
   CCMPC_STEP_TS(g_samp_ts, 1);
   for (int q = threadIdx.x; q < PB; q += blockDim.x) {

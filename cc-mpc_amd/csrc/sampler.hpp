@@ -48,13 +48,38 @@ __device__ __forceinline__ void unicycle_step(float &x, float &y, float &phi, fl
 
 // One GMM2D component's reparametrised draw (Trajectron++ GMM2D.rsample with one component):
 // a = mu + L eps, L = [[s0, 0], [s1 rho, s1 sqrt(clamp(1 - rho^2, 1e-5, 1))]], s = exp(log s);
-// the matmul row is summed before mu is added, as `mus + squeeze(L @ eps)` does.
-__device__ __forceinline__ void gmm2d_action(float mu0, float mu1, float ls0, float ls1, float rho,
-                                             float e0, float e1, float &dphi, float &acc) {
+// the matmul row is summed before mu is added, as `mus + squeeze(L @ eps)` does.  Split in two:
+// the coefficients {mu0, mu1, s0, s1 rho, s1 sqrt(.)} depend only on the parameters (per (OV,
+// latent, step) in the per-latent mode: computed once per table entry when the table is staged,
+// not per particle -- two float64 exp's per action fewer), then the draw; the float32 products
+// are the same roundings either way.
+__device__ __forceinline__ void gmm2d_coefs(float mu0, float mu1, float ls0, float ls1, float rho,
+                                            float c[5]) {
   const float s0 = exp_rn(ls0), s1 = exp_rn(ls1);
   const float omr2 = fminf(fmaxf(1.0f - rho * rho, 1e-5f), 1.0f);
-  dphi = mu0 + s0 * e0;  // + 0 * e1: adds a signed zero, never changes s0 e0 unless it is 0
-  acc = mu1 + ((s1 * rho) * e0 + (s1 * sqrtf(omr2)) * e1);
+  c[0] = mu0;
+  c[1] = mu1;
+  c[2] = s0;
+  c[3] = s1 * rho;
+  c[4] = s1 * sqrtf(omr2);
+}
+
+__device__ __forceinline__ void gmm2d_draw(const float c[5], float e0, float e1, float &dphi,
+                                           float &acc) {
+  dphi = c[0] + c[2] * e0;  // + 0 * e1: adds a signed zero, never changes s0 e0 unless it is 0
+  acc = c[1] + (c[3] * e0 + c[4] * e1);
+}
+
+// The per-latent parameter table gmm[L][T][5] of one OV as coefficient rows in LDS (threads
+// tid, tid + nth, ... of the block).
+__device__ __forceinline__ void stage_gmm_coefs(const float *__restrict__ g, int entries,
+                                                float *gmm_s, int tid, int nth) {
+  for (int e = tid; e < entries; e += nth) {
+    float c[5];
+    gmm2d_coefs(g[5 * e], g[5 * e + 1], g[5 * e + 2], g[5 * e + 3], g[5 * e + 4], c);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) gmm_s[5 * e + k] = c[k];
+  }
 }
 
 // Latent id of particle i by inverse CDF of its Philox uniform (DiscreteLatent.sample_p:
@@ -73,8 +98,8 @@ __device__ __forceinline__ int draw_latent(int64_t i, uint32_t key, uint64_t see
 }
 
 // Particle i's action at step t (GMM2D.rsample of its component): per-particle parameters at
-// gmm[ov][5t + k][N] or the per-latent row of z (from the LDS copy gmm_s when staged); noise
-// injected at eps_in[ov][2t + c][N] or drawn from Philox.
+// gmm[ov][5t + k][N] or the per-latent row of z (its coefficient row in LDS, gmm_s, when staged
+// by stage_gmm_coefs); noise injected at eps_in[ov][2t + c][N] or drawn from Philox.
 template <bool PP, bool EPSIN>
 __device__ __forceinline__ void draw_action(int t, int64_t i, int z, int ov, int T, int n_latent,
                                             int64_t N, uint32_t key, uint64_t seed,
@@ -96,11 +121,17 @@ __device__ __forceinline__ void draw_action(int t, int64_t i, int z, int ov, int
   }
   const float *g = PP ? gmm + static_cast<int64_t>(ov) * T * 5 * N + i
                       : gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
-  float p[5];
+  float c[5];
+  if (!PP && staged) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k)
-    p[k] = PP ? g[(5 * t + k) * N] : (staged ? gmm_s[(z * T + t) * 5 + k] : g[5 * t + k]);
-  gmm2d_action(p[0], p[1], p[2], p[3], p[4], e0, e1, dphi, acc);
+    for (int k = 0; k < 5; ++k) c[k] = gmm_s[(z * T + t) * 5 + k];
+  } else {
+    float p[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) p[k] = PP ? g[(5 * t + k) * N] : g[5 * t + k];
+    gmm2d_coefs(p[0], p[1], p[2], p[3], p[4], c);
+  }
+  gmm2d_draw(c, e0, e1, dphi, acc);
 }
 
 }  // namespace ccmpc

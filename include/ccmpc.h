@@ -42,7 +42,7 @@ extern "C" {
 
 typedef void *ccmpc_stream_t; /* hipStream_t */
 
-#define CCMPC_ABI_VERSION 1
+#define CCMPC_ABI_VERSION 2
 
 /* call status */
 #define CCMPC_OK 0
@@ -368,30 +368,39 @@ int ccmpc_bucket(const int32_t *z, const float *pos_in, int64_t ld_in, int64_t T
  * `predictions[idx]` / `z[idx]` reads of make_ovehicles (v8ideal/__init__.py:469-490) on the
  * 5-tuple generate_vehicle_latents returns (prediction.py:93-105):
  *  pred[row][N][T][2]  float32, scene-relative (numpy's swapaxes(predictions, 0, 1) layout)
- *  z[row][N]           latent ids, int64 (z_bytes = 8: np.argmax's dtype) or int32 (4);
- *                      clamped into [0, n_latent)
+ *  z[row][N]           latent ids, int64 (z_bytes = 8: np.argmax's dtype) or int32 (4).
+ *                      make_ovehicles indexes a list of n_latent entries by them (:488-491):
+ *                      an id in [-n_latent, 0) wraps as a Python index; any other id outside
+ *                      [0, n_latent) is where the reference raises IndexError -- it is counted
+ *                      into z_bad[o] (and clamped, for memory safety, so the output is then
+ *                      not the reference's: the caller must refuse it)
  *  rows[n_ov]          device int32: the node row of OV o (make_ovehicles skips the ego's
  *                      node); NULL = rows 0 .. n_ov-1
  *  out: pos_out        F32 sample-order store, OV o at o * ov_stride (ov_stride >= N, 4-aligned
  *                      for ccmpc_bucket): pos_out[(2t + c) * ld_out + o * ov_stride + i]
  *       z_out[n_ov][N] int32, as ccmpc_bucket reads it
- * One launch; traffic 2 x 8 T B per particle.
+ *       z_bad[n_ov]    device int32, optional (NULL): invalid ids of OV o ADDED (the caller
+ *                      zero-fills it first)
+ * One launch; traffic 2 x 8 T B per particle.  The step graph uses the one-pass placement
+ * ccmpc_bucket_predictions below instead (no sample-order store).
  * ------------------------------------------------------------------------------------- */
 int ccmpc_load_predictions(const float *pred, const void *z, int z_bytes, const int32_t *rows,
                            int64_t n_ov, int64_t N, int64_t T, int64_t n_latent, float *pos_out,
-                           int64_t ld_out, int64_t ov_stride, int32_t *z_out,
+                           int64_t ld_out, int64_t ov_stride, int32_t *z_out, int32_t *z_bad,
                            ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
- * Sampler + bucketing in three short launches, for clouds of N <= 8192 particles per OV: the same draws
- * as ccmpc_sample_unicycle_ex (same Philox streams, same float32 arithmetic) bucketed as
- * ccmpc_bucket buckets them -- every cell holds the same particles in the same order and the
- * same init_center / pmf bits.  Replaces prediction.py:81-86 + v8ideal/__init__.py:469-505 +
- * ovehicle.py:24-117 on the drop-in step's shape.
+ * Sampler + bucketing as one placement pass, for clouds of N <= 262144 particles per OV: the
+ * same draws as ccmpc_sample_unicycle_ex (same Philox streams, same float32 arithmetic)
+ * bucketed as ccmpc_bucket buckets them -- every cell holds the same particles in the same
+ * order and the same init_center / pmf bits.  Replaces prediction.py:81-86 +
+ * v8ideal/__init__.py:469-505 + ovehicle.py:24-117.  Launches: latent ids + counts, then the
+ * sampler writing each native particle straight into its cell (rare ones into a rare list),
+ * then the rare particles' placement -- one launch up to N = 8192, keys then copy above it.
  * Differences from ccmpc_bucket's output: only where the cells start.  Cell k of OV o starts at
  *   region[o] + sum_{j<k} round4(n_j + R_o)   (n_j = mode j's own particles, R_o = rare ones)
  * so region[o] needs n_kept[o] * (N + 4) free slots of pos_out.  out_z (optional, may be NULL)
- * gets the sample-order latent ids.  N > 8192: use the sampler + ccmpc_bucket.
+ * gets the sample-order latent ids.  N > 262144: the sampler + ccmpc_bucket.
  * Workspace: ccmpc_sample_bucket_workspace_bytes (0 = shape not supported), 256-byte aligned;
  * no initialisation needed (the first launch writes everything the second reads).
  * ------------------------------------------------------------------------------------- */
@@ -405,6 +414,28 @@ int ccmpc_sample_bucket(const double *init_state, const double *latent_cdf, int6
                         void *workspace, size_t workspace_bytes, int32_t *out_z, float *pos_out,
                         int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
                         double *init_center, ccmpc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * make_ovehicles (v8ideal/__init__.py:469-505, ovehicle.py:24-117) on the reference's own
+ * predictor output in ONE placement pass: ccmpc_sample_bucket's launches with the predictor's
+ * coordinates in place of the sampler (no sample-order store, no re-read + scatter of every
+ * particle).  Inputs as ccmpc_load_predictions (pred[row][N][T][2] float32 scene-relative,
+ * z[row][N] int64 / int32, rows[n_ov] or NULL); bucketing arguments and outputs as
+ * ccmpc_sample_bucket (its workspace size: ccmpc_sample_bucket_workspace_bytes(n_ov, N, T,
+ * max_k)); cells bit-identical to ccmpc_load_predictions + ccmpc_bucket.
+ *  z_bad[n_ov]  device int32, optional: the number of OV o's ids make_ovehicles' list index
+ *               would refuse (outside [-n_latent, n_latent); [-n_latent, 0) wraps) -- WRITTEN
+ *               (no zero-fill needed).  Non-zero: the reference raises IndexError there, and
+ *               the output is not the reference's (those ids were clamped).
+ * ------------------------------------------------------------------------------------- */
+int ccmpc_bucket_predictions(const float *pred, const void *z, int z_bytes, const int32_t *rows,
+                             int64_t n_ov, int64_t N, int64_t T, int64_t n_latent,
+                             const int32_t *keep_map, const int32_t *n_kept,
+                             const int32_t *cell_base, int64_t max_k, const double *minpos,
+                             const int64_t *region, void *workspace, size_t workspace_bytes,
+                             float *pos_out, int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,
+                             double *cell_pmf, double *init_center, int32_t *z_bad,
+                             ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Headings, bounding-box vertices and L4 outer approximation for every (cell, t).

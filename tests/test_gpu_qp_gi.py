@@ -103,13 +103,61 @@ def test_gi_hands_over_to_the_ipm(gpu, monkeypatch):
         return [t.cpu().numpy().copy() for t in out]
 
     ipm = run("ipm")
-    forced = run("gi", 0)
     gi = run("gi")
-    handed = 0
-    for s in range(len(seeds)):
-        if gi[4][s] > 0:          # the normal GI solve took at least one active-set step
-            assert all(a[s].tobytes() == b[s].tobytes() for a, b in zip(forced, ipm)), s
-            handed += 1
-        else:                     # no step needed: the budget never bit
-            assert all(a[s].tobytes() == b[s].tobytes() for a, b in zip(forced, gi)), s
-    assert handed > 0
+    gi_done = (gi[3] == mpc.QP_OK)   # an infeasible verdict is the IPM's (give_up)
+    handed_mid = 0
+    for budget in (0, 1, 2, 3):
+        forced = run("gi", budget)
+        handed = 0
+        for s in range(len(seeds)):
+            if gi_done[s] and gi[4][s] <= budget:   # the budget never bit
+                assert all(a[s].tobytes() == b[s].tobytes() for a, b in zip(forced, gi)), \
+                    (budget, s)
+            else:
+                # handed over after `budget` active-set changes: GI wrote IPM-owned LDS slots
+                # (row flags, per-step weights, the polish's R / active list); the IPM must not
+                # see any of it
+                assert all(a[s].tobytes() == b[s].tobytes() for a, b in zip(forced, ipm)), \
+                    (budget, s)
+                handed += 1
+                handed_mid += budget > 0
+        assert handed > 0, budget
+    assert handed_mid > 0            # some hand-over came after rows had entered
+
+
+def test_gi_verdict_on_near_parallel_rows(gpu, monkeypatch):
+    """Every cell's half-spaces twice, the copy's normal turned by 1e-7 rad and its offset moved
+    by 1e-9 (near-duplicate, near-parallel rows at every step, what several cells' tangents at
+    one t can give): GI and the IPM must return the same verdict on every scene and the same
+    minimiser where it exists.  GI's own 'no step exists' test rests on round-off-sensitive
+    comparisons, so that verdict is handed to the IPM to confirm."""
+    from ccmpc import _lib
+    T = 8
+    seeds = list(range(100, 132))
+    rec, cps, _, refs, goals, x0s = _scene_inputs(seeds, T, gpu, "halfspace")
+    h = rec.cpu().numpy().reshape(rec.shape[0], -1).view(_lib.HALFSPACE_DTYPE).copy()
+    dup = h.copy()
+    a = 1e-7
+    n0, n1 = dup["n0"].copy(), dup["n1"].copy()
+    dup["n0"], dup["n1"] = np.cos(a) * n0 - np.sin(a) * n1, np.sin(a) * n0 + np.cos(a) * n1
+    dup["d"] = dup["d"] + 1e-9
+    blocks, c = [], 0
+    for k in cps:                           # scene s: its cells, then their near copies
+        blocks += [h[c:c + k], dup[c:c + k]]
+        c += k
+    rec2 = torch.as_tensor(np.concatenate(blocks).view(np.uint8).reshape(
+        sum(cps) * 2, h.shape[1], -1), device=gpu).contiguous()
+    cps2 = [2 * k for k in cps]
+    xbar, gamma = mpc.ltv(x0s, T, lon=LON)
+    g_t, r_t = torch.as_tensor(goals, device=gpu), torch.as_tensor(refs, device=gpu)
+    k = mpc.REC_HALFSPACE
+    u0, _, c0, s0, _ = _solve(monkeypatch, "ipm", cps2, T, k, mpc.U_ORDER_F, gamma, xbar, g_t,
+                              r_t, rec2)
+    u1, _, c1, s1, _ = _solve(monkeypatch, "gi", cps2, T, k, mpc.U_ORDER_F, gamma, xbar, g_t,
+                              r_t, rec2)
+    np.testing.assert_array_equal(s1, s0)
+    ok = s0 == mpc.QP_OK
+    assert ok.sum() >= 4
+    for i in np.flatnonzero(ok):
+        tol = 1e-6 * (1.0 + np.abs(u0[i]).max())
+        assert np.abs(u1[i] - u0[i]).max() <= tol, (seeds[i], np.abs(u1[i] - u0[i]).max())

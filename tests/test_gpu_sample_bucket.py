@@ -81,8 +81,18 @@ def _assert_same(got, want):
     (2, 25, 8, 8192, 9, "heavy"),    # ~7000 rare particles: 28 rare-slot blocks per OV
     (2, 5, 8, 1000, 10, 5),          # every latent kept: no rare particle at all
     (1, 3, 6, 1, 8, None),           # a single particle
+    # N > 8192: two chain waves per place block, the rare stage as keys + copy
+    (2, 25, 8, 20_000, 21, None),
+    (1, 25, 8, 100_000, 22, None),   # C1's np = 100 000 (tests/Hz20/params.py:377)
+    (2, 25, 8, 30_000, 23, "heavy"), # ~26 000 rare particles per OV: 26 key blocks
+    (2, 9, 40, 12_000, 24, None),    # T = 40: the serial chain, 80 coordinate rows
+    (2, 9, 12, 9_000, 25, None),     # T = 12
+    (2, 10, 8, 16_384, 26, 8),       # eight kept modes
+    (2, 5, 8, 10_000, 27, 5),        # every latent kept: no rare particle
+    (2, 25, 8, 8_193, 28, 1),        # the first wide N, one kept mode
+    (1, 25, 8, 262_144, 29, None),   # the largest
 ])
-def test_fused_equals_sampler_then_bucketing(gpu, O, L, T, N, seed, kept):
+def test_fused_equals_sampler_then_bucketing(gpu, monkeypatch, O, L, T, N, seed, kept):
     from ccmpc import engine as e
     init, pmf, gmm = _inputs(O, L, T, seed, kept)
     minpos = np.tile([150.0, -120.0], (O, 1))
@@ -90,11 +100,19 @@ def test_fused_equals_sampler_then_bucketing(gpu, O, L, T, N, seed, kept):
     zf, *got = e.sample_bucket(init, pmf, gmm, N, T, minpos, seed=seed, device=gpu, with_z=True)
     np.testing.assert_array_equal(zf.cpu().numpy(), z2.cpu().numpy())
     _assert_same(got, want)
+    if N <= 8192 and N in (5000, 4097, 700, 3000):
+        # the small clouds' alternative forms (place_kernel's one-chain form, the keys + copy
+        # rare stage) give the same cells
+        for env in ("CCMPC_PLACE_V2", "CCMPC_RARE_TWO_PASS"):
+            monkeypatch.setenv(env, "1")
+            _assert_same(e.sample_bucket(init, pmf, gmm, N, T, minpos, seed=seed, device=gpu),
+                         want)
 
 
-def test_fused_with_injected_draws_and_per_particle_parameters(gpu):
+@pytest.mark.parametrize("N", [5000, 30_000])
+def test_fused_with_injected_draws_and_per_particle_parameters(gpu, N):
     from ccmpc import engine as e
-    O, L, T, N = 3, 25, 8, 5000
+    O, L, T = 3, 25, 8
     init, pmf, gmm = _inputs(O, L, T, 9)
     g = torch.Generator().manual_seed(4)
     z = torch.multinomial(torch.as_tensor(pmf), N, replacement=True, generator=g).to(torch.int32)
@@ -159,11 +177,11 @@ def test_fused_refuses_large_clouds_and_bad_args(gpu):
     from ccmpc import engine as e
     init, pmf, gmm = _inputs(1, 5, 4, 13)
     with pytest.raises(ValueError):
-        e.sample_bucket(init, pmf, gmm, 8193, 4, np.zeros((1, 2)), device=gpu)
+        e.sample_bucket(init, pmf, gmm, 262_145, 4, np.zeros((1, 2)), device=gpu)
     lib = e._lib.load()
-    assert lib.ccmpc_sample_bucket_workspace_bytes(1, 8193, 4, 1) == 0
+    assert lib.ccmpc_sample_bucket_workspace_bytes(1, 262_145, 4, 1) == 0
     assert lib.ccmpc_sample_bucket_workspace_bytes(1, 100, 41, 1) == 0
-    rc = lib.ccmpc_sample_bucket(None, None, 5, None, 0, None, None, 1, 9000, 4, 0.5, 0, None, 0,
+    rc = lib.ccmpc_sample_bucket(None, None, 5, None, 0, None, None, 1, 300_000, 4, 0.5, 0, None, 0,
                                  None, None, None, 1, None, None, None, 0, None, None, 0, None,
                                  None, None, None, None)
     assert rc == -1

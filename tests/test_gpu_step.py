@@ -180,6 +180,48 @@ def test_first_replay_is_not_signalled_by_the_capture_warmup(gpu, monkeypatch):
     assert int(g._flags[0]) == 2
 
 
+def test_capture_warmup_signals_neither_the_step_nor_its_attached_qp(gpu, monkeypatch):
+    """The same with the planning frame's QP attached (attach_qp): the warm-up also
+    runs the QP's copy-out + signal with the QP's current generation, so its word must lag by
+    one too until the held replay runs -- else PlanningQPStep.wait() returned on the warm-up's
+    signal and read the answer pack while the replay rewrote it."""
+    import torch
+    from ccmpc import mpc, step
+    init, pmf, gmm, minpos, pasts, K, eps = _inputs()
+    C = sum(K)
+    g = step.StepGraph(O, N, PH, pmf.shape[1], K, device=gpu)
+    qs = mpc.PlanningQPStep(C, PH, PH, device=gpu)
+    xbar = torch.empty((1, 4 * PH), dtype=torch.float64, device=gpu)
+    gamma = torch.empty((1, 4 * PH, 2 * PH), dtype=torch.float64, device=gpu)
+    g.attach_qp(qs, xbar, gamma, True)
+    past = np.stack([p[-1] for p in pasts])
+    risk = np.tile([[5.99, 0.95, 0.5]], (C, 1))
+    x0, goal = np.array([165.0, -72.0, 0.0, 6.0]), np.array([200.0, -70.0])
+
+    def frame(f):
+        g.set_inputs(10 + f, init, pmf, gmm, minpos, _ref(f), risk, past,
+                     np.tile([[4.5, 2.5]], (O, 1)))
+        return qs.prepare(x0, goal, _ref(f))
+    q1 = frame(1)
+    g.launch()                                            # generation 1: eager
+    g.wait()
+    r1 = qs.wait(q1)
+    held = []
+    monkeypatch.setattr(step.HipGraph, "replay", lambda self, stream=None: held.append(self))
+    q2 = frame(2)
+    g.launch()                                            # generation 2: capture, replay held
+    torch.cuda.synchronize(gpu)
+    assert g.graphs is not None and len(held) == 1
+    assert int(g._flags[0]) == 1, int(g._flags[0])
+    assert int(qs._flags[0]) == q2 - 1, (int(qs._flags[0]), q2)
+    monkeypatch.undo()
+    held[0].replay(torch.cuda.current_stream(gpu).cuda_stream)
+    g.wait()
+    r2 = qs.wait(q2)
+    assert int(g._flags[0]) == 2 and int(qs._flags[0]) == q2
+    assert r1["status"] >= 0 and r2["status"] >= 0
+
+
 def test_pack_record_view_is_the_byte_field(gpu):
     """Pack(record_views=...): a snapshot's record field covers the byte field's bytes with the
     record dtype (what predict_and_constrain hands to HalfSpaceList), in the snapshot's own

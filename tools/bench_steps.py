@@ -24,6 +24,9 @@ def main():
         "dropin_pp": lambda: bench.dropin_step(dev, with_cpu=False, per_particle=True),
         "dropin_100k": lambda: bench.dropin_step(dev, steps=100, with_cpu=False, O=1,
                                                  N=100_000, label="C1 (n_predictions = 100 000)"),
+        "dropin_pred": lambda: bench.dropin_step_predictions(dev),
+        "dropin_pred_100k": lambda: bench.dropin_step_predictions(dev, steps=100, O=1,
+                                                                  N=100_000, n_sets=4),
         "episode": lambda: bench.episode_c1(dev, with_cpu=False),
         "harness": lambda: bench.harness_episode(dev),
     }

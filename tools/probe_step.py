@@ -59,7 +59,7 @@ def main():
         f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * (nargs - 1)
     for rep in range(a.reps):
         assert lib.ccmpc_probe_sampler_timestamps(None, 1) == 0
-        for w in range(3):
+        for w in range(5):
             assert lib.ccmpc_probe_fused_timestamps(None, w, 1) == 0
         for w in range(3):
             assert lib.ccmpc_probe_bucket_timestamps(None, w, 1) == 0
@@ -73,9 +73,14 @@ def main():
         ks = [("sampler", table(lib.ccmpc_probe_sampler_timestamps, 0),
                ["staged", "z", "actions", "chain"]),
               ("latents", table(lib.ccmpc_probe_fused_timestamps, 0, 0), ["drawn"]),
-              ("place", table(lib.ccmpc_probe_fused_timestamps, 1, 0), ["counted", "acted", "headings", "chained", "summed"]),
+              ("place", table(lib.ccmpc_probe_fused_timestamps, 1, 0),
+               ["loaded/counted", "acted", "terms/sincos", "chained", "summed"]),
               ("rares", table(lib.ccmpc_probe_fused_timestamps, 2, 0),
                ["loaded", "centres", "keyed", "bins", "ranked", "copied"]),
+              ("r.keys", table(lib.ccmpc_probe_fused_timestamps, 3, 0),
+               ["loaded", "superblocks", "centres", "keyed"]),
+              ("r.copy", table(lib.ccmpc_probe_fused_timestamps, 4, 0),
+               ["loaded", "counted", "ranked", "copied"]),
               ("b.stats", table(lib.ccmpc_probe_bucket_timestamps, 0, 0),
                ["loaded", "published", "chunk last", "chunk done", "last", "done"]),
               ("b.hist", table(lib.ccmpc_probe_bucket_timestamps, 1, 0),
