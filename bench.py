@@ -581,14 +581,17 @@ def episode_c1(dev, cpu_steps=2, with_cpu=True, N=5000):
     return out
 
 
-def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8):
+def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8, on_device=False):
     """The planning step on the reference's own predictor output: generate_vehicle_latents'
     5-tuple (prediction.py:93-105) -- predictions (nodes, N, ph, 2) float32 and z (nodes, N)
     int64 as the host numpy arrays the reference returns, the ego's node in row 0 -- through
     MidlevelAgent.predict_and_constrain with StepGraph(source="predictions"): the arrays go into
-    the pinned input pack, ccmpc_load_predictions -> ccmpc_bucket (make_ovehicles, :469-505)
-    -> the Minkowski cycle -> L4 -> 9-tuple; no sampler.  `n_sets` precomputed frames of
-    particles (the sampler's own draws) are cycled, a different one each step."""
+    the pinned input pack, ccmpc_bucket_predictions (make_ovehicles, :469-505: one placement
+    pass) -> the Minkowski cycle -> L4 -> 9-tuple; no sampler.  on_device: the same arrays as
+    device tensors (generate_vehicle_latents(..., keep_on_device=True), a predictor on the same
+    GPU): copied device to device into the graph's buffers inside the timed step, nothing crosses
+    PCIe.  `n_sets` precomputed frames of particles (the sampler's own draws) are cycled, a
+    different one each step."""
     from ccmpc import engine, episode, planner
     init, pmf, gmm = episode.synthetic_gmm(O, T=ph, seed=20251015)
     minpos = np.array([150.0, -120.0])
@@ -608,6 +611,8 @@ def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8):
             pred[o + 1] = pos[:, off:off + N].reshape(ph, 2, N).transpose(2, 0, 1)
         zz = np.zeros((O + 1, N), np.int64)
         zz[1:] = z.cpu().numpy()
+        if on_device:
+            pred, zz = torch.as_tensor(pred, device=dev), torch.as_tensor(zz, device=dev)
         sets.append(dict(source="predictions", predictions=pred, z=zz,
                          rows=list(range(1, O + 1)), latent_pmf=pmf, N=N))
     agent = planner.MidlevelAgent(prediction_horizon=ph, device=dev)
@@ -624,10 +629,11 @@ def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8):
         _, out = one(i)
         ts.append(time.perf_counter() - t0)
     g = next(iter(agent._graphs.values()))
-    return {"config": f"C2 shape drop-in step on generate_vehicle_latents' 5-tuple: {O} OVs (+ the "
-                      f"ego's node) x np={N} x ph={ph}, K={K}; host numpy predictions / z in the "
-                      "pinned pack -> ccmpc_load_predictions -> ccmpc_bucket -> Minkowski cycle "
-                      "-> L4 -> 9-tuple",
+    where = ("device tensors (keep_on_device) copied device to device" if on_device else
+             "host numpy predictions / z in the pinned pack")
+    return {"config": f"drop-in step on generate_vehicle_latents' 5-tuple: {O} OVs (+ the "
+                      f"ego's node) x np={N} x ph={ph}, K={K}; {where} -> "
+                      "ccmpc_bucket_predictions -> Minkowski cycle -> L4 -> 9-tuple",
             "steps": steps, "constraints_per_step": len(out[0]),
             "graph_branch": f"source={g.source}, fused={g.fused}",
             "input_pack_bytes": int(g.inp.nbytes),
@@ -1135,10 +1141,14 @@ def main():
             out["dropin_step_c2_pp"] = dropin_step(dev, with_cpu=False, per_particle=True)
             # the reference's own predictor output (generate_vehicle_latents' 5-tuple)
             out["dropin_step_c2_predictions"] = dropin_step_predictions(dev)
+            out["dropin_step_c2_predictions_device"] = dropin_step_predictions(dev,
+                                                                               on_device=True)
             # C1's real particle count (tests/Hz20/params.py:377): the graph's non-fused branch
             out["dropin_step_c1_100k"] = dropin_step(
                 dev, steps=100, with_cpu=not args.no_cpu, O=1, N=100_000, eager_steps=20,
                 cpu_reps=2, label="C1 (n_predictions = 100 000)")
+            out["dropin_step_c1_100k_predictions_device"] = dropin_step_predictions(
+                dev, steps=100, O=1, N=100_000, n_sets=4, on_device=True)
             out["episode_c1"] = episode_c1(dev, with_cpu=not args.no_cpu)
             out["harness_episode"] = harness_episode(dev)
             # the reference's real particle count at the "np5000" label (params.py:377)

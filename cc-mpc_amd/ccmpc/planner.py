@@ -513,6 +513,10 @@ class MidlevelAgent:
         from . import prediction
         self._generate_vehicle_latents = kwargs.get("generate_vehicle_latents",
                                                     prediction.generate_vehicle_latents)
+        # opt-in (not in the reference): the predictor's z / predictions stay on the GPU
+        # (generate_vehicle_latents(..., keep_on_device=True)), so the step graph copies them
+        # device to device instead of through the pinned input pack
+        self.keep_predictions_on_device = bool(kwargs.get("keep_predictions_on_device", False))
         self._prediction_output_to_trajectories = kwargs.get(
             "prediction_output_to_trajectories", prediction.prediction_output_to_trajectories)
 
@@ -640,12 +644,13 @@ class MidlevelAgent:
                             latent_probs=np.asarray(b["latent_probs"], np.float64),
                             past_dict={timestep: scene.past(timestep, max_h=10)})
         timesteps = np.array([timestep])
+        extra = {"keep_on_device": True} if self.keep_predictions_on_device else {}
         with torch.no_grad():
             z, predictions, nodes, predictions_dict, latent_probs = \
                 self._generate_vehicle_latents(self._eval_stg, scene, timesteps,
                                                num_samples=self.n_predictions, ph=ph,
                                                z_mode=False, gmm_mode=False, full_dist=False,
-                                               all_z_sep=False)
+                                               all_z_sep=False, **extra)
         _, past_dict, ground_truth_dict = self._prediction_output_to_trajectories(
             predictions_dict, dt=scene.dt, max_h=10, ph=ph, map=None)
         return AttrDict(scene=scene, timestep=timestep, nodes=nodes, predictions=predictions,

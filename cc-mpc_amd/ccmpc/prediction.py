@@ -6,8 +6,7 @@ prediction_output_to_trajectories, which MidlevelAgent.do_prediction (v8ideal/__
 Everything here is host glue around Trajectron++'s own model objects (the encoder, p(z|x),
 the latent sampler and the GRU decoder live in eval_stg); the product path starts where the
 5-tuple ends: make_ovehicles' bucketing, the generators and the QP run on the GPU from
-predictions + z (ccmpc_load_predictions -> ccmpc_bucket -> ..., step.StepGraph with
-source="predictions").  Trajectron++ is an un-vendored submodule (absent here), so its imports
+predictions + z (ccmpc_bucket_predictions -> ..., step.StepGraph with source="predictions").  Trajectron++ is an un-vendored submodule (absent here), so its imports
 are lazy and fail the way the reference's module import does.
 """
 import numpy as np
@@ -23,7 +22,8 @@ def _trajectron():
 
 
 def generate_vehicle_latents(eval_stg, scene, timesteps, num_samples=200, ph=8, z_mode=False,
-                             gmm_mode=False, full_dist=False, all_z_sep=False):
+                             gmm_mode=False, full_dist=False, all_z_sep=False,
+                             keep_on_device=False):
     """prediction.py:19-105: one batch of the scene's VEHICLE nodes at `timesteps` through
     eval_stg's node model -- p(z|x), sample_p, p_y_xz -- returned as the reference returns it:
 
@@ -31,7 +31,14 @@ def generate_vehicle_latents(eval_stg, scene, timesteps, num_samples=200, ph=8, 
       predictions     (nodes, num_samples, ph, 2) float32, scene-relative positions
       nodes           the batch's nodes (the ego's included; make_ovehicles skips it)
       predictions_dict {timestep: {node: (1, num_samples, ph, 2)}}
-      latent_probs    (nodes, n_latent) p(z|x)"""
+      latent_probs    (nodes, n_latent) p(z|x)
+
+    keep_on_device (not in the reference, opt-in): z and predictions stay torch tensors on
+    eval_stg.device -- the same values (the argmax of a one-hot sample is its one index, so
+    torch's and numpy's agree), laid out as the numpy route lays them out -- and
+    predictions_dict holds views of them.  The only consumer is make_ovehicles' bucketing,
+    which runs on the same GPU (v8ideal/__init__.py:469-505: the arrays are only indexed by z),
+    so the particles never cross PCIe."""
     get_timesteps_data, ModeKeys = _trajectron()
     node_type = eval_stg.env.NodeType.VEHICLE
     if node_type not in eval_stg.pred_state:
@@ -61,6 +68,14 @@ def generate_vehicle_latents(eval_stg, scene, timesteps, num_samples=200, ph=8, 
         num_samples, mode, most_likely_z=z_mode, full_dist=full_dist, all_z_sep=all_z_sep)
     _, predictions = model.p_y_xz(mode, x, x_nr_t, y_r, n_s_t0, z, ph, n_samples,
                                   n_components, gmm_mode)
+    if keep_on_device:
+        import torch
+        z = torch.argmax(z.detach(), dim=-1).transpose(0, 1).contiguous()   # (nodes, samples)
+        predictions = predictions.detach().to(torch.float32)
+        pd = {}
+        for i, ts in enumerate(timesteps_o):
+            pd.setdefault(ts, {})[nodes[i]] = predictions[:, i:i + 1].transpose(0, 1)
+        return z, predictions.transpose(0, 1).contiguous(), nodes, pd, latent_probs
     z = z.cpu().detach().numpy()                    # (samples, nodes, n_latent) one-hot
     predictions = predictions.cpu().detach().numpy()  # (samples, nodes, ph, 2)
     predictions_dict = {}

@@ -413,13 +413,16 @@ class TrajectronModel:
 
 
 def generate_vehicle_latents(eval_stg, scene, timesteps, num_samples=200, ph=8, z_mode=False,
-                             gmm_mode=False, full_dist=False, all_z_sep=False):
+                             gmm_mode=False, full_dist=False, all_z_sep=False,
+                             keep_on_device=False):
     """prediction.py:19-105 for a TrajectronModel stand-in: the reference's 5-tuple
     (z (nodes, N) int64, predictions (nodes, N, ph, 2) float32 scene-relative, nodes,
     predictions_dict, latent_probs) as numpy arrays, the samples drawn by the library's own
     sampler tail (ccmpc_sample_unicycle_ex) from the inner stand-in's boundary.  The non-ego
     nodes are drawn as OVs 0 .. O-1 in node order (the Philox streams the sample_boundary route
-    keys them by), so both routes see the same particles; the ego's row is drawn after them."""
+    keys them by), so both routes see the same particles; the ego's row is drawn after them.
+    keep_on_device: z and predictions as device tensors (ccmpc.prediction's opt-in), built on
+    the GPU from the sampler's store without a host round trip."""
     from . import engine
     b = eval_stg.inner.sample_boundary(scene, int(np.asarray(timesteps).reshape(-1)[0]),
                                        num_samples, ph)
@@ -443,12 +446,22 @@ def generate_vehicle_latents(eval_stg, scene, timesteps, num_samples=200, ph=8, 
         np.asarray(b.init_state)[sel], np.asarray(b.latent_probs)[sel], pick(b.gmm), N, ph,
         seed=b.seed, device=eval_stg.device, z=pick(b.get("z")) if pp else None,
         eps=pick(b.get("eps")) if pp else None, per_particle=pp)
+    ts = int(np.asarray(timesteps).reshape(-1)[0])
+    if keep_on_device:
+        dev = store.pos.device
+        inv = torch.as_tensor(np.argsort(sel), device=dev)      # node i <- drawn row inv[i]
+        off = torch.as_tensor(np.asarray(store.offsets[:n], np.int64), device=dev)
+        idx = off[:, None] + torch.arange(N, device=dev)[None]  # (n, N) store columns
+        cols = store.pos[:, idx]                                 # (2 ph, n, N)
+        pred_d = cols.reshape(ph, 2, n, N).permute(2, 3, 0, 1)[inv].contiguous()
+        z_d = zs.to(torch.int64)[inv].contiguous()
+        pdict = {ts: {nd: pred_d[i][None] for i, nd in enumerate(nodes)}}
+        return z_d, pred_d, nodes, pdict, np.asarray(b.latent_probs, np.float64)
     pos = store.pos.cpu().numpy()
     zh = zs.cpu().numpy()
     for j, r in enumerate(rows):
         o = store.offsets[j]
         pred[r] = pos[:, o:o + N].reshape(ph, 2, N).transpose(2, 0, 1)
         z[r] = zh[j]
-    ts = int(np.asarray(timesteps).reshape(-1)[0])
     pdict = {ts: {nd: pred[i][None] for i, nd in enumerate(nodes)}}
     return z, pred, nodes, pdict, np.asarray(b.latent_probs, np.float64)

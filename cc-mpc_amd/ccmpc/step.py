@@ -282,6 +282,7 @@ class StepGraph:
             if self.eps_in:
                 self.pp_eps = torch.zeros((O, ph_, 2, N), dtype=f32, device=self.device)
         self.pr_pred = self.pr_z = None
+        self._rows_idx = None                 # set_predictions' cached device row index
         if source == "predictions" and self.pred_device:
             self.pr_pred = torch.zeros((O, N, ph_, 2), dtype=f32, device=self.device)
             self.pr_z = torch.zeros((O, N), dtype=i64, device=self.device)
@@ -657,11 +658,16 @@ class StepGraph:
         if dev:
             if predictions.device != self.device or z.device != self.device:
                 raise ValueError("predictions / z must be on the graph's device")
-            if rows == list(range(O)) and predictions.shape[0] == O:
-                self.pr_pred.copy_(predictions)
-                self.pr_z.copy_(z)
+            if rows == list(range(rows[0], rows[0] + O)) if O else True:
+                # the OVs are one run of nodes (the ego's row first or last): a view, one
+                # device-to-device copy each, nothing uploaded
+                self.pr_pred.copy_(predictions[rows[0]:rows[0] + O])
+                self.pr_z.copy_(z[rows[0]:rows[0] + O])
             else:
-                idx = torch.as_tensor(rows, device=self.device)
+                key = tuple(rows)
+                if self._rows_idx is None or self._rows_idx[0] != key:
+                    self._rows_idx = (key, torch.as_tensor(rows, device=self.device))
+                idx = self._rows_idx[1]
                 torch.index_select(predictions.to(torch.float32), 0, idx, out=self.pr_pred)
                 torch.index_select(z.to(torch.int64), 0, idx, out=self.pr_z)
             return

@@ -89,6 +89,9 @@ __device__ unsigned long long g_fused_ts[5][kStepProbeWG * kStepProbeSlots];
 #define FUSED_TS(kern, k) CCMPC_STEP_TS(nullptr, k)
 #endif
 
+constexpr int kActCoef = 64 * 40 * 5 / 4;    // P1: per-latent coefficient floats per OV (P0)
+constexpr int kSrcPred = 4;                   // P1's particle source: the predictor's output
+
 // where P0's latent ids come from
 constexpr int kZPhilox = 0;  // Philox inverse CDF of latent_cdf (the synthetic sampler mode)
 constexpr int kZIn = 1;      // injected int32 z_in[o][N] (the sampler's per-particle mode)
@@ -126,6 +129,7 @@ struct FusedArgs {
   float *rstore;   // [n_ov][2T][Npad]: rare particles' coordinates, rare-list order
   int32_t *kbuf;   // [n_ov][Npad]: rare-list slot keys (P2 keys)
   int32_t *rhist;  // [n_ov][nkb][kFusedMaxBins]: each P2 keys block's bin histogram
+  float *coef;     // [n_ov][kActCoef]: the per-latent GMM coefficient rows (P0 block 0)
   int64_t Npad;
   int G, nb0, nkb;
   // outputs
@@ -204,6 +208,9 @@ __global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
     if (lane == c) mine = n;
   }
   const int nbad = __popcll(__ballot(v && bad));
+  if (a.coef && blockIdx.x == 0)        // the OV's per-latent coefficient rows, for P1
+    stage_gmm_coefs(a.gmm + static_cast<int64_t>(o) * L * a.T * 5, L * a.T,
+                    a.coef + static_cast<int64_t>(o) * kActCoef, tid, kFThreads);
   if (g < a.G && lane <= K) a.gcnt[(static_cast<int64_t>(o) * a.G + g) * kCntStride + lane] = mine;
   if (lane <= K) wc_s[w][lane] = mine;
   if (lane == 0) wc_s[w][kMaxKept + 1] = nbad;
@@ -419,26 +426,26 @@ __global__ __launch_bounds__(kFThreads) void sample_place_kernel(FusedArgs a) {
   FUSED_TS(1, 5);
 }
 
-// P1 as one template over the particle source and the block width: MODE bit 1 = injected
-// noise, 2 = per-particle GMM parameters, 4 = the predictor's coordinates instead of the sampler
-// (no actions: the block's 64 NCH x 2T run of pred staged through LDS); NCH chain waves of 64
-// particles per block (1 for the small clouds, 2 above kFusedMaxN, so a 100 000-particle cloud
-// is 782 blocks).  Dynamic LDS (floats), sized by T:
-//   sampler    act[2][T][PB], T <= kParSteps: sc[2][T + 1][PB] (the headings' sin / cos),
-//              gmm_s[L T 5] (coefficient rows) when staged
-//   predictor  tile[PB][2T + 1]
-// The category counts come from P0's block totals (a few hundred ints, not every group's), and
-// each chain wave's category ranks are taken before the actions.
-template <int MODE, int NCH, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedArgs a,
-                                                                        int staged_gmm) {
-  constexpr bool PRED = (MODE & 4) != 0, PP = (MODE & 2) != 0, EPSIN = (MODE & 1) != 0;
-  constexpr int PB = kFP * NCH, NTH = 64 * NW;
-  static_assert(NCH <= NW, "one wave per chain");
+// P1 for the large clouds (the sampler) and for the predictor's output (MODE kSrcPred: the
+// block's 64 x 2T coordinate run staged through LDS, no actions).  One chain wave of 64
+// particles per block of NW waves (4: a 100 000-particle cloud is 1563 blocks, all resident at
+// 7 per CU); the sampler's modes (MODE bit 1 = injected noise, 2 = per-particle parameters) draw
+// the block's T x 64 actions over the waves first, with the per-latent coefficient rows P0
+// staged (no exp per block).  Measured and not kept: the draws as their own launch at full
+// occupancy (one pair per lane, or a grid-stride loop): 15 / 12 us against ~10 us inside this
+// kernel, plus a boundary.  Dynamic LDS (floats), sized by T:
+//   sampler    act[2T][64], coefficient rows [L T 5] (per-latent, when they fit), T <=
+//              kParSteps: sc[2][T + 1][64] (the headings' sin / cos) and terms[2][3][T][64]
+//              (each step's position terms)
+//   predictor  tile[64][2T + 1]
+// The category counts come from P0's block totals (a few hundred ints, not every group's).
+template <int MODE, int NW>
+__global__ __launch_bounds__(64 * NW, 7) void place_kernel(FusedArgs a) {
+  constexpr bool PRED = MODE == kSrcPred, PP = (MODE & 2) != 0, EPSIN = (MODE & 1) != 0;
+  constexpr int PB = kFP, NTH = 64 * NW;
   extern __shared__ float dyn[];
   __shared__ int keep_s[64];
   __shared__ int zs[PB];
-  __shared__ int wc_s[NCH][kMaxKept + 1];   // each chain's category counts
   __shared__ int before_s[kMaxKept + 1], total_s[kMaxKept + 1];
   __shared__ double st_s[6];                // the OV's initial state (x, y, heading, speed), minpos
   FUSED_TS(1, 0);
@@ -447,11 +454,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedAr
   const int K = a.n_kept[o], L = a.L, T = a.T, Kp1 = K + 1;
   const int64_t N = a.N;
   const int64_t i0 = static_cast<int64_t>(blk) * PB;
-  const int g0 = blk * NCH, b0 = g0 / kFWaves;
+  const int g0 = blk, b0 = g0 / kFWaves;     // (P0 blocks are kFWaves groups)
   const int64_t reg = a.region[o];
+  const int W = 2 * T, S = W + 1;
+  const int n = static_cast<int>(N - i0 < PB ? N - i0 : PB);
   // every load that needs nothing from another, issued together: own latent ids, the count
-  // rows, the tables, the OV's initial state (a global read after the barriers below is a round
-  // trip of its own on the chain), the predictor's coordinate run
+  // rows, the tables, the OV's initial state, the block's actions or coordinate run
   if (tid < PB && i0 + tid < N) zs[tid] = a.zbuf[static_cast<int64_t>(o) * a.Npad + i0 + tid];
   if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
   const int nA = a.nb0 * Kp1, E = nA + (g0 - b0 * kFWaves) * Kp1;
@@ -460,27 +468,25 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedAr
   bool ct[kC], cb[kC];
 #pragma unroll
   for (int j = 0; j < kC; ++j) cv[j] = count_elem(a, o, tid + j * NTH, nA, E, Kp1, b0, ct[j], cb[j]);
-  // (into LDS, read where used: eight VGPRs held across the f64-heavy action phase spilled)
   if (tid < 4) st_s[tid] = PRED ? 0.0 : a.init_state[4 * o + tid];
   else if (tid < 6) st_s[tid] = a.minpos[2 * o + tid - 4];
-  const uint64_t seed = PRED ? 0 : (a.seed_dev ? *a.seed_dev : a.seed);
-  const uint32_t key = a.ov_base + static_cast<uint32_t>(o);
-  const int W = 2 * T, S = W + 1;
-  float *act = dyn;                                         // sampler
-  float *sc = dyn + 2 * T * PB;                             // sin / cos of phi_0 .. phi_T
   const bool par = T <= kParSteps;
-  float *gmm_s = sc + (par ? 2 * (T + 1) * PB : 0);
   const int gsz = L * T * 5;
+  const bool staged = !PRED && !PP && a.coef != nullptr;
+  float *act = dyn;                                         // [2T][PB]
+  float *sc = act + 2 * T * PB;                             // [2][T + 1][PB] (par)
+  float *terms = sc + (par ? 2 * (T + 1) * PB : 0);         // [2][3][T][PB] (par)
+  float *coef_s = terms;   // [L T 5] when staged: read only before the terms are written
   if (PRED) {
-    const int n = static_cast<int>(N - i0 < PB ? N - i0 : PB);
     const int64_t row = a.rows ? static_cast<int64_t>(a.rows[o]) : o;
     const float *src = a.pred + (row * N + i0) * W;
     for (int e = tid; e < n * W; e += NTH) {
       const int p = e / W;
       dyn[p * S + (e - p * W)] = src[e];
     }
-  } else if (staged_gmm) {
-    stage_gmm_coefs(a.gmm + static_cast<int64_t>(o) * gsz, gsz / 5, gmm_s, tid, NTH);
+  } else if (staged) {
+    const float *cg = a.coef + static_cast<int64_t>(o) * kActCoef;
+    for (int e = tid; e < gsz; e += NTH) coef_s[e] = cg[e];
   }
   if (tid <= K) before_s[tid] = total_s[tid] = 0;
   __syncthreads();
@@ -501,57 +507,70 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedAr
       if (cb[j]) atomicAdd(&before_s[c], cv[j]);
     }
   }
-  // the chain waves' own categories and ranks (sample order: chain c's lanes)
-  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  int cat = K, rank_w = 0;
-  bool valid = false;
-  if (w < NCH) {
-    const int q = w * kFP + lane;
-    valid = i0 + q < N;
-    const int kk = valid ? keep_s[zs[q]] : -1;
-    cat = kk >= 0 ? kk : K;
-    int mine = 0;
-    for (int c = 0; c <= K; ++c) {
-      const unsigned long long m = __ballot(valid && cat == c);
-      if (cat == c) rank_w = __popcll(m & below);
-      if (lane == c) mine = __popcll(m);
-    }
-    if (lane <= K) wc_s[w][lane] = mine;
-  }
-  // ---- sampler: actions (all waves), then the headings' sin / cos in parallel --------------
-  if (!PRED) {
+  if (!PRED) {     // the block's actions: step t of particle lane on wave t mod NW
+    const uint64_t seed = a.seed_dev ? *a.seed_dev : a.seed;
+    const uint32_t key = a.ov_base + static_cast<uint32_t>(o);
+    if (lane < n) {
 #pragma unroll 1
-    for (int u = w; u < T * NCH; u += NW) {
-      const int t = u / NCH, c = u - t * NCH, q = c * kFP + lane;
-      const int64_t ip = i0 + q;
-      if (ip < N)
-        draw_action<PP, EPSIN>(t, ip, zs[q], o, T, L, N, key, seed, a.gmm, gmm_s,
-                               staged_gmm != 0, a.eps_in, act[t * PB + q], act[(T + t) * PB + q]);
+      for (int t = w; t < T; t += NW)
+        draw_action<PP, EPSIN>(t, i0 + lane, zs[lane], o, T, L, N, key, seed, a.gmm, coef_s,
+                               staged, a.eps_in, act[(2 * t) * PB + lane],
+                               act[(2 * t + 1) * PB + lane]);
+    }
+  }
+  const float dt = a.dt;
+  if (!PRED) __syncthreads();     // the actions
+  if (!PRED && par) {
+    // T <= kParSteps: the sin / cos of every heading phi_0 .. phi_T, step t of particle lane on
+    // wave t mod NW.  phi_t is the f32 running sum the chain accumulates (phi += dphi dt at a
+    // turning step), recomputed in the same order; sincos_rn(phi_t) is what unicycle_step
+    // evaluates at step t (or carries, unchanged, over a straight step: phi_t+1 == phi_t).  One
+    // sincos per heading, where evaluating each step's pair took two
+    if (lane < n) {
+#pragma unroll 1
+      for (int t = w; t <= T; t += NW) {
+        float phi = static_cast<float>(st_s[2]);
+        for (int s = 0; s < t; ++s) {
+          const float dphi = act[(2 * s) * PB + lane];
+          phi = fabsf(dphi) <= 1e-2f ? phi : phi + dphi * dt;
+        }
+        sincos_rn(phi, sc[t * PB + lane], sc[(T + 1 + t) * PB + lane]);
+      }
+    }
+    __syncthreads();
+    FUSED_TS(1, 2);
+    // each step's position terms, in unicycle_step's expressions, in parallel over the waves;
+    // the chain keeps its adds in unicycle_step's association: x + A + B (+ C), y + A + B
+    // (turning: y - A + B - C)
+    if (lane < n) {
+#pragma unroll 1
+      for (int t = w; t < T; t += NW) {
+        float v = static_cast<float>(st_s[3]);
+        for (int s = 0; s < t; ++s) v = v + act[(2 * s + 1) * PB + lane] * dt;
+        const float dphi = act[(2 * t) * PB + lane], acc = act[(2 * t + 1) * PB + lane];
+        const float s0 = sc[t * PB + lane], c0 = sc[(T + 1 + t) * PB + lane];
+        float *tx = terms + t * PB + lane, *ty = terms + (3 * T + t) * PB + lane;
+        if (fabsf(dphi) <= 1e-2f) {
+          tx[0] = v * c0 * dt;
+          tx[T * PB] = (acc / 2.0f) * c0 * dt * dt;
+          ty[0] = v * s0 * dt;
+          ty[T * PB] = (acc / 2.0f) * s0 * dt * dt;
+        } else {
+          const float s1 = sc[(t + 1) * PB + lane], c1 = sc[(T + 2 + t) * PB + lane];
+          const float dsin = (s1 - s0) / dphi, dcos = (c1 - c0) / dphi;
+          const float aw = acc / dphi;
+          tx[0] = aw * dcos;
+          tx[T * PB] = v * dsin;
+          tx[2 * T * PB] = aw * s1 * dt;
+          ty[0] = v * dcos;
+          ty[T * PB] = aw * dsin;
+          ty[2 * T * PB] = aw * c1 * dt;
+        }
+      }
     }
   }
   __syncthreads();
-  FUSED_TS(1, 2);
-  if (!PRED && par) {
-    // T <= kParSteps: the sin / cos of every heading phi_0 .. phi_T, (t, chain) pair u on wave
-    // u mod 8.  phi_t is the f32 running sum the chain accumulates (phi += dphi dt at a turning
-    // step), recomputed in the same order; sincos_rn(phi_t) is what unicycle_step evaluates at
-    // step t (or carries, unchanged, over a straight step: phi_t+1 == phi_t).  One sincos per
-    // heading, where evaluating each step's pair took two
-    const float dt = a.dt;
-#pragma unroll 1
-    for (int u = w; u < (T + 1) * NCH; u += NW) {
-      const int t = u / NCH, c = u - t * NCH, q = c * kFP + lane;
-      if (i0 + q >= N) continue;
-      float phi = static_cast<float>(st_s[2]);
-      for (int s = 0; s < t; ++s) {
-        const float dphi = act[s * PB + q];
-        phi = fabsf(dphi) <= 1e-2f ? phi : phi + dphi * dt;
-      }
-      sincos_rn(phi, sc[t * PB + q], sc[(T + 1 + t) * PB + q]);
-    }
-    __syncthreads();
-    FUSED_TS(1, 3);
-  }
+  FUSED_TS(1, 3);
   const int R = total_s[K];
   if (blk == 0 && tid <= K) {  // the OV's header for P2 (every block computed the same values)
     int32_t *h = a.hdr + static_cast<int64_t>(o) * kHdrInts;
@@ -562,11 +581,17 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedAr
       hdr_starts(h)[tid] = cur;
     }
   }
-  if (w >= NCH) return;
-  // ---- chain wave w: particles i0 + 64 w + lane ---------------------------------------------
-  const int q = w * kFP + lane;
-  int rank = rank_w;
-  for (int c = 0; c < w; ++c) rank += wc_s[c][cat];
+  if (w != 0) return;
+  // ---- the chain wave: particle i0 + lane ----------------------------------------------------
+  const bool valid = lane < n;
+  const int kk = valid ? keep_s[zs[lane]] : -1;
+  const int cat = kk >= 0 ? kk : K;
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int rank = 0;
+  for (int c = 0; c <= K; ++c) {
+    const unsigned long long m = __ballot(valid && cat == c);
+    if (cat == c) rank = __popcll(m & below);
+  }
   const bool native = cat < K;
   int64_t dst = 0;
   if (native) {
@@ -581,31 +606,22 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedAr
     float *op = native ? a.out + dst : a.rstore + static_cast<int64_t>(o) * W * a.Npad + rs;
     const int64_t ld = native ? a.ld_out : a.Npad;
     if (PRED) {
-      const float *tp = dyn + q * S;
+      const float *tp = dyn + lane * S;
       for (int r = 0; r < W; ++r) op[r * ld] = tp[r];
       x = tp[W - 2];
       y = tp[W - 1];
     } else if (par) {
-      // unicycle_step with the headings' sin / cos from LDS: what stays on the dependent path
-      // is the position adds (the terms depend only on LDS values)
       x = static_cast<float>(st_s[0]);
       y = static_cast<float>(st_s[1]);
-      float v = static_cast<float>(st_s[3]);
-      const float dt = a.dt;
       for (int t = 0; t < T; ++t) {
-        const float dphi = act[t * PB + q], acc = act[(T + t) * PB + q];
-        const float s0 = sc[t * PB + q], c0 = sc[(T + 1 + t) * PB + q];
-        if (fabsf(dphi) <= 1e-2f) {
-          x = x + v * c0 * dt + (acc / 2.0f) * c0 * dt * dt;
-          y = y + v * s0 * dt + (acc / 2.0f) * s0 * dt * dt;
+        const float *tx = terms + t * PB + lane, *ty = terms + (3 * T + t) * PB + lane;
+        if (fabsf(act[(2 * t) * PB + lane]) <= 1e-2f) {
+          x = x + tx[0] + tx[T * PB];
+          y = y + ty[0] + ty[T * PB];
         } else {
-          const float s1 = sc[(t + 1) * PB + q], c1 = sc[(T + 2 + t) * PB + q];
-          const float dsin = (s1 - s0) / dphi, dcos = (c1 - c0) / dphi;
-          const float aw = acc / dphi;
-          x = x + aw * dcos + v * dsin + aw * s1 * dt;
-          y = y - v * dcos + aw * dsin - aw * c1 * dt;
+          x = x + tx[0] + tx[T * PB] + tx[2 * T * PB];
+          y = y - ty[0] + ty[T * PB] - ty[2 * T * PB];
         }
-        v = v + acc * dt;
         op[(2 * t) * ld] = x;
         op[(2 * t + 1) * ld] = y;
       }
@@ -616,22 +632,21 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 6 : 7) void place_kernel(FusedAr
       float s0, c0;
       sincos_rn(phi, s0, c0);
       for (int t = 0; t < T; ++t) {
-        unicycle_step(x, y, phi, v, s0, c0, act[t * PB + q], act[(T + t) * PB + q], a.dt);
+        unicycle_step(x, y, phi, v, s0, c0, act[(2 * t) * PB + lane],
+                      act[(2 * t + 1) * PB + lane], dt);
         op[(2 * t) * ld] = x;
         op[(2 * t + 1) * ld] = y;
       }
     }
     if (!native) {
-      const float4 info = {x, y, __builtin_bit_cast(float, zs[q]), 0.0f};
+      const float4 info = {x, y, __builtin_bit_cast(float, zs[lane]), 0.0f};
       reinterpret_cast<float4 *>(a.rinfo)[static_cast<int64_t>(o) * npad + rs] = info;
     }
   }
   FUSED_TS(1, 4);
-  // chain wave w is centre group g0 + w: its kept-mode sums of the final world positions
-  const int g = g0 + w;
-  if (g >= a.G) return;
+  // this block is centre group g0: its kept-mode sums of the final world positions
   const double xw = static_cast<double>(x) + st_s[4], yw = static_cast<double>(y) + st_s[5];
-  double2 *gp = reinterpret_cast<double2 *>(a.gpart) + (static_cast<int64_t>(o) * a.G + g) * a.max_k;
+  double2 *gp = reinterpret_cast<double2 *>(a.gpart) + (static_cast<int64_t>(o) * a.G + g0) * a.max_k;
   for (int k = 0; k < K; ++k) {
     const bool mine = valid && cat == k;
     const double sx = group_sum64(mine ? xw : 0.0), sy = group_sum64(mine ? yw : 0.0);
@@ -826,25 +841,32 @@ __global__ __launch_bounds__(kRThreads) void rare_key_kernel(FusedArgs a) {
   FUSED_TS(3, 1);
   const int R = tot_s[K];
   if (s0 >= R && blockIdx.x != 0) return;  // uniform: no slots here (block 0 writes centres)
+  // the superblock sums: thread (k, j) sums superblock j of mode k's group partials left to
+  // right from global (S_j = 0.0 + P_64j + P_64j+1 + ...), then thread k adds the S_j left to
+  // right.  Measured and not kept: staging the partials through LDS first (3.8 us against 3.0),
+  // and P1's last arriving block per superblock summing it (keys 8.1 -> 5.5 us, but P1 25.6 ->
+  // 34.9 us: its blocks slowed down throughout, profiles/r06/README.md)
   const int G = a.G, nsup = (G + kCentreSuper - 1) / kCentreSuper;
-  const double2 *gp = reinterpret_cast<const double2 *>(a.gpart) + static_cast<int64_t>(o) * G * a.max_k;
-  for (int u = tid; u < K * nsup; u += kRThreads) {
-    const int k = u / nsup, j = u - k * nsup;
-    const int ga = j * kCentreSuper, gb = min(G, ga + kCentreSuper);
-    double2 acc = {0.0, 0.0};
-    for (int g = ga; g < gb; g += 16) {
-      double2 v[16];
+  {
+    const double2 *gp = reinterpret_cast<const double2 *>(a.gpart) + static_cast<int64_t>(o) * G * a.max_k;
+    for (int u = tid; u < K * nsup; u += kRThreads) {
+      const int k = u / nsup, jj = u - k * nsup;
+      const int ga = jj * kCentreSuper, gb = min(G, ga + kCentreSuper);
+      double2 acc = {0.0, 0.0};
+      for (int g = ga; g < gb; g += 16) {
+        double2 v[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = gp[static_cast<int64_t>(g + q < gb ? g + q : gb - 1) * a.max_k + k];
-      __builtin_amdgcn_sched_barrier(0);  // every read issued before the first add waits
+        for (int q = 0; q < 16; ++q) v[q] = gp[static_cast<int64_t>(g + q < gb ? g + q : gb - 1) * a.max_k + k];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const bool in = g + q < gb;
-        acc.x += in ? v[q].x : -0.0;      // x + -0.0 == x: the sentinel of bucket.hpp
-        acc.y += in ? v[q].y : -0.0;
+        for (int q = 0; q < 16; ++q) {
+          const bool in = g + q < gb;
+          acc.x += in ? v[q].x : -0.0;      // x + -0.0 == x: bucket.hpp's sentinel
+          acc.y += in ? v[q].y : -0.0;
+        }
       }
+      sup_s[k][jj] = acc;
     }
-    sup_s[k][j] = acc;
   }
   for (int u = tid; u < K * 16; u += kRThreads) {
     const int k = u / 16, j = nsup + (u - k * 16);
@@ -1006,7 +1028,7 @@ __global__ __launch_bounds__(kRThreads) void rare_copy_kernel(FusedArgs a) {
 }
 
 struct FusedWs {
-  size_t zbuf, gcnt, bsum, hdr, gpart, rinfo, rstore, kbuf, rhist, total;
+  size_t zbuf, gcnt, bsum, hdr, gpart, rinfo, rstore, kbuf, rhist, coef, total;
   int64_t G, nb0, nkb, Npad;
 };
 
@@ -1037,23 +1059,16 @@ inline FusedWs fused_ws(int64_t n_ov, int64_t N, int64_t T, int64_t max_k) {
   o += a256(sizeof(int32_t) * n_ov * w.Npad);
   w.rhist = o;
   o += a256(sizeof(int32_t) * n_ov * w.nkb * kFusedMaxBins);
+  const bool wide = N > kFusedMaxN;       // P0's coefficient rows for the large clouds' P1
+  w.coef = o;
+  o += wide ? a256(sizeof(float) * n_ov * kActCoef) : 0;
   w.total = o;
   return w;
 }
 
-// The rare stage of the small clouds: one pass (rare_place) or the keys + copy pair
-// (CCMPC_RARE_TWO_PASS=1, the large clouds' form, for measurement)
-// (read per call: a launch costs far more than a getenv, and tests switch it)
-inline bool env_on(const char *name) {
-  const char *e = getenv(name);
-  return e && e[0] == '1';
-}
-
-inline bool rare_two_pass(int64_t N) { return N > kFusedMaxN || env_on("CCMPC_RARE_TWO_PASS"); }
-
-// The small clouds' place kernel: the one-chain form of place_kernel (CCMPC_PLACE_V2=1) or the
-// original sample_place_kernel (reads every group's counts)
-inline bool place_v2() { return env_on("CCMPC_PLACE_V2"); }
+// The rare stage: one pass (rare_place) up to kFusedMaxN, the keys + copy pair above (measured
+// at C2's shape the pair cost 18.2 us against rare_place's 16.7, profiles/r06/README.md)
+inline bool rare_two_pass(int64_t N) { return N > kFusedMaxN; }
 
 // Raise a kernel's dynamic LDS limit above the 48 KiB default when a launch needs it (the
 // attribute is per device: set on every such launch; a failure is reported, not launched)
@@ -1065,45 +1080,34 @@ inline bool lds_fits(Kern k, size_t bytes) {
                              static_cast<int>(bytes)) == hipSuccess;
 }
 
-template <int MODE, int NCH, int NW>
+template <int MODE>
 inline int launch_place(const FusedArgs &a, int64_t n_ov, hipStream_t s) {
-  constexpr int PB = kFP * NCH;
-  constexpr bool PRED = (MODE & 4) != 0, PP = (MODE & 2) != 0;
-  const int T = a.T, gsz = a.L * T * 5;
-  size_t floats;
-  int staged = 0;
-  if (PRED) {
-    floats = static_cast<size_t>(PB) * (2 * T + 1);
-  } else {
-    floats = static_cast<size_t>(2 * T) * PB + (T <= kParSteps ? 2 * (T + 1) * PB : 0);
-    staged = !PP && gsz <= 3200;
-    floats += staged ? gsz : 0;
-  }
+  // four waves: 7 blocks per CU (72 VGPRs, LDS 21 KB), so all 1563 blocks of a 100 000-particle
+  // cloud are resident at once.  The sampler's f64 draws spill 16 VGPRs there (scratch
+  // traffic: the PMC write bytes are ~4x the placement's); two-wave blocks at 80 VGPRs spill
+  // 3 but measured no faster (span 26.0 vs 25.6 us, record path 80.4 vs 77.6 us,
+  // profiles/r06/README.md)
+  constexpr int NW = 4;
+  const int T = a.T;
+  const bool par = T <= kParSteps;
+  const size_t coef = a.coef ? static_cast<size_t>(a.L) * T * 5 : 0;
+  const size_t floats =
+      MODE == kSrcPred ? static_cast<size_t>(kFP) * (2 * T + 1)
+                       : static_cast<size_t>(kFP) * (2 * T + (par ? 2 * T + 2 : 0)) +
+                             std::max(par ? static_cast<size_t>(kFP) * 6 * T : 0, coef);
   const size_t lds = floats * sizeof(float);
-  if (!lds_fits(&place_kernel<MODE, NCH, NW>, lds)) {
+  if (!lds_fits(&place_kernel<MODE, NW>, lds)) {
     set_error("ccmpc_sample_bucket: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     return CCMPC_ERR_LAUNCH;
   }
-  const dim3 grid(static_cast<unsigned>((a.N + PB - 1) / PB), static_cast<unsigned>(n_ov));
-  hipLaunchKernelGGL((place_kernel<MODE, NCH, NW>), grid, dim3(64 * NW), lds, s, a, staged);
+  const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
+  hipLaunchKernelGGL((place_kernel<MODE, NW>), grid, dim3(64 * NW), lds, s, a);
   return CCMPC_OK;
 }
 
-// The block shape: 8 waves for one chain of 64 particles (small clouds: few blocks, each as
-// parallel as it gets); above kFusedMaxN the phases are issue-bound on the f64 draws and headings,
-// so what matters is that every block is resident at once and the CUs get even shares:
-// 4-wave blocks of one chain (1563 blocks at N = 100 000, 7 per CU), or (CCMPC_PLACE_WIDE2=1)
-// 8-wave blocks of two chains (782 blocks, 3 per CU)
-template <int MODE>
-inline int launch_place_w(const FusedArgs &a, int64_t n_ov, hipStream_t s) {
-  if (a.N > kFusedMaxN) {
-    if (env_on("CCMPC_PLACE_WIDE2")) return launch_place<MODE, 2, 8>(a, n_ov, s);
-    return launch_place<MODE, 1, 4>(a, n_ov, s);
-  }
-  return launch_place<MODE, 1, 8>(a, n_ov, s);
-}
-
-// P0 -> P1 -> the rare stage, for either particle source (pred != nullptr: the predictor's)
+// P0 -> P1 -> the rare stage, for either particle source (pred != nullptr: the predictor's).
+// Small sampler clouds: P1 = sample_place_kernel (8-wave blocks, a few per CU); large ones and
+// the predictor's: place_kernel
 inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s) {
   const dim3 zgrid(static_cast<unsigned>(a.nb0), static_cast<unsigned>(n_ov));
   if (a.pred)
@@ -1113,18 +1117,18 @@ inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s) {
   else
     hipLaunchKernelGGL(latent_count_kernel<kZPhilox>, zgrid, dim3(kFThreads), 0, s, a);
   const bool eps = a.eps_in != nullptr;
+  const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
   int rc = CCMPC_OK;
   if (a.pred) {
-    rc = launch_place_w<4>(a, n_ov, s);
-  } else if (a.N > kFusedMaxN || place_v2()) {
+    rc = launch_place<kSrcPred>(a, n_ov, s);
+  } else if (a.N > kFusedMaxN) {
     switch ((pp ? 2 : 0) | (eps ? 1 : 0)) {
-      case 0: rc = launch_place_w<0>(a, n_ov, s); break;
-      case 1: rc = launch_place_w<1>(a, n_ov, s); break;
-      case 2: rc = launch_place_w<2>(a, n_ov, s); break;
-      default: rc = launch_place_w<3>(a, n_ov, s); break;
+      case 0: rc = launch_place<0>(a, n_ov, s); break;
+      case 1: rc = launch_place<1>(a, n_ov, s); break;
+      case 2: rc = launch_place<2>(a, n_ov, s); break;
+      default: rc = launch_place<3>(a, n_ov, s); break;
     }
   } else {
-    const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
 #define CCMPC_FUSED(PP, EPSIN) \
   hipLaunchKernelGGL((sample_place_kernel<PP, EPSIN>), grid, dim3(kFThreads), 0, s, a)
     switch ((pp ? 2 : 0) | (eps ? 1 : 0)) {
@@ -1161,6 +1165,7 @@ inline void fused_args_ws(FusedArgs &a, const FusedWs &L, void *workspace) {
   a.rstore = reinterpret_cast<float *>(ws + L.rstore);
   a.kbuf = reinterpret_cast<int32_t *>(ws + L.kbuf);
   a.rhist = reinterpret_cast<int32_t *>(ws + L.rhist);
+  a.coef = nullptr;                      // set by ccmpc_sample_bucket for the per-latent P1
   a.Npad = L.Npad;
   a.G = static_cast<int>(L.G);
   a.nb0 = static_cast<int>(L.nb0);
@@ -1257,6 +1262,8 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
   a.cell_cnt = cell_cnt;
   a.cell_pmf = cell_pmf;
   a.init_center = init_center;
+  if (N > kFusedMaxN && !pp && n_latent * T * 5 <= kActCoef)
+    a.coef = reinterpret_cast<float *>(static_cast<char *>(workspace) + L.coef);
   const int rc = fused_launch(a, n_ov, pp, as_stream(stream));
   if (rc != CCMPC_OK) return rc;
   CCMPC_LAUNCH_CHECK();

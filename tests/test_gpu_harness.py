@@ -14,6 +14,7 @@ Checked per planning step:
     draws), and the QP against the oracle QP on the oracle's records.
 """
 import numpy as np
+import torch
 import pytest
 
 from oracle import ccmpc_oracle as orc
@@ -203,7 +204,8 @@ def test_filter_pmf_reaches_every_stage(gpu):
         assert len(out[0]) == K.sum() * per_cell
 
 
-def _latents_route(gpu, per_particle, device_tensors=False, run_interval=10):
+def _latents_route(gpu, per_particle, device_tensors=False, run_interval=10,
+                   keep_on_device=False):
     """The same scenario with an eval_stg shaped like a real Trajectron++ model (no
     sample_boundary): do_prediction calls generate_vehicle_latents and the step graph takes
     its predictions + z (source='predictions')."""
@@ -218,13 +220,17 @@ def _latents_route(gpu, per_particle, device_tensors=False, run_interval=10):
             return (torch.as_tensor(z, device=gpu), torch.as_tensor(pred, device=gpu), nodes,
                     pdict, lp)
     scen.agent_kwargs["generate_vehicle_latents"] = gvl
+    if keep_on_device:          # the opt-in: generate_vehicle_latents(..., keep_on_device=True)
+        scen.agent_kwargs["keep_predictions_on_device"] = True
     return scen
 
 
-@pytest.mark.parametrize("per_particle,device_tensors", [(False, False), (True, False),
-                                                         (False, True)],
-                         ids=["per_latent", "per_particle", "device_tensors"])
-def test_reference_predictor_output_drives_run_step(gpu, per_particle, device_tensors):
+@pytest.mark.parametrize("per_particle,device_tensors,keep", [
+    (False, False, False), (True, False, False), (False, True, False), (False, False, True),
+    (True, False, True)],
+    ids=["per_latent", "per_particle", "device_tensors", "keep_on_device",
+         "keep_on_device_per_particle"])
+def test_reference_predictor_output_drives_run_step(gpu, per_particle, device_tensors, keep):
     """an eval_stg without sample_boundary takes the reference's route --
     generate_vehicle_latents (prediction.py:19-105) -> the 5-tuple -> make_ovehicles on
     predictions + z (v8ideal/__init__.py:469-505) -> generator -> QP, no sampler in the step
@@ -233,7 +239,7 @@ def test_reference_predictor_output_drives_run_step(gpu, per_particle, device_te
     from ccmpc import step
     a = _scenario(gpu, per_particle)
     a.episode(0)
-    b = _latents_route(gpu, per_particle, device_tensors)
+    b = _latents_route(gpu, per_particle, device_tensors, keep_on_device=keep)
     b.episode(0)
     assert len(a.steps) == len(b.steps) == 10
     for sa, sb in zip(a.steps, b.steps):
@@ -244,6 +250,9 @@ def test_reference_predictor_output_drives_run_step(gpu, per_particle, device_te
         assert sa["angles"].tobytes() == sb["angles"].tobytes()
     keys = [k for k in step._POOL if k[1][9] == "predictions"]
     assert keys, "the predictions-source graphs were not used"
+    if keep or device_tensors:      # the device route: pred_device graphs, no host pack
+        assert any(k[1][10] for k in keys)
+        assert torch.is_tensor(b.steps[0]["sampler"]["predictions"])
 
 
 def test_make_ovehicles_on_the_reference_5_tuple(gpu):

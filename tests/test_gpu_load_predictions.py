@@ -102,20 +102,17 @@ def _pred_scene(O, N, T, L, seed, heavy=False):
     return pred, z, pmf
 
 
-@pytest.mark.parametrize("O,N,T,L,two_pass", [
-    (3, 3000, 8, 6, False), (3, 3000, 8, 6, True), (4, 5000, 8, 25, False),
-    (2, 129, 12, 9, False), (1, 1, 8, 4, False), (2, 700, 40, 9, False),
-    (1, 100_000, 8, 25, False), (2, 20_000, 12, 25, False), (1, 30_000, 40, 9, False),
-    (1, 262_144, 8, 25, False)])
-def test_bucket_predictions_equals_load_then_bucket(gpu, monkeypatch, O, N, T, L, two_pass):
+@pytest.mark.parametrize("O,N,T,L", [
+    (3, 3000, 8, 6), (4, 5000, 8, 25), (2, 129, 12, 9), (1, 1, 8, 4), (2, 700, 40, 9),
+    (1, 100_000, 8, 25), (2, 20_000, 12, 25), (1, 30_000, 40, 9), (3, 8_193, 8, 25),
+    (1, 262_144, 8, 25)])
+def test_bucket_predictions_equals_load_then_bucket(gpu, O, N, T, L):
     """ccmpc_bucket_predictions (one placement pass: the predictor's coordinates written
     straight into the cells, the rare ones through a rare list) holds in every cell exactly the
     particles of ccmpc_load_predictions + ccmpc_bucket, in the same order, with the same pmf and
     centre bits; only the cell offsets differ.  Rows gathered with the ego's node skipped, both
     rare-stage forms (one pass <= 8192 particles, keys + copy above), ragged N."""
     from ccmpc import engine
-    if two_pass:
-        monkeypatch.setenv("CCMPC_RARE_TWO_PASS", "1")
     pred, z, pmf = _pred_scene(O + 1, N, T, L, N + T, heavy=N == 30_000)
     rows = list(range(1, O + 1))
     minpos = np.tile([150.0, -120.0], (O, 1))

@@ -92,7 +92,7 @@ def _assert_same(got, want):
     (2, 25, 8, 8_193, 28, 1),        # the first wide N, one kept mode
     (1, 25, 8, 262_144, 29, None),   # the largest
 ])
-def test_fused_equals_sampler_then_bucketing(gpu, monkeypatch, O, L, T, N, seed, kept):
+def test_fused_equals_sampler_then_bucketing(gpu, O, L, T, N, seed, kept):
     from ccmpc import engine as e
     init, pmf, gmm = _inputs(O, L, T, seed, kept)
     minpos = np.tile([150.0, -120.0], (O, 1))
@@ -100,13 +100,6 @@ def test_fused_equals_sampler_then_bucketing(gpu, monkeypatch, O, L, T, N, seed,
     zf, *got = e.sample_bucket(init, pmf, gmm, N, T, minpos, seed=seed, device=gpu, with_z=True)
     np.testing.assert_array_equal(zf.cpu().numpy(), z2.cpu().numpy())
     _assert_same(got, want)
-    if N <= 8192 and N in (5000, 4097, 700, 3000):
-        # the small clouds' alternative forms (place_kernel's one-chain form, the keys + copy
-        # rare stage) give the same cells
-        for env in ("CCMPC_PLACE_V2", "CCMPC_RARE_TWO_PASS"):
-            monkeypatch.setenv(env, "1")
-            _assert_same(e.sample_bucket(init, pmf, gmm, N, T, minpos, seed=seed, device=gpu),
-                         want)
 
 
 @pytest.mark.parametrize("N", [5000, 30_000])

@@ -163,12 +163,15 @@ def test_per_particle_particle_minor_input_is_used_in_place(gpu):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
-def test_reference_particle_count_nonfused_graph_step(gpu):
-    """C1's real particle count (100 000 per OV, params.py:377): the graph's non-fused branch
-    (sampler -> ccmpc_bucket inside the graph), two frames through one graph equal to the eager
-    calls, and frame 0 against the oracle (records, L4)."""
+@pytest.mark.parametrize("N", [100_000, 300_000])
+def test_reference_particle_count_graph_step(gpu, N):
+    """C1's real particle count (100 000 per OV, params.py:377): the graph's one-pass placement
+    (ccmpc_sample_bucket: natives straight into their cells, rare particles keyed then copied),
+    two frames through one graph equal to the eager calls (sampler -> ccmpc_bucket), and frame 0
+    against the oracle (records, L4); above 262 144 particles the graph's sampler ->
+    ccmpc_bucket branch."""
     from ccmpc import episode, planner
-    O, N = 1, 100_000
+    O = 1
     init, pmf, gmm, minpos, pasts, K, eps_ura = _scene_inputs(O, seed=20251015)
     ag = planner.MidlevelAgent(prediction_horizon=PH, device=gpu)
     ae = planner.MidlevelAgent(prediction_horizon=PH, device=gpu)
@@ -181,15 +184,17 @@ def test_reference_particle_count_nonfused_graph_step(gpu):
                               _ref(frame), gpu)
         _same(out_g, out_e, ovs_g, ovs_e, K)
         if frame == 0:
-            _oracle_check(ovs_g, out_g, pasts, _ref(frame), K)
+            if N == 100_000:
+                _oracle_check(ovs_g, out_g, pasts, _ref(frame), K)
     g = next(iter(ag._graphs.values()))
-    assert not g.fused
+    assert g.fused == (N <= 262_144)
     assert sum(len(p) for p in ovs_g[0].pred_positions) == N
 
 
-def test_reference_particle_count_per_particle_nonfused(gpu):
-    """The same count in the per-particle mode (4 OVs x 20 000 = the non-fused branch with
-    device-side z / parameters / noise) against the eager calls."""
+def test_reference_particle_count_per_particle(gpu):
+    """The same count in the per-particle mode (4 OVs x 20 000: the large clouds' placement --
+    the actions kernel on device-side z / parameters / noise, then the placement) against the
+    eager calls."""
     from ccmpc import episode, planner
     O, N = 4, 20_000
     init, pmf, gmm, minpos, pasts, K, eps_ura = _scene_inputs(O, seed=99)
@@ -204,7 +209,7 @@ def test_reference_particle_count_per_particle_nonfused(gpu):
     ovs_e, out_e = _eager(ae, init, pmf, pp, N, 0, minpos, pasts, params, eps_ura, _ref(0),
                           gpu, z=z, eps=eps, pp=True)
     _same(out_g, out_e, ovs_g, ovs_e, K)
-    assert not next(iter(ag._graphs.values())).fused
+    assert next(iter(ag._graphs.values())).fused
 
 
 def test_stale_frame_reads_raise(gpu):
@@ -289,7 +294,7 @@ def test_kept_mode_without_draws_fails_like_the_reference(gpu):
 def test_predictions_source_at_the_reference_particle_count(gpu, as_tensors):
     """generate_vehicle_latents' 5-tuple at C1's 100 000 particles per OV (with an ego node in
     row 0, as the reference's batch has it): the step graph built with source='predictions'
-    (ccmpc_load_predictions -> ccmpc_bucket -> cycle) gives the records, moments and
+    (ccmpc_bucket_predictions -> cycle) gives the records, moments and
     per-cell counts of the sampler route's graph on the same particles, frame after frame, and
     of the shrinking (ideal) and receding (affine) kinds."""
     from ccmpc import engine, episode, planner
@@ -320,4 +325,4 @@ def test_predictions_source_at_the_reference_particle_count(gpu, as_tensors):
         assert np.array(b.last_records).tobytes() == rec_a, (frame, kind)
         np.testing.assert_array_equal(np.asarray(out_a[6][0][0]), np.asarray(out_b[6][0][0]))
     g = [g for k, g in b._graphs.items() if "predictions" in k]
-    assert g and all(x.source == "predictions" and not x.fused for x in g)
+    assert g and all(x.source == "predictions" and x.fused for x in g)   # one placement pass

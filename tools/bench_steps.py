@@ -27,6 +27,9 @@ def main():
         "dropin_pred": lambda: bench.dropin_step_predictions(dev),
         "dropin_pred_100k": lambda: bench.dropin_step_predictions(dev, steps=100, O=1,
                                                                   N=100_000, n_sets=4),
+        "dropin_pred_dev": lambda: bench.dropin_step_predictions(dev, on_device=True),
+        "dropin_pred_100k_dev": lambda: bench.dropin_step_predictions(
+            dev, steps=100, O=1, N=100_000, n_sets=4, on_device=True),
         "episode": lambda: bench.episode_c1(dev, with_cpu=False),
         "harness": lambda: bench.harness_episode(dev),
     }
