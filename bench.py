@@ -629,6 +629,9 @@ def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8, on_devi
         _, out = one(i)
         ts.append(time.perf_counter() - t0)
     g = next(iter(agent._graphs.values()))
+    t_graph = time_graph_replay(g, dev)
+    cfg = ("step_pred_" + ("dev_" if on_device else "") +
+           ("c2" if (O, N) == (4, 5000) else "100k" if (O, N) == (1, 100_000) else "x"))
     where = ("device tensors (keep_on_device) copied device to device" if on_device else
              "host numpy predictions / z in the pinned pack")
     return {"config": f"drop-in step on generate_vehicle_latents' 5-tuple: {O} OVs (+ the "
@@ -639,8 +642,9 @@ def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8, on_devi
             "input_pack_bytes": int(g.inp.nbytes),
             "dropin_step_us_median": round(statistics.median(ts) * 1e6, 1),
             "dropin_step_us_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
-            "graph_replay_us": round(time_graph_replay(g, dev) * 1e6, 1),
-            "record_path_latency_us": round(time_record_path(g, dev) * 1e6, 1)}
+            "graph_replay_us": round(t_graph * 1e6, 1),
+            "record_path_latency_us": round(time_record_path(g, dev) * 1e6, 1),
+            "roofline": step_roofline(g, t_graph, cfg, predictions=True)}
 
 
 def v8_milp(dev, with_cpu=True, seeds=range(20, 28), T=8, O=2):
@@ -827,6 +831,9 @@ def dropin_step(dev, steps=300, with_cpu=True, O=4, N=5000, ph=8, per_particle=F
            "dropin_step_us_p90": round(float(np.percentile(ts, 90)) * 1e6, 1),
            "graph_replay_us": round(t_graph * 1e6, 1),
            "record_path_latency_us": round(t_rec * 1e6, 1),
+           "roofline": step_roofline(g, t_graph, None if per_particle else (
+               "step_c2" if (O, N) == (4, 5000) else
+               "step_c1_100k" if (O, N) == (1, 100_000) else None)),
            "eager_calls_step_us_median": round(statistics.median(te) * 1e6, 1),
            "note": "wall clock per call on the host, host inputs from host memory (per-particle "
                    "tensors: device-to-device copies inside the step), outputs (records, "
@@ -894,6 +901,43 @@ def time_record_path(g, dev, n=200):
         ts.append(time.perf_counter() - t0)
     torch.cuda.synchronize(dev)
     return statistics.median(ts)
+
+
+def step_roofline(g, t_graph, config, predictions=False):
+    """The planning step's roofline: ALGORITHMIC bytes per step over the graph's replay time
+    (HIP events, both branches).  Per particle (T = ph steps, f32 positions): the placement's
+    write of the bucketed store (8 T B), the cycle's read (8 T), the L4 passes' two reads
+    (16 T) and the latent id written and read (8) = 32 T + 8 B; the predictor's route adds its
+    input, the predictions and z read once (8 T + 8).  `traffic` = the HBM bytes per step of
+    every kernel of the step from the committed PMC summary of this configuration
+    (profiles/r*/configs/<config>_summary.json, tools/step_replay.py under
+    profiles/collect_configs.sh: FETCH_SIZE x2 + WRITE_SIZE, each kernel weighted by its calls
+    per step), with the kernels' summed time per step beside it."""
+    T, n = g.ph, g.O * g.N
+    alg = n * (32 * T + 8 + ((8 * T + 8) if predictions else 0))
+    out = {"bound": "hbm", "alg_bytes_per_step": alg, "graph_us": round(t_graph * 1e6, 2),
+           "achieved": round(alg / t_graph / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+           "frac": round(alg / t_graph / HBM_PEAK, 5), "traffic": None,
+           "formula": "particles x (32 T + 8)" + (" + particles x (8 T + 8)" if predictions
+                                                   else "")}
+    rounds = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))
+    for rdir in reversed(rounds):
+        path = os.path.join(rdir, "configs", f"{config}_summary.json")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            summ = json.load(f)
+        steps = max((d.get("calls", 0) for k, d in summ.items()
+                     if k.startswith("void ccmpc::latent_count_kernel")), default=0)
+        if not steps:
+            break
+        b = sum(d.get("hbm_bytes_avg", 0.0) * d.get("calls", 0) / steps for d in summ.values())
+        busy = sum(d.get("avg_ns", 0.0) * d.get("calls", 0) / steps for d in summ.values())
+        out.update(traffic=int(b), counter_over_alg=round(b / alg, 3),
+                   kernel_us_per_step=round(busy / 1e3, 2),
+                   traffic_source=os.path.relpath(path, ROOT))
+        break
+    return out
 
 
 def pmc_traffic(kernel_prefix, config=None):
