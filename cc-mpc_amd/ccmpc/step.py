@@ -258,6 +258,9 @@ class StepGraph:
         O4 = -(-O // 4) * 4               # (16-byte copies)
         if source == "predictions":       # zeroed on the device by every copy-in
             gmm_field += [("zbad0", (O4,), i32)]
+        if source == "predictions" and self.pred_device:
+            # the addresses of this launch's predictions / z (ccmpc_bucket_predictions_indirect)
+            gmm_field += [("pptr", (2,), i64)]
         fields = ([("gen", (2,), i64), ("seed", (1,), i64), ("init", (O, 4), f64),
                    ("cdf", (O, L_), f64)] + gmm_field +
                   [("keep", (O, L_), i32), ("nk", (O,), i32), ("base", (O,), i32),
@@ -283,6 +286,7 @@ class StepGraph:
                 self.pp_eps = torch.zeros((O, ph_, 2, N), dtype=f32, device=self.device)
         self.pr_pred = self.pr_z = None
         self._rows_idx = None                 # set_predictions' cached device row index
+        self._held = None                     # the predictor's tensors the next launch reads
         if source == "predictions" and self.pred_device:
             self.pr_pred = torch.zeros((O, N, ph_, 2), dtype=f32, device=self.device)
             self.pr_z = torch.zeros((O, N), dtype=i64, device=self.device)
@@ -386,13 +390,14 @@ class StepGraph:
         else:
             gmm, layout, z_in, eps = p(i.d("gmm")), _lib.GMM_PER_LATENT, None, None
         if self.fused and self.source == "predictions":
-            pred, z = ((self.pr_pred, self.pr_z) if self.pred_device
-                       else (i.d("pred"), i.d("zin")))
-            return [(lib.ccmpc_bucket_predictions, (
-                p(pred), p(z), 8, None, O, N, T, L, p(i.d("keep")), p(i.d("nk")), p(i.d("base")),
-                self.max_k, p(i.d("minpos")), p(i.d("region")), p(ws), ws.numel(), p(st.pos),
-                st.ld, p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")), p(o.d("centre")),
-                p(o.d("zbad")), s))]
+            tail = (O, N, T, L, p(i.d("keep")), p(i.d("nk")), p(i.d("base")), self.max_k,
+                    p(i.d("minpos")), p(i.d("region")), p(ws), ws.numel(), p(st.pos), st.ld,
+                    p(o.d("off")), p(o.d("cnt")), p(o.d("pmf")), p(o.d("centre")),
+                    p(o.d("zbad")), s)
+            if self.pred_device:        # the tensors' addresses travel in the input pack
+                return [(lib.ccmpc_bucket_predictions_indirect, (p(i.d("pptr")), 8, None) + tail)]
+            return [(lib.ccmpc_bucket_predictions, (p(i.d("pred")), p(i.d("zin")), 8, None) +
+                     tail)]
         if self.fused:
             return [(lib.ccmpc_sample_bucket, (
                 p(i.d("init")), p(i.d("cdf")), L, gmm, layout, z_in, eps,
@@ -658,9 +663,21 @@ class StepGraph:
         if dev:
             if predictions.device != self.device or z.device != self.device:
                 raise ValueError("predictions / z must be on the graph's device")
-            if rows == list(range(rows[0], rows[0] + O)) if O else True:
-                # the OVs are one run of nodes (the ego's row first or last): a view, one
-                # device-to-device copy each, nothing uploaded
+            run = rows == list(range(rows[0], rows[0] + O)) if O else True
+            if (self.fused and run and predictions.dtype == torch.float32 and
+                    z.dtype == torch.int64 and
+                    predictions.is_contiguous() and z.is_contiguous()):
+                # the OVs are one run of nodes (the ego's row first or last) of tensors in the
+                # kernels' layout: the launch reads them in place -- their addresses go into
+                # the input pack, nothing is copied (held until the next set_predictions; the
+                # caller reads the outputs before that)
+                r0 = rows[0] if O else 0
+                pv, zv = predictions[r0:r0 + O], z[r0:r0 + O]
+                self.inp.h("pptr")[:] = (pv.data_ptr(), zv.data_ptr())
+                self._held = (predictions, z)
+                return
+            if run:
+                # a view, one device-to-device copy each (converting), nothing uploaded
                 self.pr_pred.copy_(predictions[rows[0]:rows[0] + O])
                 self.pr_z.copy_(z[rows[0]:rows[0] + O])
             else:
@@ -670,6 +687,8 @@ class StepGraph:
                 idx = self._rows_idx[1]
                 torch.index_select(predictions.to(torch.float32), 0, idx, out=self.pr_pred)
                 torch.index_select(z.to(torch.int64), 0, idx, out=self.pr_z)
+            self.inp.h("pptr")[:] = (self.pr_pred.data_ptr(), self.pr_z.data_ptr())
+            self._held = None
             return
         hp, hz = self.inp.h("pred"), self.inp.h("zin")
         for o, r in enumerate(rows):             # straight into the pinned pack, no temporary

@@ -113,6 +113,7 @@ struct FusedArgs {
   const void *zsrc;
   int z_bytes;
   const int32_t *rows;
+  const uint64_t *ptrs;  // or in device memory: {pred, z} addresses, read at run time
   // bucketing (bucket.hip)
   const int32_t *keep_map, *n_kept, *cell_base;
   int max_k;
@@ -185,8 +186,9 @@ __global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
     z = z < 0 ? 0 : (z >= L ? L - 1 : z);
   } else if (ZSRC == kZPred && v) {
     const int64_t e = (a.rows ? static_cast<int64_t>(a.rows[o]) : o) * N + i;
-    int64_t zz = a.z_bytes == 8 ? static_cast<const int64_t *>(a.zsrc)[e]
-                                : static_cast<int64_t>(static_cast<const int32_t *>(a.zsrc)[e]);
+    const void *zp = a.ptrs ? reinterpret_cast<const void *>(a.ptrs[1]) : a.zsrc;
+    int64_t zz = a.z_bytes == 8 ? static_cast<const int64_t *>(zp)[e]
+                                : static_cast<int64_t>(static_cast<const int32_t *>(zp)[e]);
     if (zz < 0 && zz >= -L) zz += L;
     bad = zz < 0 || zz >= L;
     z = bad ? 0 : static_cast<int>(zz);
@@ -479,7 +481,8 @@ __global__ __launch_bounds__(64 * NW, 7) void place_kernel(FusedArgs a) {
   float *coef_s = terms;   // [L T 5] when staged: read only before the terms are written
   if (PRED) {
     const int64_t row = a.rows ? static_cast<int64_t>(a.rows[o]) : o;
-    const float *src = a.pred + (row * N + i0) * W;
+    const float *pp = a.ptrs ? reinterpret_cast<const float *>(a.ptrs[0]) : a.pred;
+    const float *src = pp + (row * N + i0) * W;
     for (int e = tid; e < n * W; e += NTH) {
       const int p = e / W;
       dyn[p * S + (e - p * W)] = src[e];
@@ -1270,16 +1273,15 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
   return CCMPC_OK;
 }
 
-extern "C" int ccmpc_bucket_predictions(const float *pred, const void *z, int z_bytes,
-                                        const int32_t *rows, int64_t n_ov, int64_t N, int64_t T,
-                                        int64_t n_latent, const int32_t *keep_map,
-                                        const int32_t *n_kept, const int32_t *cell_base,
-                                        int64_t max_k, const double *minpos,
-                                        const int64_t *region, void *workspace,
-                                        size_t workspace_bytes, float *pos_out, int64_t ld_out,
-                                        int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
-                                        double *init_center, int32_t *z_bad,
-                                        ccmpc_stream_t stream) {
+static int bucket_predictions_impl(const float *pred, const void *z, const uint64_t *ptrs,
+                                   int z_bytes, const int32_t *rows, int64_t n_ov, int64_t N,
+                                   int64_t T, int64_t n_latent, const int32_t *keep_map,
+                                   const int32_t *n_kept, const int32_t *cell_base,
+                                   int64_t max_k, const double *minpos, const int64_t *region,
+                                   void *workspace, size_t workspace_bytes, float *pos_out,
+                                   int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,
+                                   double *cell_pmf, double *init_center, int32_t *z_bad,
+                                   ccmpc_stream_t stream) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
   CCMPC_REQUIRE(N >= 1 && N <= kWideMaxN, "N must be in [1, 262144] (ccmpc_load_predictions + "
@@ -1289,8 +1291,8 @@ extern "C" int ccmpc_bucket_predictions(const float *pred, const void *z, int z_
                 "max_k out of range");
   CCMPC_REQUIRE(n_ov >= 0 && n_ov < 65536, "bad n_ov");
   if (n_ov == 0) return CCMPC_OK;
-  CCMPC_REQUIRE(pred && z && keep_map && n_kept && cell_base && minpos && region && pos_out &&
-                    cell_off && cell_cnt && cell_pmf && init_center,
+  CCMPC_REQUIRE(((pred && z) || ptrs) && keep_map && n_kept && cell_base && minpos && region &&
+                    pos_out && cell_off && cell_cnt && cell_pmf && init_center,
                 "null pointer");
   CCMPC_REQUIRE(ld_out >= 1 && ld_out * 2 * T < (int64_t(1) << 40), "bad ld_out");
   const FusedWs L = fused_ws(n_ov, N, T, max_k);
@@ -1299,8 +1301,9 @@ extern "C" int ccmpc_bucket_predictions(const float *pred, const void *z, int z_
     return CCMPC_ERR_WORKSPACE;
   }
   FusedArgs a = {};
-  a.pred = pred;
+  a.pred = ptrs ? reinterpret_cast<const float *>(ptrs) : pred;  // (non-null: the source)
   a.zsrc = z;
+  a.ptrs = ptrs;
   a.z_bytes = z_bytes;
   a.rows = rows;
   a.L = static_cast<int>(n_latent);
@@ -1324,4 +1327,38 @@ extern "C" int ccmpc_bucket_predictions(const float *pred, const void *z, int z_
   if (rc != CCMPC_OK) return rc;
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
+}
+
+extern "C" int ccmpc_bucket_predictions(const float *pred, const void *z, int z_bytes,
+                                        const int32_t *rows, int64_t n_ov, int64_t N, int64_t T,
+                                        int64_t n_latent, const int32_t *keep_map,
+                                        const int32_t *n_kept, const int32_t *cell_base,
+                                        int64_t max_k, const double *minpos,
+                                        const int64_t *region, void *workspace,
+                                        size_t workspace_bytes, float *pos_out, int64_t ld_out,
+                                        int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
+                                        double *init_center, int32_t *z_bad,
+                                        ccmpc_stream_t stream) {
+  return bucket_predictions_impl(pred, z, nullptr, z_bytes, rows, n_ov, N, T, n_latent, keep_map,
+                                 n_kept, cell_base, max_k, minpos, region, workspace,
+                                 workspace_bytes, pos_out, ld_out, cell_off, cell_cnt, cell_pmf,
+                                 init_center, z_bad, stream);
+}
+
+extern "C" int ccmpc_bucket_predictions_indirect(const uint64_t *ptrs, int z_bytes,
+                                                 const int32_t *rows, int64_t n_ov, int64_t N,
+                                                 int64_t T, int64_t n_latent,
+                                                 const int32_t *keep_map, const int32_t *n_kept,
+                                                 const int32_t *cell_base, int64_t max_k,
+                                                 const double *minpos, const int64_t *region,
+                                                 void *workspace, size_t workspace_bytes,
+                                                 float *pos_out, int64_t ld_out,
+                                                 int64_t *cell_off, int64_t *cell_cnt,
+                                                 double *cell_pmf, double *init_center,
+                                                 int32_t *z_bad, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(ptrs, "null ptrs");
+  return bucket_predictions_impl(nullptr, nullptr, ptrs, z_bytes, rows, n_ov, N, T, n_latent,
+                                 keep_map, n_kept, cell_base, max_k, minpos, region, workspace,
+                                 workspace_bytes, pos_out, ld_out, cell_off, cell_cnt, cell_pmf,
+                                 init_center, z_bad, stream);
 }

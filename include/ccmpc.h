@@ -436,6 +436,19 @@ int ccmpc_bucket_predictions(const float *pred, const void *z, int z_bytes, cons
                              float *pos_out, int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,
                              double *cell_pmf, double *init_center, int32_t *z_bad,
                              ccmpc_stream_t stream);
+/* The same with the predictor's tensors named at RUN time: ptrs (device memory, e.g. a field of
+ * a captured graph's input pack) holds the addresses {pred, z} of that launch's tensors, so a
+ * graph captured once reads each frame's predictor output in place (no device-to-device copy
+ * into buffers of its own).  The tensors must stay alive until the launch's outputs are read. */
+int ccmpc_bucket_predictions_indirect(const uint64_t *ptrs, int z_bytes, const int32_t *rows,
+                                      int64_t n_ov, int64_t N, int64_t T, int64_t n_latent,
+                                      const int32_t *keep_map, const int32_t *n_kept,
+                                      const int32_t *cell_base, int64_t max_k,
+                                      const double *minpos, const int64_t *region,
+                                      void *workspace, size_t workspace_bytes, float *pos_out,
+                                      int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,
+                                      double *cell_pmf, double *init_center, int32_t *z_bad,
+                                      ccmpc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Headings, bounding-box vertices and L4 outer approximation for every (cell, t).

@@ -326,3 +326,38 @@ def test_predictions_source_at_the_reference_particle_count(gpu, as_tensors):
         np.testing.assert_array_equal(np.asarray(out_a[6][0][0]), np.asarray(out_b[6][0][0]))
     g = [g for k, g in b._graphs.items() if "predictions" in k]
     assert g and all(x.source == "predictions" and x.fused for x in g)   # one placement pass
+
+
+def test_device_predictions_read_in_place_or_copied(gpu):
+    """A pred_device graph reads the predictor's tensors in place when the OVs are one run of
+    nodes in the kernels' layout (float32 predictions, int64 z: their addresses travel in the
+    input pack, ccmpc_bucket_predictions_indirect), and copies them into its own buffers
+    otherwise (rows out of order, int32 z); both give the host-array route's records."""
+    import torch
+    from ccmpc import engine, episode, planner
+    O, N = 2, 3000
+    init, pmf, gmm, minpos, pasts, K, eps_ura = _scene_inputs(O, seed=77)
+    z, store = engine.sample_unicycle(init, pmf, gmm, N, PH, seed=5, device=gpu)
+    pred = torch.zeros((4, N, PH, 2), dtype=torch.float32, device=gpu)
+    Z = torch.zeros((4, N), dtype=torch.int64, device=gpu)
+    for o, r in enumerate((1, 2)):                  # nodes 1 and 2: a run
+        off = store.offsets[o]
+        pred[r] = store.pos[:, off:off + N].reshape(PH, 2, N).permute(2, 0, 1)
+        Z[r] = z[o].to(torch.int64)
+    perm = [3, 0]                                   # the same OVs at nodes 3 and 0: no run
+    pred2, Z2 = pred.clone(), Z.clone()
+    pred2[3], pred2[0], Z2[3], Z2[0] = pred[1], pred[2], Z[1], Z[2]
+    params = episode.Params(O, K, 0)
+    recs = []
+    for P, ZZ, rows in ((pred.cpu().numpy(), Z.cpu().numpy(), [1, 2]), (pred, Z, [1, 2]),
+                        (pred2, Z2.to(torch.int32), perm)):
+        ag = planner.MidlevelAgent(prediction_horizon=PH, device=gpu)
+        s = dict(source="predictions", predictions=P, z=ZZ, rows=rows, latent_pmf=pmf, N=N)
+        for _ in range(3):                          # eager, capture, replay
+            ag.predict_and_constrain(params, s, eps_ura, PH, _ref(0), minpos, pasts)
+        recs.append(np.array(ag.last_records).tobytes())
+        g = next(iter(ag._graphs.values()))
+        if torch.is_tensor(P):
+            in_place = rows == [1, 2]
+            assert (g._held is not None) == in_place
+    assert recs[0] == recs[1] == recs[2]
