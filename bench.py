@@ -1198,6 +1198,12 @@ def main():
             # the reference's real particle count at the "np5000" label (params.py:377)
             out["episode_c1_np100k"] = episode_c1(dev, with_cpu=False, N=100_000)
             out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
+            # one frame's QP (the reference solves one per planning step) at T = 8 and at C4's
+            # horizon T = 12 (n = 24 > 16: the four-wave interior point), and the T = 12 batch
+            out["planning_qp_single_t8"] = planning_qp(dev, args.seed, scenes=1, with_cpu=False)
+            out["planning_qp_single_t12"] = planning_qp(dev, args.seed, scenes=1, T=12,
+                                                        with_cpu=False)
+            out["planning_qp_t12"] = planning_qp(dev, args.seed, T=12, with_cpu=False)
             out["v8_milp"] = v8_milp(dev, with_cpu=not args.no_cpu)
     if not args.no_sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)

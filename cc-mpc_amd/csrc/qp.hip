@@ -143,6 +143,8 @@ struct QpArgs {
   int gi_max_steps;   // the active-set step budget (< 0: 8 (n + 16)); a test hook forces the
                       // hand-over to the IPM with 0
   int fallback_only;  // the IPM pass after an active-set-only launch (kQpNeedIpm scenes only)
+  int gi_nostep;      // GI's "no step exists" verdict: 0 kept, 1 always confirmed by the IPM,
+                      // 2 kept when it is certain (the default; see gi_solve)
   int64_t max_cells;
   double tol, early;  // early: the early polish threshold on mu / max(mu0, 1) (0 = none)
   const double *gamma, *xbar, *ubar, *u_prev, *goal, *ref;
@@ -1653,10 +1655,25 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
                   ? __ffsll(static_cast<long long>(__ballot(lane < q && ratio == t1))) - 1
                   : -1;
           const double t2 = zero_step ? INFINITY : -sp / d2;
-          // no step exists: the rows look infeasible.  That test rests on round-off-sensitive
-          // comparisons (zero_step, rk > 0) which near-parallel rows of several cells at one t
-          // can tip, so the verdict is the IPM's: it confirms infeasibility or finds the point
-          if (!(t1 < INFINITY) && !(t2 < INFINITY)) return give_up();
+          // no step exists: the entering row's normal lies in the span of the active normals
+          // (d2 ~ 0) with coefficients r <= 0, and the row is violated at a point where every
+          // active row holds -- a Farkas certificate that the rows are infeasible (the
+          // reference's solve failure): any z meeting the active rows has m.z <= sum_j r_j
+          // beta_j = beta + sp < beta.  Its tests compare against round-off scales (zero_step,
+          // rk > 0), which near-parallel rows of several cells at one t can tip;
+          // an entry r_j ~ 0 of the wrong sign moves m.z by |r_j| |n_j . z| only, so the
+          // verdict is kept when the entering row's violation is far above that scale (1e-6 of
+          // its gradient's norm), and a marginal one is handed to the IPM, which confirms it
+          // or finds the point
+          if (!(t1 < INFINITY) && !(t2 < INFINITY)) {
+            const double viol = -sp * inorm[pr];
+            const bool certain = viol > 1e-6;
+            if (A.gi_nostep == 1 || (A.gi_nostep == 2 && !certain)) return give_up();
+            status = CCMPC_QP_MAXITER;
+            infeasible = true;
+            it = steps;
+            return true;
+          }
           GI_ACC(2);
           const double t = fmin(t1, t2);
           wave_sync();
@@ -2305,6 +2322,8 @@ static int mpc_qp_impl(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T, int
   {
     const char *e = getenv("CCMPC_QP_GI_MAX_STEPS");  // per call (test hook)
     a.gi_max_steps = e ? atoi(e) : -1;
+    const char *ns = getenv("CCMPC_QP_GI_NOSTEP");    // per call (A/B and tests)
+    a.gi_nostep = ns ? atoi(ns) : 2;
   }
   {
     const char *e = getenv("CCMPC_QP_EARLY_POLISH");  // per call (a test switches it)
@@ -2362,11 +2381,10 @@ static int mpc_qp_impl(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T, int
   // 488 VGPRs, far fewer SGPR spills), then an IPM pass that solves only the scenes it handed
   // over -- the IPM's own answer, byte for byte, as the combined instance's hand-over gives;
   // a single scene keeps the combined instance (the second launch would cost it more)
-  static const bool split_env = [] {
-    const char *e = getenv("CCMPC_QP_GI_SPLIT");
-    return !(e && e[0] == '0');
-  }();
-  if (gi && n_scenes > 1 && split_env) {
+  // (CCMPC_QP_GI_SPLIT: 0 never, 1 batches -- the default --, 2 a single scene too)
+  const char *se = getenv("CCMPC_QP_GI_SPLIT");
+  const int split_env = se ? atoi(se) : 1;
+  if (gi && split_env > 0 && (n_scenes > 1 || split_env > 1)) {
     attr = in_lds ? launch_qp<true, 16, 1, true, true>(grid, lds, s, a)
                   : launch_qp<false, 16, 1, true, true>(grid, lds, s, a);
     if (attr == hipSuccess) {

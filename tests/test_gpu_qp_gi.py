@@ -92,6 +92,10 @@ def test_gi_hands_over_to_the_ipm(gpu, monkeypatch):
     goal = torch.as_tensor(goals, device=gpu)
     ref = torch.as_tensor(refs, device=gpu)
 
+    # every infeasibility verdict through the IPM here (CCMPC_QP_GI_NOSTEP=1), so that "GI
+    # finished" is exactly "GI solved it"
+    monkeypatch.setenv("CCMPC_QP_GI_NOSTEP", "1")
+
     def run(method, steps=None):
         monkeypatch.setenv("CCMPC_QP_METHOD", method)
         if steps is None:
@@ -104,7 +108,7 @@ def test_gi_hands_over_to_the_ipm(gpu, monkeypatch):
 
     ipm = run("ipm")
     gi = run("gi")
-    gi_done = (gi[3] == mpc.QP_OK)   # an infeasible verdict is the IPM's (give_up)
+    gi_done = (gi[3] == mpc.QP_OK)
     handed_mid = 0
     for budget in (0, 1, 2, 3):
         forced = run("gi", budget)
@@ -130,7 +134,8 @@ def test_gi_verdict_on_near_parallel_rows(gpu, monkeypatch):
     by 1e-9 (near-duplicate, near-parallel rows at every step, what several cells' tangents at
     one t can give): GI and the IPM must return the same verdict on every scene and the same
     minimiser where it exists.  GI's own 'no step exists' test rests on round-off-sensitive
-    comparisons, so that verdict is handed to the IPM to confirm."""
+    comparisons, so a marginal verdict is handed to the IPM to confirm; the test
+    runs both that default and every verdict through the IPM."""
     from ccmpc import _lib
     T = 8
     seeds = list(range(100, 132))
@@ -153,11 +158,13 @@ def test_gi_verdict_on_near_parallel_rows(gpu, monkeypatch):
     k = mpc.REC_HALFSPACE
     u0, _, c0, s0, _ = _solve(monkeypatch, "ipm", cps2, T, k, mpc.U_ORDER_F, gamma, xbar, g_t,
                               r_t, rec2)
-    u1, _, c1, s1, _ = _solve(monkeypatch, "gi", cps2, T, k, mpc.U_ORDER_F, gamma, xbar, g_t,
-                              r_t, rec2)
-    np.testing.assert_array_equal(s1, s0)
-    ok = s0 == mpc.QP_OK
-    assert ok.sum() >= 4
-    for i in np.flatnonzero(ok):
-        tol = 1e-6 * (1.0 + np.abs(u0[i]).max())
-        assert np.abs(u1[i] - u0[i]).max() <= tol, (seeds[i], np.abs(u1[i] - u0[i]).max())
+    for policy in ("2", "1"):
+        monkeypatch.setenv("CCMPC_QP_GI_NOSTEP", policy)
+        u1, _, c1, s1, _ = _solve(monkeypatch, "gi", cps2, T, k, mpc.U_ORDER_F, gamma, xbar,
+                                  g_t, r_t, rec2)
+        np.testing.assert_array_equal(s1, s0)
+        ok = s0 == mpc.QP_OK
+        assert ok.sum() >= 4 and (~ok).sum() >= 1
+        for i in np.flatnonzero(ok):
+            tol = 1e-6 * (1.0 + np.abs(u0[i]).max())
+            assert np.abs(u1[i] - u0[i]).max() <= tol, (seeds[i], np.abs(u1[i] - u0[i]).max())

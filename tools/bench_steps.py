@@ -30,6 +30,10 @@ def main():
         "dropin_pred_dev": lambda: bench.dropin_step_predictions(dev, on_device=True),
         "dropin_pred_100k_dev": lambda: bench.dropin_step_predictions(
             dev, steps=100, O=1, N=100_000, n_sets=4, on_device=True),
+        "qp": lambda: bench.planning_qp(dev, 0, with_cpu=False),
+        "qp1_t8": lambda: bench.planning_qp(dev, 0, scenes=1, with_cpu=False),
+        "qp1_t12": lambda: bench.planning_qp(dev, 0, scenes=1, T=12, with_cpu=False),
+        "qp_t12": lambda: bench.planning_qp(dev, 0, T=12, with_cpu=False),
         "episode": lambda: bench.episode_c1(dev, with_cpu=False),
         "harness": lambda: bench.harness_episode(dev),
     }
