@@ -589,8 +589,8 @@ def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8, on_devi
     the pinned input pack, ccmpc_bucket_predictions (make_ovehicles, :469-505: one placement
     pass) -> the Minkowski cycle -> L4 -> 9-tuple; no sampler.  on_device: the same arrays as
     device tensors (generate_vehicle_latents(..., keep_on_device=True), a predictor on the same
-    GPU): copied device to device into the graph's buffers inside the timed step, nothing crosses
-    PCIe.  `n_sets` precomputed frames of particles (the sampler's own draws) are cycled, a
+    GPU): the step graph reads them in place (their addresses in the input pack,
+    ccmpc_bucket_predictions_indirect), nothing crosses PCIe.  `n_sets` precomputed frames of particles (the sampler's own draws) are cycled, a
     different one each step."""
     from ccmpc import engine, episode, planner
     init, pmf, gmm = episode.synthetic_gmm(O, T=ph, seed=20251015)
@@ -632,11 +632,11 @@ def dropin_step_predictions(dev, steps=300, O=4, N=5000, ph=8, n_sets=8, on_devi
     t_graph = time_graph_replay(g, dev)
     cfg = ("step_pred_" + ("dev_" if on_device else "") +
            ("c2" if (O, N) == (4, 5000) else "100k" if (O, N) == (1, 100_000) else "x"))
-    where = ("device tensors (keep_on_device) copied device to device" if on_device else
+    where = ("device tensors (keep_on_device) read in place" if on_device else
              "host numpy predictions / z in the pinned pack")
     return {"config": f"drop-in step on generate_vehicle_latents' 5-tuple: {O} OVs (+ the "
                       f"ego's node) x np={N} x ph={ph}, K={K}; {where} -> "
-                      "ccmpc_bucket_predictions -> Minkowski cycle -> L4 -> 9-tuple",
+                      "ccmpc_bucket_predictions(_indirect) -> Minkowski cycle -> L4 -> 9-tuple",
             "steps": steps, "constraints_per_step": len(out[0]),
             "graph_branch": f"source={g.source}, fused={g.fused}",
             "input_pack_bytes": int(g.inp.nbytes),
