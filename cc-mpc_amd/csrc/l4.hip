@@ -242,20 +242,25 @@ __global__ __launch_bounds__(kL4Threads) void l4_kernel(
 // ---- split over workgroups: every (cell, t) on S workgroups ------------------------------------
 // One workgroup per (cell, t) is issue-bound on its f64 atan2 / division work for large clouds
 // (a 5000-particle cell: 17 us on one CU; 100k particles would take ~0.3 ms), and uses one CU of
-// 256.  The split form runs two launches of (cell, t, chunk) workgroups:
-//   pass 1  headings of the chunk, partial sums (heading, shifted heading and its square for
-//           t = 0) published write-through; the (cell, t)'s last arriver sums them in chunk order
-//           -> theta, the yaw statistics, and theta for pass 2 in the workspace;
-//   pass 2  the chunk's corners and the four support-value maxima, published the same way; the
-//           last arriver takes the max over chunks (order-free) -> b.
+// 256.  The split form spreads each (cell, t) over S chunk workgroups in two phases:
+//   phase 1  headings of the chunk, partial sums (heading, shifted heading and its square for
+//            t = 0) published write-through; the (cell, t)'s last arriver sums them in chunk
+//            order -> theta, the yaw statistics, and theta for phase 2;
+//   phase 2  the chunk's corners and the four support-value maxima, published the same way; the
+//            last arriver takes the max over chunks (order-free) -> b.
 // The hand-off is the moment reduction's (gram.hpp: sc1 stores, drain, agent-scope ticket, sc1
 // loads); the counters at the head of the zero-filled workspace return to zero every call.
+//
+// Measured as ONE launch (start tickets; ticket j ran phase 1 of chunk j, then phase 2 of chunk
+// j - S after its (cell, t)'s theta, deadlock-free in any residency): no faster (C2 step graph
+// 75.6 vs 75.0 us, 100k 107.2 vs 106.8; the 100k phases are f64-issue bound and the overlap
+// only shares the SIMDs), so two launches (profiles/r06/README.md).
 struct L4Split {
   int S;              // workgroups per (cell, t)
   int32_t *ctr;       // [2][n_cells T] arrival counters
   double *part1;      // [n_cells T][S][4]: sum yaw, sum (yaw - shift), sum (yaw - shift)^2, 0
   double *part2;      // [n_cells T][S][4]: the four maxima
-  double *theta;      // [n_cells T]
+  double *theta;      // [n_cells T][2]: theta, 0 (16-byte slots for the sc1 hand-off)
 };
 
 inline size_t l4_split_bytes(int64_t T, int64_t n_cells, int S, size_t *o1, size_t *o2,
@@ -267,18 +272,9 @@ inline size_t l4_split_bytes(int64_t T, int64_t n_cells, int S, size_t *o1, size
   *o2 = o;
   o += ct * S * 4 * sizeof(double);
   *o3 = o;
-  o += ct * sizeof(double);
+  o += ct * 2 * sizeof(double);
   return (o + 255) / 256 * 256;
 }
-
-// Average particles per cell up to which ccmpc_l4_split is ONE launch (pass 2 in the (cell, t)'s
-// last arriver of pass 1).  Measured at the drop-in step's C2 shape (~2200 particles per cell):
-// 139.6 us per step against 136.2 with the two launches (profiles/r02/v35_l4_one_launch.txt) --
-// the last arriver's whole-cell pass costs more than the second launch saves.  Off (0).
-#ifndef CCMPC_L4_TAIL2_MAX
-#define CCMPC_L4_TAIL2_MAX 0
-#endif
-constexpr int64_t kL4Tail2Max = CCMPC_L4_TAIL2_MAX;
 
 constexpr int kL4MaxSplit = 64;  // workgroups per (cell, t): one wave holds their partials
 
@@ -299,105 +295,149 @@ inline int l4_split_factor(int64_t n_cells, int64_t n_bound) {
   return static_cast<int>(S < 1 ? 1 : (S > kL4MaxSplit ? kL4MaxSplit : S));
 }
 
-// Pass 2's per-particle work over [i0, i1) of one (cell, t): the bbox corners at the particle's
-// own heading and the running maxima of the four support values of A (midlevel/util.py:109-124,
-// :171-200).  fmax is exact and order-free, so any split of the particles gives the same b.
+// Workgroup sums / maxima of several values at once: each value reduced exactly as block_sum /
+// block_max reduce it (the xor butterfly, then the waves in order), one barrier pair for all.
+template <int K>
+__device__ __forceinline__ void block_sums(double (&v)[K], double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+    if (lane == 0) red[k * 16 + w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = 0.0;
+    for (int j = 0; j < nw; ++j) s += red[k * 16 + j];
+    v[k] = s;
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void block_max4(double (&v)[4], double *red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] = fmax(v[k], __shfl_xor(v[k], o, 64));
+    if (lane == 0) red[k * 16 + w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double s = -INFINITY;
+    for (int j = 0; j < nw; ++j) s = fmax(s, red[k * 16 + j]);
+    v[k] = s;
+  }
+  __syncthreads();
+}
+
+// One (cell, t)'s geometry, as the chunk workgroups read it
+struct L4Cell {
+  int ct, cell, t, part;
+  int64_t off, n, i0, i1;
+  double o0, o1, px, py;
+};
+__device__ __forceinline__ L4Cell l4_cell(const L4Split &sp, int T, int chunk_id,
+                                          const double *__restrict__ origin,
+                                          const int64_t *__restrict__ cell_off,
+                                          const int64_t *__restrict__ cell_cnt,
+                                          const double *__restrict__ past_last) {
+  L4Cell c;
+  c.ct = chunk_id / sp.S;
+  c.part = chunk_id % sp.S;
+  c.cell = c.ct / T;
+  c.t = c.ct % T;
+  c.off = cell_off[c.cell];
+  c.n = cell_cnt[c.cell];
+  c.o0 = origin ? origin[2 * c.cell] : 0.0;
+  c.o1 = origin ? origin[2 * c.cell + 1] : 0.0;
+  c.px = past_last[2 * c.cell];
+  c.py = past_last[2 * c.cell + 1];
+  const int64_t chunk = (c.n + sp.S - 1) / sp.S;
+  c.i0 = c.part * chunk;
+  c.i1 = min(c.n, c.i0 + chunk);
+  return c;
+}
+
+// particles per thread whose loads are issued together, before their arithmetic: 4 covers a
+// 2048-particle chunk at 512 threads
+constexpr int kL4Pre = 4;
+
+// A particle's step delta (step 0 from past[-1], ovehicle.py:72-76) and its position
 template <typename P>
-__device__ __forceinline__ void corner_maxima(const P *base, int64_t ld, int t, int64_t i0,
-                                              int64_t i1, int64_t off, double o0, double o1,
-                                              double px, double py, double lon, double lat,
-                                              const double (&A)[4][2], double (&mx)[4],
-                                              double *__restrict__ out_vertices) {
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const double x = world(base, ld, 2 * t, i, o0), y = world(base, ld, 2 * t + 1, i, o1);
-    const double xp = t == 0 ? px : world(base, ld, 2 * t - 2, i, o0);
-    const double yp = t == 0 ? py : world(base, ld, 2 * t - 1, i, o1);
-    const double dx = x - xp, dy = y - yp;
-    double S, C;
-    const double r = sqrt(dx * dx + dy * dy);
-    if (r > 0.0 && isfinite(r)) {  // cos / sin of the heading without the atan2 (heading_cs)
-      C = dx / r;
-      S = dy / r;
-    } else {
-      sincos(atan2(dy, dx), &S, &C);
-    }
-    // rows of Rot per corner (midlevel/util.py:109-118), disp = 0.5 * Rot @ [lon, lat]
-    const double ddx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
-                           0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
-    const double ddy[4] = {0.5 * (S * lon - C * lat), 0.5 * (S * lon + C * lat),
-                           0.5 * (-S * lon + C * lat), 0.5 * (-S * lon - C * lat)};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double vx = x + ddx[c], vy = y + ddy[c];
-      if (out_vertices) {
-        double *vp = out_vertices + (static_cast<int64_t>(t) * 8 + 2 * c) * ld + off + i;
-        vp[0] = vx;
-        vp[ld] = vy;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) mx[q] = fmax(mx[q], A[q][0] * vx + A[q][1] * vy);
-    }
+__device__ __forceinline__ void step_delta(const P *base, int64_t ld, const L4Cell &c, int64_t i,
+                                           double &dx, double &dy, double *x = nullptr,
+                                           double *y = nullptr) {
+  const double xx = world(base, ld, 2 * c.t, i, c.o0), yy = world(base, ld, 2 * c.t + 1, i, c.o1);
+  const double xp = c.t == 0 ? c.px : world(base, ld, 2 * c.t - 2, i, c.o0);
+  const double yp = c.t == 0 ? c.py : world(base, ld, 2 * c.t - 1, i, c.o1);
+  dx = xx - xp;
+  dy = yy - yp;
+  if (x) {
+    *x = xx;
+    *y = yy;
   }
 }
 
-__device__ __forceinline__ void support_rows(double theta, double (&A)[4][2]) {
-  const double ct_ = cos(theta), st_ = sin(theta);
-  A[0][0] = ct_; A[0][1] = st_;
-  A[1][0] = -st_; A[1][1] = ct_;
-  A[2][0] = -ct_; A[2][1] = -st_;
-  A[3][0] = st_; A[3][1] = -ct_;
-}
-
-template <typename P, bool TAIL2>
-__global__ __launch_bounds__(kL4SplitThreads) void l4_pass1_kernel(
-    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
-    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
-    const double *__restrict__ past_last, const double *__restrict__ bbox, L4Split sp,
-    double *__restrict__ out_yaw_mean, double *__restrict__ out_yaw0_var,
-    double *__restrict__ out_yaw, double *__restrict__ out_A, double *__restrict__ out_b) {
-  __shared__ double red[16];
-  __shared__ double theta_s;
-  __shared__ int flag;
-  L4S_TS(0, 0);
-  const int ct = blockIdx.x / sp.S, part = blockIdx.x % sp.S;
-  const int cell = ct / T, t = ct % T;
-  const int64_t off = cell_off[cell], n = cell_cnt[cell];
-  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
-  const double px = past_last[2 * cell], py = past_last[2 * cell + 1];
-  const P *base = pos + off;
-  const int64_t chunk = (n + sp.S - 1) / sp.S;
-  const int64_t i0 = part * chunk, i1 = min(n, i0 + chunk);
-  const double shift = (t == 0 && n > 0) ? heading(base, ld, 0, 0, o0, o1, px, py) : 0.0;
-  L4S_TS(0, 1);
-  double s = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const double y = heading(base, ld, t, i, o0, o1, px, py);
-    s += y;
+// Phase 1 of one chunk: the headings' partial sums, published; the (cell, t)'s last arriver sums
+// the chunks in chunk order and writes theta (also to sp.theta, for phase 2) and the yaw
+// statistics.  Returns true in the last arriver (every thread), with theta in *theta_s.
+template <typename P>
+__device__ __forceinline__ bool l4_phase1(const P *__restrict__ pos, int64_t ld, const L4Cell &c,
+                                          const L4Split &sp, double *red, int *flag,
+                                          double *theta_s, double *__restrict__ out_yaw_mean,
+                                          double *__restrict__ out_yaw0_var,
+                                          double *__restrict__ out_yaw) {
+  const P *base = pos + c.off;
+  const int t = c.t;
+  const double shift = (t == 0 && c.n > 0) ? heading(base, ld, 0, 0, c.o0, c.o1, c.px, c.py) : 0.0;
+  double v[3] = {0.0, 0.0, 0.0};
+  auto take = [&](int64_t i, double y) {
+    v[0] += y;
     if (t == 0) {
       const double d = y - shift;
-      s1 += d;
-      s2 += d * d;
+      v[1] += d;
+      v[2] += d * d;
     }
-    if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + off + i] = y;
+    if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + c.off + i] = y;
+  };
+  // the first kL4Pre particles' loads all in flight before their atan2s (one memory round trip,
+  // not one per particle), then the rest one by one; summed in particle order either way
+  double dx[kL4Pre], dy[kL4Pre];
+#pragma unroll
+  for (int k = 0; k < kL4Pre; ++k) {
+    const int64_t i = c.i0 + threadIdx.x + static_cast<int64_t>(k) * blockDim.x;
+    if (i < c.i1) step_delta(base, ld, c, i, dx[k], dy[k]);
   }
-  L4S_TS(0, 2);
-  s = block_sum(s, red);
-  if (t == 0) {
-    s1 = block_sum(s1, red);
-    s2 = block_sum(s2, red);
+#pragma unroll
+  for (int k = 0; k < kL4Pre; ++k) {
+    const int64_t i = c.i0 + threadIdx.x + static_cast<int64_t>(k) * blockDim.x;
+    if (i < c.i1) take(i, atan2(dy[k], dx[k]));
   }
-  double *mine = sp.part1 + (static_cast<int64_t>(ct) * sp.S + part) * 4;
+  for (int64_t i = c.i0 + threadIdx.x + static_cast<int64_t>(kL4Pre) * blockDim.x; i < c.i1;
+       i += blockDim.x) {
+    double ddx, ddy;
+    step_delta(base, ld, c, i, ddx, ddy);
+    take(i, atan2(ddy, ddx));
+  }
+  L4S_TS(0, 1);
+  if (t == 0)
+    block_sums<3>(v, red);
+  else
+    block_sums<1>(reinterpret_cast<double(&)[1]>(v), red);
+  double *mine = sp.part1 + (static_cast<int64_t>(c.ct) * sp.S + c.part) * 4;
   const __amdgpu_buffer_rsrc_t rm = slab_rsrc(mine);
   if (threadIdx.x == 0) {
-    st2_sc1(rm, 0, s, s1);
-    st2_sc1(rm, 16, s2, 0.0);
+    st2_sc1(rm, 0, v[0], v[1]);
+    st2_sc1(rm, 16, v[2], 0.0);
   }
-  L4S_TS(0, 3);
-  if (!arrive_last(sp.ctr + ct, sp.S, &flag)) return;
-  L4S_TS(0, 4);
+  L4S_TS(0, 2);
+  if (!arrive_last(sp.ctr + c.ct, sp.S, flag)) return false;
   // every chunk's partials loaded at once (thread k: chunk k), then summed in chunk order by one
   // thread from LDS: deterministic, and one L2 round trip instead of S dependent ones
-  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part1 + static_cast<int64_t>(ct) * sp.S * 4);
+  const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part1 + static_cast<int64_t>(c.ct) * sp.S * 4);
   __shared__ double2 pu[kL4MaxSplit], pv[kL4MaxSplit];
   if (threadIdx.x < sp.S) {
     pu[threadIdx.x] = ld2_sc1(rp, 32 * threadIdx.x);
@@ -411,75 +451,93 @@ __global__ __launch_bounds__(kL4SplitThreads) void l4_pass1_kernel(
       b1 += pu[k].y;
       b2 += pv[k].x;
     }
-    const double nn = static_cast<double>(n);
+    const double nn = static_cast<double>(c.n);
     const double theta = a / nn;
-    sp.theta[ct] = theta;
-    theta_s = theta;
-    out_yaw_mean[ct] = theta;
-    if (t == 0) out_yaw0_var[cell] = (b2 - b1 * b1 / nn) / (nn - 1.0);
+    st2_sc1(slab_rsrc(sp.theta + 2 * static_cast<int64_t>(c.ct)), 0, theta, 0.0);
+    *theta_s = theta;
+    out_yaw_mean[c.ct] = theta;
+    if (t == 0) out_yaw0_var[c.cell] = (b2 - b1 * b1 / nn) / (nn - 1.0);
   }
-  L4S_TS(0, 5);
-  if (!TAIL2) return;
-  // small cells: the (cell, t)'s last arriver runs pass 2 over the whole cell itself (no second
-  // launch, no second hand-off; the maxima are order-free, so b is the two-pass b bit for bit)
   __syncthreads();
-  double A[4][2];
-  support_rows(theta_s, A);
-  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  corner_maxima(base, ld, t, 0, n, off, o0, o1, px, py, bbox[2 * cell], bbox[2 * cell + 1], A, mx,
-                static_cast<double *>(nullptr));
-  double bm[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bm[q] = block_max(mx[q], red);
-  if (threadIdx.x == 0)
-    for (int q = 0; q < 4; ++q) {
-      out_A[static_cast<int64_t>(ct) * 8 + 2 * q] = A[q][0];
-      out_A[static_cast<int64_t>(ct) * 8 + 2 * q + 1] = A[q][1];
-      out_b[static_cast<int64_t>(ct) * 4 + q] = bm[q];
-    }
+  return true;
 }
 
-template <typename P>
-__global__ __launch_bounds__(kL4SplitThreads) void l4_pass2_kernel(
-    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
-    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
-    const double *__restrict__ past_last, const double *__restrict__ bbox, L4Split sp,
-    double *__restrict__ out_A, double *__restrict__ out_b, double *__restrict__ out_vertices) {
-  __shared__ double red[16];
-  __shared__ int flag;
-  L4S_TS(1, 0);
-  const int ct = blockIdx.x / sp.S, part = blockIdx.x % sp.S;
-  const int cell = ct / T, t = ct % T;
-  const int64_t off = cell_off[cell], n = cell_cnt[cell];
-  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
-  const double px = past_last[2 * cell], py = past_last[2 * cell + 1];
-  const double lon = bbox[2 * cell], lat = bbox[2 * cell + 1];
-  const P *base = pos + off;
-  const int64_t chunk = (n + sp.S - 1) / sp.S;
-  const int64_t i0 = part * chunk, i1 = min(n, i0 + chunk);
-  const double theta = sp.theta[ct];  // written by pass 1 (an earlier launch)
-  double A[4][2];
-  support_rows(theta, A);
-  L4S_TS(1, 1);
-  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  corner_maxima(base, ld, t, i0, i1, off, o0, o1, px, py, lon, lat, A, mx, out_vertices);
-  L4S_TS(1, 2);
-  double bm[4];
+__device__ __forceinline__ void support_rows(double theta, double (&A)[4][2]) {
+  const double ct_ = cos(theta), st_ = sin(theta);
+  A[0][0] = ct_; A[0][1] = st_;
+  A[1][0] = -st_; A[1][1] = ct_;
+  A[2][0] = -ct_; A[2][1] = -st_;
+  A[3][0] = st_; A[3][1] = -ct_;
+}
+
+// A particle's step delta and the cos / sin of its heading without the atan2: (dx, dy) times
+// 1 / |(dx, dy)| from the hardware rsqrt with one Newton step (within 2 ulp of cos / sin of the
+// rounded atan2); a zero step keeps sincos of atan2, whose signed-zero cases the ratio cannot
+// express
+__device__ __forceinline__ void heading_cs_rsq(double dx, double dy, double &S, double &C) {
+  const double n2 = dx * dx + dy * dy;
+  if (n2 > 0.0 && n2 < INFINITY) {
+    double r = __builtin_amdgcn_rsq(n2);
+    r = r * fma(-0.5 * n2 * r, r, 1.5);
+    C = dx * r;
+    S = dy * r;
+  } else {
+    sincos(atan2(dy, dx), &S, &C);
+  }
+}
+
+// One particle's bbox (midlevel/util.py:109-118: corners x + 0.5 Rot(phi) [+-lon, +-lat]) into
+// the running maxima of the four support values of A (util.py:171-200), A = [a; b; -a; -b],
+// a = (cos theta, sin theta), b = (-sin theta, cos theta).  Over the four corners,
+// max_k a . v_k = a . p + 0.5 (lon |a . Rot e_x| + lat |a . Rot e_y|) -- the corners themselves
+// are not formed (within a few ulp of max_k over the rounded corner projections).  fmax is
+// exact and order-free, so any split of the particles gives the same b.
+__device__ __forceinline__ void support_max(double x, double y, double S, double C, double lon,
+                                            double lat, double ct, double st, double (&mx)[4]) {
+  const double u = ct * C + st * S;  // a . Rot e_x  ( = b . Rot e_y)
+  const double w = st * C - ct * S;  // a . Rot e_y  ( = -b . Rot e_x)
+  const double ap = ct * x + st * y, bp = ct * y - st * x;
+  const double h0 = 0.5 * (lon * fabs(u) + lat * fabs(w));
+  const double h1 = 0.5 * (lon * fabs(w) + lat * fabs(u));
+  mx[0] = fmax(mx[0], ap + h0);
+  mx[1] = fmax(mx[1], bp + h1);
+  mx[2] = fmax(mx[2], h0 - ap);
+  mx[3] = fmax(mx[3], h1 - bp);
+}
+
+// The particle's four corners into out_vertices (rows 8 t + 2 k, 8 t + 2 k + 1 at vp)
+__device__ __forceinline__ void write_corners(double x, double y, double S, double C, double lon,
+                                              double lat, double *__restrict__ vp, int64_t ld) {
+  const double ddx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
+                         0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
+  const double ddy[4] = {0.5 * (S * lon - C * lat), 0.5 * (S * lon + C * lat),
+                         0.5 * (-S * lon + C * lat), 0.5 * (-S * lon - C * lat)};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) bm[q] = block_max(mx[q], red);
-  double *mine = sp.part2 + (static_cast<int64_t>(ct) * sp.S + part) * 4;
+  for (int k = 0; k < 4; ++k) {
+    vp[2 * k * ld] = x + ddx[k];
+    vp[(2 * k + 1) * ld] = y + ddy[k];
+  }
+}
+
+// Phase 2 of one chunk after theta: the maxima published; the (cell, t)'s last arriver takes the
+// max over chunks and writes A and b.  Returns true in the last arriver.
+__device__ __forceinline__ bool l4_phase2_finish(const L4Cell &c, const L4Split &sp, int nct,
+                                                 const double (&A)[4][2], double (&mx)[4],
+                                                 double *red, int *flag,
+                                                 double *__restrict__ out_A,
+                                                 double *__restrict__ out_b) {
+  block_max4(mx, red);
+  double *mine = sp.part2 + (static_cast<int64_t>(c.ct) * sp.S + c.part) * 4;
   const __amdgpu_buffer_rsrc_t rm = slab_rsrc(mine);
   if (threadIdx.x == 0) {
-    st2_sc1(rm, 0, bm[0], bm[1]);
-    st2_sc1(rm, 16, bm[2], bm[3]);
+    st2_sc1(rm, 0, mx[0], mx[1]);
+    st2_sc1(rm, 16, mx[2], mx[3]);
   }
-  L4S_TS(1, 3);
-  const int nct = gridDim.x / sp.S;
-  if (!arrive_last(sp.ctr + nct + ct, sp.S, &flag)) return;
-  L4S_TS(1, 4);
+  if (!arrive_last(sp.ctr + nct + c.ct, sp.S, flag)) return false;
   // the maxima over chunks (order-free): the first wave loads them all at once and reduces
   if (threadIdx.x < 64) {
-    const __amdgpu_buffer_rsrc_t rp = slab_rsrc(sp.part2 + static_cast<int64_t>(ct) * sp.S * 4);
+    const __amdgpu_buffer_rsrc_t rp =
+        slab_rsrc(sp.part2 + static_cast<int64_t>(c.ct) * sp.S * 4);
     double b[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     if (threadIdx.x < sp.S) {
       const double2 u = ld2_sc1(rp, 32 * threadIdx.x), v = ld2_sc1(rp, 32 * threadIdx.x + 16);
@@ -494,12 +552,72 @@ __global__ __launch_bounds__(kL4SplitThreads) void l4_pass2_kernel(
       for (int o = 32; o > 0; o >>= 1) b[q] = fmax(b[q], __shfl_xor(b[q], o, 64));
     if (threadIdx.x == 0)
       for (int q = 0; q < 4; ++q) {
-        out_A[static_cast<int64_t>(ct) * 8 + 2 * q] = A[q][0];
-        out_A[static_cast<int64_t>(ct) * 8 + 2 * q + 1] = A[q][1];
-        out_b[static_cast<int64_t>(ct) * 4 + q] = b[q];
+        out_A[static_cast<int64_t>(c.ct) * 8 + 2 * q] = A[q][0];
+        out_A[static_cast<int64_t>(c.ct) * 8 + 2 * q + 1] = A[q][1];
+        out_b[static_cast<int64_t>(c.ct) * 4 + q] = b[q];
       }
   }
-  L4S_TS(1, 5);
+  return true;
+}
+
+template <typename P>
+__global__ __launch_bounds__(kL4SplitThreads) void l4_pass1_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
+    const double *__restrict__ past_last, L4Split sp, double *__restrict__ out_yaw_mean,
+    double *__restrict__ out_yaw0_var, double *__restrict__ out_yaw) {
+  __shared__ double red[64];
+  __shared__ double theta_s;
+  __shared__ int flag;
+  L4S_TS(0, 0);
+  const L4Cell c = l4_cell(sp, T, blockIdx.x, origin, cell_off, cell_cnt, past_last);
+  l4_phase1(pos, ld, c, sp, red, &flag, &theta_s, out_yaw_mean, out_yaw0_var, out_yaw);
+  L4S_TS(0, 3);
+}
+
+template <typename P>
+__global__ __launch_bounds__(kL4SplitThreads) void l4_pass2_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
+    const double *__restrict__ past_last, const double *__restrict__ bbox, L4Split sp,
+    double *__restrict__ out_A, double *__restrict__ out_b, double *__restrict__ out_vertices) {
+  __shared__ double red[64];
+  __shared__ int flag;
+  L4S_TS(1, 0);
+  const L4Cell c = l4_cell(sp, T, blockIdx.x, origin, cell_off, cell_cnt, past_last);
+  const double lon = bbox[2 * c.cell], lat = bbox[2 * c.cell + 1];
+  const P *base = pos + c.off;
+  double A[4][2];
+  support_rows(sp.theta[2 * c.ct], A);  // written by pass 1 (an earlier launch)
+  L4S_TS(1, 1);
+  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  double *vbase = out_vertices ? out_vertices + static_cast<int64_t>(c.t) * 8 * ld + c.off : nullptr;
+  auto take = [&](int64_t i, double x, double y, double dx, double dy) {
+    double S, C;
+    heading_cs_rsq(dx, dy, S, C);
+    support_max(x, y, S, C, lon, lat, A[0][0], A[0][1], mx);
+    if (vbase) write_corners(x, y, S, C, lon, lat, vbase + i, ld);
+  };
+  double px[kL4Pre], py[kL4Pre], dx[kL4Pre], dy[kL4Pre];  // loads first, as in phase 1
+#pragma unroll
+  for (int k = 0; k < kL4Pre; ++k) {
+    const int64_t i = c.i0 + threadIdx.x + static_cast<int64_t>(k) * blockDim.x;
+    if (i < c.i1) step_delta(base, ld, c, i, dx[k], dy[k], &px[k], &py[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kL4Pre; ++k) {
+    const int64_t i = c.i0 + threadIdx.x + static_cast<int64_t>(k) * blockDim.x;
+    if (i < c.i1) take(i, px[k], py[k], dx[k], dy[k]);
+  }
+  for (int64_t i = c.i0 + threadIdx.x + static_cast<int64_t>(kL4Pre) * blockDim.x; i < c.i1;
+       i += blockDim.x) {
+    double x, y, ddx, ddy;
+    step_delta(base, ld, c, i, ddx, ddy, &x, &y);
+    take(i, x, y, ddx, ddy);
+  }
+  L4S_TS(1, 2);
+  l4_phase2_finish(c, sp, gridDim.x / sp.S, A, mx, red, &flag, out_A, out_b);
+  L4S_TS(1, 3);
 }
 
 }  // namespace ccmpc
@@ -585,26 +703,17 @@ extern "C" int ccmpc_l4_split(const void *positions, int dtype, int64_t ld, int6
     return CCMPC_ERR_WORKSPACE;
   }
   char *w = static_cast<char *>(workspace);
+  const int64_t nct = n_cells * T;
   const L4Split sp{S, reinterpret_cast<int32_t *>(w), reinterpret_cast<double *>(w + o1),
                    reinterpret_cast<double *>(w + o2), reinterpret_cast<double *>(w + o3)};
-  const dim3 grid(static_cast<unsigned>(n_cells * T * S));
   hipStream_t s = as_stream(stream);
   const int Ti = static_cast<int>(T);
-  // small cells (<= kL4Tail2Max particles on average, no vertex output): one launch, pass 2 in
-  // the (cell, t)'s last arriver of pass 1
-  const bool tail2 = !out_vertices && n_particles_bound <= kL4Tail2Max * n_cells;
+  const dim3 grid(static_cast<unsigned>(nct * S));
   auto run = [&](auto tag) {
     using P = decltype(tag);
     const P *p = static_cast<const P *>(positions);
-    if (tail2) {
-      hipLaunchKernelGGL((l4_pass1_kernel<P, true>), grid, dim3(kL4SplitThreads), 0, s, p, ld, Ti,
-                         origin, cell_off, cell_cnt, past_last, bbox, sp, out_yaw_mean,
-                         out_yaw0_var, out_yaw, out_A, out_b);
-      return;
-    }
-    hipLaunchKernelGGL((l4_pass1_kernel<P, false>), grid, dim3(kL4SplitThreads), 0, s, p, ld, Ti,
-                       origin, cell_off, cell_cnt, past_last, bbox, sp, out_yaw_mean,
-                       out_yaw0_var, out_yaw, out_A, out_b);
+    hipLaunchKernelGGL((l4_pass1_kernel<P>), grid, dim3(kL4SplitThreads), 0, s, p, ld, Ti, origin,
+                       cell_off, cell_cnt, past_last, sp, out_yaw_mean, out_yaw0_var, out_yaw);
     hipLaunchKernelGGL((l4_pass2_kernel<P>), grid, dim3(kL4SplitThreads), 0, s, p, ld, Ti, origin,
                        cell_off, cell_cnt, past_last, bbox, sp, out_A, out_b, out_vertices);
   };

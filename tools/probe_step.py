@@ -89,9 +89,12 @@ def main():
                ["loaded", "done"]),
               ("cycle", table(lib.ccmpc_probe_timestamps, 0, wg=8192), None),
               ("l4.pass1", table(lib.ccmpc_probe_l4_split_timestamps, 0, 0),
-               ["located", "loop", "published", "last", "done"]),
+               ["loop", "published", "done"]),
               ("l4.pass2", table(lib.ccmpc_probe_l4_split_timestamps, 1, 0),
-               ["located", "loop", "published", "last", "done"])]
+               ["located", "loop", "done"])]
+        if not len(ks[-1][1]):      # one launch (l4_fused_kernel): its stamps are table 0's
+            ks[-2] = ("l4.fused", ks[-2][1], ["p1 loop", "p1 published", "p1 done", "p2 prep",
+                                              "theta seen", "p2 done"])
         ks = [k for k in ks if len(k[1])]
         t0 = ks[0][1][:, 0].min()
         print(f"--- replay {rep} ({'direct' if a.direct else 'graph'}), N={N}, times in us "
