@@ -139,7 +139,7 @@ struct QpArgs {
   int T, Tf, n_ref, u_order, rec_kind, max_iter, rows_in_lds, polish;
   int rec_compact;    // records are ccmpc_gather_rec (32 bytes), rec_kind their source kind
   int early_discard;  // test hook: attempt the early polish, never keep its answer
-  int method;         // CCMPC_QP_METHOD_IPM, or _GI (one wave, n <= 16; else the IPM)
+  int method;         // CCMPC_QP_METHOD_IPM, or _GI (one wave, n <= 32; else the IPM)
   int gi_max_steps;   // the active-set step budget (< 0: 8 (n + 16)); a test hook forces the
                       // hand-over to the IPM with 0
   int fallback_only;  // the IPM pass after an active-set-only launch (kQpNeedIpm scenes only)
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     lb[j] = c == 0 ? p.min_a : -p.max_delta;
     z[j] = 0.0;
   }
-  if constexpr (NW == 1)  // launched only for n <= 16, where the layout reserves the table
+  if constexpr (NW == 1 && NM == 16)  // n <= 16, where the layout reserves the table
     for (int e = tid; e < n * n; e += NTH) Hc[e] = hctrl(e / n, e % n, T, order, p);
   qp_sync<NW>();
   QS_MARK(0);
@@ -852,7 +852,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   QS_MARK(1);
   // f = Gs^T qf (the scaling of the dual residual; kept in LDS for the polish)
   double fmax_ = 0.0;
-  if constexpr (NW == 1) {  // a quad per control, DPP sum (as the IPM's rd)
+  if constexpr (NW == 1 && NM == 16) {  // a quad per control, DPP sum (as the IPM's rd)
     const int j = lane >> 2, kq = lane & 3, jj = j < n ? j : 0;
     double v = 0.0;
 #pragma unroll
@@ -973,7 +973,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     double *fu = lds + lay.f, *y0 = rh, *rs = e2, *lam = q, *zp = dz, *yp = yd;
     PQ_MARK(0);
     // H (no barrier terms) into M; f in control space (fu) is the setup's
-    if constexpr (NW == 1) {  // as the IPM's M: lane column jm, rows (lane >> 4) + 4 m
+    if constexpr (NW == 1 && NM == 16) {  // as the IPM's M: lane column jm, rows (lane >> 4) + 4 m
       const int jm = lane & 15, jc = jm < n ? jm : 0;
       double hx[8], hy[8];
 #pragma unroll
@@ -1319,7 +1319,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // M = H_ctrl + D_box + sum_t Gs_t^T B_t Gs_t (the barrier-weighted normal matrix of I2).
   // A lambda so a failed early polish, which factors H in M's storage, can rebuild it.
   auto normal_matrix = [&]() {
-    if constexpr (NW == 1) {
+    if constexpr (NW == 1 && NM == 16) {
       // lane column jm = lane & 15 (its weighted Gs columns in registers), rows
       // im = (lane >> 4) + 4 m
       const int jm = lane & 15, jc = jm < n ? jm : 0;
@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
     }
   };
 
-  // ---- Goldfarb-Idnani dual active-set solve (one wave, n <= 16; CCMPC_QP_METHOD_GI) --------
+  // ---- Goldfarb-Idnani dual active-set solve (one wave, n <= 32; CCMPC_QP_METHOD_GI) --------
   // The strictly convex QP  min 1/2 z^T H z + f^T z  s.t.  g_r(z) <= 0  from its unconstrained
   // minimum: the most violated row (normalised by its gradient's norm) enters the active set,
   // primal steps along J2 d2 and dual steps along R^{-1} d1 keep the active multipliers >= 0
@@ -1385,7 +1385,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
   // Each active-set change is a handful of wave-wide LDS phases, and a T = 8 frame enters only
   // a few rows, where the IPM spends ~5 iterations and a polish (~130 us).
   bool gi_done = false;
-  if constexpr (GI && NW == 1 && NM == 16) {
+  if constexpr (GI && NW == 1 && (NM == 16 || NM == 32)) {
     auto gi_solve = [&]() -> bool {
 #ifdef CCMPC_QP_TRACE
       uint64_t gmark[6] = {}, gacc[6] = {}, gt = 0;
@@ -1415,7 +1415,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         if (lane < T3) {
           double v = 0.0;
   #pragma unroll
-          for (int j = 0; j < 16; ++j)
+          for (int j = 0; j < NM; ++j)
             if (j < n) v = fma(Gs[lane * n + j], z[j], v);
           y[lane] = v;
         }
@@ -1429,8 +1429,21 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         wave_sync();
         return false;
       };
-      // H (no barrier terms) into M's lower triangle, as the polish builds it
-      {
+      // H (no barrier terms) into M's lower triangle, as the polish builds it (n <= 32: entry by
+      // entry, as the four-wave polish does)
+      if constexpr (NM == 32) {
+        for (int e = lane; e < n * n; e += 64) {
+          const int i = e / n, j = e % n;
+          if (j > i) continue;
+          double v = hctrl(i, j, T, order, p);
+          for (int t = 0; t < T; ++t) {
+            const double wp = 2.0 * (p.w_ref + (t == T - 1 ? p.w_final : 0.0));
+            v += wp * (Gs[(3 * t) * n + i] * Gs[(3 * t) * n + j] +
+                       Gs[(3 * t + 1) * n + i] * Gs[(3 * t + 1) * n + j]);
+          }
+          M[i * ldm + j] = v;
+        }
+      } else {
         const int jm = lane & 15, jc = jm < n ? jm : 0;
         double hx[8], hy[8];
   #pragma unroll
@@ -1455,20 +1468,20 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         }
       }
       wave_sync();
-      double La[16], Ldl = 0.0;
+      double La[NM], Ldl = 0.0;
   #pragma unroll
-      for (int k = 0; k < 16; ++k) {
+      for (int k = 0; k < NM; ++k) {
         const double v = M[li * ldm + (k < n ? k : 0)];
         La[k] = (lane < n && k <= lane) ? v : (k == lane ? 1.0 : 0.0);
       }
-      if (reg_cholesky<16, false>(La, Ldl)) return give_up();
+      if (reg_cholesky<NM, false>(La, Ldl)) return give_up();
       GI_MARK(1);
       // L (rows) and 1 / L_ii into R's storage (free until the first row enters) for the
       // column-parallel inverse below
       double *Ls = Rm, *Ldi = lds + lay.dinv;
       if (lane < n) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
+        for (int k = 0; k < NM; ++k)
           if (k <= lane && k < n) Ls[lane * ldm + k] = La[k];
         Ldi[lane] = Ldl;
       }
@@ -1476,9 +1489,9 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       GI_MARK(2);
       // J = L^{-T}: lane c solves L x = e_c (all columns at once, L's entries broadcast from
       // LDS), x_k = L^{-1}[k][c] = J[c][k] -- lane c ends with row c of J
-      double Jrow[16];
+      double Jrow[NM];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
+      for (int k = 0; k < NM; ++k) {
         double acc = (k == lane) ? 1.0 : 0.0;
 #pragma unroll
         for (int j = 0; j < k; ++j)
@@ -1487,7 +1500,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       }
       if (lane < n) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
+        for (int k = 0; k < NM; ++k)
           if (k < n) Jm[lane * ldm + k] = Jrow[k];
       }
       // row gradient norms (the violation's scale) from each step's output-row Gram: an
@@ -1497,7 +1510,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       if (lane < T) {
         double xx = 0.0, xy = 0.0, yy = 0.0, vv = 0.0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < NM; ++j) {
           if (j >= n) continue;
           const double gx = Gs[(3 * lane) * n + j], gy = Gs[(3 * lane + 1) * n + j],
                        gv = Gs[(3 * lane + 2) * n + j];
@@ -1531,10 +1544,10 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       // the unconstrained minimum z = -J L^{-1} f (the forward solve on lane = row, then each
       // lane's row of J against it)
       {
-        const double y0 = reg_forward<16>(La, Ldl, lane < n ? fu[lane] : 0.0);
+        const double y0 = reg_forward<NM>(La, Ldl, lane < n ? fu[lane] : 0.0);
         double zi = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
+        for (int k = 0; k < NM; ++k)
           if (k < n) zi = fma(Jrow[k], lane_bcast(y0, k), zi);
         wave_sync();
         if (lane < n) z[lane] = -zi;
@@ -1549,7 +1562,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
       auto store_j = [&]() {
         if (lane < n) {
 #pragma unroll
-          for (int k = 0; k < 16; ++k)
+          for (int k = 0; k < NM; ++k)
             if (k < n) Jm[lane * ldm + k] = Jrow[k];
         }
       };
@@ -1612,14 +1625,14 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
         // the kernel's SGPR spilling
         double *mvec = lds + lay.rh, *dvec = lds + lay.e2;
         wave_sync();
-        if (lane < 16) mvec[lane] = mj;
+        if (lane < n) mvec[lane] = mj;
         wave_sync();
         while (true) {
           if (++steps > max_steps) return give_up();
           // d = J^T m (lane j), r = R^{-1} d[:q] (lane k < q)
           double dj = 0.0;
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
+          for (int i = 0; i < NM; ++i)
             if (i < n) dj = fma(Jm[i * ldm + li], mvec[i], dj);
           double rhs = dj, rk = 0.0;
           for (int j = q - 1; j >= 0; --j) {
@@ -1628,15 +1641,15 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
             if (lane < j) rhs = fma(-Rm[lane * ldm + j], xj, rhs);
           }
           GI_ACC(1);
-          double dd[16];
+          double dd[NM];
           wave_sync();
-          if (lane < 16) dvec[lane] = dj;
+          if (lane < n) dvec[lane] = dj;
           wave_sync();
 #pragma unroll
-          for (int k = 0; k < 16; ++k) dd[k] = dvec[k];
+          for (int k = 0; k < NM; ++k) dd[k] = dvec[k < n ? k : 0];
           double d2 = 0.0, dn2 = 0.0, zi = 0.0;
 #pragma unroll
-          for (int k = 0; k < 16; ++k) {
+          for (int k = 0; k < NM; ++k) {
             if (k >= n) continue;
             dn2 = fma(dd[k], dd[k], dn2);
             if (k >= q) {
@@ -1684,11 +1697,9 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
           const bool full = !zero_step && t2 <= t1;
           if (full) {
             // add the row: rotate d[q:] onto d[q] (J's columns q .. n-1), R's new column
-            double dv[16];
+            double (&dv)[NM] = dd;  // rotated in place (dd is not read again)
 #pragma unroll
-            for (int k = 0; k < 16; ++k) dv[k] = dd[k];
-#pragma unroll
-            for (int j = 15; j >= 1; --j) {
+            for (int j = NM - 1; j >= 1; --j) {
               if (j >= n || j <= q) continue;
               double c, s, h;
               givens(dv[j - 1], dv[j], c, s, h);
@@ -1700,12 +1711,12 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
             }
             double rqq = 0.0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
+            for (int k = 0; k < NM; ++k)
               if (k == q) rqq = dv[k];
             if (rqq < 0.0) {
               rqq = -rqq;
 #pragma unroll
-              for (int k = 0; k < 16; ++k)
+              for (int k = 0; k < NM; ++k)
                 if (k == q) Jrow[k] = -Jrow[k];
             }
             if (!(rqq > 1e-300)) return give_up();  // dependent row with a primal step
@@ -1728,16 +1739,16 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
           // drop active row l: R's columns l+1 .. q-1 shift left (lane = column), then
           // rotations on rows (k, k+1), k = l .. q-2, restore the triangle; J's columns
           // (k, k+1) likewise
-          double Rc[16];
+          double Rc[NM];
           {
             const int col = (lane >= l && lane < q - 1) ? lane + 1 : (lane < q ? lane : 0);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) Rc[i] = (i < q) ? Rm[i * ldm + col] : 0.0;
+            for (int i = 0; i < NM; ++i) Rc[i] = (i < q) ? Rm[i * ldm + col] : 0.0;
           }
           for (int k = l; k < q - 1; ++k) {
             double a = 0.0, b = 0.0;
 #pragma unroll
-            for (int i = 0; i < 15; ++i)
+            for (int i = 0; i < NM - 1; ++i)
               if (i == k) {
                 a = Rc[i];
                 b = Rc[i + 1];
@@ -1745,7 +1756,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
             double c, s, h;
             givens(lane_bcast(a, k), lane_bcast(b, k), c, s, h);
 #pragma unroll
-            for (int i = 0; i < 15; ++i)
+            for (int i = 0; i < NM - 1; ++i)
               if (i == k) {
                 const double r0 = Rc[i], r1 = Rc[i + 1];
                 Rc[i] = fma(c, r0, s * r1);
@@ -1757,7 +1768,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
           }
           double rdg = 1.0;
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
+          for (int i = 0; i < NM; ++i)
             if (i == lane) rdg = Rc[i];
           const double act_next = actv[(lane + 1 < q ? lane + 1 : 0)];
           const double u_next = uact[(lane + 1 < q ? lane + 1 : 0)];
@@ -1765,7 +1776,7 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
           wave_sync();
           if (lane < q - 1) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
+            for (int i = 0; i < NM; ++i)
               if (i <= lane) Rm[i * ldm + lane] = Rc[i];
             Rdi[lane] = 1.0 / rdg;
             if (lane >= l) {
@@ -2384,7 +2395,19 @@ static int mpc_qp_impl(const ccmpc_qp_ltv *ltv, int64_t n_scenes, int64_t T, int
   // (CCMPC_QP_GI_SPLIT: 0 never, 1 batches -- the default --, 2 a single scene too)
   const char *se = getenv("CCMPC_QP_GI_SPLIT");
   const int split_env = se ? atoi(se) : 1;
-  if (gi && split_env > 0 && (n_scenes > 1 || split_env > 1)) {
+  // n = 17 .. 32 (T = 9 .. 16): the active-set pass on one wave (factor and J in registers,
+  // 32 per lane), then the four-wave IPM pass for the scenes it handed over
+  const bool gi32 = n > 16 && n <= 32 && a.method == CCMPC_QP_METHOD_GI && plan.polish;
+  if (gi32) {
+    attr = in_lds ? launch_qp<true, 32, 1, true, true>(grid, lds, s, a)
+                  : launch_qp<false, 32, 1, true, true>(grid, lds, s, a);
+    if (attr == hipSuccess) {
+      QpArgs f = a;
+      f.fallback_only = 1;
+      attr = in_lds ? launch_qp<true, 0, 4>(grid, lds, s, f)
+                    : launch_qp<false, 0, 4>(grid, lds, s, f);
+    }
+  } else if (gi && split_env > 0 && (n_scenes > 1 || split_env > 1)) {
     attr = in_lds ? launch_qp<true, 16, 1, true, true>(grid, lds, s, a)
                   : launch_qp<false, 16, 1, true, true>(grid, lds, s, a);
     if (attr == hipSuccess) {

@@ -15,6 +15,8 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
+SEED = 20251015  # bench.py's --seed default, so the QP lines are the same scenes
+
 
 def main():
     which = sys.argv[1:] or ["dropin", "dropin_pp", "dropin_100k", "episode", "harness"]
@@ -30,10 +32,10 @@ def main():
         "dropin_pred_dev": lambda: bench.dropin_step_predictions(dev, on_device=True),
         "dropin_pred_100k_dev": lambda: bench.dropin_step_predictions(
             dev, steps=100, O=1, N=100_000, n_sets=4, on_device=True),
-        "qp": lambda: bench.planning_qp(dev, 0, with_cpu=False),
-        "qp1_t8": lambda: bench.planning_qp(dev, 0, scenes=1, with_cpu=False),
-        "qp1_t12": lambda: bench.planning_qp(dev, 0, scenes=1, T=12, with_cpu=False),
-        "qp_t12": lambda: bench.planning_qp(dev, 0, T=12, with_cpu=False),
+        "qp": lambda: bench.planning_qp(dev, SEED, with_cpu=False),
+        "qp1_t8": lambda: bench.planning_qp(dev, SEED, scenes=1, with_cpu=False),
+        "qp1_t12": lambda: bench.planning_qp(dev, SEED, scenes=1, T=12, with_cpu=False),
+        "qp_t12": lambda: bench.planning_qp(dev, SEED, T=12, with_cpu=False),
         "episode": lambda: bench.episode_c1(dev, with_cpu=False),
         "harness": lambda: bench.harness_episode(dev),
     }
