@@ -87,17 +87,28 @@ __device__ __forceinline__ double uniform53(uint32_t a, uint32_t b) {
          (1.0 / 9007199254740992.0);
 }
 
-// Box-Muller pair, float64 (oracle/philox.py normal_pair)
-__device__ __forceinline__ void normal_pair(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                            uint64_t seed, double &z0, double &z1) {
+// Box-Muller pair, float64 (oracle/philox.py normal_pair), in two halves a caller may run in
+// separate passes: the radius sqrt(-2 log u1) and the angle's uniform, then the sin / cos.  A
+// loop of whole pairs keeps both halves' polynomial coefficients in registers (the compiler
+// hoists them out of the loop); two passes keep only one set live at a time.
+__device__ __forceinline__ void normal_radius(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint64_t seed, double &r, double &u2) {
   const u32x4 w = philox4x32(c0, c1, c2, c3, seed);
   const double u1 = 1.0 - uniform53(w.x, w.y);
-  const double u2 = uniform53(w.z, w.w);
-  const double r = sqrt(-2.0 * log(u1));
+  u2 = uniform53(w.z, w.w);
+  r = sqrt(-2.0 * log(u1));
+}
+__device__ __forceinline__ void normal_angle(double r, double u2, double &z0, double &z1) {
   double s, c;
   sincos(2.0 * M_PI * u2, &s, &c);
   z0 = r * c;
   z1 = r * s;
+}
+__device__ __forceinline__ void normal_pair(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint64_t seed, double &z0, double &z1) {
+  double r, u2;
+  normal_radius(c0, c1, c2, c3, seed, r, u2);
+  normal_angle(r, u2, z0, z1);
 }
 
 // ---- diagnostic timestamps (PROBE=4 builds only) -------------------------------------------

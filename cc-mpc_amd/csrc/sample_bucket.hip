@@ -513,7 +513,29 @@ __global__ __launch_bounds__(64 * NW, 7) void place_kernel(FusedArgs a) {
   if (!PRED) {     // the block's actions: step t of particle lane on wave t mod NW
     const uint64_t seed = a.seed_dev ? *a.seed_dev : a.seed;
     const uint32_t key = a.ov_base + static_cast<uint32_t>(o);
-    if (lane < n) {
+    if (!EPSIN && T <= 2 * NW) {
+      // at most two Philox pairs per lane: every radius first, then every angle (one set of
+      // polynomial coefficients in registers at a time: a loop of whole pairs spilled them)
+      double rr[2], uu[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int t = w + j * NW;
+        if (lane < n && t < T)
+          normal_radius(static_cast<uint32_t>(i0 + lane), static_cast<uint32_t>(t), key,
+                        STREAM_SAMPLER_EPS, seed, rr[j], uu[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int t = w + j * NW;
+        if (lane < n && t < T) {
+          double e0, e1;
+          normal_angle(rr[j], uu[j], e0, e1);
+          action_from_noise<PP>(t, i0 + lane, zs[lane], o, T, L, N, a.gmm, coef_s, staged,
+                                static_cast<float>(e0), static_cast<float>(e1),
+                                act[(2 * t) * PB + lane], act[(2 * t + 1) * PB + lane]);
+        }
+      }
+    } else if (lane < n) {
 #pragma unroll 1
       for (int t = w; t < T; t += NW)
         draw_action<PP, EPSIN>(t, i0 + lane, zs[lane], o, T, L, N, key, seed, a.gmm, coef_s,

@@ -97,9 +97,31 @@ __device__ __forceinline__ int draw_latent(int64_t i, uint32_t key, uint64_t see
   return z;
 }
 
-// Particle i's action at step t (GMM2D.rsample of its component): per-particle parameters at
-// gmm[ov][5t + k][N] or the per-latent row of z (its coefficient row in LDS, gmm_s, when staged
-// by stage_gmm_coefs); noise injected at eps_in[ov][2t + c][N] or drawn from Philox.
+// Particle i's action at step t from its standard-normal pair (e0, e1): GMM2D.rsample of its
+// component, per-particle parameters at gmm[ov][5t + k][N] or the per-latent row of z (its
+// coefficient row in LDS, gmm_s, when staged by stage_gmm_coefs).
+template <bool PP>
+__device__ __forceinline__ void action_from_noise(int t, int64_t i, int z, int ov, int T,
+                                                  int n_latent, int64_t N,
+                                                  const float *__restrict__ gmm,
+                                                  const float *gmm_s, bool staged, float e0,
+                                                  float e1, float &dphi, float &acc) {
+  const float *g = PP ? gmm + static_cast<int64_t>(ov) * T * 5 * N + i
+                      : gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
+  float c[5];
+  if (!PP && staged) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) c[k] = gmm_s[(z * T + t) * 5 + k];
+  } else {
+    float p[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) p[k] = PP ? g[(5 * t + k) * N] : g[5 * t + k];
+    gmm2d_coefs(p[0], p[1], p[2], p[3], p[4], c);
+  }
+  gmm2d_draw(c, e0, e1, dphi, acc);
+}
+
+// Particle i's action at step t: noise injected at eps_in[ov][2t + c][N] or drawn from Philox
 template <bool PP, bool EPSIN>
 __device__ __forceinline__ void draw_action(int t, int64_t i, int z, int ov, int T, int n_latent,
                                             int64_t N, uint32_t key, uint64_t seed,
@@ -119,19 +141,7 @@ __device__ __forceinline__ void draw_action(int t, int64_t i, int z, int ov, int
     e0 = static_cast<float>(e0d);
     e1 = static_cast<float>(e1d);
   }
-  const float *g = PP ? gmm + static_cast<int64_t>(ov) * T * 5 * N + i
-                      : gmm + (static_cast<int64_t>(ov) * n_latent + z) * T * 5;
-  float c[5];
-  if (!PP && staged) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k) c[k] = gmm_s[(z * T + t) * 5 + k];
-  } else {
-    float p[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) p[k] = PP ? g[(5 * t + k) * N] : g[5 * t + k];
-    gmm2d_coefs(p[0], p[1], p[2], p[3], p[4], c);
-  }
-  gmm2d_draw(c, e0, e1, dphi, acc);
+  action_from_noise<PP>(t, i, z, ov, T, n_latent, N, gmm, gmm_s, staged, e0, e1, dphi, acc);
 }
 
 }  // namespace ccmpc
