@@ -140,6 +140,32 @@ struct FusedArgs {
   int64_t *cell_off, *cell_cnt;
   double *cell_pmf, *init_center;
   int32_t *z_bad;  // optional [n_ov]: invalid latent ids per OV
+  int wt;          // the particle stores may go write-through (every offset < 2^31 bytes)
+};
+
+
+// Particle coordinate stores of place_kernel and rare_copy_kernel (build knob CCMPC_WT_STORES):
+// write-through (sc1 buffer stores) when every byte offset from the buffer's base fits the 31-bit
+// buffer range (a.wt), plain stores otherwise.  The kernel then ends with none of those lines
+// dirty in L2 for the end-of-kernel write-back: at 100 000 particles the gaps after place and
+// copy shrank 4.5 -> 1.6 and 3.6 -> 2.5 us while the two kernels took 2.8 and 1.7 us longer
+// (4-byte sc1 stores cost more than plain ones); step graph 104.3 -> 101.8 us, record path
+// 76.1 -> 74.0 (profiles/r06/README.md)
+#ifndef CCMPC_WT_STORES
+#define CCMPC_WT_STORES 1
+#endif
+struct OutStore {
+  __amdgpu_buffer_rsrc_t r;
+  float *base;
+  bool wt;
+  __device__ __forceinline__ OutStore(float *b, bool w) : r(slab_rsrc(reinterpret_cast<double *>(b))), base(b), wt(w) {}
+  __device__ __forceinline__ void put(int64_t e, float v) const {
+    if (CCMPC_WT_STORES && wt)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r,
+                                            static_cast<int>(e * 4), 0, 16);
+    else
+      base[e] = v;
+  }
 };
 
 __device__ __forceinline__ int64_t *hdr_starts(int32_t *h) {
@@ -627,12 +653,15 @@ __global__ __launch_bounds__(64 * NW, 7) void place_kernel(FusedArgs a) {
   const int rs = native ? 0 : before_s[K] + rank;  // slot in the rare list
   const int npad = static_cast<int>(a.Npad);
   float x = 0.0f, y = 0.0f;
+  // both destinations' stores from uniform bases (a.out, the OV's rare list)
+  const OutStore so(a.out, a.wt != 0), sr(a.rstore + static_cast<int64_t>(o) * W * a.Npad, a.wt != 0);
   if (valid) {
-    float *op = native ? a.out + dst : a.rstore + static_cast<int64_t>(o) * W * a.Npad + rs;
+    const OutStore &st = native ? so : sr;
+    const int64_t e0 = native ? dst : rs;
     const int64_t ld = native ? a.ld_out : a.Npad;
     if (PRED) {
       const float *tp = dyn + lane * S;
-      for (int r = 0; r < W; ++r) op[r * ld] = tp[r];
+      for (int r = 0; r < W; ++r) st.put(e0 + r * ld, tp[r]);
       x = tp[W - 2];
       y = tp[W - 1];
     } else if (par) {
@@ -647,8 +676,8 @@ __global__ __launch_bounds__(64 * NW, 7) void place_kernel(FusedArgs a) {
           x = x + tx[0] + tx[T * PB] + tx[2 * T * PB];
           y = y - ty[0] + ty[T * PB] - ty[2 * T * PB];
         }
-        op[(2 * t) * ld] = x;
-        op[(2 * t + 1) * ld] = y;
+        st.put(e0 + (2 * t) * ld, x);
+        st.put(e0 + (2 * t + 1) * ld, y);
       }
     } else {
       x = static_cast<float>(st_s[0]);
@@ -659,8 +688,8 @@ __global__ __launch_bounds__(64 * NW, 7) void place_kernel(FusedArgs a) {
       for (int t = 0; t < T; ++t) {
         unicycle_step(x, y, phi, v, s0, c0, act[(2 * t) * PB + lane],
                       act[(2 * t + 1) * PB + lane], dt);
-        op[(2 * t) * ld] = x;
-        op[(2 * t + 1) * ld] = y;
+        st.put(e0 + (2 * t) * ld, x);
+        st.put(e0 + (2 * t + 1) * ld, y);
       }
     }
     if (!native) {
@@ -1044,10 +1073,11 @@ __global__ __launch_bounds__(kRThreads) void rare_copy_kernel(FusedArgs a) {
   if (own) {
     int before = pre[kr] + rank;
     for (int u = 0; u < w; ++u) before += wcnt[u][kr];
-    float *out = a.out + reg + bstart[kr] + before;
+    const OutStore so(a.out, a.wt != 0);
+    const int64_t e0 = reg + bstart[kr] + before;
 #pragma unroll
     for (int rr = 0; rr < 80; ++rr)
-      if (rr < rows) out[static_cast<int64_t>(rr) * a.ld_out] = v[rr];
+      if (rr < rows) so.put(e0 + static_cast<int64_t>(rr) * a.ld_out, v[rr]);
   }
   FUSED_TS(4, 4);
 }
@@ -1134,6 +1164,9 @@ inline int launch_place(const FusedArgs &a, int64_t n_ov, hipStream_t s) {
 // Small sampler clouds: P1 = sample_place_kernel (8-wave blocks, a few per CU); large ones and
 // the predictor's: place_kernel
 inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s) {
+  // write-through particle stores need every byte offset within the 31-bit buffer range
+  a.wt = (int64_t(8) * a.T * a.ld_out < (int64_t(1) << 31)) &&
+         (int64_t(8) * a.T * a.Npad < (int64_t(1) << 31));
   const dim3 zgrid(static_cast<unsigned>(a.nb0), static_cast<unsigned>(n_ov));
   if (a.pred)
     hipLaunchKernelGGL(latent_count_kernel<kZPred>, zgrid, dim3(kFThreads), 0, s, a);
