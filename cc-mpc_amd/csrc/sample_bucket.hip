@@ -709,6 +709,9 @@ __global__ __launch_bounds__(64 * NW, 7) void place_kernel(FusedArgs a) {
   FUSED_TS(1, 5);
 }
 
+// VR: the coordinate rows a thread holds (2T <= VR); KB: rare records per thread and round of
+// the key pass (T <= 8: 16 rows leave room for 16 records, a C2-shape rare list in one round)
+template <int VR, int KB>
 __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   __shared__ double2 gp_s[kFGroups * kMaxKept + 1];  // the OV's centre partials [g][k], -0.0
   __shared__ int hist[kFusedMaxBins];             // rare particles per bin in slots >= r0
@@ -736,9 +739,9 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
   const int r = r0 + tid;
   const float *src = a.rstore + static_cast<int64_t>(o) * 2 * T * a.Npad + (r < npad ? r : npad - 1);
-  float v[80];
+  float v[VR];
 #pragma unroll
-  for (int rr = 0; rr < 80; ++rr)
+  for (int rr = 0; rr < VR; ++rr)
     if (rr < rows) v[rr] = src[static_cast<int64_t>(rr) * npad];
   const int ng = a.G * K;
   const double2 *gp = reinterpret_cast<const double2 *>(a.gpart) + static_cast<int64_t>(o) * a.G * a.max_k;
@@ -747,7 +750,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
   // the first batch of rare records too: R is not known yet, so the slots are clamped into the
   // list's storage (a launch's first kB * 256 records cover the C2 shape's whole rare list)
   const float4 *info = reinterpret_cast<const float4 *>(a.rinfo) + static_cast<int64_t>(o) * npad;
-  constexpr int kB = CCMPC_RARE_BATCH;
+  constexpr int kB = KB;
   float4 f[kB];
 #pragma unroll
   for (int j = 0; j < kB; ++j) {
@@ -856,7 +859,7 @@ __global__ __launch_bounds__(kRThreads) void rare_place_kernel(FusedArgs a) {
     for (int u = 0; u < w; ++u) before += wcnt[u][kr];
     float *out = a.out + reg + bstart[kr] + before;
 #pragma unroll
-    for (int rr = 0; rr < 80; ++rr)
+    for (int rr = 0; rr < VR; ++rr)
       if (rr < rows) out[static_cast<int64_t>(rr) * a.ld_out] = v[rr];
   }
   FUSED_TS(2, 6);
@@ -1207,7 +1210,12 @@ inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s) {
   } else {
     const dim3 rgrid(static_cast<unsigned>((a.N + kRThreads - 1) / kRThreads),
                      static_cast<unsigned>(n_ov));
-    hipLaunchKernelGGL(rare_place_kernel, rgrid, dim3(kRThreads), 0, s, a);
+    if (a.T <= 8)
+      hipLaunchKernelGGL((rare_place_kernel<16, 2 * CCMPC_RARE_BATCH>), rgrid, dim3(kRThreads), 0,
+                         s, a);
+    else
+      hipLaunchKernelGGL((rare_place_kernel<80, CCMPC_RARE_BATCH>), rgrid, dim3(kRThreads), 0, s,
+                         a);
   }
   return CCMPC_OK;
 }
