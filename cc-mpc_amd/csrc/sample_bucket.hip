@@ -969,6 +969,7 @@ __global__ __launch_bounds__(kRThreads) void rare_key_kernel(FusedArgs a) {
 // starts) and its count in the P2 blocks before B; the keys of B's slots before r0 add the rest
 // of the count before this block; a scan of each wave's 64 keys gives the stable ranks.  Block 0
 // writes the cells' offsets, counts and pmf (and the invalid-id count).
+template <int VR>  // the coordinate rows a thread holds (2T <= VR), as rare_place_kernel
 __global__ __launch_bounds__(kRThreads) void rare_copy_kernel(FusedArgs a) {
   __shared__ int binsum[kFusedMaxBins];   // rare particles per bin, whole OV
   __shared__ int pre[kFusedMaxBins];      // ... in rare-list slots before this block's
@@ -991,9 +992,9 @@ __global__ __launch_bounds__(kRThreads) void rare_copy_kernel(FusedArgs a) {
   const int32_t *kb = a.kbuf + static_cast<int64_t>(o) * npad;
   const int kown = kb[rc];
   const float *src = a.rstore + static_cast<int64_t>(o) * rows * a.Npad + rc;
-  float v[80];
+  float v[VR];
 #pragma unroll
-  for (int rr = 0; rr < 80; ++rr)
+  for (int rr = 0; rr < VR; ++rr)
     if (rr < rows) v[rr] = src[static_cast<int64_t>(rr) * npad];
   constexpr int kPre = kKeySlots / kRThreads - 1;  // B's slots before r0: up to 3 per thread
   int pk[kPre];
@@ -1079,7 +1080,7 @@ __global__ __launch_bounds__(kRThreads) void rare_copy_kernel(FusedArgs a) {
     const OutStore so(a.out, a.wt != 0);
     const int64_t e0 = reg + bstart[kr] + before;
 #pragma unroll
-    for (int rr = 0; rr < 80; ++rr)
+    for (int rr = 0; rr < VR; ++rr)
       if (rr < rows) so.put(e0 + static_cast<int64_t>(rr) * a.ld_out, v[rr]);
   }
   FUSED_TS(4, 4);
@@ -1206,7 +1207,10 @@ inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s) {
     hipLaunchKernelGGL(rare_key_kernel, kgrid, dim3(kRThreads), 0, s, a);
     const dim3 cgrid(static_cast<unsigned>((a.Npad + kRThreads - 1) / kRThreads),
                      static_cast<unsigned>(n_ov));
-    hipLaunchKernelGGL(rare_copy_kernel, cgrid, dim3(kRThreads), 0, s, a);
+    if (a.T <= 8)
+      hipLaunchKernelGGL(rare_copy_kernel<16>, cgrid, dim3(kRThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL(rare_copy_kernel<80>, cgrid, dim3(kRThreads), 0, s, a);
   } else {
     const dim3 rgrid(static_cast<unsigned>((a.N + kRThreads - 1) / kRThreads),
                      static_cast<unsigned>(n_ov));
