@@ -10,5 +10,5 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 timeout -k 10 600 python -u bench.py > gpurun_out/final${T}_bench.json 2> gpurun_out/final${T}_bench.err
 timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/final${T}_bench_steps20.json 2> gpurun_out/final${T}_bench_steps20.err
 if [ -n "${ROCPROF:-}" ]; then
-  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/final${T}_prof -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu > gpurun_out/final${T}_bench_rocprof_run.json 2> gpurun_out/final${T}_rocprof.err
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final${T}_prof -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu > gpurun_out/final${T}_bench_rocprof_run.json 2> gpurun_out/final${T}_rocprof.err
 fi
