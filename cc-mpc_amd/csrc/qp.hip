@@ -1634,11 +1634,20 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #pragma unroll
           for (int i = 0; i < NM; ++i)
             if (i < n) dj = fma(Jm[i * ldm + li], mvec[i], dj);
+          // back substitution with this lane's row of R and 1 / R_jj read from LDS up front
+          // (independent loads), the chain unrolled over j: a broadcast and an FMA per column
+          // instead of a dependent LDS round trip (the same operations, the same bits)
           double rhs = dj, rk = 0.0;
-          for (int j = q - 1; j >= 0; --j) {
-            const double xj = lane_bcast(rhs, j) * Rdi[j];
+          double Rrow[NM];
+#pragma unroll
+          for (int k = 0; k < NM; ++k) Rrow[k] = Rm[li * ldm + k];
+          const double rdl = Rdi[li];
+#pragma unroll
+          for (int j = NM - 1; j >= 0; --j) {
+            if (j >= q) continue;  // uniform
+            const double xj = lane_bcast(rhs, j) * lane_bcast(rdl, j);
             if (lane == j) rk = xj;
-            if (lane < j) rhs = fma(-Rm[lane * ldm + j], xj, rhs);
+            if (lane < j) rhs = fma(-Rrow[j], xj, rhs);
           }
           GI_ACC(1);
           double dd[NM];
@@ -1745,26 +1754,18 @@ __global__ __launch_bounds__(64 * NW) void mpc_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int i = 0; i < NM; ++i) Rc[i] = (i < q) ? Rm[i * ldm + col] : 0.0;
           }
-          for (int k = l; k < q - 1; ++k) {
-            double a = 0.0, b = 0.0;
+          // (k unrolled: registers indexed directly, no select over the whole row per rotation)
 #pragma unroll
-            for (int i = 0; i < NM - 1; ++i)
-              if (i == k) {
-                a = Rc[i];
-                b = Rc[i + 1];
-              }
+          for (int k = 0; k < NM - 1; ++k) {
+            if (k < l || k >= q - 1) continue;  // uniform
             double c, s, h;
-            givens(lane_bcast(a, k), lane_bcast(b, k), c, s, h);
-#pragma unroll
-            for (int i = 0; i < NM - 1; ++i)
-              if (i == k) {
-                const double r0 = Rc[i], r1 = Rc[i + 1];
-                Rc[i] = fma(c, r0, s * r1);
-                Rc[i + 1] = fma(-s, r0, c * r1);
-                const double x0 = Jrow[i], x1 = Jrow[i + 1];
-                Jrow[i] = fma(c, x0, s * x1);
-                Jrow[i + 1] = fma(-s, x0, c * x1);
-              }
+            givens(lane_bcast(Rc[k], k), lane_bcast(Rc[k + 1], k), c, s, h);
+            const double r0 = Rc[k], r1 = Rc[k + 1];
+            Rc[k] = fma(c, r0, s * r1);
+            Rc[k + 1] = fma(-s, r0, c * r1);
+            const double x0 = Jrow[k], x1 = Jrow[k + 1];
+            Jrow[k] = fma(c, x0, s * x1);
+            Jrow[k + 1] = fma(-s, x0, c * x1);
           }
           double rdg = 1.0;
 #pragma unroll

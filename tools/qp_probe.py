@@ -5,6 +5,8 @@ hand-overs to the IPM show.
     python tools/qp_probe.py [T] [scenes]
 
 QP_ONE=1: one solve per setting, no timing (for the CCMPC_QP_TRACE build's printf phases).
+QP_FIRST=k: start at the batch's scene k (QP_ONE with scenes = 1: that scene alone).
+QP_ITERS=1: print every scene's verdict and iteration count (gi default).
 """
 import os
 import sys
@@ -24,7 +26,8 @@ def main():
     from ccmpc import cycle, engine, mpc, synthetic
     dev = torch.device("cuda", 0)
     cells, K, cps, x0s, goals, refs = [], [], [], [], [], []
-    for sc in range(scenes):
+    first = int(os.environ.get("QP_FIRST", "0"))   # the batch's scenes first .. first + scenes - 1
+    for sc in range(first, first + scenes):
         c, k, ref, goal, x0, _ = synthetic.crossing_scene(20251015 + 5000 + sc, O=2, N=5000, T=T)
         cells += c
         K.append(k)
@@ -56,6 +59,8 @@ def main():
             t = bench.time_kernel_live(fn, dev, per_graph=5, replays=5)
             fn()
         st, it = qp.status.cpu().numpy(), qp.iters.cpu().numpy()
+        if os.environ.get("QP_ITERS") and name == "gi (default)":
+            print("scene status iters:", [(i, int(st[i]), int(it[i])) for i in range(len(st))])
         u = qp.u.cpu().numpy()
         ok = st == mpc.QP_OK
         line = (f"{name:14s} {t * 1e6:8.1f} us  solved {ok.sum():3d}  infeasible "
