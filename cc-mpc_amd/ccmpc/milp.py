@@ -19,6 +19,8 @@ reference's constraint list with any variable type that supports + * >= (docplex
 `coo` gives the same rows as a sparse G z >= h for a batched QP/MILP assembly, and
 `satisfied` evaluates them numerically.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -497,6 +499,10 @@ class MilpBnB:
         return best
 
 
+# CCMPC_MILP_ROUND_GRAPH=0: every round's launches issued one by one (A/B)
+_ROUND_GRAPHS = os.environ.get("CCMPC_MILP_ROUND_GRAPH", "1") == "1"
+
+
 class _RoundIO:
     """A branch-and-bound round's device side for S nodes of `cells` record cells: the batched
     PlanningQP, its inputs and outputs as pinned packs (step.Pack), the LTV model repeated S
@@ -537,6 +543,21 @@ class _RoundIO:
         self.flags = torch.zeros(2, dtype=i64, pin_memory=True)
         self._flags = self.flags.numpy()
         self.gen, self.frame = 0, None
+        # the round's launches (copy-in, the solve, copy-out + signal) replay as one captured
+        # graph from the second round of this shape on (the first runs them eagerly, which also
+        # allocates everything the capture must not)
+        self.graph, self.runs = None, 0
+
+    def _enqueue(self):
+        from . import _lib, engine
+        lib, p, s = _lib.load(), engine._p, engine._stream()
+        i, o = self.inp, self.out
+        _lib.check(lib.ccmpc_copy_kernel_async(p(i.dev), p(i.host), i.nbytes, s),
+                   "ccmpc_copy_async")
+        self.qp.solve(self.gamma, self.xbar, i.d("goal"), i.d("ref"), i.d("rec"),
+                      u_prev=i.d("uprev") if self.Tf > self.T else None)
+        _lib.check(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
+                                               p(i.d("gen")), s), "ccmpc_copy_signal_async")
 
     def set_frame(self, bnb):
         """The frame's LTV model (device copies), goal, reference and executed controls."""
@@ -552,17 +573,20 @@ class _RoundIO:
     def run(self):
         """Records (already in the pinned pack) up, the batched solve, the answer down; returns
         host copies (status, u, X, cost)."""
-        from . import _lib, engine, step
-        lib, p, s = _lib.load(), engine._p, engine._stream()
+        from . import step
         i, o = self.inp, self.out
+        if self.graph is None and self.runs >= 1 and _ROUND_GRAPHS:
+            cap = torch.cuda.Stream(device=self.dev)
+            torch.cuda.current_stream(self.dev).synchronize()
+            cap.synchronize()
+            self.graph = step.HipGraph(self.dev, self._enqueue, cap)
         self.gen += 1
         i.h("gen")[0] = self.gen
-        _lib.check(lib.ccmpc_copy_kernel_async(p(i.dev), p(i.host), i.nbytes, s),
-                   "ccmpc_copy_async")
-        self.qp.solve(self.gamma, self.xbar, i.d("goal"), i.d("ref"), i.d("rec"),
-                      u_prev=i.d("uprev") if self.Tf > self.T else None)
-        _lib.check(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
-                                               p(i.d("gen")), s), "ccmpc_copy_signal_async")
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._enqueue()
+        self.runs += 1
         step.poll_word(self._flags, 0, self.gen, self.dev, "branch-and-bound round")
         return (o.h("status").copy(), o.h("u").copy(), o.h("X").copy(), o.h("cost").copy())
 
