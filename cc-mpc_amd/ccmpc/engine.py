@@ -244,14 +244,27 @@ def ideal_minkowski_cycle(prev_mean, prev_cov, src_cell, T, n_samples, ref_traj,
     return out_mean, out_cov, status, rec, pl
 
 
-def l4(store, past_last, bbox, with_yaw=False, with_vertices=False, split=True,
+# L4 in one workgroup per (cell, t) (ccmpc_l4, one launch) while the average cell holds at most
+# this many particles; the split form (ccmpc_l4_split, two launches) above it.  The two sum the
+# headings in different orders (same result to rounding), so the step graph and the eager calls
+# choose by this one rule.
+_L4_ONE_WG_MAX = int(os.environ.get("CCMPC_L4_ONE_WG_MAX", "8192"))
+
+
+def l4_one_workgroup(n_cells, n_bound):
+    return n_bound <= _L4_ONE_WG_MAX * max(int(n_cells), 1)
+
+
+def l4(store, past_last, bbox, with_yaw=False, with_vertices=False, split=None,
        workspace=None):
     """Headings, L4 outer approximation and t=0 yaw stats per (cell, t): ccmpc_l4_split (every
     (cell, t) over several workgroups, two launches) or, split=False, ccmpc_l4 (one workgroup
-    per (cell, t)).  Returns dict(A [C,T,4,2], b [C,T,4], yaw_mean [C,T], yaw0_var [C], yaw?,
-    vertices?)."""
+    per (cell, t)); split=None chooses by l4_one_workgroup.  Returns dict(A [C,T,4,2], b [C,T,4],
+    yaw_mean [C,T], yaw0_var [C], yaw?, vertices?)."""
     lib = _lib.load()
     C, T, dev = store.n_cells, store.T, store.device
+    if split is None:
+        split = not l4_one_workgroup(C, store.n_bound)
     out = dict(A=torch.empty((C, T, 4, 2), dtype=torch.float64, device=dev),
                b=torch.empty((C, T, 4), dtype=torch.float64, device=dev),
                yaw_mean=torch.empty((C, T), dtype=torch.float64, device=dev),

@@ -506,6 +506,12 @@ class StepGraph:
         i, o, q, st = self.inp, self.out, self.out_l4s[parity], self.store
         lws = self.l4_ws.buf
         chk = engine._lib.check
+        if engine.l4_one_workgroup(self.C, st.n_bound):
+            chk(lib.ccmpc_l4(p(st.pos), engine.F32, st.ld, self.ph, p(st.origin),
+                             p(o.d("off")), p(o.d("cnt")), self.C, p(i.d("past")),
+                             p(i.d("bbox")), p(q.d("A")), p(q.d("b")), p(q.d("yaw_mean")),
+                             p(q.d("yaw0_var")), None, None, s), "ccmpc_l4")
+            return
         chk(lib.ccmpc_l4_split(p(st.pos), engine.F32, st.ld, self.ph, p(st.origin),
                                p(o.d("off")), p(o.d("cnt")), self.C, st.n_bound,
                                p(i.d("past")), p(i.d("bbox")), p(lws), lws.numel(),

@@ -66,178 +66,13 @@ __device__ __forceinline__ double heading(const P *pos, int64_t ld, int t, int64
   return atan2(y - yp, x - xp);
 }
 
-__device__ __forceinline__ double block_sum(double v, double *red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  double s = 0.0;
-  const int nw = blockDim.x >> 6;
-  for (int k = 0; k < nw; ++k) s += red[k];
-  __syncthreads();
-  return s;
-}
-
-__device__ __forceinline__ double block_max(double v, double *red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  double s = -INFINITY;
-  const int nw = blockDim.x >> 6;
-  for (int k = 0; k < nw; ++k) s = fmax(s, red[k]);
-  __syncthreads();
-  return s;
-}
-
-// A particle's heading and the (cos, sin) of it.  cos(atan2(dy, dx)) = dx / r and sin = dy / r
-// with r = hypot(dx, dy): two divisions instead of a second transcendental (within 2 ulp of
-// cos / sin of the rounded atan2, far below the 1e-13 vertex tolerance); a zero step keeps
-// sincos of atan2, whose signed-zero cases the ratio cannot express.
-__device__ __forceinline__ void heading_cs(double dx, double dy, double &yaw, double &S, double &C) {
-#if CCMPC_L4_PROBE_NOATAN  // diagnostic build only: the transcendental's share of the kernel
-  yaw = dy * dx;
-#else
-  yaw = atan2(dy, dx);
-#endif
-  const double r = sqrt(dx * dx + dy * dy);
-  if (r > 0.0 && isfinite(r)) {
-    C = dx / r;
-    S = dy / r;
-  } else {
-    sincos(yaw, &S, &C);
-  }
-}
-
 #ifndef CCMPC_L4_THREADS
-#define CCMPC_L4_THREADS 512
+#define CCMPC_L4_THREADS 1024
 #endif
-constexpr int kL4Threads = CCMPC_L4_THREADS;  // 8 waves: 2 per SIMD, f64 chains overlap
-constexpr int kL4Cache = 12;     // headings kept in registers between the passes (6144 particles)
-
-template <typename P>
-__global__ __launch_bounds__(kL4Threads) void l4_kernel(
-    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
-    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
-    const double *__restrict__ past_last, const double *__restrict__ bbox,
-    double *__restrict__ out_A, double *__restrict__ out_b, double *__restrict__ out_yaw_mean,
-    double *__restrict__ out_yaw0_var, double *__restrict__ out_yaw,
-    double *__restrict__ out_vertices) {
-  __shared__ double red[16];
-  L4_TS(0);
-  const int cell = blockIdx.x / T, t = blockIdx.x % T;
-  const int64_t off = cell_off[cell], n = cell_cnt[cell];
-  const double o0 = origin ? origin[2 * cell] : 0.0, o1 = origin ? origin[2 * cell + 1] : 0.0;
-  const double px = past_last[2 * cell], py = past_last[2 * cell + 1];
-  const double lon = bbox[2 * cell], lat = bbox[2 * cell + 1];
-  const P *base = pos + off;
-  const int nth = blockDim.x;
-
-  // the step delta of particle i (step 0 measured from past[-1], ovehicle.py:72-76)
-  auto delta = [&](int64_t i, double &x, double &y, double &dx, double &dy) {
-    x = world(base, ld, 2 * t, i, o0);
-    y = world(base, ld, 2 * t + 1, i, o1);
-    const double xp = t == 0 ? px : world(base, ld, 2 * t - 2, i, o0);
-    const double yp = t == 0 ? py : world(base, ld, 2 * t - 1, i, o1);
-    dx = x - xp;
-    dy = y - yp;
-  };
-
-  // pass 1: headings, mean (and the t = 0 variance, shifted by the first particle's heading);
-  // the first kL4Cache headings of each thread (and their cos / sin) stay in registers
-  double s = 0.0, s1 = 0.0, s2 = 0.0;
-  const double shift = (t == 0 && n > 0) ? heading(base, ld, 0, 0, o0, o1, px, py) : 0.0;
-  double yc[kL4Cache], sc[kL4Cache], cc[kL4Cache], xc[kL4Cache], vc[kL4Cache];
-  auto take = [&](int64_t i, double y) {
-    s += y;
-    if (t == 0) {
-      const double d = y - shift;
-      s1 += d;
-      s2 += d * d;
-    }
-    if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + off + i] = y;
-  };
-#pragma unroll
-  for (int j = 0; j < kL4Cache; ++j) {
-    const int64_t i = threadIdx.x + static_cast<int64_t>(j) * nth;
-    if (i < n) {
-      double dx, dy;
-      delta(i, xc[j], vc[j], dx, dy);
-      heading_cs(dx, dy, yc[j], sc[j], cc[j]);
-      take(i, yc[j]);
-    }
-  }
-  for (int64_t i = threadIdx.x + static_cast<int64_t>(kL4Cache) * nth; i < n; i += nth) {
-    double x, y, dx, dy;
-    delta(i, x, y, dx, dy);
-    take(i, atan2(dy, dx));
-  }
-  L4_TS(1);
-  const double nn = static_cast<double>(n);
-  const double theta = block_sum(s, red) / nn;
-  L4_TS(2);
-  if (t == 0) {
-    const double a = block_sum(s1, red), b2 = block_sum(s2, red);
-    if (threadIdx.x == 0) out_yaw0_var[cell] = (b2 - a * a / nn) / (nn - 1.0);
-  }
-
-  L4_TS(3);
-  // pass 2: corners and the four support values of A = [I; -I] R(theta)
-  const double ct = cos(theta), st = sin(theta);
-  const double A[4][2] = {{ct, st}, {-st, ct}, {-ct, -st}, {st, -ct}};
-  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  auto corners = [&](int64_t i, double x, double y, double S, double C) {
-    // rows of Rot per corner (midlevel/util.py:109-118), disp = 0.5 * Rot @ [lon, lat]
-    const double dx[4] = {0.5 * (C * lon + S * lat), 0.5 * (C * lon - S * lat),
-                          0.5 * (-C * lon - S * lat), 0.5 * (-C * lon + S * lat)};
-    const double dy[4] = {0.5 * (S * lon - C * lat), 0.5 * (S * lon + C * lat),
-                          0.5 * (-S * lon + C * lat), 0.5 * (-S * lon - C * lat)};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double vx = x + dx[c], vy = y + dy[c];
-      if (out_vertices) {
-        double *vp = out_vertices + (static_cast<int64_t>(t) * 8 + 2 * c) * ld + off + i;
-        vp[0] = vx;
-        vp[ld] = vy;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx[r] = fmax(mx[r], A[r][0] * vx + A[r][1] * vy);
-    }
-  };
-#pragma unroll
-  for (int j = 0; j < kL4Cache; ++j) {
-    const int64_t i = threadIdx.x + static_cast<int64_t>(j) * nth;
-    if (i < n) corners(i, xc[j], vc[j], sc[j], cc[j]);
-  }
-  for (int64_t i = threadIdx.x + static_cast<int64_t>(kL4Cache) * nth; i < n; i += nth) {
-    double x, y, dx, dy, S, C;
-    delta(i, x, y, dx, dy);
-    const double r = sqrt(dx * dx + dy * dy);
-    if (r > 0.0 && isfinite(r)) {  // cos / sin of the heading without the atan2 (heading_cs)
-      C = dx / r;
-      S = dy / r;
-    } else {
-      sincos(atan2(dy, dx), &S, &C);
-    }
-    corners(i, x, y, S, C);
-  }
-  L4_TS(4);
-  double bm[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) bm[r] = block_max(mx[r], red);
-  L4_TS(5);
-  if (threadIdx.x == 0) {
-    const int64_t ct_idx = static_cast<int64_t>(cell) * T + t;
-    for (int r = 0; r < 4; ++r) {
-      out_A[ct_idx * 8 + 2 * r] = A[r][0];
-      out_A[ct_idx * 8 + 2 * r + 1] = A[r][1];
-      out_b[ct_idx * 4 + r] = bm[r];
-    }
-    out_yaw_mean[ct_idx] = theta;
-  }
-}
+// one workgroup per (cell, t): 16 waves, 4 per SIMD, so the f64 atan2 chains of a 5000-particle
+// cell overlap (C2 step: 14.8 us against 16.2 at 512 threads, profiles/r06/probes/l4wg_*)
+constexpr int kL4Threads = CCMPC_L4_THREADS;
+constexpr int kL4Cache = 5120 / kL4Threads;  // particles per thread kept in registers between passes
 
 // ---- split over workgroups: every (cell, t) on S workgroups ------------------------------------
 // One workgroup per (cell, t) is issue-bound on its f64 atan2 / division work for large clouds
@@ -285,7 +120,7 @@ constexpr int kL4MaxSplit = 64;  // workgroups per (cell, t): one wave holds the
 #define CCMPC_L4_SPLIT_CHUNK 2048
 #endif
 #ifndef CCMPC_L4_SPLIT_THREADS  // threads per split workgroup (build knob)
-#define CCMPC_L4_SPLIT_THREADS kL4Threads
+#define CCMPC_L4_SPLIT_THREADS 512
 #endif
 constexpr int kL4SplitThreads = CCMPC_L4_SPLIT_THREADS;
 
@@ -516,6 +351,108 @@ __device__ __forceinline__ void write_corners(double x, double y, double S, doub
   for (int k = 0; k < 4; ++k) {
     vp[2 * k * ld] = x + ddx[k];
     vp[(2 * k + 1) * ld] = y + ddy[k];
+  }
+}
+
+// One workgroup per (cell, t) (ccmpc_l4): pass 1's headings and pass 2's support maxima in one
+// launch with no hand-off; the first kL4Cache particles of each thread keep their position and
+// heading cos / sin in registers between the passes.  The split form's arithmetic (rsqrt cos /
+// sin, the closed-form box support); the mean heading's sum runs over the workgroup's threads in
+// one order (block_sums), so it differs from the split form's chunk order by rounding only.
+template <typename P>
+__global__ __launch_bounds__(kL4Threads) void l4_kernel(
+    const P *__restrict__ pos, int64_t ld, int T, const double *__restrict__ origin,
+    const int64_t *__restrict__ cell_off, const int64_t *__restrict__ cell_cnt,
+    const double *__restrict__ past_last, const double *__restrict__ bbox,
+    double *__restrict__ out_A, double *__restrict__ out_b, double *__restrict__ out_yaw_mean,
+    double *__restrict__ out_yaw0_var, double *__restrict__ out_yaw,
+    double *__restrict__ out_vertices) {
+  __shared__ double red[64];
+  L4_TS(0);
+  L4Split one{};
+  one.S = 1;
+  const L4Cell c = l4_cell(one, T, blockIdx.x, origin, cell_off, cell_cnt, past_last);
+  const int t = c.t;
+  const int64_t n = c.n, off = c.off;
+  const double lon = bbox[2 * c.cell], lat = bbox[2 * c.cell + 1];
+  const P *base = pos + off;
+  const int nth = blockDim.x;
+
+  // pass 1: headings, mean (and the t = 0 variance, shifted by the first particle's heading)
+  const double shift = (t == 0 && n > 0) ? heading(base, ld, 0, 0, c.o0, c.o1, c.px, c.py) : 0.0;
+  double v[3] = {0.0, 0.0, 0.0};
+  auto take = [&](int64_t i, double y) {
+    v[0] += y;
+    if (t == 0) {
+      const double d = y - shift;
+      v[1] += d;
+      v[2] += d * d;
+    }
+    if (out_yaw) out_yaw[static_cast<int64_t>(t) * ld + off + i] = y;
+  };
+  double xc[kL4Cache], yc[kL4Cache], dxc[kL4Cache], dyc[kL4Cache];
+#pragma unroll
+  for (int j = 0; j < kL4Cache; ++j) {   // every cached particle's loads first
+    const int64_t i = threadIdx.x + static_cast<int64_t>(j) * nth;
+    if (i < n) step_delta(base, ld, c, i, dxc[j], dyc[j], &xc[j], &yc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < kL4Cache; ++j) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(j) * nth;
+#if CCMPC_L4_PROBE_NOATAN  // diagnostic build only: the transcendental's share of the kernel
+    if (i < n) take(i, dyc[j] * dxc[j]);
+#else
+    if (i < n) take(i, atan2(dyc[j], dxc[j]));
+#endif
+  }
+  for (int64_t i = threadIdx.x + static_cast<int64_t>(kL4Cache) * nth; i < n; i += nth) {
+    double dx, dy;
+    step_delta(base, ld, c, i, dx, dy);
+    take(i, atan2(dy, dx));
+  }
+  L4_TS(1);
+  if (t == 0)
+    block_sums<3>(v, red);
+  else
+    block_sums<1>(reinterpret_cast<double(&)[1]>(v), red);
+  const double nn = static_cast<double>(n);
+  const double theta = v[0] / nn;
+  L4_TS(2);
+  if (t == 0 && threadIdx.x == 0) out_yaw0_var[c.cell] = (v[2] - v[1] * v[1] / nn) / (nn - 1.0);
+  L4_TS(3);
+  // pass 2: the four support values of A = [I; -I] R(theta) over every particle's box
+  double A[4][2];
+  support_rows(theta, A);
+  double mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  double *vbase = out_vertices ? out_vertices + static_cast<int64_t>(t) * 8 * ld + off : nullptr;
+#pragma unroll
+  for (int j = 0; j < kL4Cache; ++j) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(j) * nth;
+    if (i < n) {
+      double S, C;
+      heading_cs_rsq(dxc[j], dyc[j], S, C);
+      support_max(xc[j], yc[j], S, C, lon, lat, A[0][0], A[0][1], mx);
+      if (vbase) write_corners(xc[j], yc[j], S, C, lon, lat, vbase + i, ld);
+    }
+  }
+  for (int64_t i = threadIdx.x + static_cast<int64_t>(kL4Cache) * nth; i < n; i += nth) {
+    double x, y, dx, dy, S, C;
+    step_delta(base, ld, c, i, dx, dy, &x, &y);
+    heading_cs_rsq(dx, dy, S, C);
+    support_max(x, y, S, C, lon, lat, A[0][0], A[0][1], mx);
+    if (vbase) write_corners(x, y, S, C, lon, lat, vbase + i, ld);
+  }
+  L4_TS(4);
+  block_max4(mx, red);
+  L4_TS(5);
+  if (threadIdx.x == 0) {
+    const int64_t ct_idx = static_cast<int64_t>(c.cell) * T + t;
+    for (int r = 0; r < 4; ++r) {
+      out_A[ct_idx * 8 + 2 * r] = A[r][0];
+      out_A[ct_idx * 8 + 2 * r + 1] = A[r][1];
+      out_b[ct_idx * 4 + r] = mx[r];
+    }
+    out_yaw_mean[ct_idx] = theta;
   }
 }
 

@@ -344,8 +344,8 @@ def test_l4_split_equals_one_workgroup_form(gpu, dtype, T, N):
     bbox = np.tile([4.5, 2.5], (store.n_cells, 1))
     one = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, split=False)
     ws = engine.Workspace(gpu)
-    a = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, workspace=ws)
-    b = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, workspace=ws)
+    a = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, split=True, workspace=ws)
+    b = engine.l4(store, past, bbox, with_yaw=True, with_vertices=True, split=True, workspace=ws)
     cols = torch.as_tensor(np.concatenate([np.arange(o, o + n) for o, n in
                                            zip(store.offsets, store.counts)]), device=gpu)
     for x in (one, a, b):       # the per-particle outputs, at the particles' slots only

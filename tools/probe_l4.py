@@ -32,14 +32,15 @@ def main():
                                 gmm=gmm, N=N, seed=1), eps, ph, ref, minpos, pasts)
     g = next(iter(agent._graphs.values()))
     lib, p, o, i, st = engine._lib.load(), engine._p, g.out, g.inp, g.store
+    q = g.out_l4s[0]
     lib.ccmpc_probe_l4_timestamps.restype = ctypes.c_int
     lib.ccmpc_probe_l4_timestamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 
     def l4():
         engine._lib.check(lib.ccmpc_l4(
             p(st.pos), engine.F32, st.ld, ph, p(st.origin), p(o.d("off")), p(o.d("cnt")), g.C,
-            p(i.d("past")), p(i.d("bbox")), p(o.d("A")), p(o.d("b")), p(o.d("yaw_mean")),
-            p(o.d("yaw0_var")), None, None, engine._stream()), "ccmpc_l4")
+            p(i.d("past")), p(i.d("bbox")), p(q.d("A")), p(q.d("b")), p(q.d("yaw_mean")),
+            p(q.d("yaw0_var")), None, None, engine._stream()), "ccmpc_l4")
     for _ in range(5):
         l4()
     torch.cuda.synchronize()
@@ -59,7 +60,7 @@ def main():
     print("  pass 2    ", stats(rel[:, 4] - rel[:, 3]))
     print("  maxima    ", stats(rel[:, 5] - rel[:, 4]))
     print("  end at    ", stats(rel[:, 5]))
-    counts = o.h("cnt") if False else g.out.d("cnt").cpu().numpy()
+    counts = g.out.d("cnt").cpu().numpy()
     order = np.argsort(rel[:, 5])[::-1][:12]
     print("  slowest (wg = cell*T + t: cell count, start, pass1, end):",
           [(int(w), int(counts[w // ph]), round(rel[w, 0] / 100, 1),
