@@ -337,41 +337,48 @@ class MilpBnB:
 
     # ---- one round -------------------------------------------------------------------------
     def _records(self, nodes):
-        """(S, Cb + C + F, T) compact affine records of the nodes' relaxations."""
-        S, T, Cb, C = len(nodes), self.T, self.Cb, self.C
+        """(S, Cb + C + F, T) compact affine records of the nodes' relaxations (every node's
+        rows at once: the fixed faces and polytopes gathered into index arrays)."""
+        S, T, Cb, C, seg = len(nodes), self.T, self.Cb, self.C, self.seg
         rec = np.zeros((S, Cb + C + self.F, T), _GATHER)
         rec["status"] = 1                                   # left out unless set below
         rec["t_tau"] = np.arange(T)
-        seg = self.seg
-        for s, (faces, segs) in enumerate(nodes):
-            if Cb:
-                shift = np.zeros(T)
-                keep = self.blive.copy()
-                for t in range(T):
-                    if seg is None:
-                        continue
-                    if t in segs:
-                        shift[t] = 0.0 if seg.junction[segs[t]] else self.M
-                    elif seg.any_open:      # a free step: S_t may relax the sbig '<=' rows
-                        keep[:, t] &= ~(self.bsbig[:, t] & (self.bside[:, t] == -1))
-                b = rec[s, :Cb]
-                b["n0"], b["n1"] = self.bn[..., 0], self.bn[..., 1]
-                b["rhs"] = self.brhs + np.where(self.bsbig, shift[None, :], 0.0)
-                b["side"] = self.bside
-                b["status"] = np.where(keep, 0, 1)
-            for (c, t), l in faces.items():
-                if seg is not None and t not in segs and seg.any_open:
-                    continue                                # S_t may relax it
-                st = self.M if (seg is not None and t in segs and not seg.junction[segs[t]]) \
-                    else 0.0
-                r = rec[s, Cb + c, t]
-                r["n0"], r["n1"] = self.fA[c, t, l]
-                r["rhs"], r["side"], r["status"] = self.frhs[c, t, l] - st, 1, 0
+        fixed = np.full((S, T), -1, np.int64)               # each step's fixed polytope, or -1
+        for s, (_, segs) in enumerate(nodes):
             for t, i in segs.items():
-                r = rec[s, Cb + C:, t]
-                r["n0"], r["n1"] = seg.A[i, :, 0], seg.A[i, :, 1]
-                r["rhs"], r["side"] = seg.b[i], -1
-                r["status"] = np.where(seg.live[i], 0, 1)
+                fixed[s, t] = i
+        isfix = fixed >= 0
+        if seg is not None:                                 # S_t: M_big on a fixed non-junction
+            shift = np.where(isfix & ~seg.junction[np.maximum(fixed, 0)], self.M, 0.0)
+        else:
+            shift = np.zeros((S, T))
+        if Cb:
+            keep = np.broadcast_to(self.blive, (S, Cb, T))
+            if seg is not None and seg.any_open:    # a free step: S_t may relax the sbig '<='
+                keep = keep & ~((self.bsbig & (self.bside == -1))[None] & ~isfix[:, None, :])
+            b = rec[:, :Cb]
+            b["n0"], b["n1"] = self.bn[None, ..., 0], self.bn[None, ..., 1]
+            b["rhs"] = self.brhs[None] + np.where(self.bsbig[None], shift[:, None, :], 0.0)
+            b["side"] = self.bside[None]
+            b["status"] = np.where(keep, 0, 1)
+        fe = [(s, c, t, l) for s, (faces, _) in enumerate(nodes) for (c, t), l in faces.items()]
+        if fe:
+            s_, c_, t_, l_ = np.array(fe, np.int64).T
+            if seg is not None and seg.any_open:            # S_t may relax it: left out
+                k = isfix[s_, t_]
+                s_, c_, t_, l_ = s_[k], c_[k], t_[k], l_[k]
+            at = (s_, Cb + c_, t_)
+            rec["n0"][at], rec["n1"][at] = self.fA[c_, t_, l_, 0], self.fA[c_, t_, l_, 1]
+            rec["rhs"][at] = self.frhs[c_, t_, l_] - shift[s_, t_]
+            rec["side"][at], rec["status"][at] = 1, 0
+        se = [(s, t, i) for s, (_, segs) in enumerate(nodes) for t, i in segs.items()]
+        if se:
+            s_, t_, i_ = (x[:, None] for x in np.array(se, np.int64).T)
+            at = (s_, Cb + C + np.arange(self.F)[None, :], t_)
+            i_ = i_[:, 0]
+            rec["n0"][at], rec["n1"][at] = seg.A[i_, :, 0], seg.A[i_, :, 1]
+            rec["rhs"][at], rec["side"][at] = seg.b[i_], -1
+            rec["status"][at] = np.where(seg.live[i_], 0, 1)
         return rec
 
     def _solve_batch(self, nodes):
