@@ -95,6 +95,19 @@ SIGNATURES = {
     "ccmpc_bucket_predictions_indirect": (ctypes.c_int, [_P, ctypes.c_int, _P, _I64, _I64, _I64,
                                                          _I64, _P, _P, _P, _I64, _P, _P, _P, _SZ,
                                                          _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "ccmpc_bucket_predictions_packed": (ctypes.c_int, [_P, _P, _SZ, _P, _P, ctypes.c_int, _P,
+                                                       _I64, _I64, _I64, _I64, _P, _P, _P, _I64,
+                                                       _P, _P, _P, _SZ, _P, _I64, _P, _P, _P, _P,
+                                                       _P, _P]),
+    "ccmpc_bucket_predictions_indirect_packed": (ctypes.c_int, [_P, _P, _SZ, _P, ctypes.c_int,
+                                                                _P, _I64, _I64, _I64, _I64, _P,
+                                                                _P, _P, _I64, _P, _P, _P, _SZ,
+                                                                _P, _I64, _P, _P, _P, _P, _P,
+                                                                _P]),
+    "ccmpc_sample_bucket_packed": (ctypes.c_int, [_P, _P, _SZ, _P, _P, _I64, _P, _I32, _P, _P,
+                                                  _I64, _I64, _I64, _D, _U64, _P, _I64, _P, _P,
+                                                  _P, _I64, _P, _P, _P, _SZ, _P, _P, _I64, _P,
+                                                  _P, _P, _P, _P]),
     "ccmpc_sample_bucket_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "ccmpc_sample_bucket": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P, _P, _I64, _I64, _I64, _D,
                                            _U64, _P, _I64, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P,

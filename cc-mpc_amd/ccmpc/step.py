@@ -50,6 +50,7 @@ import torch
 from . import _lib, engine, risk
 
 _ALIGN = 256
+_STEP_PACKED = int(os.environ.get("CCMPC_STEP_PACKED", "1"))
 
 
 class Pack:
@@ -376,10 +377,27 @@ class StepGraph:
         self._l4_snap = {}                  # generation -> snapshot of its L4 outputs
 
     # ---------------------------------------------------------------------------------------
-    def _sample_calls(self, s):
-        """The sampling + bucketing stage's C-ABI calls: [(fn, args)]."""
+    def _packed_p0(self):
+        """The input pack's copy in the placement's first launch (ccmpc_*_packed: the latent-id
+        pass reads its inputs from the pinned host side meanwhile) instead of a copy kernel of
+        its own -- for the fused placement of the predictor's output with the kernel copy, not
+        beside the ideal rollout (whose fork waits on the copy).  Measured (profiles/r06/ab/
+        packed_*): predictor output on the device, graph 64.8 -> 62.1 us at C2's shape with the
+        same record path; the synthetic sampler's route, whose latent draws then wait on host
+        reads of the CDF and seed, graph -1.4 us but record path +1.6 us, so not there.
+        CCMPC_STEP_PACKED=0: never; =2: the sampler's route too (A/B)."""
+        if not (_STEP_PACKED and self.fused and self.copy_kernel and self.kind != "ideal"):
+            return False
+        return self.source == "predictions" or _STEP_PACKED == 2
+
+    def _sample_calls(self, s, pack=None):
+        """The sampling + bucketing stage's C-ABI calls: [(fn, args)]; pack = (device side,
+        host side, bytes) of the input pack to copy in the placement's first launch."""
         lib, p = _lib.load(), engine._p
         i, o, st = self.inp, self.out, self.store
+        if pack is not None:
+            return [(getattr(lib, fn.__name__ + "_packed"), tuple(pack) + args)
+                    for fn, args in self._sample_calls(s)]
         O, N, T, L = self.O, self.N, self.ph, self.L
         ws = self.bucket_ws
         if self.source == "predictions":
@@ -437,7 +455,9 @@ class StepGraph:
         ev = self._ev[parity]
         chk = engine._lib.check
         copy = lib.ccmpc_copy_kernel_async if self.copy_kernel else lib.ccmpc_copy_async
-        chk(copy(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
+        packed = self._packed_p0()
+        if not packed:
+            chk(copy(p(i.dev), p(i.host), i.nbytes, s), "ccmpc_copy_async")
         main = torch.cuda.current_stream(self.device)
         if self.kind == "ideal":
             # the rollout needs only the saved moments: a branch beside the sampling
@@ -452,7 +472,8 @@ class StepGraph:
                     p(i.d("ref")), None, p(i.d("risk")), self.R, self.tol, self.maxiter,
                     p(o.d("imean")), p(o.d("icov")), p(o.d("status")), p(o.d("rec")),
                     p(o.d("pl")), engine._stream()), "ccmpc_ideal_minkowski_cycle_ex")
-        for fn, args in self._sample_calls(s):
+        for fn, args in self._sample_calls(s, (p(i.dev), p(i.host), i.nbytes) if packed
+                                           else None):
             chk(fn(*args), fn.__name__)
         mws = self.ws.buf
         if self.kind == "minkowski":

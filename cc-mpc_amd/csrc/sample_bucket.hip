@@ -192,17 +192,20 @@ __device__ __forceinline__ void write_z_bad(const FusedArgs &a, int o) {
 // there -- it is counted (and clamped for memory safety); the injected sampler ids must lie in
 // [0, L).
 template <int ZSRC>
-__global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
+__device__ __forceinline__ void latent_count_block(const FusedArgs &a, int bx, int o) {
   __shared__ double cdf_s[64];
   __shared__ int keep_s[64];
   __shared__ int wc_s[kFWaves][kMaxKept + 2];   // per wave: categories 0..K, then invalid ids
   FUSED_TS(0, 0);
-  const int o = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int K = a.n_kept[o], L = a.L;
   const int64_t N = a.N;
+  // the seed with the other loads (from the host side of the pack in copy_latent_count_kernel:
+  // a PCIe round trip, not to be paid twice)
+  const uint64_t seed = ZSRC == kZPhilox ? (a.seed_dev ? *a.seed_dev : a.seed) : 0;
   if (ZSRC == kZPhilox && tid < L) cdf_s[tid] = a.latent_cdf[static_cast<int64_t>(o) * L + tid];
   if (tid < L) keep_s[tid] = a.keep_map[o * L + tid];
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kFThreads + tid;
+  const int64_t i = static_cast<int64_t>(bx) * kFThreads + tid;
   const bool v = i < N;
   int z = 0;
   bool bad = false;
@@ -221,29 +224,28 @@ __global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
   }
   __syncthreads();
   if (ZSRC == kZPhilox && v)
-    z = draw_latent(i, a.ov_base + static_cast<uint32_t>(o), a.seed_dev ? *a.seed_dev : a.seed,
-                    cdf_s, L);
+    z = draw_latent(i, a.ov_base + static_cast<uint32_t>(o), seed, cdf_s, L);
   if (v) {
     a.zbuf[static_cast<int64_t>(o) * a.Npad + i] = z;
     if (a.out_z) a.out_z[static_cast<int64_t>(o) * N + i] = z;
   }
   const int kk = keep_s[z];
   const int cat = kk >= 0 ? kk : K;
-  const int g = blockIdx.x * kFWaves + w;
+  const int g = bx * kFWaves + w;
   int mine = 0;
   for (int c = 0; c <= K; ++c) {
     const int n = __popcll(__ballot(v && cat == c));
     if (lane == c) mine = n;
   }
   const int nbad = __popcll(__ballot(v && bad));
-  if (a.coef && blockIdx.x == 0)        // the OV's per-latent coefficient rows, for P1
+  if (a.coef && bx == 0)        // the OV's per-latent coefficient rows, for P1
     stage_gmm_coefs(a.gmm + static_cast<int64_t>(o) * L * a.T * 5, L * a.T,
                     a.coef + static_cast<int64_t>(o) * kActCoef, tid, kFThreads);
   if (g < a.G && lane <= K) a.gcnt[(static_cast<int64_t>(o) * a.G + g) * kCntStride + lane] = mine;
   if (lane <= K) wc_s[w][lane] = mine;
   if (lane == 0) wc_s[w][kMaxKept + 1] = nbad;
   __syncthreads();
-  int32_t *bs = a.bsum + (static_cast<int64_t>(o) * a.nb0 + blockIdx.x) * kCntStride;
+  int32_t *bs = a.bsum + (static_cast<int64_t>(o) * a.nb0 + bx) * kCntStride;
   if (tid <= K || tid == kBadSlot) {
     const int c = tid <= K ? tid : kMaxKept + 1;
     int s = 0;
@@ -252,6 +254,38 @@ __global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
     bs[tid] = s;
   }
   FUSED_TS(0, 1);
+}
+
+template <int ZSRC>
+__global__ __launch_bounds__(kFThreads) void latent_count_kernel(FusedArgs a) {
+  latent_count_block<ZSRC>(a, blockIdx.x, blockIdx.y);
+}
+
+// P0 in the same launch as the step's input copy (ccmpc_*_packed): blocks [0, ncopy) copy the
+// pinned host pack to its device side, the others are P0's blocks, whose FusedArgs (rebased by
+// the host) read their inputs -- latent CDF, keep map, seed, z -- from the host side of the pack
+// directly, so nothing in this launch waits on the copy.  One kernel boundary less on the step.
+template <int ZSRC>
+__global__ __launch_bounds__(kFThreads) void copy_latent_count_kernel(FusedArgs a, uint4 *dst,
+                                                                      const uint4 *src, size_t n,
+                                                                      int ncopy) {
+  if (static_cast<int>(blockIdx.x) < ncopy) {
+    constexpr int U = 4;  // loads in flight per thread before their stores (PCIe latency)
+    const size_t stride = static_cast<size_t>(ncopy) * blockDim.x;
+    for (size_t base = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; base < n;
+         base += U * stride) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (base + u * stride < n) v[u] = src[base + u * stride];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (base + u * stride < n) dst[base + u * stride] = v[u];
+    }
+    return;
+  }
+  const int b = static_cast<int>(blockIdx.x) - ncopy;
+  latent_count_block<ZSRC>(a, b % a.nb0, b / a.nb0);
 }
 
 // The category counts P1 block `blk` needs, into LDS (zeroed by the caller, the first batch of
@@ -1167,17 +1201,57 @@ inline int launch_place(const FusedArgs &a, int64_t n_ov, hipStream_t s) {
 // P0 -> P1 -> the rare stage, for either particle source (pred != nullptr: the predictor's).
 // Small sampler clouds: P1 = sample_place_kernel (8-wave blocks, a few per CU); large ones and
 // the predictor's: place_kernel
-inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s) {
+// The step's input pack: n 16-byte words from the pinned host side src to the device side dst
+struct PackCopy {
+  uint4 *dst;
+  const uint4 *src;
+  size_t n;
+};
+
+// p itself, or its image on the host side when it points into the pack's device side
+template <typename T>
+inline T *pack_host_image(T *p, const PackCopy &k) {
+  const char *c = reinterpret_cast<const char *>(p), *lo = reinterpret_cast<const char *>(k.dst);
+  if (!p || c < lo || c >= lo + 16 * k.n) return p;
+  return reinterpret_cast<T *>(
+      const_cast<char *>(reinterpret_cast<const char *>(k.src) + (c - lo)));
+}
+
+template <int ZSRC>
+inline void launch_latents(const FusedArgs &a, int64_t n_ov, const PackCopy *pk, hipStream_t s) {
+  if (!pk || pk->n == 0) {
+    const dim3 zgrid(static_cast<unsigned>(a.nb0), static_cast<unsigned>(n_ov));
+    hipLaunchKernelGGL(latent_count_kernel<ZSRC>, zgrid, dim3(kFThreads), 0, s, a);
+    return;
+  }
+  FusedArgs ah = a;  // P0's inputs from the host side of the pack
+  ah.latent_cdf = pack_host_image(a.latent_cdf, *pk);
+  ah.gmm = pack_host_image(a.gmm, *pk);
+  ah.z_in = pack_host_image(a.z_in, *pk);
+  ah.zsrc = pack_host_image(a.zsrc, *pk);
+  ah.rows = pack_host_image(a.rows, *pk);
+  ah.ptrs = pack_host_image(a.ptrs, *pk);
+  ah.seed_dev = pack_host_image(a.seed_dev, *pk);
+  ah.keep_map = pack_host_image(a.keep_map, *pk);
+  ah.n_kept = pack_host_image(a.n_kept, *pk);
+  const size_t per = static_cast<size_t>(kFThreads) * 4;
+  const int ncopy = static_cast<int>(std::min<size_t>(64, (pk->n + per - 1) / per));
+  const unsigned grid = static_cast<unsigned>(ncopy + a.nb0 * n_ov);
+  hipLaunchKernelGGL(copy_latent_count_kernel<ZSRC>, dim3(grid), dim3(kFThreads), 0, s, ah,
+                     pk->dst, pk->src, pk->n, ncopy);
+}
+
+inline int fused_launch(FusedArgs &a, int64_t n_ov, bool pp, hipStream_t s,
+                        const PackCopy *pk = nullptr) {
   // write-through particle stores need every byte offset within the 31-bit buffer range
   a.wt = (int64_t(8) * a.T * a.ld_out < (int64_t(1) << 31)) &&
          (int64_t(8) * a.T * a.Npad < (int64_t(1) << 31));
-  const dim3 zgrid(static_cast<unsigned>(a.nb0), static_cast<unsigned>(n_ov));
   if (a.pred)
-    hipLaunchKernelGGL(latent_count_kernel<kZPred>, zgrid, dim3(kFThreads), 0, s, a);
+    launch_latents<kZPred>(a, n_ov, pk, s);
   else if (a.z_in)
-    hipLaunchKernelGGL(latent_count_kernel<kZIn>, zgrid, dim3(kFThreads), 0, s, a);
+    launch_latents<kZIn>(a, n_ov, pk, s);
   else
-    hipLaunchKernelGGL(latent_count_kernel<kZPhilox>, zgrid, dim3(kFThreads), 0, s, a);
+    launch_latents<kZPhilox>(a, n_ov, pk, s);
   const bool eps = a.eps_in != nullptr;
   const dim3 grid(static_cast<unsigned>(a.G), static_cast<unsigned>(n_ov));
   int rc = CCMPC_OK;
@@ -1272,17 +1346,28 @@ extern "C" size_t ccmpc_sample_bucket_workspace_bytes(int64_t n_ov, int64_t N, i
   return fused_ws(n_ov, N, T, max_k).total;
 }
 
-extern "C" int ccmpc_sample_bucket(const double *init_state, const double *latent_cdf,
-                                   int64_t n_latent, const float *gmm, int32_t gmm_layout,
-                                   const int32_t *z_in, const float *eps_in, int64_t n_ov,
-                                   int64_t N, int64_t T, double dt, uint64_t seed,
-                                   const uint64_t *seed_dev, int64_t ov_base,
-                                   const int32_t *keep_map, const int32_t *n_kept,
-                                   const int32_t *cell_base, int64_t max_k, const double *minpos,
-                                   const int64_t *region, void *workspace,
-                                   size_t workspace_bytes, int32_t *out_z, float *pos_out,
-                                   int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,
-                                   double *cell_pmf, double *init_center, ccmpc_stream_t stream) {
+// The pack arguments of the *_packed entry points, checked
+static bool pack_args(void *pack_dev, const void *pack_host, size_t pack_bytes, PackCopy &pk) {
+  if (!pack_dev || !pack_host || pack_bytes % 16 != 0 || !aligned(pack_dev, 16) ||
+      !aligned(pack_host, 16)) {
+    set_error("pack: null, or bytes and pointers not 16-byte aligned");
+    return false;
+  }
+  pk = PackCopy{static_cast<uint4 *>(pack_dev), static_cast<const uint4 *>(pack_host),
+                pack_bytes / 16};
+  return true;
+}
+
+static int sample_bucket_impl(const double *init_state, const double *latent_cdf,
+                              int64_t n_latent, const float *gmm, int32_t gmm_layout,
+                              const int32_t *z_in, const float *eps_in, int64_t n_ov, int64_t N,
+                              int64_t T, double dt, uint64_t seed, const uint64_t *seed_dev,
+                              int64_t ov_base, const int32_t *keep_map, const int32_t *n_kept,
+                              const int32_t *cell_base, int64_t max_k, const double *minpos,
+                              const int64_t *region, void *workspace, size_t workspace_bytes,
+                              int32_t *out_z, float *pos_out, int64_t ld_out, int64_t *cell_off,
+                              int64_t *cell_cnt, double *cell_pmf, double *init_center,
+                              ccmpc_stream_t stream, const PackCopy *pk) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
   CCMPC_REQUIRE(N >= 1 && N <= kWideMaxN, "N must be in [1, 262144] (bucket.hip beyond)");
@@ -1334,10 +1419,34 @@ extern "C" int ccmpc_sample_bucket(const double *init_state, const double *laten
   a.init_center = init_center;
   if (N > kFusedMaxN && !pp && n_latent * T * 5 <= kActCoef)
     a.coef = reinterpret_cast<float *>(static_cast<char *>(workspace) + L.coef);
-  const int rc = fused_launch(a, n_ov, pp, as_stream(stream));
+  const int rc = fused_launch(a, n_ov, pp, as_stream(stream), pk);
   if (rc != CCMPC_OK) return rc;
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
+}
+
+#define CCMPC_SAMPLE_BUCKET_PARAMS                                                             \
+  const double *init_state, const double *latent_cdf, int64_t n_latent, const float *gmm,      \
+      int32_t gmm_layout, const int32_t *z_in, const float *eps_in, int64_t n_ov, int64_t N,   \
+      int64_t T, double dt, uint64_t seed, const uint64_t *seed_dev, int64_t ov_base,          \
+      const int32_t *keep_map, const int32_t *n_kept, const int32_t *cell_base, int64_t max_k, \
+      const double *minpos, const int64_t *region, void *workspace, size_t workspace_bytes,    \
+      int32_t *out_z, float *pos_out, int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,    \
+      double *cell_pmf, double *init_center, ccmpc_stream_t stream
+#define CCMPC_SAMPLE_BUCKET_ARGS                                                               \
+  init_state, latent_cdf, n_latent, gmm, gmm_layout, z_in, eps_in, n_ov, N, T, dt, seed,       \
+      seed_dev, ov_base, keep_map, n_kept, cell_base, max_k, minpos, region, workspace,        \
+      workspace_bytes, out_z, pos_out, ld_out, cell_off, cell_cnt, cell_pmf, init_center, stream
+
+extern "C" int ccmpc_sample_bucket(CCMPC_SAMPLE_BUCKET_PARAMS) {
+  return sample_bucket_impl(CCMPC_SAMPLE_BUCKET_ARGS, nullptr);
+}
+
+extern "C" int ccmpc_sample_bucket_packed(void *pack_dev, const void *pack_host,
+                                          size_t pack_bytes, CCMPC_SAMPLE_BUCKET_PARAMS) {
+  PackCopy pk;
+  if (!pack_args(pack_dev, pack_host, pack_bytes, pk)) return CCMPC_ERR_ARG;
+  return sample_bucket_impl(CCMPC_SAMPLE_BUCKET_ARGS, &pk);
 }
 
 static int bucket_predictions_impl(const float *pred, const void *z, const uint64_t *ptrs,
@@ -1348,7 +1457,7 @@ static int bucket_predictions_impl(const float *pred, const void *z, const uint6
                                    void *workspace, size_t workspace_bytes, float *pos_out,
                                    int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,
                                    double *cell_pmf, double *init_center, int32_t *z_bad,
-                                   ccmpc_stream_t stream) {
+                                   ccmpc_stream_t stream, const PackCopy *pk = nullptr) {
   CCMPC_REQUIRE(T >= 1 && T <= 40, "T must be in [1, 40]");
   CCMPC_REQUIRE(n_latent >= 1 && n_latent <= 64, "n_latent must be in [1, 64]");
   CCMPC_REQUIRE(N >= 1 && N <= kWideMaxN, "N must be in [1, 262144] (ccmpc_load_predictions + "
@@ -1390,7 +1499,7 @@ static int bucket_predictions_impl(const float *pred, const void *z, const uint6
   a.cell_pmf = cell_pmf;
   a.init_center = init_center;
   a.z_bad = z_bad;
-  const int rc = fused_launch(a, n_ov, false, as_stream(stream));
+  const int rc = fused_launch(a, n_ov, false, as_stream(stream), pk);
   if (rc != CCMPC_OK) return rc;
   CCMPC_LAUNCH_CHECK();
   return CCMPC_OK;
@@ -1428,4 +1537,35 @@ extern "C" int ccmpc_bucket_predictions_indirect(const uint64_t *ptrs, int z_byt
                                  keep_map, n_kept, cell_base, max_k, minpos, region, workspace,
                                  workspace_bytes, pos_out, ld_out, cell_off, cell_cnt, cell_pmf,
                                  init_center, z_bad, stream);
+}
+
+extern "C" int ccmpc_bucket_predictions_packed(
+    void *pack_dev, const void *pack_host, size_t pack_bytes, const float *pred, const void *z,
+    int z_bytes, const int32_t *rows, int64_t n_ov, int64_t N, int64_t T, int64_t n_latent,
+    const int32_t *keep_map, const int32_t *n_kept, const int32_t *cell_base, int64_t max_k,
+    const double *minpos, const int64_t *region, void *workspace, size_t workspace_bytes,
+    float *pos_out, int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
+    double *init_center, int32_t *z_bad, ccmpc_stream_t stream) {
+  PackCopy pk;
+  if (!pack_args(pack_dev, pack_host, pack_bytes, pk)) return CCMPC_ERR_ARG;
+  return bucket_predictions_impl(pred, z, nullptr, z_bytes, rows, n_ov, N, T, n_latent, keep_map,
+                                 n_kept, cell_base, max_k, minpos, region, workspace,
+                                 workspace_bytes, pos_out, ld_out, cell_off, cell_cnt, cell_pmf,
+                                 init_center, z_bad, stream, &pk);
+}
+
+extern "C" int ccmpc_bucket_predictions_indirect_packed(
+    void *pack_dev, const void *pack_host, size_t pack_bytes, const uint64_t *ptrs, int z_bytes,
+    const int32_t *rows, int64_t n_ov, int64_t N, int64_t T, int64_t n_latent,
+    const int32_t *keep_map, const int32_t *n_kept, const int32_t *cell_base, int64_t max_k,
+    const double *minpos, const int64_t *region, void *workspace, size_t workspace_bytes,
+    float *pos_out, int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt, double *cell_pmf,
+    double *init_center, int32_t *z_bad, ccmpc_stream_t stream) {
+  CCMPC_REQUIRE(ptrs, "null ptrs");
+  PackCopy pk;
+  if (!pack_args(pack_dev, pack_host, pack_bytes, pk)) return CCMPC_ERR_ARG;
+  return bucket_predictions_impl(nullptr, nullptr, ptrs, z_bytes, rows, n_ov, N, T, n_latent,
+                                 keep_map, n_kept, cell_base, max_k, minpos, region, workspace,
+                                 workspace_bytes, pos_out, ld_out, cell_off, cell_cnt, cell_pmf,
+                                 init_center, z_bad, stream, &pk);
 }

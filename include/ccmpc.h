@@ -450,6 +450,48 @@ int ccmpc_bucket_predictions_indirect(const uint64_t *ptrs, int z_bytes, const i
                                       double *cell_pmf, double *init_center, int32_t *z_bad,
                                       ccmpc_stream_t stream);
 
+/* The three placement calls above with the caller's input pack copied in the same first launch
+ * (the planning-step graph's packed H2D copy): equal to
+ *   ccmpc_copy_kernel_async(pack_dev, pack_host, pack_bytes, stream)
+ * followed by the unpacked call, whose pointer arguments may point into pack_dev.  The latent-id
+ * pass reads its own inputs (latent CDF, keep map, seed, z or the predictor's addresses) from the
+ * pinned host side while the copy runs, so the copy's kernel boundary leaves the step.
+ * pack_host: pinned host memory (device-accessible by its host address); pack_bytes % 16 == 0,
+ * both pointers 16-byte aligned. */
+int ccmpc_sample_bucket_packed(void *pack_dev, const void *pack_host, size_t pack_bytes,
+                               const double *init_state, const double *latent_cdf,
+                               int64_t n_latent, const float *gmm, int32_t gmm_layout,
+                               const int32_t *z_in, const float *eps_in, int64_t n_ov, int64_t N,
+                               int64_t T, double dt, uint64_t seed, const uint64_t *seed_dev,
+                               int64_t ov_base, const int32_t *keep_map, const int32_t *n_kept,
+                               const int32_t *cell_base, int64_t max_k, const double *minpos,
+                               const int64_t *region, void *workspace, size_t workspace_bytes,
+                               int32_t *out_z, float *pos_out, int64_t ld_out, int64_t *cell_off,
+                               int64_t *cell_cnt, double *cell_pmf, double *init_center,
+                               ccmpc_stream_t stream);
+int ccmpc_bucket_predictions_packed(void *pack_dev, const void *pack_host, size_t pack_bytes,
+                                    const float *pred, const void *z, int z_bytes,
+                                    const int32_t *rows, int64_t n_ov, int64_t N, int64_t T,
+                                    int64_t n_latent, const int32_t *keep_map,
+                                    const int32_t *n_kept, const int32_t *cell_base,
+                                    int64_t max_k, const double *minpos, const int64_t *region,
+                                    void *workspace, size_t workspace_bytes, float *pos_out,
+                                    int64_t ld_out, int64_t *cell_off, int64_t *cell_cnt,
+                                    double *cell_pmf, double *init_center, int32_t *z_bad,
+                                    ccmpc_stream_t stream);
+int ccmpc_bucket_predictions_indirect_packed(void *pack_dev, const void *pack_host,
+                                             size_t pack_bytes, const uint64_t *ptrs,
+                                             int z_bytes, const int32_t *rows, int64_t n_ov,
+                                             int64_t N, int64_t T, int64_t n_latent,
+                                             const int32_t *keep_map, const int32_t *n_kept,
+                                             const int32_t *cell_base, int64_t max_k,
+                                             const double *minpos, const int64_t *region,
+                                             void *workspace, size_t workspace_bytes,
+                                             float *pos_out, int64_t ld_out, int64_t *cell_off,
+                                             int64_t *cell_cnt, double *cell_pmf,
+                                             double *init_center, int32_t *z_bad,
+                                             ccmpc_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * Headings, bounding-box vertices and L4 outer approximation for every (cell, t).
  * Replaces ovehicle.py:72-76 (yaws = atan2 of step deltas, step 0 from past[-1]),

@@ -67,8 +67,12 @@ def _same(out_g, out_e, ovs_g, ovs_e, K, T):
             np.testing.assert_array_equal(pg, pe)
 
 
-def test_graph_step_equals_eager_drop_in_calls(gpu):
-    from ccmpc import episode, planner
+@pytest.mark.parametrize("packed", [1, 2])
+def test_graph_step_equals_eager_drop_in_calls(gpu, packed, monkeypatch):
+    """packed = 2: the sampler route's input copy inside the placement's first launch
+    (ccmpc_sample_bucket_packed, CCMPC_STEP_PACKED=2) -- the same bits."""
+    from ccmpc import episode, planner, step
+    monkeypatch.setattr(step, "_STEP_PACKED", packed)
     init, pmf, gmm, minpos, pasts, K, eps = _inputs()
     ag = planner.MidlevelAgent(prediction_horizon=PH, n_ideal=200_000, device=gpu)
     ae = planner.MidlevelAgent(prediction_horizon=PH, n_ideal=200_000, device=gpu)

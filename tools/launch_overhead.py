@@ -1,10 +1,11 @@
-"""Per-step cost of the C2 cycle under different host launch paths (GPU box):
+"""The headline loop's fixed cost (GPU box): bench.py's timed region (K direct C-ABI launches of
+the C2 cycle between synchronisations) at several K, with the host's issue time of the K
+launches apart, so elapsed = fixed + K * per-launch can be read off.
 
-  graph      torch.cuda.CUDAGraph.replay() per step (what bench.py times)
-  ctypes     one ccmpc_minkowski_cycle C-ABI call per step, no graph
-  events     device time per step from HIP events around the same replay loop
+    python tools/launch_overhead.py
 """
 import os
+import statistics
 import sys
 import time
 
@@ -13,38 +14,43 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "cc-mpc_amd")]
 
 import torch  # noqa: E402
 
-from ccmpc import cycle, engine, synthetic  # noqa: E402
-
-
-def timed(fn, steps, dev):
-    for _ in range(50):
-        fn()
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record()
-    for _ in range(steps):
-        fn()
-    e1.record()
-    host = time.perf_counter() - t0
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    return host / steps * 1e6, wall / steps * 1e6, e0.elapsed_time(e1) * 1e3 / steps
+import bench  # noqa: E402
 
 
 def main():
-    dev = torch.device("cuda:0")
-    ovs, ref, _ = synthetic.scene(0, O=4, N=5000, T=8)
-    K = [len(o) for o in ovs]
+    from ccmpc import cycle, engine, synthetic
+    spun = bench.spin_sync(0)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ovs, ref, _ = synthetic.scene(20251015, O=4, N=5000, T=8)
     store = engine.ParticleStore.from_cells([c for o in ovs for c in o], device=dev)
-    cyc = cycle.MinkowskiCycle(store, K, ref)
-    cyc_g = cycle.MinkowskiCycle(store, K, ref).capture()
-    cyc_b = cycle.MinkowskiCycle(store, K, ref).bind()
-    for name, fn in (("graph replay", cyc_g.replay), ("ctypes direct", cyc.run),
-                     ("bound launch", cyc_b.launch)):
-        h, w, d = timed(fn, 2000, dev)
-        print(f"{name:14s}: host enqueue {h:7.2f} us/step, wall {w:7.2f} us/step, "
-              f"device {d:7.2f} us/step", flush=True)
+    cyc = cycle.MinkowskiCycle(store, [len(o) for o in ovs], ref)
+    step = cyc.bind().launch
+    for _ in range(200):
+        step()
+    torch.cuda.synchronize(dev)
+    print("spin sync:", spun)
+    t = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        torch.cuda.synchronize(dev)
+        t.append(time.perf_counter() - t0)
+    print(f"empty synchronize: {1e6 * statistics.median(t):.2f} us")
+    for K in (1, 2, 5, 10, 20, 50, 200):
+        iss, tot = [], []
+        for _ in range(30):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(K):
+                step()
+            t1 = time.perf_counter()
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            iss.append(t1 - t0)
+            tot.append(t2 - t0)
+        mi, mt = statistics.median(iss), statistics.median(tot)
+        print(f"K {K:4d}: issue {1e6 * mi / K:6.2f} us/launch, elapsed {1e6 * mt:8.1f} us "
+              f"= {1e6 * mt / K:6.2f} us/step", flush=True)
 
 
 if __name__ == "__main__":
