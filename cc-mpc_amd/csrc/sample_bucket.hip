@@ -276,11 +276,15 @@ __global__ __launch_bounds__(kFThreads) void copy_latent_count_kernel(FusedArgs 
          base += U * stride) {
       uint4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (base + u * stride < n) v[u] = src[base + u * stride];
+      for (int u = 0; u < U; ++u) {  // clamped, branch-free: all U loads in flight together
+        const size_t i = base + u * stride;
+        v[u] = src[i < n ? i : n - 1];
+      }
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (base + u * stride < n) dst[base + u * stride] = v[u];
+      for (int u = 0; u < U; ++u) {  // past the end: src[n - 1] again into dst[n - 1], harmless
+        const size_t i = base + u * stride;
+        dst[i < n ? i : n - 1] = v[u];
+      }
     }
     return;
   }
