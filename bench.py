@@ -227,7 +227,7 @@ def _backend():
     return dist.get_backend() if dist.is_initialized() else None
 
 
-def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True):
+def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True, first=0):
     """The caller side of the path: do_highlevel_control's QP
     (v8ideal/__init__.py:2850-2930) for `scenes` planning steps whose obstacles cross the ego's
     path (ccmpc.synthetic.crossing_scene: O OVs x 2 modes, N particles per OV, T steps), solved
@@ -236,7 +236,7 @@ def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True):
     is absent).  Not part of `value`."""
     from ccmpc import cycle, engine, mpc, synthetic
     cells, K, cps, x0s, goals, refs = [], [], [], [], [], []
-    for sc in range(scenes):
+    for sc in range(first, first + scenes):         # the batch's scenes first .. first+scenes-1
         c, k, ref, goal, x0, _ = synthetic.crossing_scene(seed + 5000 + sc, O=O, N=N, T=T)
         cells += c
         K.append(k)
@@ -262,7 +262,8 @@ def planning_qp(dev, seed, scenes=64, O=2, N=5000, T=8, with_cpu=True):
            "scenes": scenes, "halfspaces": cyc.n_constraints, "kernel_us": round(t * 1e6, 2),
            "qps_per_s": round(scenes / t, 1), "solved": int(ok.sum()),
            "infeasible": int((status == mpc.QP_MAXITER).sum()),
-           "iters_solved_max": int(iters[ok].max()) if ok.any() else None}
+           "iters_solved_max": int(iters[ok].max()) if ok.any() else None,
+           "first_solved_scene": first + int(np.argmax(ok)) if ok.any() else None}
     if with_cpu and ok.any():
         from oracle import mpc_oracle as mo
         i = int(np.argmax(ok))
@@ -1199,11 +1200,17 @@ def main():
             out["episode_c1_np100k"] = episode_c1(dev, with_cpu=False, N=100_000)
             out["planning_qp"] = planning_qp(dev, args.seed, with_cpu=not args.no_cpu)
             # one frame's QP (the reference solves one per planning step) at T = 8 and at C4's
-            # horizon T = 12 (n = 24 > 16: the four-wave interior point), and the T = 12 batch
+            # horizon T = 12 (n = 24: the active set on NM = 32 rows): the batch's first scene
+            # (infeasible at T = 12: the certificate, then the interior point) and its first
+            # solved scene, and the T = 12 batch
             out["planning_qp_single_t8"] = planning_qp(dev, args.seed, scenes=1, with_cpu=False)
             out["planning_qp_single_t12"] = planning_qp(dev, args.seed, scenes=1, T=12,
                                                         with_cpu=False)
             out["planning_qp_t12"] = planning_qp(dev, args.seed, T=12, with_cpu=False)
+            f12 = out["planning_qp_t12"]["first_solved_scene"]
+            if f12 is not None:
+                out["planning_qp_single_t12_solved"] = planning_qp(
+                    dev, args.seed, scenes=1, T=12, with_cpu=False, first=f12)
             out["v8_milp"] = v8_milp(dev, with_cpu=not args.no_cpu)
     if not args.no_sweep and rank == 0:
         out["roofline_sweep"] = sweep(dev, args.seed)

@@ -36,6 +36,9 @@ def main():
         "qp1_t8": lambda: bench.planning_qp(dev, SEED, scenes=1, with_cpu=False),
         "qp1_t12": lambda: bench.planning_qp(dev, SEED, scenes=1, T=12, with_cpu=False),
         "qp_t12": lambda: bench.planning_qp(dev, SEED, T=12, with_cpu=False),
+        "qp1_t12_solved": lambda: bench.planning_qp(
+            dev, SEED, scenes=1, T=12, with_cpu=False,
+            first=bench.planning_qp(dev, SEED, T=12, with_cpu=False)["first_solved_scene"]),
         "episode": lambda: bench.episode_c1(dev, with_cpu=False),
         "harness": lambda: bench.harness_episode(dev),
     }
