@@ -198,7 +198,10 @@ __device__ __forceinline__ L4Cell l4_cell(const L4Split &sp, int T, int chunk_id
 
 // particles per thread whose loads are issued together, before their arithmetic: 4 covers a
 // 2048-particle chunk at 512 threads
-constexpr int kL4Pre = 4;
+#ifndef CCMPC_L4_PRE
+#define CCMPC_L4_PRE 4
+#endif
+constexpr int kL4Pre = CCMPC_L4_PRE;
 
 // A particle's step delta (step 0 from past[-1], ovehicle.py:72-76) and its position
 template <typename P>
