@@ -1,6 +1,7 @@
-"""Kernel statistics from a rocprofv3 results database (the default rocpd SQLite output):
+"""Kernel statistics from a rocprofv3 results database (the default rocpd SQLite output) or
+from its CSV kernel trace (--output-format csv):
 
-    python profiles/rocpd_stats.py RUN_results.db OUT_PREFIX
+    python profiles/rocpd_stats.py RUN_results.db|RUN_kernel_trace.csv OUT_PREFIX
 
 writes OUT_PREFIX_kernel_stats.csv (name, calls, total / average / median / min / max ns) and
 OUT_PREFIX_by_grid.csv (the same per (kernel, grid size, workgroup size): one bench line's
@@ -15,10 +16,15 @@ from collections import defaultdict
 
 def main():
     db, prefix = sys.argv[1], sys.argv[2]
-    con = sqlite3.connect(db)
     by_name, by_grid = defaultdict(list), defaultdict(list)
-    for name, gx, wx, dur in con.execute(
-            "select name, grid_x, workgroup_x, duration from kernels"):
+    if db.endswith(".csv"):
+        rows = ((r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]),
+                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                for r in csv.DictReader(open(db)))
+    else:
+        rows = sqlite3.connect(db).execute(
+            "select name, grid_x, workgroup_x, duration from kernels")
+    for name, gx, wx, dur in rows:
         by_name[name].append(dur)
         by_grid[(name, gx, wx)].append(dur)
 

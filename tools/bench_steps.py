@@ -39,6 +39,7 @@ def main():
         "qp1_t12_solved": lambda: bench.planning_qp(
             dev, SEED, scenes=1, T=12, with_cpu=False,
             first=bench.planning_qp(dev, SEED, T=12, with_cpu=False)["first_solved_scene"]),
+        "milp": lambda: bench.v8_milp(dev, with_cpu=False),
         "episode": lambda: bench.episode_c1(dev, with_cpu=False),
         "harness": lambda: bench.harness_episode(dev),
     }
