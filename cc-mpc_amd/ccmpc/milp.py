@@ -129,8 +129,8 @@ class MidlevelAgentV8(planner.MidlevelAgent):
         T = self.control_horizon
         scene = self._scene(ovehicles)
         vertices, A_union, b_union = self._l4_lists(scene)
-        l4 = scene.l4()
-        rows = BigMRows(l4["A"].cpu().numpy(), l4["b"].cpu().numpy(), diag, T, self.M_big)
+        l4 = scene.l4_host()
+        rows = BigMRows(l4["A"], l4["b"], diag, T, self.M_big)
         if X is None:
             return rows, vertices, A_union, b_union
         S_big = None
@@ -390,7 +390,9 @@ class MilpBnB:
         S, T = len(nodes), self.T
         rec = self._records(nodes)
         io = _RoundIO.get(self, S, rec.shape[1])
-        if io.frame is not self:            # this frame's model on the cached buffers
+        # this frame's model on the cached buffers (the shared model rows may hold another
+        # tree's since this shape last ran)
+        if io.frame is not self or (io.model is not None and io.model["frame"] is not self):
             io.set_frame(self)
         io.rec_h[...] = rec
         st, u, X, cost = io.run()
@@ -445,6 +447,33 @@ class MilpBnB:
                        for t in range(T)], 1) if self.C else np.zeros((0, T))
         return tv, [int(i) for i in choice], fv
 
+    def _violations_all(self, X, nodes):
+        """_violations(X[s], *nodes[s]) for every node of a round at once (no road segments:
+        the same operations on the same values, so the same bits; with segments, per node)."""
+        if self.seg is not None:
+            return [self._violations(Xi, f, g) for Xi, (f, g) in zip(X, nodes)]
+        S, T = len(nodes), self.T
+        xy = np.asarray(X)[:, :T, :2]
+        nrm = lambda r: 1.0 + np.abs(r)                      # noqa: E731
+        if self.Cb:
+            lhs = np.einsum("ctj,stj->sct", self.bn, xy)
+            rhs = self.brhs + np.where(self.bsbig, 0.0, 0.0)
+            v = np.where(self.bside == 1, rhs - lhs, lhs - rhs) / nrm(rhs)
+            base_v = np.where(self.blive, v, -np.inf).max(1)
+        else:
+            base_v = np.full((S, T), -np.inf)
+        if self.C:
+            fv = (self.frhs - 0.0 - np.einsum("ctlj,stj->sctl", self.fA, xy)) / nrm(self.frhs)
+            fv = fv.min(-1)
+            for s, (faces, _) in enumerate(nodes):
+                for (c, t), l in faces.items():
+                    fv[s, c, t] = (self.frhs[c, t, l] - 0.0 - self.fA[c, t, l] @ xy[s, t]) / nrm(
+                        self.frhs[c, t, l])
+        else:
+            fv = np.full((S, 0, T), -np.inf)
+        tv = np.maximum(base_v, fv.max(1, initial=-np.inf))
+        return [(tv[s], [None] * T, fv[s]) for s in range(S)]
+
     def solve(self):
         """Returns dict(u, X, cost, faces (C, T), segments (T,) chosen polytope per t, nodes,
         launches) or None when the MILP is infeasible (the reference's CPLEX failure path)."""
@@ -456,11 +485,12 @@ class MilpBnB:
         tie = lambda c: 1e-12 * (1 + abs(c))                # noqa: E731
         while pending:
             u, X, cost, ok = self._solve_batch([n for n, _ in pending])
-            for ((faces, segs), _), ui, Xi, ci, oki in zip(pending, u, X, cost, ok):
+            viol = self._violations_all(X, [n for n, _ in pending])
+            for ((faces, segs), _), ui, Xi, ci, oki, vi in zip(pending, u, X, cost, ok, viol):
                 self.stats["nodes"] += 1
                 if not oki or (best is not None and ci >= best["cost"] - tie(best["cost"])):
                     continue
-                tv, choice, fv = self._violations(Xi, faces, segs)
+                tv, choice, fv = vi
                 if tv.max() <= self.tol:                    # feasible for the MILP
                     fc = np.zeros((self.C, self.T), np.int64)
                     if self.C:
@@ -506,6 +536,7 @@ class MilpBnB:
         return best
 
 
+_MODEL_ROWS = 64          # scenes of the shared per-frame LTV model buffer (_RoundIO)
 # CCMPC_MILP_ROUND_GRAPH=0: every round's launches issued one by one (A/B)
 _ROUND_GRAPHS = os.environ.get("CCMPC_MILP_ROUND_GRAPH", "1") == "1"
 
@@ -544,8 +575,14 @@ class _RoundIO:
         o = self.out
         self.qp.u, self.qp.X, self.qp.cost = o.d("u"), o.d("X"), o.d("cost")
         self.qp.status, self.qp.iters = o.d("status"), o.d("iters")
-        self.gamma = torch.empty((S, 4 * Tf, 2 * Tf), dtype=f64, device=dev)
-        self.xbar = torch.empty((S, 4 * Tf), dtype=f64, device=dev)
+        # the LTV model repeated per scene: rows of one buffer per (device, horizon) shared by
+        # every round shape, so a frame fills it once, not once per shape (S <= 64)
+        self.model = _RoundIO._frame_model(dev, Tf) if S <= _MODEL_ROWS else None
+        if self.model is not None:
+            self.gamma, self.xbar = self.model["gamma"][:S], self.model["xbar"][:S]
+        else:
+            self.gamma = torch.empty((S, 4 * Tf, 2 * Tf), dtype=f64, device=dev)
+            self.xbar = torch.empty((S, 4 * Tf), dtype=f64, device=dev)
         self.rec_h = self.inp.h("rec").reshape(-1).view(_GATHER).reshape(S, cells, T)
         self.flags = torch.zeros(2, dtype=i64, pin_memory=True)
         self._flags = self.flags.numpy()
@@ -566,10 +603,29 @@ class _RoundIO:
         _lib.check(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
                                                p(i.d("gen")), s), "ccmpc_copy_signal_async")
 
+    _models = {}
+
+    @classmethod
+    def _frame_model(cls, dev, Tf):
+        key = (str(dev), Tf)
+        m = cls._models.get(key)
+        if m is None:
+            m = cls._models[key] = dict(
+                frame=None,
+                gamma=torch.empty((_MODEL_ROWS, 4 * Tf, 2 * Tf), dtype=torch.float64, device=dev),
+                xbar=torch.empty((_MODEL_ROWS, 4 * Tf), dtype=torch.float64, device=dev))
+        return m
+
     def set_frame(self, bnb):
         """The frame's LTV model (device copies), goal, reference and executed controls."""
-        self.gamma.copy_(bnb.gamma.expand(self.S, -1, -1))
-        self.xbar.copy_(bnb.xbar.expand(self.S, -1))
+        m = self.model
+        if m is None:
+            self.gamma.copy_(bnb.gamma.expand(self.S, -1, -1))
+            self.xbar.copy_(bnb.xbar.expand(self.S, -1))
+        elif m["frame"] is not bnb:         # the first of this frame's round shapes
+            m["gamma"].copy_(bnb.gamma.expand(_MODEL_ROWS, -1, -1))
+            m["xbar"].copy_(bnb.xbar.expand(_MODEL_ROWS, -1))
+            m["frame"] = bnb
         i = self.inp
         i.h("goal")[...] = bnb.goal
         i.h("ref")[...] = bnb.ref[None]

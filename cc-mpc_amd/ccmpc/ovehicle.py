@@ -72,6 +72,24 @@ class ScenePredictions:
                                  with_yaw=with_yaw, with_vertices=with_vertices)
         return self._l4
 
+    _L4_HOST = ("A", "b", "yaw_mean", "yaw0_var")
+
+    def l4_host(self):
+        """The per-(cell, t) L4 outputs (A, b, yaw_mean, yaw0_var) as host arrays, brought over
+        in ONE device-to-host copy and kept with the scene's L4 (each .cpu() is a synchronising
+        round trip of its own)."""
+        l4 = self.l4()
+        h = l4.get("_host")
+        if h is None:
+            flat = torch.cat([l4[k].reshape(-1) for k in self._L4_HOST]).cpu().numpy()
+            h, o = {}, 0
+            for k in self._L4_HOST:
+                n = l4[k].numel()
+                h[k] = flat[o:o + n].reshape(tuple(l4[k].shape))
+                o += n
+            l4["_host"] = h
+        return h
+
 
 class OVehicle:
     """Mirror of ovehicle.py:OVehicle (fields :119-131), backed by a ScenePredictions."""

@@ -846,8 +846,8 @@ class MidlevelAgent:
         yaw = (yaw_mean at t = 0 [C], yaw0_var [C]) when already on the host."""
         K = scene.K
         if yaw is None:
-            l4 = scene.l4()
-            ym, yv = l4["yaw_mean"][:, 0].cpu().numpy(), l4["yaw0_var"].cpu().numpy()
+            l4 = scene.l4_host()
+            ym, yv = l4["yaw_mean"][:, 0], l4["yaw0_var"]
         else:
             ym, yv = yaw
         K = list(K)
@@ -858,8 +858,8 @@ class MidlevelAgent:
 
     def _l4_lists(self, scene):
         ph = self.prediction_horizon
-        l4 = scene.l4()
-        A, b = l4["A"].cpu().numpy(), l4["b"].cpu().numpy()
+        l4 = scene.l4_host()
+        A, b = l4["A"], l4["b"]
         A_union = _object_grid(ph, max(scene.K), scene.O)
         b_union = _object_grid(ph, max(scene.K), scene.O)
         for c, (o, k) in enumerate(scene.cell_of):

@@ -253,3 +253,26 @@ def test_bnb_tree_on_oracle_qps_v8_faces_and_road():
     plain = _OracleBnB(G, xbar, T, goal, None, p, "C", faces=(A, rhs)).solve()
     ref = mo.milp_bnb(G, xbar, T, goal, A, rhs)
     assert plain["cost"] == pytest.approx(ref["cost"], rel=1e-9)
+
+
+def test_round_violations_at_once_equal_per_node():
+    """MilpBnB._violations_all (a round's nodes at once) against _violations node by node:
+    the same bits, with and without base rows, for nodes with fixed faces."""
+    T, C, L = 6, 3, 4
+    rng = np.random.default_rng(7)
+    faces = (rng.standard_normal((C, T, L, 2)), rng.standard_normal((C, T, L)))
+    base = dict(n=rng.standard_normal((2, T, 2)), rhs=rng.standard_normal((2, T)),
+                side=np.where(rng.random((2, T)) < 0.5, 1, -1),
+                live=rng.random((2, T)) < 0.8, sbig=rng.random((2, T)) < 0.5)
+    for b in (None, base):
+        bnb = milp.MilpBnB.__new__(milp.MilpBnB)
+        bnb._host_init(T, np.zeros(2), None, milp.v8_qp_params(), 0, T, b, faces, None,
+                       milp.M_BIG, 64, 1e-7, 1000)
+        nodes = [({}, {})] + [({(int(rng.integers(C)), int(rng.integers(T))): int(rng.integers(L))
+                                for _ in range(k)}, {}) for k in range(1, 9)]
+        X = rng.standard_normal((len(nodes), T, 4)) * 5.0
+        got = bnb._violations_all(X, nodes)
+        for Xi, (f, g), (tv, ch, fv) in zip(X, nodes, got):
+            tv1, ch1, fv1 = bnb._violations(Xi, f, g)
+            assert tv.tobytes() == tv1.tobytes() and fv.tobytes() == fv1.tobytes()
+            assert ch == ch1
