@@ -664,9 +664,13 @@ def v8_milp(dev, with_cpu=True, seeds=range(20, 28), T=8, O=2):
         agent = milp.MidlevelAgentV8(prediction_horizon=T, control_horizon=T, device=dev)
         params = AttrDict(x_init=x_init, goal=goal, diag=milp.ego_diag(3.7, 1.79), O=O, K=K)
         # warm: allocations, then the round graphs (each round shape is captured at its second
-        # use): the timed call is a steady-state frame
+        # use): the timed call is a steady-state frame, on a fresh scene of the same particles
+        # (so its L4 and the L4's copy to the host are inside the frame, as they are for a new
+        # prediction)
         agent.do_highlevel_control(params, ovs)
         agent.do_highlevel_control(params, ovs)
+        ovs = ovehicle.scene_from_positions([[c] for c in cells],
+                                            [p.reshape(1, 2) for p in pasts], device=dev)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         out, err = agent.do_highlevel_control(params, ovs)

@@ -273,8 +273,10 @@ def l4(store, past_last, bbox, with_yaw=False, with_vertices=False, split=None,
                   else None)
     out["vertices"] = (torch.empty((T * 8, store.ld), dtype=torch.float64, device=dev)
                        if with_vertices else None)
-    past_last = torch.as_tensor(np.asarray(past_last, np.float64).reshape(C, 2), device=dev)
-    bbox = torch.as_tensor(np.asarray(bbox, np.float64).reshape(C, 2), device=dev)
+    # both small host inputs in one host-to-device copy
+    pb = torch.as_tensor(np.stack([np.asarray(past_last, np.float64).reshape(C, 2),
+                                   np.asarray(bbox, np.float64).reshape(C, 2)]), device=dev)
+    past_last, bbox = pb[0], pb[1]
     if split:
         need = lib.ccmpc_l4_workspace_bytes(T, C, store.n_bound)
         ws = (workspace or Workspace(dev)).get(need)

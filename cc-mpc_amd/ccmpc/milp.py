@@ -283,12 +283,19 @@ class MilpBnB:
 
     def __init__(self, T, gamma, xbar, goal, ref=None, params=None, u_order=None, T_full=None,
                  u_prev=None, base=None, faces=None, segments=None, M_big=M_BIG, batch=64,
-                 tol=1e-7, max_nodes=100000, device="cuda"):
+                 tol=1e-7, max_nodes=100000, device="cuda", ltv=None):
         from . import engine, mpc
         self.dev = engine.require_device(device)
         T_full = int(T_full or T)
-        self.gamma = gamma.reshape(1, 4 * T_full, 2 * T_full).to(self.dev)
-        self.xbar = xbar.reshape(1, 4 * T_full).to(self.dev)
+        # ltv: (x_init (4,), Ts, lon) -- the model about u = 0 rebuilt inside each round's QP
+        # launch from x_init in the round's input pack (ccmpc_mpc_qp_ltv), no gamma / xbar given
+        self.ltv = None if ltv is None else (np.asarray(ltv[0], np.float64).reshape(4),
+                                             float(ltv[1]), float(ltv[2]))
+        if self.ltv is None:
+            self.gamma = gamma.reshape(1, 4 * T_full, 2 * T_full).to(self.dev)
+            self.xbar = xbar.reshape(1, 4 * T_full).to(self.dev)
+        else:
+            self.gamma = self.xbar = None
         self.u_prev_h = None if u_prev is None else np.asarray(u_prev, np.float64).reshape(-1)
         self.u_prev = None if u_prev is None else torch.as_tensor(
             self.u_prev_h.reshape(1, -1), device=self.dev)
@@ -551,7 +558,7 @@ class _RoundIO:
     @classmethod
     def get(cls, bnb, S, cells):
         key = (str(bnb.dev), S, cells, bnb.T, bnb.T_full, bnb.ref.shape[0], bnb.u_order,
-               bytes(bnb.params))
+               bytes(bnb.params), None if bnb.ltv is None else bnb.ltv[1:])
         io = cls._cache.get(key)
         if io is None:
             while len(cls._cache) >= 32:
@@ -565,9 +572,11 @@ class _RoundIO:
         f64, i32, i64 = torch.float64, torch.int32, torch.int64
         self.S, self.T, self.Tf, self.dev = S, T, Tf, dev
         nref = bnb.ref.shape[0]
+        self.ltv = None if bnb.ltv is None else bnb.ltv[1:]      # (Ts, lon): fused rebuild
         self.inp = step.Pack([("gen", (2,), i64), ("rec", (S * cells, T, 32), torch.uint8),
                               ("goal", (S, 2), f64), ("ref", (S, nref, 2), f64),
-                              ("uprev", (S, max(2 * (Tf - T), 1)), f64)], dev)
+                              ("uprev", (S, max(2 * (Tf - T), 1)), f64),
+                              ("x0", (S, 4), f64)], dev)
         self.out = step.Pack([("u", (S, 2 * T), f64), ("X", (S, T, 4), f64), ("cost", (S,), f64),
                               ("status", (S,), i32), ("iters", (S,), i32)], dev)
         self.qp = mpc.PlanningQP([cells] * S, T, T_full=Tf, kind=mpc.REC_AFFINE_COMPACT,
@@ -577,7 +586,8 @@ class _RoundIO:
         self.qp.status, self.qp.iters = o.d("status"), o.d("iters")
         # the LTV model repeated per scene: rows of one buffer per (device, horizon) shared by
         # every round shape, so a frame fills it once, not once per shape (S <= 64)
-        self.model = _RoundIO._frame_model(dev, Tf) if S <= _MODEL_ROWS else None
+        self.model = (_RoundIO._frame_model(dev, Tf) if S <= _MODEL_ROWS and self.ltv is None
+                      else None)
         if self.model is not None:
             self.gamma, self.xbar = self.model["gamma"][:S], self.model["xbar"][:S]
         else:
@@ -599,7 +609,8 @@ class _RoundIO:
         _lib.check(lib.ccmpc_copy_kernel_async(p(i.dev), p(i.host), i.nbytes, s),
                    "ccmpc_copy_async")
         self.qp.solve(self.gamma, self.xbar, i.d("goal"), i.d("ref"), i.d("rec"),
-                      u_prev=i.d("uprev") if self.Tf > self.T else None)
+                      u_prev=i.d("uprev") if self.Tf > self.T else None,
+                      ltv=None if self.ltv is None else (i.d("x0"),) + self.ltv)
         _lib.check(lib.ccmpc_copy_signal_async(p(o.host), p(o.dev), o.nbytes, p(self.flags),
                                                p(i.d("gen")), s), "ccmpc_copy_signal_async")
 
@@ -619,7 +630,9 @@ class _RoundIO:
     def set_frame(self, bnb):
         """The frame's LTV model (device copies), goal, reference and executed controls."""
         m = self.model
-        if m is None:
+        if self.ltv is not None:            # the model is rebuilt in the launch from x_init
+            self.inp.h("x0")[...] = bnb.ltv[0][None]
+        elif m is None:
             self.gamma.copy_(bnb.gamma.expand(self.S, -1, -1))
             self.xbar.copy_(bnb.xbar.expand(self.S, -1))
         elif m["frame"] is not bnb:         # the first of this frame's round shapes
@@ -665,8 +678,7 @@ class BranchAndBound(MilpBnB):
         from . import engine, mpc
         T = int(T)
         dev = engine.require_device(device)
-        xbar, gamma = mpc.ltv(np.asarray(x_init, np.float64).reshape(1, 4), T, Ts=Ts, lon=lon)
-        super().__init__(T, gamma, xbar, goal, params=params or v8_qp_params(),
+        super().__init__(T, None, None, goal, params=params or v8_qp_params(),
                          u_order=mpc.U_ORDER_C, faces=(rows.A, rows.rhs), segments=segments,
                          M_big=rows.M_big, batch=batch, tol=tol, max_nodes=max_nodes,
-                         device=dev)
+                         device=dev, ltv=(x_init, Ts, lon))

@@ -1,5 +1,5 @@
 """cProfile of the v8 MILP frames (bench.py's v8_milp scenes, GPU box, repo root) in steady
-state: where the host's share of a frame goes.    python tools/profile_milp_host.py"""
+state, each frame on a fresh scene: where the host's share of a frame goes.    python tools/profile_milp_host.py"""
 import cProfile
 import os
 import pstats
@@ -24,14 +24,20 @@ for seed in range(20, 28):
     params = AttrDict(x_init=x_init, goal=goal, diag=milp.ego_diag(3.7, 1.79), O=O, K=K)
     agent.do_highlevel_control(params, ovs)
     agent.do_highlevel_control(params, ovs)
-    cases.append((agent, params, ovs))
+    cases.append((agent, params, (cells, pasts)))
 torch.cuda.synchronize(dev)
+
+
+def fresh(cp):   # a new scene of the same particles (its L4 computed inside the frame)
+    cells, pasts = cp
+    return ovehicle.scene_from_positions([[c] for c in cells], [p.reshape(1, 2) for p in pasts],
+                                         device=dev)
 
 
 def frames():
     for _ in range(20):
-        for agent, params, ovs in cases:
-            agent.do_highlevel_control(params, ovs)
+        for agent, params, cp in cases:
+            agent.do_highlevel_control(params, fresh(cp))
 
 
 cProfile.run("frames()", "/tmp/milp.prof")
