@@ -70,6 +70,8 @@ SIGNATURES = {
     "ccmpc_minkowski": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _D, _D, _I32, _P, _P,
                                        _P]),
     "ccmpc_affine": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _D, _P, _P]),
+    "ccmpc_minkowski_cycle_args": (ctypes.c_int, [_P]),
+    "ccmpc_cycle_args_size": (_SZ, []),
     "ccmpc_minkowski_cycle": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _I64,
                                              _I64, _P, _SZ, _P, _P, _P, _D, _D, _I32, _P, _P,
                                              _P, _P, _P]),
@@ -137,6 +139,18 @@ SIGNATURES = {
 }
 
 SELFTEST_MVOE, SELFTEST_TANGENT, SELFTEST_BOUND, SELFTEST_PAIR = 0, 1, 2, 3
+
+
+class CycleArgs(ctypes.Structure):
+    """ccmpc_cycle_args (include/ccmpc.h): ccmpc_minkowski_cycle's arguments in one struct."""
+    _fields_ = [("positions", _P), ("dtype", ctypes.c_int32), ("maxiter", ctypes.c_int32),
+                ("ld", ctypes.c_int64), ("T", ctypes.c_int64), ("origin", _P),
+                ("cell_off", _P), ("cell_cnt", _P), ("n_cells", ctypes.c_int64),
+                ("n_particles_bound", ctypes.c_int64), ("workspace", _P),
+                ("workspace_bytes", ctypes.c_size_t), ("ref_traj", _P), ("cell_ref", _P),
+                ("cell_risk", _P), ("R", ctypes.c_double), ("tol", ctypes.c_double),
+                ("out_mean", _P), ("out_cov", _P), ("out_rec", _P), ("out_prob_lower", _P),
+                ("stream", _P)]
 
 
 class CcmpcError(RuntimeError):

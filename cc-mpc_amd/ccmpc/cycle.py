@@ -12,6 +12,8 @@ Every buffer is allocated up front and every call enqueues on the current stream
 ``capture()`` records the whole cycle into one hipGraph (torch.cuda.CUDAGraph) and ``replay()``
 costs one graph launch.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -86,19 +88,26 @@ class MinkowskiCycle:
                                out_prob_lower=self.prob_lower)
 
     def bind(self):
-        """Pre-convert every argument of the one-launch C-ABI call for the current stream, so
-        `launch()` costs one foreign call (the host side of a planning step, ~4x cheaper than
-        re-deriving pointers per call).  Rebind after changing streams or buffers."""
+        """Fill the one-launch C-ABI call's argument struct for the current stream once
+        (ccmpc_minkowski_cycle_args), so `launch()` costs one single-pointer foreign call (the
+        host side of a planning step: a 22-argument ctypes call is ~2-3 us of marshalling in
+        front of every launch).  Rebind after changing streams or buffers."""
+        from . import _lib as L
         lib = engine._lib.load()
         st = self.store
         ws = self.ws.get(lib.ccmpc_moments_workspace_bytes(self.T, st.n_cells, st.n_bound))
         p = engine._p
-        self._fn = lib.ccmpc_minkowski_cycle
-        self._args = (p(st.pos), st.ccmpc_dtype, st.ld, self.T, p(st.origin), p(st.cell_off),
-                      p(st.cell_cnt), st.n_cells, st.n_bound, p(ws), ws.numel(), p(self.ref),
-                      p(self.cell_ref), p(self.risk), float(self.R), float(self.tol),
-                      int(self.maxiter), p(self.mean), p(self.cov), p(self.rec), p(self.prob_lower),
-                      engine._stream())
+        self._fn = lib.ccmpc_minkowski_cycle_args
+        self._argst = L.CycleArgs(
+            positions=p(st.pos), dtype=st.ccmpc_dtype, maxiter=int(self.maxiter), ld=st.ld,
+            T=self.T, origin=p(st.origin), cell_off=p(st.cell_off), cell_cnt=p(st.cell_cnt),
+            n_cells=st.n_cells, n_particles_bound=st.n_bound, workspace=p(ws),
+            workspace_bytes=ws.numel(), ref_traj=p(self.ref), cell_ref=p(self.cell_ref),
+            cell_risk=p(self.risk), R=float(self.R), tol=float(self.tol), out_mean=p(self.mean),
+            out_cov=p(self.cov), out_rec=p(self.rec), out_prob_lower=p(self.prob_lower),
+            stream=engine._stream())
+        self._args = (ctypes.addressof(self._argst),)
+        self._keep = ws
         return self
 
     def launch(self):

@@ -1089,3 +1089,14 @@ extern "C" int ccmpc_minkowski_cycle(const void *positions, int dtype, int64_t l
                    n_particles_bound, workspace, workspace_bytes, out_mean, out_cov, mp, stream,
                    "ccmpc_minkowski_cycle");
 }
+
+extern "C" int ccmpc_minkowski_cycle_args(const ccmpc_cycle_args *a) {
+  CCMPC_REQUIRE(a, "null args");
+  return ccmpc_minkowski_cycle(a->positions, a->dtype, a->ld, a->T, a->origin, a->cell_off,
+                               a->cell_cnt, a->n_cells, a->n_particles_bound, a->workspace,
+                               a->workspace_bytes, a->ref_traj, a->cell_ref, a->cell_risk, a->R,
+                               a->tol, a->maxiter, a->out_mean, a->out_cov, a->out_rec,
+                               a->out_prob_lower, a->stream);
+}
+
+extern "C" size_t ccmpc_cycle_args_size(void) { return sizeof(ccmpc_cycle_args); }

@@ -201,6 +201,31 @@ int ccmpc_minkowski_cycle(const void *positions, int dtype, int64_t ld, int64_t 
                           double *out_mean, double *out_cov, ccmpc_halfspace *out_rec,
                           double *out_prob_lower, ccmpc_stream_t stream);
 
+/* The same call with its arguments in one struct, filled once by a caller that launches the
+ * same cycle every step (the argument marshalling of a 22-argument foreign call is microseconds
+ * of host time in front of every launch from an interpreter).  ccmpc_cycle_args_size() =
+ * sizeof(ccmpc_cycle_args), for a binding to check its layout. */
+typedef struct ccmpc_cycle_args {
+  const void *positions;
+  int32_t dtype, maxiter;
+  int64_t ld, T;
+  const double *origin;
+  const int64_t *cell_off, *cell_cnt;
+  int64_t n_cells, n_particles_bound;
+  void *workspace;
+  size_t workspace_bytes;
+  const double *ref_traj;
+  const int32_t *cell_ref;
+  const double *cell_risk;
+  double R, tol;
+  double *out_mean, *out_cov;
+  ccmpc_halfspace *out_rec;
+  double *out_prob_lower;
+  ccmpc_stream_t stream;
+} ccmpc_cycle_args;
+int ccmpc_minkowski_cycle_args(const ccmpc_cycle_args *args);
+size_t ccmpc_cycle_args_size(void);
+
 /* ---------------------------------------------------------------------------------------
  * GMM-affine half-spaces for every (cell, t).  Replaces v8ideal/__init__.py:1470-1515.
  *  cell_gamma[c] = norm.ppf(1 - eps_ura[ov,k]/ph) (:1481-1482); out_rec[c][T].

@@ -61,3 +61,18 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f
+
+
+def test_cycle_args_struct_matches_the_header():
+    """ccmpc._lib.CycleArgs mirrors ccmpc_cycle_args: the same size as the library's, and the
+    fields in the header's order (no GPU call: the size query is host code)."""
+    import ctypes
+    import re
+    from ccmpc import _lib
+    lib = _lib.load()
+    assert lib.ccmpc_cycle_args_size() == ctypes.sizeof(_lib.CycleArgs)
+    hdr = open(os.path.join(ROOT, "include", "ccmpc.h")).read()
+    body = hdr[hdr.index("typedef struct ccmpc_cycle_args {"):hdr.index("} ccmpc_cycle_args;")]
+    names = [n for decl in body.split("{", 1)[1].split(";") if decl.strip()
+             for n in re.findall(r"\*?\s*(\w+)\s*(?:,|$)", decl.strip())]
+    assert names == [f for f, _ in _lib.CycleArgs._fields_]
