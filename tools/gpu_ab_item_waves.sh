@@ -15,3 +15,7 @@ for v in main nw2 main nw2; do
 done
 CCMPC_LIB=cc-mpc_amd/csrc/build_nw2/libccmpc.so timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests \
   > gpurun_out/ab_item_waves_tests.log 2>&1
+CCMPC_LIB=cc-mpc_amd/csrc/build_nw2/libccmpc.so timeout -k 10 600 python -u bench.py \
+  > gpurun_out/ab_item_waves_bench.json 2> gpurun_out/ab_item_waves_bench.err
+CCMPC_LIB=cc-mpc_amd/csrc/build_nw2/libccmpc.so timeout -k 10 600 python -u bench.py --steps 20 \
+  --warmup 5 > gpurun_out/ab_item_waves_bench20.json 2> gpurun_out/ab_item_waves_bench20.err
