@@ -34,9 +34,9 @@ inline int row_blocks(int64_t T) { return static_cast<int>((2 * T + 15) / 16); }
 // (one CU's 4 matrix pipes need ~4 us for a 2000-particle T=8 cell), so latency-bound sizes
 // use WQ = 64 (one load group per wave, one tree level); bandwidth-bound sizes use WQ = 256
 // (fewer slabs, shallower tree).  A cell that fits one item never leaves its workgroup.
-#ifndef CCMPC_LG_NW1  // log2 waves per work item at RB = 1 (T <= 8); build-time knob
-#define CCMPC_LG_NW1 3
-#endif
+#ifndef CCMPC_LG_NW1  // log2 waves per work item at RB = 1 (T <= 8); build-time knob: 4-wave
+#define CCMPC_LG_NW1 2  // items (256 particles) against 8-wave ones: C2 cycle 11.33 -> 10.78 us,
+#endif                  // C3 np=1e3 -9.7 -> 9.1, np=2e4 / 1e5 +0.3 / +0.5 us (r06/ab/cycle_item_waves_*)
 #ifndef CCMPC_LG_NW_BIG  // log2 waves per work item at RB >= 3 (T > 24); build-time knob
 #define CCMPC_LG_NW_BIG 3
 #endif
